@@ -1,0 +1,133 @@
+/*
+ * jiebahip.h — C ABI of libjiebahip.so, the MI355X (gfx950) segmentation path
+ * behind jieba-go's Tokenizer API.
+ *
+ * The reference (ericlingit/jieba-go) is a pure-Go package with no FFI; its
+ * boundary is its public Go API.  Each entry point below names
+ * the reference interface it replaces.  A Go caller binds these through cgo
+ * (INTEGRATION.md); the C++ mirror jieba-go_amd/host/tokenizer.hpp and the
+ * Python ctypes binding jieba-go_amd/python/jiebahip.py sit on the same calls.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Every function returns JB_OK (0) or a
+ *    negative JB_E* code; the library never aborts the process (the reference
+ *    calls log.Fatal / panic on load errors, tokenizer.go:397,405,416,443,452,656,660).
+ *  - The caller owns every input buffer; nothing is retained past return.
+ *  - Outputs returned in jb_spans are owned by the library until jb_spans_free.
+ *  - A jb_ctx may be used by several threads at once for cutting (the reference
+ *    takes pd.lock.RLock in Cut/CutParallel, tokenizer.go:82-83,152-153);
+ *    jb_add_word takes the exclusive lock.
+ *  - Token k of the output is the byte range [start[k], end[k]) of the input.
+ *    A 1-byte token whose byte is >= 0x80 is an invalid UTF-8 byte, which the
+ *    reference emits as "�" (range loop in cutNonZh, tokenizer.go:301-306).
+ */
+#ifndef JIEBAHIP_H
+#define JIEBAHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JB_OK 0
+#define JB_EINVAL (-1)  /* bad argument */
+#define JB_EIO (-2)     /* file cannot be read (reference: log.Fatal, tokenizer.go:397,443) */
+#define JB_EPARSE (-3)  /* dictionary / emission parse error (reference: log.Fatal / panic) */
+#define JB_EDEVICE (-4) /* HIP runtime error (no device, launch failure, ...) */
+#define JB_ENOMEM (-5)
+#define JB_EPANIC (-6)  /* input on which the reference panics (cutDAG slice with tail -1) */
+#define JB_ELIMIT (-7)  /* unsupported size (document >= 2 GiB, word > 255 runes) */
+
+typedef struct jb_ctx jb_ctx;
+typedef struct jb_image jb_image;
+
+/* Dictionary semantics. */
+#define JB_DICT_TXT 0    /* NewTokenizer(dictionaryFile): newPrefixDictionaryFromFile, tokenizer.go:61,389-437
+                            (first occurrence wins, size = sum of first occurrences, no prefix entries) */
+#define JB_DICT_PREFIX 1 /* NewJiebaTokenizer(): prefix_dictionary.gob = buildPrefixDictionary output,
+                            tokenizer.go:69,340-366,439-458 (last value wins, freq-0 prefix entries) */
+
+typedef struct {
+    const char *dict_path;   /* dict.txt-format file ("word freq [tag]" lines); NULL: use dict_buf */
+    const char *dict_buf;
+    size_t dict_len;
+    int dict_kind;           /* JB_DICT_TXT or JB_DICT_PREFIX */
+    int64_t size_override;   /* > 0 replaces pd.size; NewJiebaTokenizer hard-codes 60_101_967 (tokenizer.go:454) */
+    const char *emit_path;   /* prob_emit.json (tokenizer.go:654); NULL: use emit_buf */
+    const char *emit_buf;
+    size_t emit_len;
+    int device;              /* first HIP device ordinal */
+    int ndevices;            /* >= 1: documents are sharded over devices device..device+ndevices-1 */
+} jb_config;
+
+typedef struct {
+    uint64_t ntokens;
+    uint64_t *start;   /* byte offset of each token in the batch */
+    uint64_t *end;
+    uint64_t *doc_tok; /* ndocs + 1 entries: tokens of document d are [doc_tok[d], doc_tok[d+1]) */
+    uint32_t ndocs;
+} jb_spans;
+
+/* Replaces NewTokenizer (tokenizer.go:61) and NewJiebaTokenizer (tokenizer.go:69):
+ * parse the dictionary and emission table, build the device image and upload it
+ * to every configured device. */
+int jb_open(const jb_config *cfg, jb_ctx **out);
+void jb_close(jb_ctx *ctx);
+/* Last error message of the calling thread (never NULL). */
+const char *jb_last_error(void);
+
+/* Replaces Tokenizer.Cut (tokenizer.go:151) for one document. */
+int jb_cut(jb_ctx *ctx, const uint8_t *text, size_t len, int hmm, jb_spans *out);
+
+/* Replaces Tokenizer.CutParallel (tokenizer.go:81) and batches of Cut calls:
+ * ndocs documents concatenated in `text`, document d = [doc_off[d], doc_off[d+1]).
+ * Output tokens are in document order (CutParallel with ordered=true; the
+ * reference's ordered=false is a block permutation of the same tokens). */
+int jb_cut_batch(jb_ctx *ctx, const uint8_t *text, const uint64_t *doc_off, uint32_t ndocs, int hmm,
+                 jb_spans *out);
+void jb_spans_free(jb_spans *s);
+
+/* Device-resident form for pipelines and benchmarks: d_text (nbytes, plus 16
+ * readable padding bytes) and d_doc_off (ndocs+1 offsets, d_doc_off[0] == 0,
+ * d_doc_off[ndocs] == nbytes) are device pointers on ctx's first device; the
+ * work is queued on `stream` (a hipStream_t; NULL = default stream) and the
+ * call returns without synchronising.  Results stay in ctx-owned device memory
+ * until the next call: *d_start / *d_end (u32 token spans), *d_doc_tok
+ * (u64[ndocs+1]) and *d_ntok (u64 token count). */
+int jb_cut_device(jb_ctx *ctx, const uint8_t *d_text, uint64_t nbytes, const uint64_t *d_doc_off,
+                  uint32_t ndocs, int hmm, void *stream, uint32_t **d_start, uint32_t **d_end,
+                  uint64_t **d_doc_tok, uint64_t **d_ntok);
+
+/* Replaces Tokenizer.AddWord (tokenizer.go:372; the reference deadlocks there,
+ * :376 + :581).  freq < 1 takes suggestFreq's value (tokenizer.go:589-614). */
+int jb_add_word(jb_ctx *ctx, const char *word, size_t len, int64_t freq);
+
+/* Dictionary introspection (prefixDictionary.termFreq / size, tokenizer.go:382-383). */
+int jb_dict_get(jb_ctx *ctx, const char *word, size_t len, int64_t *freq); /* 1 found, 0 absent */
+int64_t jb_dict_size(jb_ctx *ctx);
+
+/* Per-kernel timing with HIP events on the launch stream (bench / profiling). */
+int jb_profile_enable(jb_ctx *ctx, int on);
+/* Fills up to cap entries: kernel name, total ms, launches. Synchronises. Returns #entries. */
+int jb_profile_read(jb_ctx *ctx, const char **names, double *ms, uint64_t *launches, int cap);
+int jb_profile_reset(jb_ctx *ctx);
+
+/* ---- host-only image access (no GPU needed; used by CPU tests) ---------- */
+int jb_image_build(const jb_config *cfg, jb_image **out);
+void jb_image_free(jb_image *img);
+/* Look up a key as the device walk sees it: returns 1 if reachable, with freq and w. */
+int jb_image_lookup(const jb_image *img, const char *word, size_t len, int64_t *freq, double *w);
+/* nodes stored, hash capacity, pages, max key length in runes, size, -Log(size) */
+int jb_image_stats(const jb_image *img, uint64_t *nodes, uint64_t *cap, uint32_t *npages, uint32_t *maxlen,
+                   int64_t *size, double *w_absent);
+/* emitP[state][string(rune)] as the device sees it (minFloat if absent). */
+double jb_image_emit(const jb_image *img, int state, uint32_t rune);
+/* Go math.Log as used for the weights (src/math/log.go algorithm). */
+double jb_go_log(double x);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JIEBAHIP_H */

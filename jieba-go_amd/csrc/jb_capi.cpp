@@ -1,0 +1,645 @@
+// jb_capi.cpp — the C ABI of libjiebahip.so (include/jiebahip.h).
+//
+// Host orchestration only: load the model files, build and upload the device
+// image, size per-device workspaces, shard batches over devices, run the
+// kernel pipeline (jb_kernels.hip) and hand spans back.  No segmentation
+// happens on the CPU: without a usable HIP device every cut returns
+// JB_EDEVICE.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <memory>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/jiebahip.h"
+#include "jb_image.h"
+#include "jb_kernels.h"
+
+using namespace jb;
+
+static thread_local std::string g_err = "";
+
+static int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(x)                                                                              \
+    do {                                                                                       \
+        hipError_t _e = (x);                                                                   \
+        if (_e != hipSuccess) return fail(JB_EDEVICE, "%s: %s", #x, hipGetErrorString(_e));   \
+    } while (0)
+
+struct jb_image {
+    Dictionary dict;
+    Emission emit;
+    Image img;
+    int dict_kind = 0;
+};
+
+namespace {
+
+// Per-launch HIP events, recorded on the launch stream.
+struct EventTimer final : KernelTimer {
+    struct Rec { int id; hipEvent_t a, b; };
+    std::vector<hipEvent_t> pool;
+    std::vector<Rec> recs;
+    size_t used = 0;
+    hipEvent_t cur_a = nullptr;
+    double ms[K_NUM] = {0};
+    uint64_t launches[K_NUM] = {0};
+    hipEvent_t take() {
+        if (used == pool.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            pool.push_back(e);
+        }
+        return pool[used++];
+    }
+    void begin(int, hipStream_t s) override {
+        cur_a = take();
+        if (cur_a) (void)hipEventRecord(cur_a, s);
+    }
+    void end(int id, hipStream_t s) override {
+        hipEvent_t b = take();
+        if (b && cur_a) {
+            (void)hipEventRecord(b, s);
+            recs.push_back(Rec{id, cur_a, b});
+        }
+    }
+    void harvest() {
+        for (const Rec& r : recs) {
+            (void)hipEventSynchronize(r.b);
+            float t = 0;
+            if (hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) {
+                ms[r.id] += t;
+                launches[r.id]++;
+            }
+        }
+        recs.clear();
+        used = 0;
+    }
+    void reset() {
+        harvest();
+        for (int k = 0; k < K_NUM; k++) { ms[k] = 0; launches[k] = 0; }
+    }
+    ~EventTimer() override {
+        for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+    }
+};
+
+struct Device {
+    int ordinal = 0;
+    std::mutex mu;  // one pipeline at a time per device workspace
+    hipStream_t stream = nullptr;
+    // image
+    uint16_t* pagemap = nullptr;
+    uint32_t* l1 = nullptr;
+    double* emit = nullptr;
+    jb_node* nodes = nullptr;
+    DevImage dim{};
+    // workspace
+    Work w{};
+    uint8_t* text = nullptr;   // staging for host batches (padded)
+    uint64_t* doc_off = nullptr;
+    uint64_t text_cap = 0;
+    uint32_t doc_cap = 0;
+    uint32_t ncu = 0;
+    EventTimer timer;
+    bool profile = false;
+};
+
+void dfree(void* p) {
+    if (p) (void)hipFree(p);
+}
+
+}  // namespace
+
+struct jb_ctx {
+    std::unique_ptr<jb_image> im;
+    std::vector<std::unique_ptr<Device>> devs;
+    std::shared_mutex lock;  // prefixDictionary.lock: cuts share, AddWord excludes
+    uint32_t ring = 16;
+};
+
+// ---------------------------------------------------------------------------
+// image
+// ---------------------------------------------------------------------------
+static int read_file(const char* path, std::string* out) {
+    FILE* f = fopen(path, "rb");
+    if (!f) return fail(JB_EIO, "open %s: %s", path, strerror(errno));
+    std::string s;
+    char buf[1 << 16];
+    size_t n;
+    while ((n = fread(buf, 1, sizeof buf, f)) > 0) s.append(buf, n);
+    const bool err = ferror(f);
+    fclose(f);
+    if (err) return fail(JB_EIO, "read %s failed", path);
+    *out = std::move(s);
+    return JB_OK;
+}
+
+extern "C" int jb_image_build(const jb_config* cfg, jb_image** out) {
+    if (!cfg || !out) return fail(JB_EINVAL, "jb_image_build: null argument");
+    if (cfg->dict_kind != JB_DICT_TXT && cfg->dict_kind != JB_DICT_PREFIX)
+        return fail(JB_EINVAL, "unknown dict_kind %d", cfg->dict_kind);
+    std::string dbuf, ebuf;
+    const char* d = cfg->dict_buf;
+    size_t dl = cfg->dict_len;
+    const char* e = cfg->emit_buf;
+    size_t el = cfg->emit_len;
+    int rc;
+    if (cfg->dict_path) {
+        if ((rc = read_file(cfg->dict_path, &dbuf))) return rc;
+        d = dbuf.data();
+        dl = dbuf.size();
+    }
+    if (cfg->emit_path) {
+        if ((rc = read_file(cfg->emit_path, &ebuf))) return rc;
+        e = ebuf.data();
+        el = ebuf.size();
+    }
+    if (!d && dl) return fail(JB_EINVAL, "no dictionary given");
+    if (!e) return fail(JB_EINVAL, "no emission table given (prob_emit.json)");
+    auto im = std::make_unique<jb_image>();
+    im->dict_kind = cfg->dict_kind;
+    std::string err;
+    if ((rc = parse_dictionary(d ? d : "", dl, cfg->dict_kind, &im->dict, &err))) return fail(rc, "%s", err.c_str());
+    if (cfg->size_override > 0) im->dict.size = cfg->size_override;
+    if ((rc = parse_emission(e, el, &im->emit, &err))) return fail(rc, "%s", err.c_str());
+    build_image(im->dict, im->emit, &im->img);
+    if (im->img.maxlen > 255) return fail(JB_ELIMIT, "dictionary word of %u runes (max 255)", im->img.maxlen);
+    *out = im.release();
+    return JB_OK;
+}
+
+extern "C" void jb_image_free(jb_image* img) { delete img; }
+
+extern "C" int jb_image_lookup(const jb_image* img, const char* word, size_t len, int64_t* freq, double* w) {
+    if (!img || (!word && len)) return fail(JB_EINVAL, "jb_image_lookup: null argument");
+    std::vector<uint32_t> runes;
+    size_t i = 0;
+    while (i < len) {
+        uint32_t x = 0;
+        for (size_t k = 0; k < 4 && i + k < len; k++) x |= (uint32_t)(uint8_t)word[i + k] << (8 * k);
+        uint32_t r;
+        const uint32_t wd = jb_decode(x, (uint32_t)std::min<size_t>(4, len - i), &r);
+        runes.push_back(r);
+        i += wd;
+    }
+    const uint32_t id = image_lookup(img->img, runes.data(), runes.size());
+    if (id == JB_EMPTY) return 0;
+    const jb_node& n = img->img.nodes[id];
+    if (freq) {
+        const uint32_t fc = n.rune_fc >> JB_FC_SHIFT;
+        auto it = img->dict.term_freq.find(std::string(word, len));
+        *freq = it != img->dict.term_freq.end() ? it->second : (fc == JB_FC_ZERO ? 0 : -1);
+    }
+    if (w) *w = n.w;
+    return 1;
+}
+
+extern "C" int jb_image_stats(const jb_image* img, uint64_t* nodes, uint64_t* cap, uint32_t* npages,
+                              uint32_t* maxlen, int64_t* size, double* w_absent) {
+    if (!img) return fail(JB_EINVAL, "null image");
+    if (nodes) *nodes = img->img.nnodes;
+    if (cap) *cap = img->img.nodes.size();
+    if (npages) *npages = img->img.npages;
+    if (maxlen) *maxlen = img->img.maxlen;
+    if (size) *size = img->img.size;
+    if (w_absent) *w_absent = img->img.w_absent;
+    return JB_OK;
+}
+
+extern "C" double jb_image_emit(const jb_image* img, int state, uint32_t rune) {
+    if (!img || state < 0 || state > 3 || rune >= 0x110000u) return JB_MIN_FLOAT;
+    const Image& m = img->img;
+    return m.emit[((size_t)m.pagemap[rune >> 8] * 256 + (rune & 255)) * 4 + state];
+}
+
+extern "C" double jb_go_log(double x) { return go_log(x); }
+
+// ---------------------------------------------------------------------------
+// devices
+// ---------------------------------------------------------------------------
+static uint32_t ring_for(uint32_t maxlen) {
+    uint32_t r = 8;
+    while (r <= maxlen) r <<= 1;
+    return r;
+}
+
+static int upload_image(Device* d, const Image& img) {
+    HIPCHK(hipSetDevice(d->ordinal));
+    dfree(d->pagemap);
+    dfree(d->l1);
+    dfree(d->emit);
+    dfree(d->nodes);
+    d->pagemap = nullptr; d->l1 = nullptr; d->emit = nullptr; d->nodes = nullptr;
+    HIPCHK(hipMalloc(&d->pagemap, img.pagemap.size() * sizeof(uint16_t)));
+    HIPCHK(hipMalloc(&d->l1, img.l1.size() * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&d->emit, img.emit.size() * sizeof(double)));
+    HIPCHK(hipMalloc(&d->nodes, img.nodes.size() * sizeof(jb_node)));
+    HIPCHK(hipMemcpy(d->pagemap, img.pagemap.data(), img.pagemap.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d->l1, img.l1.data(), img.l1.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d->emit, img.emit.data(), img.emit.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d->nodes, img.nodes.data(), img.nodes.size() * sizeof(jb_node), hipMemcpyHostToDevice));
+    d->dim.pagemap = d->pagemap;
+    d->dim.l1 = d->l1;
+    d->dim.emit = d->emit;
+    d->dim.nodes = d->nodes;
+    d->dim.mask = (uint32_t)(img.nodes.size() - 1);
+    d->dim.w_absent = img.w_absent;
+    return JB_OK;
+}
+
+static void free_work(Work* w) {
+    dfree(w->docbits); dfree(w->sbits); dfree(w->ebits); dfree(w->tile_cnt); dfree(w->tile_off);
+    dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->blk); dfree(w->lists); dfree(w->scr);
+    dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters);
+    *w = Work{};
+}
+
+// Grow-only workspace for nbytes of text and ndocs documents.
+static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
+    Work& w = d->w;
+    if (nbytes <= w.cap_bytes && ndocs <= w.cap_docs && w.counters) return JB_OK;
+    const uint64_t nb = std::max<uint64_t>(std::max(nbytes, w.cap_bytes), 4096);
+    const uint32_t ndc = std::max(std::max(ndocs, w.cap_docs), 1024u);
+    free_work(&w);
+    const uint64_t nwords = (nb + 31) / 32 + 8;
+    const uint64_t ntiles = (nb + kTileBytes - 1) / kTileBytes + 1;
+    const uint64_t nttiles = (nwords + kTokTileWords - 1) / kTokTileWords + 1;
+    HIPCHK(hipMalloc(&w.docbits, nwords * 4));
+    HIPCHK(hipMalloc(&w.sbits, nwords * 4));
+    HIPCHK(hipMalloc(&w.ebits, nwords * 4));
+    HIPCHK(hipMalloc(&w.tile_cnt, ntiles * sizeof(uint2)));
+    HIPCHK(hipMalloc(&w.tile_off, ntiles * sizeof(uint2)));
+    HIPCHK(hipMalloc(&w.ttile_cnt, nttiles * sizeof(uint2)));
+    HIPCHK(hipMalloc(&w.ttile_off, nttiles * sizeof(uint2)));
+    HIPCHK(hipMalloc(&w.blk, (nb + 4) * 4));
+    HIPCHK(hipMalloc(&w.lists, (nb + 4) * 4));
+    HIPCHK(hipMalloc(&w.scr, nb + 16));
+    HIPCHK(hipMalloc(&w.tok_start, (nb + 4) * 4));
+    HIPCHK(hipMalloc(&w.tok_end, (nb + 4) * 4));
+    HIPCHK(hipMalloc(&w.doc_tok, ((uint64_t)ndc + 2) * 8));
+    HIPCHK(hipMalloc(&w.counters, 64 * 4));
+    w.cap_bytes = nb;
+    w.cap_docs = ndc;
+    return JB_OK;
+}
+
+static int ensure_staging(Device* d, uint64_t nbytes, uint32_t ndocs) {
+    if (nbytes + 64 > d->text_cap) {
+        dfree(d->text);
+        d->text = nullptr;
+        const uint64_t cap = std::max<uint64_t>(nbytes + 64, d->text_cap * 3 / 2);
+        HIPCHK(hipMalloc(&d->text, cap));
+        d->text_cap = cap;
+    }
+    if (ndocs + 1 > d->doc_cap) {
+        dfree(d->doc_off);
+        d->doc_off = nullptr;
+        const uint32_t cap = std::max<uint32_t>(ndocs + 1, d->doc_cap * 3 / 2);
+        HIPCHK(hipMalloc(&d->doc_off, (uint64_t)cap * 8));
+        d->doc_cap = cap;
+    }
+    return JB_OK;
+}
+
+static int launch(jb_ctx* ctx, Device* d, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off,
+                  uint32_t ndocs, bool hmm, hipStream_t s) {
+    const uint32_t wg = zh_threads_for_ring(ctx->ring);
+    const uint32_t grid_zh = d->ncu * std::max(1u, zh_blocks_per_cu(hmm, ctx->ring, wg));
+    const uint32_t grid_nz = d->ncu * std::max(1u, std::min(4u, nonzh_blocks_per_cu()));
+    const hipError_t e = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, ctx->ring, wg, grid_zh,
+                                      grid_nz, s, d->profile ? &d->timer : nullptr);
+    if (e != hipSuccess) return fail(JB_EDEVICE, "pipeline launch: %s", hipGetErrorString(e));
+    return JB_OK;
+}
+
+extern "C" int jb_open(const jb_config* cfg, jb_ctx** out) {
+    if (!cfg || !out) return fail(JB_EINVAL, "jb_open: null argument");
+    *out = nullptr;
+    jb_image* img = nullptr;
+    int rc = jb_image_build(cfg, &img);
+    if (rc) return rc;
+    auto ctx = std::make_unique<jb_ctx>();
+    ctx->im.reset(img);
+    ctx->ring = ring_for(img->img.maxlen);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(JB_EDEVICE, "no HIP device available");
+    const int nuse = cfg->ndevices > 0 ? cfg->ndevices : 1;
+    if (cfg->device < 0 || cfg->device + nuse > ndev)
+        return fail(JB_EINVAL, "devices %d..%d requested, %d present", cfg->device, cfg->device + nuse - 1, ndev);
+    for (int k = 0; k < nuse; k++) {
+        auto d = std::make_unique<Device>();
+        d->ordinal = cfg->device + k;
+        HIPCHK(hipSetDevice(d->ordinal));
+        hipDeviceProp_t prop;
+        HIPCHK(hipGetDeviceProperties(&prop, d->ordinal));
+        d->ncu = (uint32_t)prop.multiProcessorCount;
+        HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        if ((rc = upload_image(d.get(), img->img))) return rc;
+        ctx->devs.push_back(std::move(d));
+    }
+    *out = ctx.release();
+    return JB_OK;
+}
+
+extern "C" void jb_close(jb_ctx* ctx) {
+    if (!ctx) return;
+    for (auto& d : ctx->devs) {
+        (void)hipSetDevice(d->ordinal);
+        (void)hipStreamSynchronize(d->stream);
+        d->timer.reset();
+        free_work(&d->w);
+        dfree(d->text); dfree(d->doc_off); dfree(d->pagemap); dfree(d->l1); dfree(d->emit); dfree(d->nodes);
+        (void)hipStreamDestroy(d->stream);
+    }
+    delete ctx;
+}
+
+extern "C" const char* jb_last_error(void) { return g_err.c_str(); }
+
+// ---------------------------------------------------------------------------
+// cutting
+// ---------------------------------------------------------------------------
+static const uint64_t kChunkBytes = 1ull << 30;  // device offsets are u32 with a zh flag bit
+
+// Cut documents [d0, d1) of a host batch on one device; appends spans.
+static int cut_range(jb_ctx* ctx, Device* d, const uint8_t* text, const uint64_t* doc_off, uint32_t d0, uint32_t d1,
+                     bool hmm, std::vector<uint64_t>* st, std::vector<uint64_t>* en, std::vector<uint64_t>* per_doc) {
+    std::lock_guard<std::mutex> g(d->mu);
+    HIPCHK(hipSetDevice(d->ordinal));
+    uint32_t a = d0;
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> hs, he;
+    std::vector<uint64_t> hdt;
+    while (a < d1) {
+        // whole documents up to kChunkBytes (a single larger document is an error)
+        uint32_t b = a + 1;
+        if (doc_off[b] - doc_off[a] >= (1ull << 31))
+            return fail(JB_ELIMIT, "document %u is %llu bytes (limit 2 GiB)", a,
+                        (unsigned long long)(doc_off[b] - doc_off[a]));
+        while (b < d1 && doc_off[b + 1] - doc_off[a] <= kChunkBytes) b++;
+        const uint64_t base = doc_off[a], nbytes = doc_off[b] - base;
+        const uint32_t nd = b - a;
+        int rc;
+        if ((rc = ensure_staging(d, nbytes, nd))) return rc;
+        if ((rc = ensure_work(d, nbytes, nd))) return rc;
+        off.resize(nd + 1);
+        for (uint32_t k = 0; k <= nd; k++) off[k] = doc_off[a + k] - base;
+        HIPCHK(hipMemcpyAsync(d->text, text + base, nbytes, hipMemcpyHostToDevice, d->stream));
+        HIPCHK(hipMemsetAsync(d->text + nbytes, 0, 16, d->stream));
+        HIPCHK(hipMemcpyAsync(d->doc_off, off.data(), (nd + 1) * 8, hipMemcpyHostToDevice, d->stream));
+        if ((rc = launch(ctx, d, d->text, nbytes, d->doc_off, nd, hmm, d->stream))) return rc;
+        uint32_t cnt[8];
+        HIPCHK(hipMemcpyAsync(cnt, d->w.counters, sizeof cnt, hipMemcpyDeviceToHost, d->stream));
+        HIPCHK(hipStreamSynchronize(d->stream));
+        if (cnt[CNT_ERR]) return fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)");
+        if (cnt[CNT_NTOK] != cnt[CNT_NTOKE])
+            return fail(JB_EDEVICE, "internal: %u token starts vs %u ends", cnt[CNT_NTOK], cnt[CNT_NTOKE]);
+        const uint32_t nt = cnt[CNT_NTOK];
+        hs.resize(nt);
+        he.resize(nt);
+        hdt.resize(nd + 1);
+        if (nt) {
+            HIPCHK(hipMemcpyAsync(hs.data(), d->w.tok_start, (uint64_t)nt * 4, hipMemcpyDeviceToHost, d->stream));
+            HIPCHK(hipMemcpyAsync(he.data(), d->w.tok_end, (uint64_t)nt * 4, hipMemcpyDeviceToHost, d->stream));
+        }
+        HIPCHK(hipMemcpyAsync(hdt.data(), d->w.doc_tok, (uint64_t)(nd + 1) * 8, hipMemcpyDeviceToHost, d->stream));
+        HIPCHK(hipStreamSynchronize(d->stream));
+        const size_t o = st->size();
+        st->resize(o + nt);
+        en->resize(o + nt);
+        for (uint32_t k = 0; k < nt; k++) {
+            (*st)[o + k] = base + hs[k];
+            (*en)[o + k] = base + he[k];
+        }
+        for (uint32_t k = 0; k < nd; k++) per_doc->push_back(hdt[k + 1] - hdt[k]);
+        a = b;
+    }
+    return JB_OK;
+}
+
+extern "C" int jb_cut_batch(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off, uint32_t ndocs, int hmm,
+                            jb_spans* out) {
+    if (!ctx || !out || (!doc_off && ndocs)) return fail(JB_EINVAL, "jb_cut_batch: null argument");
+    memset(out, 0, sizeof *out);
+    for (uint32_t k = 0; k < ndocs; k++)
+        if (doc_off[k + 1] < doc_off[k]) return fail(JB_EINVAL, "doc_off not monotonic at %u", k);
+    if (ndocs && !text && doc_off[ndocs] > doc_off[0]) return fail(JB_EINVAL, "null text");
+    std::shared_lock<std::shared_mutex> rl(ctx->lock);
+    const size_t nd = ctx->devs.size();
+    // contiguous byte-balanced document ranges, one per device
+    std::vector<uint32_t> cut(nd + 1, ndocs);
+    cut[0] = 0;
+    const uint64_t total = ndocs ? doc_off[ndocs] - doc_off[0] : 0;
+    for (size_t k = 1; k < nd; k++) {
+        const uint64_t target = (ndocs ? doc_off[0] : 0) + total * k / nd;
+        uint32_t lo = cut[k - 1];
+        while (lo < ndocs && doc_off[lo + 1] <= target) lo++;
+        cut[k] = lo;
+    }
+    std::vector<std::vector<uint64_t>> st(nd), en(nd), pd(nd);
+    std::vector<int> rcs(nd, JB_OK);
+    std::vector<std::string> errs(nd);
+    auto work = [&](size_t k) {
+        if (cut[k] < cut[k + 1]) {
+            rcs[k] = cut_range(ctx, ctx->devs[k].get(), text, doc_off, cut[k], cut[k + 1], hmm != 0, &st[k], &en[k],
+                               &pd[k]);
+            if (rcs[k]) errs[k] = g_err;
+        }
+    };
+    if (nd == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t k = 0; k < nd; k++) th.emplace_back(work, k);
+        for (auto& t : th) t.join();
+    }
+    for (size_t k = 0; k < nd; k++)
+        if (rcs[k]) return fail(rcs[k], "%s", errs[k].c_str());
+    uint64_t nt = 0;
+    for (size_t k = 0; k < nd; k++) nt += st[k].size();
+    out->ntokens = nt;
+    out->ndocs = ndocs;
+    out->start = (uint64_t*)malloc(std::max<uint64_t>(nt, 1) * 8);
+    out->end = (uint64_t*)malloc(std::max<uint64_t>(nt, 1) * 8);
+    out->doc_tok = (uint64_t*)malloc(((uint64_t)ndocs + 1) * 8);
+    if (!out->start || !out->end || !out->doc_tok) {
+        jb_spans_free(out);
+        return fail(JB_ENOMEM, "out of host memory for %llu tokens", (unsigned long long)nt);
+    }
+    uint64_t w = 0, di = 0;
+    out->doc_tok[0] = 0;
+    for (size_t k = 0; k < nd; k++) {
+        if (!st[k].empty()) {
+            memcpy(out->start + w, st[k].data(), st[k].size() * 8);
+            memcpy(out->end + w, en[k].data(), en[k].size() * 8);
+        }
+        uint64_t acc = w;
+        for (uint64_t c : pd[k]) {
+            acc += c;
+            out->doc_tok[++di] = acc;
+        }
+        w += st[k].size();
+    }
+    while (di < ndocs) out->doc_tok[++di] = w;
+    return JB_OK;
+}
+
+extern "C" int jb_cut(jb_ctx* ctx, const uint8_t* text, size_t len, int hmm, jb_spans* out) {
+    const uint64_t off[2] = {0, (uint64_t)len};
+    static const uint8_t empty[1] = {0};
+    return jb_cut_batch(ctx, text ? text : empty, off, 1, hmm, out);
+}
+
+extern "C" void jb_spans_free(jb_spans* s) {
+    if (!s) return;
+    free(s->start);
+    free(s->end);
+    free(s->doc_tok);
+    memset(s, 0, sizeof *s);
+}
+
+extern "C" int jb_cut_device(jb_ctx* ctx, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off,
+                             uint32_t ndocs, int hmm, void* stream, uint32_t** d_start, uint32_t** d_end,
+                             uint64_t** d_doc_tok, uint64_t** d_ntok) {
+    if (!ctx || (!d_text && nbytes) || !d_doc_off) return fail(JB_EINVAL, "jb_cut_device: null argument");
+    if (nbytes >= (1ull << 31)) return fail(JB_ELIMIT, "device batch of %llu bytes (limit 2 GiB)",
+                                            (unsigned long long)nbytes);
+    if (((uintptr_t)d_text & 15u) != 0) return fail(JB_EINVAL, "d_text must be 16-byte aligned");
+    std::shared_lock<std::shared_mutex> rl(ctx->lock);
+    Device* d = ctx->devs[0].get();
+    std::lock_guard<std::mutex> g(d->mu);
+    HIPCHK(hipSetDevice(d->ordinal));
+    int rc;
+    if ((rc = ensure_work(d, nbytes, ndocs))) return rc;
+    if ((rc = launch(ctx, d, d_text, nbytes, d_doc_off, ndocs, hmm != 0, (hipStream_t)stream))) return rc;
+    if (d_start) *d_start = d->w.tok_start;
+    if (d_end) *d_end = d->w.tok_end;
+    if (d_doc_tok) *d_doc_tok = d->w.doc_tok;
+    if (d_ntok) *d_ntok = reinterpret_cast<uint64_t*>(d->w.counters + CNT_NWORDS);
+    return JB_OK;
+}
+
+// ---------------------------------------------------------------------------
+// dictionary mutation / introspection
+// ---------------------------------------------------------------------------
+extern "C" int jb_dict_get(jb_ctx* ctx, const char* word, size_t len, int64_t* freq) {
+    if (!ctx || (!word && len)) return fail(JB_EINVAL, "jb_dict_get: null argument");
+    std::shared_lock<std::shared_mutex> rl(ctx->lock);
+    auto it = ctx->im->dict.term_freq.find(std::string(word ? word : "", len));
+    if (it == ctx->im->dict.term_freq.end()) return 0;
+    if (freq) *freq = it->second;
+    return 1;
+}
+
+extern "C" int64_t jb_dict_size(jb_ctx* ctx) {
+    if (!ctx) return 0;
+    std::shared_lock<std::shared_mutex> rl(ctx->lock);
+    return ctx->im->dict.size;
+}
+
+// suggestFreq (tokenizer.go:589-614)
+static int suggest_freq(jb_ctx* ctx, const char* word, size_t len, int64_t* out) {
+    const Dictionary& dict = ctx->im->dict;
+    double dsize = (double)dict.size;
+    if (dsize < 1.0) dsize = 1.0;
+    double freq = 1.0;
+    jb_spans sp;
+    int rc = jb_cut(ctx, (const uint8_t*)word, len, 0, &sp);
+    if (rc) return rc;
+    for (uint64_t k = 0; k < sp.ntokens; k++) {
+        std::string piece;
+        if (sp.end[k] - sp.start[k] == 1 && (uint8_t)word[sp.start[k]] >= 0x80) piece = "\xEF\xBF\xBD";
+        else piece.assign(word + sp.start[k], sp.end[k] - sp.start[k]);
+        auto it = dict.term_freq.find(piece);
+        const int64_t pf = it != dict.term_freq.end() ? it->second : 1;
+        freq *= (double)pf / dsize;
+    }
+    jb_spans_free(&sp);
+    const int64_t a = (int64_t)(freq * dsize) + 1;
+    int64_t b = 1;
+    auto it = dict.term_freq.find(std::string(word, len));
+    if (it != dict.term_freq.end()) b = it->second;
+    *out = a > b ? a : b;
+    return JB_OK;
+}
+
+extern "C" int jb_add_word(jb_ctx* ctx, const char* word, size_t len, int64_t freq) {
+    if (!ctx || (!word && len)) return fail(JB_EINVAL, "jb_add_word: null argument");
+    int rc;
+    if (freq < 1) {
+        std::shared_lock<std::shared_mutex> rl(ctx->lock);
+        if ((rc = suggest_freq(ctx, word, len, &freq))) return rc;
+    }
+    std::unique_lock<std::shared_mutex> wl(ctx->lock);
+    // addTerm (tokenizer.go:580-585): no prefix entries are added
+    Dictionary& dict = ctx->im->dict;
+    dict.term_freq[std::string(word, len)] = freq;
+    dict.size += freq;
+    build_image(dict, ctx->im->emit, &ctx->im->img);
+    if (ctx->im->img.maxlen > 255) return fail(JB_ELIMIT, "dictionary word of %u runes (max 255)", ctx->im->img.maxlen);
+    ctx->ring = ring_for(ctx->im->img.maxlen);
+    for (auto& d : ctx->devs) {
+        std::lock_guard<std::mutex> g(d->mu);
+        (void)hipSetDevice(d->ordinal);
+        (void)hipStreamSynchronize(d->stream);
+        if ((rc = upload_image(d.get(), ctx->im->img))) return rc;
+    }
+    return JB_OK;
+}
+
+// ---------------------------------------------------------------------------
+// profiling
+// ---------------------------------------------------------------------------
+extern "C" int jb_profile_enable(jb_ctx* ctx, int on) {
+    if (!ctx) return fail(JB_EINVAL, "null ctx");
+    for (auto& d : ctx->devs) d->profile = on != 0;
+    return JB_OK;
+}
+
+extern "C" int jb_profile_reset(jb_ctx* ctx) {
+    if (!ctx) return fail(JB_EINVAL, "null ctx");
+    for (auto& d : ctx->devs) {
+        (void)hipSetDevice(d->ordinal);
+        d->timer.reset();
+    }
+    return JB_OK;
+}
+
+extern "C" int jb_profile_read(jb_ctx* ctx, const char** names, double* ms, uint64_t* launches, int cap) {
+    if (!ctx) return fail(JB_EINVAL, "null ctx");
+    double tot_ms[K_NUM] = {0};
+    uint64_t tot_n[K_NUM] = {0};
+    for (auto& d : ctx->devs) {
+        (void)hipSetDevice(d->ordinal);
+        d->timer.harvest();
+        for (int k = 0; k < K_NUM; k++) {
+            tot_ms[k] += d->timer.ms[k];
+            tot_n[k] += d->timer.launches[k];
+        }
+    }
+    int n = 0;
+    for (int k = 0; k < K_NUM && n < cap; k++, n++) {
+        if (names) names[n] = kKernelNames[k];
+        if (ms) ms[n] = tot_ms[k];
+        if (launches) launches[n] = tot_n[k];
+    }
+    return n;
+}

@@ -1,0 +1,142 @@
+// jb_common.h — layout of the device-resident segmentation image, shared by the
+// host builder (jb_image.cpp) and the gfx950 kernels (jb_kernels.hip).
+//
+// The image replaces the reference's two Go maps:
+//   prefixDictionary.termFreq map[string]int  (tokenizer.go:381-387)
+//   hiddenMarkovModel.emitP   map[string]map[string]float64 (tokenizer.go:616-621)
+// with flat arrays that a wavefront can probe without strings:
+//
+//   pagemap[0x110000 >> 8]  u16   rune page -> dense page id (page 0 = empty page)
+//   l1[npages * 256]        u32   single-rune key -> node id  (JB_EMPTY if absent)
+//   emit[npages * 256][4]   f64   emitP[B|M|E|S][string(rune)], minFloat if absent
+//   nodes[cap]              16 B  open-addressing hash of trie edges:
+//                                 key (parent node id, rune) -> {freq class, w}
+//                                 w = math.Log(float64(freq)) - math.Log(float64(size))
+//                                 computed on the host with Go's Log algorithm.
+//
+// A node id is the index of the node's own hash slot, so walking one more rune is
+// one hash probe (usually one 16-byte load).  Only keys that the reference's walk
+// can reach are stored: keys made of valid Han runes whose every proper prefix is
+// itself a key (buildDag breaks at the first absent string, tokenizer.go:475-478).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define JB_HD __host__ __device__ __forceinline__
+#else
+#define JB_HD static inline
+#endif
+
+#define JB_EMPTY 0xFFFFFFFFu
+#define JB_ROOT 0xFFFFFFFEu
+#define JB_NPAGES_MAX (0x110000u >> 8)
+
+// freq class, stored in bits 24..25 of jb_node.rune_fc
+#define JB_FC_ZERO 0u   // freq == 0: a prefix-only entry (e.g. "撙", tokenizer_test.go:126)
+#define JB_FC_POS 1u    // freq > 0: a DAG edge (tokenizer.go:479)
+#define JB_FC_NEG 2u    // freq < 0: present, no edge, walk continues
+#define JB_FC_SHIFT 24
+#define JB_RUNE_MASK 0x1FFFFFu
+
+struct alignas(16) jb_node {
+    uint32_t parent;   // parent node id (JB_ROOT for single runes), JB_EMPTY = free slot
+    uint32_t rune_fc;  // rune | (freq class << 24)
+    double w;          // Log(freq) - Log(size)
+};
+
+// 32-bit mix of (parent, rune); identical on host and device.
+JB_HD uint32_t jb_hash(uint32_t parent, uint32_t rune) {
+    uint32_t h = parent * 0x9E3779B1u ^ (rune * 0x85EBCA77u + 0x165667B1u);
+    h ^= h >> 16;
+    h *= 0x7FEB352Du;
+    h ^= h >> 15;
+    h *= 0x846CA68Bu;
+    h ^= h >> 16;
+    return h;
+}
+
+// tokenizer.go:19
+#define JB_MIN_FLOAT (-3.14e100)
+
+// HMM states in the reference's HMMstates order (tokenizer.go:685)
+enum { JB_B = 0, JB_M = 1, JB_E = 2, JB_S = 3 };
+
+// Unicode 13.0.0 Script=Han = Go 1.18 unicode.Han (the `zh` regex, tokenizer.go:21).
+JB_HD bool jb_is_han(uint32_t r) {
+    if (r >= 0x4E00u) {
+        if (r <= 0x9FFCu) return true;
+        if (r < 0xF900u) return false;
+        if (r <= 0xFA6Du) return true;
+        if (r < 0xFA70u) return false;
+        if (r <= 0xFAD9u) return true;
+        if (r < 0x16FF0u) return false;
+        if (r <= 0x16FF1u) return true;
+        if (r < 0x20000u) return false;
+        if (r <= 0x2A6DDu) return true;
+        if (r < 0x2A700u) return false;
+        if (r <= 0x2B734u) return true;
+        if (r < 0x2B740u) return false;
+        if (r <= 0x2B81Du) return true;
+        if (r < 0x2B820u) return false;
+        if (r <= 0x2CEA1u) return true;
+        if (r < 0x2CEB0u) return false;
+        if (r <= 0x2EBE0u) return true;
+        if (r < 0x2F800u) return false;
+        if (r <= 0x2FA1Du) return true;
+        if (r < 0x30000u) return false;
+        return r <= 0x3134Au;
+    }
+    if (r >= 0x3400u) return r <= 0x4DBFu;
+    if (r < 0x2E80u) return false;
+    if (r <= 0x2E99u) return true;
+    if (r < 0x2E9Bu) return false;
+    if (r <= 0x2EF3u) return true;
+    if (r < 0x2F00u) return false;
+    if (r <= 0x2FD5u) return true;
+    if (r == 0x3005u || r == 0x3007u) return true;
+    if (r >= 0x3021u && r <= 0x3029u) return true;
+    return r >= 0x3038u && r <= 0x303Bu;
+}
+
+// Go unicode.IsSpace (cutNonZh drops these runes, tokenizer.go:302-304).
+JB_HD bool jb_is_space(uint32_t r) {
+    if (r <= 0xFFu) return (r >= 0x09u && r <= 0x0Du) || r == 0x20u || r == 0x85u || r == 0xA0u;
+    return r == 0x1680u || (r >= 0x2000u && r <= 0x200Au) || r == 0x2028u || r == 0x2029u ||
+           r == 0x202Fu || r == 0x205Fu || r == 0x3000u;
+}
+
+// The `alnum` regex class [a-zA-Z0-9] (tokenizer.go:22).
+JB_HD bool jb_is_alnum(uint32_t b) {
+    return (b - 'a' < 26u) || (b - 'A' < 26u) || (b - '0' < 10u);
+}
+
+// Go utf8.DecodeRune on the 4 bytes packed little-endian in x, with `lim`
+// (1..4) bytes available. Invalid, truncated, surrogate and overlong sequences
+// decode as U+FFFD with width 1. Returns width; writes the rune.
+JB_HD uint32_t jb_decode(uint32_t x, uint32_t lim, uint32_t* rune) {
+    const uint32_t b0 = x & 0xFFu, b1 = (x >> 8) & 0xFFu, b2 = (x >> 16) & 0xFFu, b3 = x >> 24;
+    if (b0 < 0x80u) { *rune = b0; return 1; }
+    uint32_t need, lo = 0x80u, hi = 0xBFu, cp;
+    if (b0 >= 0xC2u && b0 <= 0xDFu) { need = 2; cp = b0 & 0x1Fu; }
+    else if (b0 >= 0xE0u && b0 <= 0xEFu) {
+        need = 3; cp = b0 & 0x0Fu;
+        if (b0 == 0xE0u) lo = 0xA0u;
+        if (b0 == 0xEDu) hi = 0x9Fu;
+    } else if (b0 >= 0xF0u && b0 <= 0xF4u) {
+        need = 4; cp = b0 & 0x07u;
+        if (b0 == 0xF0u) lo = 0x90u;
+        if (b0 == 0xF4u) hi = 0x8Fu;
+    } else { *rune = 0xFFFDu; return 1; }
+    if (need > lim || b1 < lo || b1 > hi) { *rune = 0xFFFDu; return 1; }
+    cp = (cp << 6) | (b1 & 0x3Fu);
+    if (need >= 3) {
+        if ((b2 & 0xC0u) != 0x80u) { *rune = 0xFFFDu; return 1; }
+        cp = (cp << 6) | (b2 & 0x3Fu);
+    }
+    if (need == 4) {
+        if ((b3 & 0xC0u) != 0x80u) { *rune = 0xFFFDu; return 1; }
+        cp = (cp << 6) | (b3 & 0x3Fu);
+    }
+    *rune = cp;
+    return need;
+}

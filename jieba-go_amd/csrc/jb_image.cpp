@@ -1,0 +1,429 @@
+// jb_image.cpp — host loaders for the reference's model files and the builder
+// of the device image (jb_common.h).  Host code only.
+//
+//   dict.txt          parse_dictionary  (tokenizer.go:389-437 and :340-366)
+//   prob_emit.json    parse_emission    (tokenizer.go:653-661)
+//   device image      build_image       (replaces termFreq/emitP map lookups,
+//                                         tokenizer.go:468,475,516,689,708)
+#include "jb_image.h"
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cstdlib>
+
+#include "../../include/jiebahip.h"
+
+namespace jb {
+
+// Go 1.18 math.Log (src/math/log.go; the amd64 assembly performs the same
+// operations in the same order).  Built with -ffp-contract=off so that no
+// multiply-add is fused, as on Go/amd64.
+double go_log(double x) {
+    static const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10,
+                        L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01,
+                        L3 = 2.857142874366239149e-01, L4 = 2.222219843214978396e-01,
+                        L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+                        L7 = 1.479819860511658591e-01;
+    if (std::isnan(x) || x == INFINITY) return x;
+    if (x < 0) return NAN;
+    if (x == 0) return -INFINITY;
+    int ki;
+    double f1 = frexp(x, &ki);
+    if (f1 < 0.70710678118654752440) {  // Sqrt2/2
+        f1 *= 2;
+        ki--;
+    }
+    const double f = f1 - 1;
+    const double k = (double)ki;
+    const double s = f / (2 + f);
+    const double s2 = s * s;
+    const double s4 = s2 * s2;
+    const double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+    const double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+    const double R = t1 + t2;
+    const double hfsq = 0.5 * f * f;
+    return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+
+// ---------------------------------------------------------------------------
+// UTF-8 helpers (Go semantics)
+// ---------------------------------------------------------------------------
+static uint32_t decode_at(const uint8_t* s, size_t n, uint32_t* r) {
+    uint32_t x = 0;
+    const size_t take = n < 4 ? n : 4;
+    for (size_t k = 0; k < take; k++) x |= (uint32_t)s[k] << (8 * k);
+    return jb_decode(x, (uint32_t)take, r);
+}
+
+static void append_utf8(std::string* o, uint32_t r) {
+    if (r > 0x10FFFF || (r >= 0xD800 && r <= 0xDFFF)) r = 0xFFFD;
+    if (r < 0x80) o->push_back((char)r);
+    else if (r < 0x800) { o->push_back((char)(0xC0 | (r >> 6))); o->push_back((char)(0x80 | (r & 0x3F))); }
+    else if (r < 0x10000) {
+        o->push_back((char)(0xE0 | (r >> 12)));
+        o->push_back((char)(0x80 | ((r >> 6) & 0x3F)));
+        o->push_back((char)(0x80 | (r & 0x3F)));
+    } else {
+        o->push_back((char)(0xF0 | (r >> 18)));
+        o->push_back((char)(0x80 | ((r >> 12) & 0x3F)));
+        o->push_back((char)(0x80 | ((r >> 6) & 0x3F)));
+        o->push_back((char)(0x80 | (r & 0x3F)));
+    }
+}
+
+// Runes of a key when every byte sequence is valid UTF-8; false otherwise.
+static bool valid_runes(const std::string& k, std::vector<uint32_t>* out) {
+    out->clear();
+    const uint8_t* s = (const uint8_t*)k.data();
+    size_t i = 0;
+    while (i < k.size()) {
+        uint32_t r;
+        uint32_t w = decode_at(s + i, k.size() - i, &r);
+        if (r == 0xFFFD && w == 1) return false;
+        out->push_back(r);
+        i += w;
+    }
+    return true;
+}
+
+// strconv.Atoi, base 10, 64-bit.
+static bool atoi64(const char* s, size_t n, int64_t* v) {
+    if (n == 0) return false;
+    size_t i = 0;
+    bool neg = false;
+    if (s[0] == '+' || s[0] == '-') { neg = s[0] == '-'; i = 1; }
+    if (i == n) return false;
+    unsigned __int128 acc = 0;
+    for (; i < n; i++) {
+        if (s[i] < '0' || s[i] > '9') return false;
+        acc = acc * 10 + (unsigned)(s[i] - '0');
+        if (acc > ((unsigned __int128)1 << 63)) return false;
+    }
+    if (!neg && acc > (unsigned __int128)INT64_MAX) return false;
+    *v = neg ? (int64_t)(0 - (uint64_t)acc) : (int64_t)acc;
+    return true;
+}
+
+int parse_dictionary(const char* buf, size_t len, int kind, Dictionary* out, std::string* err) {
+    out->term_freq.clear();
+    out->term_freq.reserve(len / (kind == JB_DICT_TXT ? 14 : 8) + 16);
+    out->size = 0;
+    int64_t total = 0;
+    size_t pos = 0, lineno = 0;
+    std::string piece;
+    std::vector<uint32_t> runes;
+    while (pos < len) {
+        // bufio.ScanLines: split at '\n', drop one trailing '\r'
+        size_t e = pos;
+        while (e < len && buf[e] != '\n') e++;
+        size_t l = e - pos;
+        const char* line = buf + pos;
+        pos = e < len ? e + 1 : e;
+        lineno++;
+        if (l > 0 && line[l - 1] == '\r') l--;
+        if (l > 65535) break;  // bufio.Scanner stops at ErrTooLong; the reference ignores the error
+        // strings.SplitN(line, " ", 3): parts[0] word, parts[1] count
+        const char* sp = (const char*)memchr(line, ' ', l);
+        if (!sp) {
+            *err = "dictionary line " + std::to_string(lineno) + ": no count field (the reference panics)";
+            return JB_EPARSE;
+        }
+        const size_t wl = (size_t)(sp - line);
+        const char* c = sp + 1;
+        const size_t rest = l - wl - 1;
+        const char* sp2 = (const char*)memchr(c, ' ', rest);
+        const size_t cl = sp2 ? (size_t)(sp2 - c) : rest;
+        int64_t count;
+        if (!atoi64(c, cl, &count)) {
+            *err = "dictionary line " + std::to_string(lineno) + ": strconv.Atoi: invalid count";
+            return JB_EPARSE;
+        }
+        std::string word(line, wl);
+        if (kind == JB_DICT_TXT) {
+            // first occurrence wins; size sums first occurrences (tokenizer.go:418-423)
+            auto ins = out->term_freq.emplace(std::move(word), count);
+            if (ins.second) out->size += count;
+        } else {
+            // last value wins, every line counted, prefixes added with 0 (tokenizer.go:343-362)
+            total += count;
+            if (word.empty()) {
+                *err = "dictionary line " + std::to_string(lineno) + ": empty word (the reference panics)";
+                return JB_EPARSE;
+            }
+            out->term_freq[word] = count;
+            // prefix pieces are built rune by rune: invalid bytes become U+FFFD
+            const uint8_t* s = (const uint8_t*)word.data();
+            size_t i = 0;
+            piece.clear();
+            runes.clear();
+            while (i < word.size()) {
+                uint32_t r;
+                i += decode_at(s + i, word.size() - i, &r);
+                runes.push_back(r);
+            }
+            for (size_t k = 0; k + 1 < runes.size(); k++) {
+                append_utf8(&piece, runes[k]);
+                out->term_freq.emplace(piece, 0);  // only if absent
+            }
+        }
+    }
+    if (kind != JB_DICT_TXT) out->size = total;
+    return JB_OK;
+}
+
+// ---------------------------------------------------------------------------
+// prob_emit.json: encoding/json into map[string]map[string]float64
+// ---------------------------------------------------------------------------
+namespace {
+struct Json {
+    const char* s;
+    size_t n, i = 0;
+    void ws() {
+        while (i < n && (s[i] == ' ' || s[i] == '\t' || s[i] == '\n' || s[i] == '\r')) i++;
+    }
+    bool lit(char c) {
+        ws();
+        if (i < n && s[i] == c) { i++; return true; }
+        return false;
+    }
+    bool hex4(uint32_t* v) {
+        if (i + 4 > n) return false;
+        uint32_t x = 0;
+        for (int k = 0; k < 4; k++) {
+            const char c = s[i++];
+            x <<= 4;
+            if (c >= '0' && c <= '9') x |= (uint32_t)(c - '0');
+            else if (c >= 'a' && c <= 'f') x |= (uint32_t)(c - 'a' + 10);
+            else if (c >= 'A' && c <= 'F') x |= (uint32_t)(c - 'A' + 10);
+            else return false;
+        }
+        *v = x;
+        return true;
+    }
+    bool str(std::string* o) {
+        ws();
+        o->clear();
+        if (i >= n || s[i] != '"') return false;
+        i++;
+        while (i < n) {
+            const uint8_t c = (uint8_t)s[i];
+            if (c == '"') { i++; return true; }
+            if (c == '\\') {
+                if (++i >= n) return false;
+                const char e = s[i++];
+                switch (e) {
+                    case '"': o->push_back('"'); break;
+                    case '\\': o->push_back('\\'); break;
+                    case '/': o->push_back('/'); break;
+                    case 'b': o->push_back('\b'); break;
+                    case 'f': o->push_back('\f'); break;
+                    case 'n': o->push_back('\n'); break;
+                    case 'r': o->push_back('\r'); break;
+                    case 't': o->push_back('\t'); break;
+                    case 'u': {
+                        uint32_t r;
+                        if (!hex4(&r)) return false;
+                        if (r >= 0xD800 && r < 0xDC00) {
+                            const size_t save = i;
+                            uint32_t r2;
+                            if (i + 1 < n && s[i] == '\\' && s[i + 1] == 'u') {
+                                i += 2;
+                                if (!hex4(&r2)) return false;
+                                if (r2 >= 0xDC00 && r2 < 0xE000) r = 0x10000 + ((r - 0xD800) << 10) + (r2 - 0xDC00);
+                                else { r = 0xFFFD; i = save; }
+                            } else {
+                                r = 0xFFFD;
+                            }
+                        } else if (r >= 0xDC00 && r < 0xE000) {
+                            r = 0xFFFD;
+                        }
+                        append_utf8(o, r);
+                        break;
+                    }
+                    default: return false;
+                }
+            } else if (c < 0x80) {
+                o->push_back((char)c);
+                i++;
+            } else {
+                uint32_t r;
+                i += decode_at((const uint8_t*)s + i, n - i, &r);
+                append_utf8(o, r);  // invalid UTF-8 becomes U+FFFD
+            }
+        }
+        return false;
+    }
+    bool num(double* v) {
+        ws();
+        const size_t st = i;
+        while (i < n && (strchr("+-.eE0123456789", s[i]) != nullptr) && s[i] != 0) i++;
+        if (i == st || i - st > 120) return false;
+        char tmp[128];
+        memcpy(tmp, s + st, i - st);
+        tmp[i - st] = 0;
+        char* end;
+        *v = strtod(tmp, &end);  // correctly rounded, as strconv.ParseFloat
+        return *end == 0;
+    }
+    bool null() {
+        ws();
+        if (i + 4 <= n && memcmp(s + i, "null", 4) == 0) { i += 4; return true; }
+        return false;
+    }
+};
+}  // namespace
+
+int parse_emission(const char* buf, size_t len, Emission* out, std::string* err) {
+    for (auto& m : out->by_rune) m.clear();
+    Json j{buf, len};
+    std::string key, k2;
+    auto fail = [&](const char* what) {
+        *err = std::string("prob_emit.json: ") + what + " near byte " + std::to_string(j.i);
+        return JB_EPARSE;
+    };
+    if (!j.lit('{')) return fail("expected object");
+    if (j.lit('}')) return JB_OK;
+    for (;;) {
+        if (!j.str(&key)) return fail("expected key");
+        if (!j.lit(':')) return fail("expected ':'");
+        int st = -1;
+        if (key == "B") st = JB_B;
+        else if (key == "M") st = JB_M;
+        else if (key == "E") st = JB_E;
+        else if (key == "S") st = JB_S;
+        // a repeated outer key decodes into a fresh inner map (last one wins)
+        if (st >= 0) out->by_rune[st].clear();
+        if (!j.null()) {
+            if (!j.lit('{')) return fail("expected inner object");
+            if (!j.lit('}')) {
+                for (;;) {
+                    if (!j.str(&k2)) return fail("expected inner key");
+                    if (!j.lit(':')) return fail("expected ':'");
+                    double v;
+                    if (!j.num(&v)) return fail("expected number");
+                    if (st >= 0) {
+                        uint32_t r;
+                        const uint32_t w = decode_at((const uint8_t*)k2.data(), k2.size(), &r);
+                        if (!k2.empty() && w == k2.size()) out->by_rune[st][r] = v;
+                    }
+                    if (j.lit(',')) continue;
+                    if (j.lit('}')) break;
+                    return fail("expected ',' or '}'");
+                }
+            }
+        }
+        if (j.lit(',')) continue;
+        if (j.lit('}')) break;
+        return fail("expected ',' or '}'");
+    }
+    return JB_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Device image
+// ---------------------------------------------------------------------------
+static uint32_t freq_class(int64_t f) { return f > 0 ? JB_FC_POS : (f == 0 ? JB_FC_ZERO : JB_FC_NEG); }
+
+void build_image(const Dictionary& d, const Emission& e, Image* img) {
+    img->size = d.size;
+    img->total = go_log((double)d.size);       // calcDagProba: total := math.Log(float64(pd.size))
+    img->w_absent = go_log(1.0) - img->total;  // tf := 1.0 when the piece is absent (tokenizer.go:515)
+
+    // Reachable keys: valid Han runes, every proper prefix a key.  Insert level
+    // by level so that a parent's node id exists before its children.
+    struct Key { std::vector<uint32_t> r; int64_t f; };
+    std::vector<Key> keys;
+    keys.reserve(d.term_freq.size());
+    std::vector<uint32_t> runes;
+    for (const auto& kv : d.term_freq) {
+        if (!valid_runes(kv.first, &runes) || runes.empty()) continue;
+        bool han = true;
+        for (uint32_t r : runes) han = han && jb_is_han(r);
+        if (!han) continue;  // a Han run can never spell this key
+        keys.push_back(Key{runes, kv.second});
+    }
+    std::sort(keys.begin(), keys.end(), [](const Key& a, const Key& b) {
+        if (a.r.size() != b.r.size()) return a.r.size() < b.r.size();
+        return a.r < b.r;
+    });
+    uint64_t cap = 1024;
+    while (cap < keys.size() * 2) cap <<= 1;
+    img->nodes.assign(cap, jb_node{JB_EMPTY, 0, 0.0});
+    img->maxlen = 0;
+    img->nnodes = 0;
+
+    std::vector<uint8_t> page_used(JB_NPAGES_MAX, 0);
+    std::vector<std::pair<uint32_t, uint32_t>> level1;  // rune -> node id
+    const uint64_t mask = cap - 1;
+    auto find = [&](uint32_t parent, uint32_t r) -> uint32_t {
+        uint64_t h = jb_hash(parent, r) & mask;
+        for (;;) {
+            const jb_node& n = img->nodes[h];
+            if (n.parent == JB_EMPTY) return JB_EMPTY;
+            if (n.parent == parent && (n.rune_fc & JB_RUNE_MASK) == r) return (uint32_t)h;
+            h = (h + 1) & mask;
+        }
+    };
+    // node id by key prefix: resolve through the table itself
+    for (const Key& k : keys) {
+        uint32_t parent = JB_ROOT;
+        bool ok = true;
+        for (size_t i = 0; i + 1 < k.r.size() && ok; i++) {
+            parent = find(parent, k.r[i]);
+            ok = parent != JB_EMPTY;
+        }
+        if (!ok) continue;  // a proper prefix is not a key: unreachable (tokenizer.go:475-478)
+        const uint32_t r = k.r.back();
+        uint64_t h = jb_hash(parent, r) & mask;
+        while (img->nodes[h].parent != JB_EMPTY) h = (h + 1) & mask;
+        jb_node& n = img->nodes[h];
+        n.parent = parent;
+        n.rune_fc = r | (freq_class(k.f) << JB_FC_SHIFT);
+        n.w = go_log((double)k.f) - img->total;  // pieceFreq := math.Log(tf) - total (tokenizer.go:519)
+        img->nnodes++;
+        img->maxlen = std::max<uint32_t>(img->maxlen, (uint32_t)k.r.size());
+        if (parent == JB_ROOT) {
+            level1.emplace_back(r, (uint32_t)h);
+            page_used[r >> 8] = 1;
+        }
+    }
+    for (int s = 0; s < 4; s++)
+        for (const auto& kv : e.by_rune[s])
+            if (kv.first < 0x110000u) page_used[kv.first >> 8] = 1;
+    img->pagemap.assign(JB_NPAGES_MAX, 0);
+    img->npages = 1;  // page 0: the empty page
+    for (uint32_t p = 0; p < JB_NPAGES_MAX; p++)
+        if (page_used[p]) img->pagemap[p] = (uint16_t)img->npages++;
+    img->l1.assign((size_t)img->npages * 256, JB_EMPTY);
+    img->emit.assign((size_t)img->npages * 256 * 4, JB_MIN_FLOAT);  // not found -> minFloat (tokenizer.go:690,710)
+    for (const auto& p : level1) img->l1[(size_t)img->pagemap[p.first >> 8] * 256 + (p.first & 255)] = p.second;
+    for (int s = 0; s < 4; s++)
+        for (const auto& kv : e.by_rune[s]) {
+            if (kv.first >= 0x110000u) continue;
+            img->emit[((size_t)img->pagemap[kv.first >> 8] * 256 + (kv.first & 255)) * 4 + s] = kv.second;
+        }
+}
+
+uint32_t image_lookup(const Image& img, const uint32_t* runes, size_t n) {
+    if (n == 0) return JB_EMPTY;
+    const uint64_t mask = img.nodes.size() - 1;
+    const uint32_t r0 = runes[0];
+    if (r0 >= 0x110000u) return JB_EMPTY;
+    uint32_t id = img.l1[(size_t)img.pagemap[r0 >> 8] * 256 + (r0 & 255)];
+    for (size_t i = 1; i < n && id != JB_EMPTY; i++) {
+        uint64_t h = jb_hash(id, runes[i]) & mask;
+        uint32_t found = JB_EMPTY;
+        for (;;) {
+            const jb_node& nd = img.nodes[h];
+            if (nd.parent == JB_EMPTY) break;
+            if (nd.parent == id && (nd.rune_fc & JB_RUNE_MASK) == runes[i]) { found = (uint32_t)h; break; }
+            h = (h + 1) & mask;
+        }
+        id = found;
+    }
+    return id;
+}
+
+}  // namespace jb

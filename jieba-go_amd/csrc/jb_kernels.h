@@ -1,0 +1,80 @@
+// jb_kernels.h — host-side launch interface of the gfx950 segmentation kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "jb_common.h"
+
+namespace jb {
+
+// Device copy of the image (jb_common.h), passed by value to kernels.
+struct DevImage {
+    const uint16_t* pagemap;
+    const uint32_t* l1;
+    const double* emit;
+    const jb_node* nodes;
+    uint32_t mask;     // hash capacity - 1
+    double w_absent;   // math.Log(1.0) - math.Log(size)
+};
+
+// Device counters (u32 slots unless noted)
+enum {
+    CNT_NBLK = 0,   // all blocks (zh + non-zh)
+    CNT_NZH = 1,    // zh blocks
+    CNT_NTOK = 2,   // token starts
+    CNT_NTOKE = 3,  // token ends (== CNT_NTOK when consistent)
+    CNT_ERR = 4,    // bit 0: a zh block reached a tail index -1 (the reference panics)
+    CNT_NWORDS = 8  // u32 slots reserved; u64 token count lives at byte offset 32
+};
+
+constexpr int kTileBytes = 4096;       // k_blocks: 256 threads x 16 bytes
+constexpr int kTokTileWords = 1024;    // k_tok: 256 threads x 4 words (32 KiB of text)
+
+// Per-call device workspace, sized for `nbytes` of text.
+struct Work {
+    uint32_t* docbits;     // 1 bit per byte: a document starts here
+    uint32_t* sbits;       // 1 bit per byte: a token starts here
+    uint32_t* ebits;       // 1 bit per byte: a token ends here (last byte)
+    uint2* tile_cnt;       // per k_blocks tile (all, zh) counts, then exclusive offsets
+    uint2* tile_off;
+    uint2* ttile_cnt;      // per token tile (starts, ends)
+    uint2* ttile_off;
+    uint32_t* blk;         // block start | zh << 31, then sentinel nbytes
+    uint32_t* lists;       // zh block ids from the front, non-zh block ids from the back
+    uint8_t* scr;          // per rune-start byte: chosen piece length / Viterbi back-pointers
+    uint32_t* tok_start;
+    uint32_t* tok_end;
+    uint64_t* doc_tok;
+    uint32_t* counters;    // CNT_* (+ u64 ntok at counters + 8)
+    uint64_t cap_bytes = 0;
+    uint32_t cap_docs = 0;
+};
+
+// Kernel ids for per-launch timing.
+enum KernelId {
+    K_DOCBITS = 0, K_BLOCKS_COUNT, K_SCAN_BLOCKS, K_BLOCKS_WRITE, K_ZH, K_NONZH,
+    K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_NUM
+};
+extern const char* const kKernelNames[K_NUM];
+
+// Optional per-launch timer (HIP events recorded on the launch stream).
+struct KernelTimer {
+    virtual void begin(int kernel_id, hipStream_t s) = 0;
+    virtual void end(int kernel_id, hipStream_t s) = 0;
+    virtual ~KernelTimer() {}
+};
+
+// Enqueue the whole Cut pipeline on `stream`.  Returns hipSuccess or the first
+// launch error.  ring = power-of-two ring size (> longest key), wg = threads per
+// workgroup for k_zh, grid_zh = persistent grid.
+hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text, uint64_t nbytes,
+                        const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, uint32_t ring, uint32_t zh_wg,
+                        uint32_t grid_zh, uint32_t grid_nz, hipStream_t stream, KernelTimer* timer);
+
+// Threads per k_zh workgroup for a given ring size (LDS budget 32 KiB per workgroup).
+uint32_t zh_threads_for_ring(uint32_t ring);
+// Resident k_zh workgroups per CU (occupancy API), 0 if the ring size is unsupported.
+uint32_t zh_blocks_per_cu(bool hmm, uint32_t ring, uint32_t wg);
+uint32_t nonzh_blocks_per_cu();
+
+}  // namespace jb

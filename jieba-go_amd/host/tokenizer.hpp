@@ -1,0 +1,61 @@
+// tokenizer.hpp — C++ mirror of jieba-go's public Tokenizer API
+// (/root/reference/tokenizer.go:52-162, 372-379) over libjiebahip.so.
+//
+// The Go toolchain is absent from this image, so the host side above the C ABI
+// is written in C++ (the reference is compiled code); the cgo binding a Go
+// maintainer would add instead is jieba-go_amd/go/tokenizer.go.
+//
+// Same names and argument meaning as the reference.  Where the reference calls
+// log.Fatal / panic (constructor load errors, tokenizer.go:397-416,443,452,656,660;
+// the cutDAG slice panic), this mirror throws jiebago::Error.
+#pragma once
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "jiebahip.h"
+
+namespace jiebago {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+class Tokenizer {
+public:
+    // NewTokenizer(dictionaryFile) (tokenizer.go:61): dict.txt semantics, HMM from
+    // "prob_emit.json" in the working directory (tokenizer.go:654).
+    static std::unique_ptr<Tokenizer> NewTokenizer(const std::string& dictionaryFile, int device = 0);
+    // NewJiebaTokenizer() (tokenizer.go:69): prefix-dictionary semantics with
+    // size 60_101_967 (tokenizer.go:454).  The prefix map is rebuilt from
+    // "dict.txt" in the working directory (buildPrefixDictionary, tokenizer.go:340),
+    // which is what prefix_dictionary.gob caches.
+    static std::unique_ptr<Tokenizer> NewJiebaTokenizer(int device = 0);
+    // Full control (paths, semantics, size override, devices).
+    static std::unique_ptr<Tokenizer> Open(const jb_config& cfg);
+
+    ~Tokenizer();
+    Tokenizer(const Tokenizer&) = delete;
+    Tokenizer& operator=(const Tokenizer&) = delete;
+
+    // Cut (tokenizer.go:151)
+    std::vector<std::string> Cut(const std::string& text, bool useHmm);
+    // CutParallel (tokenizer.go:81).  Blocks are segmented in parallel on the
+    // GPU; numWorkers is accepted for API compatibility.  Output is always in
+    // text order (ordered=false in the reference is a block permutation).
+    std::vector<std::string> CutParallel(const std::string& text, bool hmm, int numWorkers, bool ordered);
+    // Many documents in one device pass (what CutParallel is used for).
+    std::vector<std::vector<std::string>> CutBatch(const std::vector<std::string>& docs, bool hmm);
+    // AddWord (tokenizer.go:372) without the reference's self-deadlock.
+    void AddWord(const std::string& word, int freq);
+
+    jb_ctx* handle() { return ctx_; }
+
+private:
+    explicit Tokenizer(jb_ctx* c) : ctx_(c) {}
+    jb_ctx* ctx_;
+};
+
+}  // namespace jiebago

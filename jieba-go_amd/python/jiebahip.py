@@ -1,0 +1,302 @@
+"""ctypes binding of libjiebahip.so (include/jiebahip.h).
+
+A thin Python view of the same C ABI the Go cgo wrapper binds
+(jieba-go_amd/go/tokenizer.go): used by tests/, bench.py and
+__graft_entry__.py.  `Tokenizer` mirrors jieba-go's API (tokenizer.go:52-162,
+372-379): NewTokenizer / NewJiebaTokenizer / Cut / CutParallel / AddWord.
+
+The library is loaded from jieba-go_amd/lib/ (built in-tree by
+`make -C jieba-go_amd`); a missing or unloadable library raises — there is no
+CPU fallback.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libjiebahip.so")
+
+JB_OK, JB_EINVAL, JB_EIO, JB_EPARSE, JB_EDEVICE, JB_ENOMEM, JB_EPANIC, JB_ELIMIT = 0, -1, -2, -3, -4, -5, -6, -7
+JB_DICT_TXT, JB_DICT_PREFIX = 0, 1
+JIEBA_SIZE = 60_101_967  # tokenizer.go:454
+
+# Every symbol include/jiebahip.h declares.
+EXPORTS = [
+    "jb_open", "jb_close", "jb_last_error", "jb_cut", "jb_cut_batch", "jb_spans_free", "jb_cut_device",
+    "jb_add_word", "jb_dict_get", "jb_dict_size", "jb_profile_enable", "jb_profile_read", "jb_profile_reset",
+    "jb_image_build", "jb_image_free", "jb_image_lookup", "jb_image_stats", "jb_image_emit", "jb_go_log",
+]
+
+
+class JbError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class jb_config(C.Structure):
+    _fields_ = [
+        ("dict_path", C.c_char_p), ("dict_buf", C.c_char_p), ("dict_len", C.c_size_t), ("dict_kind", C.c_int),
+        ("size_override", C.c_int64), ("emit_path", C.c_char_p), ("emit_buf", C.c_char_p), ("emit_len", C.c_size_t),
+        ("device", C.c_int), ("ndevices", C.c_int),
+    ]
+
+
+class jb_spans(C.Structure):
+    _fields_ = [
+        ("ntokens", C.c_uint64), ("start", C.POINTER(C.c_uint64)), ("end", C.POINTER(C.c_uint64)),
+        ("doc_tok", C.POINTER(C.c_uint64)), ("ndocs", C.c_uint32),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise JbError(JB_EIO, f"{LIB_PATH} not built: run `make -C jieba-go_amd` (no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        vp, cp = C.c_void_p, C.c_char_p
+        L.jb_open.argtypes = [C.POINTER(jb_config), C.POINTER(vp)]
+        L.jb_close.argtypes = [vp]
+        L.jb_close.restype = None
+        L.jb_last_error.restype = cp
+        L.jb_cut.argtypes = [vp, vp, C.c_size_t, C.c_int, C.POINTER(jb_spans)]
+        L.jb_cut_batch.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, C.POINTER(jb_spans)]
+        L.jb_spans_free.argtypes = [C.POINTER(jb_spans)]
+        L.jb_spans_free.restype = None
+        L.jb_cut_device.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_int, vp, C.POINTER(vp), C.POINTER(vp),
+                                    C.POINTER(vp), C.POINTER(vp)]
+        L.jb_add_word.argtypes = [vp, cp, C.c_size_t, C.c_int64]
+        L.jb_dict_get.argtypes = [vp, cp, C.c_size_t, C.POINTER(C.c_int64)]
+        L.jb_dict_size.argtypes = [vp]
+        L.jb_dict_size.restype = C.c_int64
+        L.jb_profile_enable.argtypes = [vp, C.c_int]
+        L.jb_profile_reset.argtypes = [vp]
+        L.jb_profile_read.argtypes = [vp, C.POINTER(cp), C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.c_int]
+        L.jb_image_build.argtypes = [C.POINTER(jb_config), C.POINTER(vp)]
+        L.jb_image_free.argtypes = [vp]
+        L.jb_image_free.restype = None
+        L.jb_image_lookup.argtypes = [vp, cp, C.c_size_t, C.POINTER(C.c_int64), C.POINTER(C.c_double)]
+        L.jb_image_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32),
+                                     C.POINTER(C.c_uint32), C.POINTER(C.c_int64), C.POINTER(C.c_double)]
+        L.jb_image_emit.argtypes = [vp, C.c_int, C.c_uint32]
+        L.jb_image_emit.restype = C.c_double
+        L.jb_go_log.argtypes = [C.c_double]
+        L.jb_go_log.restype = C.c_double
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc < 0:
+        raise JbError(rc, lib().jb_last_error().decode("utf-8", "replace"))
+    return rc
+
+
+def _b(s):
+    return s.encode("utf-8") if isinstance(s, str) else bytes(s)
+
+
+def make_config(dict_path=None, emit_path=None, dict_bytes=None, emit_bytes=None, kind=JB_DICT_TXT,
+                size_override=0, device=0, ndevices=1):
+    cfg = jb_config()
+    keep = []
+    if dict_path is not None:
+        cfg.dict_path = os.fsencode(dict_path)
+    else:
+        d = _b(dict_bytes or b"")
+        keep.append(d)
+        cfg.dict_buf, cfg.dict_len = d, len(d)
+    if emit_path is not None:
+        cfg.emit_path = os.fsencode(emit_path)
+    else:
+        e = _b(emit_bytes or b"{}")
+        keep.append(e)
+        cfg.emit_buf, cfg.emit_len = e, len(e)
+    cfg.dict_kind = kind
+    cfg.size_override = size_override
+    cfg.device = device
+    cfg.ndevices = ndevices
+    cfg._keep = keep
+    return cfg
+
+
+def spans_to_tokens(text, starts, ends):
+    """(start, end) byte spans -> Go strings; an invalid UTF-8 byte becomes "�"."""
+    t = _b(text)
+    out = []
+    for a, b in zip(starts, ends):
+        if b - a == 1 and t[a] >= 0x80:
+            out.append("�")
+        else:
+            out.append(t[a:b].decode("utf-8"))
+    return out
+
+
+class Image:
+    """Host-only device image (no GPU needed): loader + table builder."""
+
+    def __init__(self, cfg):
+        h = C.c_void_p()
+        _check(lib().jb_image_build(C.byref(cfg), C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().jb_image_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def lookup(self, word):
+        w = _b(word)
+        f, x = C.c_int64(), C.c_double()
+        r = _check(lib().jb_image_lookup(self.h, w, len(w), C.byref(f), C.byref(x)))
+        return (f.value, x.value) if r else None
+
+    def stats(self):
+        n, cap, sz = C.c_uint64(), C.c_uint64(), C.c_int64()
+        npg, ml = C.c_uint32(), C.c_uint32()
+        wa = C.c_double()
+        _check(lib().jb_image_stats(self.h, C.byref(n), C.byref(cap), C.byref(npg), C.byref(ml), C.byref(sz),
+                                    C.byref(wa)))
+        return dict(nodes=n.value, cap=cap.value, npages=npg.value, maxlen=ml.value, size=sz.value,
+                    w_absent=wa.value)
+
+    def emit(self, state, ch):
+        return lib().jb_image_emit(self.h, "BMES".index(state), ord(ch))
+
+
+class Tokenizer:
+    """jieba-go Tokenizer over the MI355X path."""
+
+    def __init__(self, cfg):
+        h = C.c_void_p()
+        _check(lib().jb_open(C.byref(cfg), C.byref(h)))
+        self.h = h
+
+    @classmethod
+    def NewTokenizer(cls, dictionaryFile, emit_path="prob_emit.json", device=0):
+        """tokenizer.go:61 — dict.txt semantics."""
+        return cls(make_config(dict_path=dictionaryFile, emit_path=emit_path, kind=JB_DICT_TXT, device=device))
+
+    @classmethod
+    def NewJiebaTokenizer(cls, dict_path="dict.txt", emit_path="prob_emit.json", device=0):
+        """tokenizer.go:69 — prefix-dictionary semantics, size 60,101,967."""
+        return cls(make_config(dict_path=dict_path, emit_path=emit_path, kind=JB_DICT_PREFIX,
+                               size_override=JIEBA_SIZE, device=device))
+
+    def close(self):
+        if self.h:
+            lib().jb_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- cutting ---------------------------------------------------------
+    def cut_spans(self, text, hmm):
+        t = _b(text)
+        sp = jb_spans()
+        _check(lib().jb_cut(self.h, t, len(t), int(hmm), C.byref(sp)))
+        try:
+            n = sp.ntokens
+            s = np.ctypeslib.as_array(sp.start, (max(n, 1),))[:n].copy()
+            e = np.ctypeslib.as_array(sp.end, (max(n, 1),))[:n].copy()
+        finally:
+            lib().jb_spans_free(C.byref(sp))
+        return s, e
+
+    def Cut(self, text, useHmm):
+        """Tokenizer.Cut (tokenizer.go:151)."""
+        s, e = self.cut_spans(text, useHmm)
+        return spans_to_tokens(text, s.tolist(), e.tolist())
+
+    def CutParallel(self, text, hmm, numWorkers=1, ordered=True):
+        """Tokenizer.CutParallel (tokenizer.go:81): always in text order."""
+        return self.Cut(text, hmm)
+
+    def cut_batch(self, buf, doc_off, hmm):
+        """Host batch -> (starts u64, ends u64, doc_tok u64[ndocs+1])."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
+        nd = len(doc_off) - 1
+        sp = jb_spans()
+        _check(lib().jb_cut_batch(self.h, buf.ctypes.data, doc_off.ctypes.data, nd, int(hmm), C.byref(sp)))
+        try:
+            n = sp.ntokens
+            s = np.ctypeslib.as_array(sp.start, (max(n, 1),))[:n].copy()
+            e = np.ctypeslib.as_array(sp.end, (max(n, 1),))[:n].copy()
+            d = np.ctypeslib.as_array(sp.doc_tok, (nd + 1,)).copy()
+        finally:
+            lib().jb_spans_free(C.byref(sp))
+        return s, e, d
+
+    def cut_device(self, d_text_ptr, nbytes, d_doc_off_ptr, ndocs, hmm, stream_ptr=0):
+        """Device-resident cut; returns device pointers (start, end, doc_tok, ntok)."""
+        a, b, c, d = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+        _check(lib().jb_cut_device(self.h, C.c_void_p(d_text_ptr), nbytes, C.c_void_p(d_doc_off_ptr), ndocs,
+                                   int(hmm), C.c_void_p(stream_ptr), C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
+        return a.value, b.value, c.value, d.value
+
+    # -- dictionary ------------------------------------------------------
+    def AddWord(self, word, freq):
+        """Tokenizer.AddWord (tokenizer.go:372) without the reference's deadlock."""
+        w = _b(word)
+        _check(lib().jb_add_word(self.h, w, len(w), freq))
+
+    def dict_get(self, word):
+        w = _b(word)
+        f = C.c_int64()
+        return f.value if _check(lib().jb_dict_get(self.h, w, len(w), C.byref(f))) else None
+
+    @property
+    def size(self):
+        return lib().jb_dict_size(self.h)
+
+    # -- profiling -------------------------------------------------------
+    def profile(self, on=True):
+        _check(lib().jb_profile_enable(self.h, int(on)))
+
+    def profile_reset(self):
+        _check(lib().jb_profile_reset(self.h))
+
+    def profile_read(self):
+        names = (C.c_char_p * 32)()
+        ms = (C.c_double * 32)()
+        n = (C.c_uint64 * 32)()
+        k = _check(lib().jb_profile_read(self.h, names, ms, n, 32))
+        return {names[i].decode(): (ms[i], n[i]) for i in range(k)}
+
+
+_hip = None
+
+
+def dev_to_host(ptr, nbytes, dtype):
+    """Copy nbytes of device memory at a raw pointer into a numpy array."""
+    global _hip
+    if _hip is None:
+        _hip = C.CDLL("libamdhip64.so")
+        _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    out = np.empty(nbytes // np.dtype(dtype).itemsize, dtype)
+    if nbytes:
+        rc = _hip.hipMemcpy(out.ctypes.data, C.c_void_p(ptr), nbytes, 2)  # hipMemcpyDeviceToHost
+        if rc != 0:
+            raise JbError(JB_EDEVICE, f"hipMemcpy failed: {rc}")
+    return out
+
+
+def go_log(x):
+    return lib().jb_go_log(float(x))

@@ -1,0 +1,225 @@
+"""GPU parity: the MI355X path (through the C ABI) against the oracle,
+bit-exact token boundaries.  Every test here runs kernels and needs the GPU."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+import jiebahip as J
+import oracle as O
+import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(dp, ep, kind=J.JB_DICT_TXT, size_override=0):
+    tk = J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep, kind=kind, size_override=size_override))
+    o = O.Oracle.from_files(dp, ep, kind, size_override)
+    return tk, o
+
+
+@pytest.fixture(scope="module")
+def small(syn_small):
+    dp, ep, s = syn_small
+    tk, o = _pair(dp, ep)
+    yield tk, o, s
+    tk.close()
+
+
+@pytest.fixture(scope="module")
+def full(syn_full):
+    dp, ep, s = syn_full
+    tk, o = _pair(dp, ep)
+    yield tk, o, s
+    tk.close()
+
+
+def _cmp_batch(tk, o, buf, off, hmm, label=""):
+    gs, ge, gd = tk.cut_batch(buf, off, hmm)
+    os_, oe, od = o.cut_batch(buf, off, hmm, nthreads=8)
+    if not (np.array_equal(gs, os_) and np.array_equal(ge, oe)):
+        n = min(len(gs), len(os_))
+        bad = int(np.argmax((gs[:n] != os_[:n]) | (ge[:n] != oe[:n]))) if n else 0
+        lo = int(min(gs[bad] if len(gs) > bad else 0, os_[bad] if len(os_) > bad else 0))
+        ctx = bytes(np.asarray(buf)[max(0, lo - 30):lo + 60]).decode("utf-8", "replace")
+        raise AssertionError(f"{label}: {len(gs)} vs {len(os_)} tokens; first diff #{bad} near byte {lo}: {ctx!r}; "
+                             f"gpu={list(zip(gs[bad:bad+5], ge[bad:bad+5]))} ref={list(zip(os_[bad:bad+5], oe[bad:bad+5]))}")
+    assert np.array_equal(gd, od), label
+
+
+def _batch_of(texts):
+    bs = [t.encode("utf-8") if isinstance(t, str) else t for t in texts]
+    off = np.zeros(len(bs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(b) for b in bs])
+    buf = np.frombuffer(b"".join(bs) + b"\0" * 16, np.uint8)
+    return buf, off
+
+
+def test_reference_kats_mini_dict(kats, mini_paths):
+    for kind in (J.JB_DICT_TXT, J.JB_DICT_PREFIX):
+        tk = J.Tokenizer(J.make_config(dict_path=mini_paths[0], emit_path=mini_paths[1], kind=kind))
+        o = O.Oracle.from_files(*mini_paths, kind=kind)
+        cases = {c["name"]: c for c in kats["cut_real_data"]["cases"]}
+        for name in ("cut 8", "cut 10", "cut 4", "cut 5", "cut 6", "cut 7"):
+            c = cases[name]
+            assert tk.Cut(c["text"], c["hmm"]) == c["want"], name
+        for c in kats["cut_real_data"]["cases"] + [{"text": x["text"], "hmm": h} for x in kats["split_text"]["cases"]
+                                                   for h in (False, True)]:
+            assert tk.Cut(c["text"], c["hmm"]) == o.cut(c["text"], c["hmm"]), c["text"]
+        for c in kats["cut_nonzh"]["cases"]:
+            assert tk.Cut(c["text"], False) == c["want"]
+        tk.close()
+
+
+EDGE_TEXTS = [
+    "", " ", "\t\n", "a", "中", "中文", "，", "。。。", "abc", "abc 中文 def", "中文abc中文",
+    "english번역『하다』今天天氣很好，ステーションabc1231+1=2我昨天去上海*important*去",
+    "　全角空格　中文　abc x\u0085y z",
+    "𠀀𠀁𠀂中𪜀文",          # 4-byte Han (Ext-B/C)
+    "㐀㐁㐂一二三㐃",        # Ext-A: absent from dict and emissions
+    "丁" * 300,
+    "一㐀丁" * 50,
+    b"\xff\xfe" + "中文".encode() + b"\x80abc\xe4\xb8",
+    "中文".encode() + b"\xed\xa0\x80\xc0\xaf\xf4\x90\x80\x80" + "文".encode() + b"\xe0\x80\xaf",
+    "⺀⺙⺛⻳⼀⿕々〇〡〩〸〻豈鶴侮頻𖿰𖿱",  # every Han range edge
+    "〆ゝ中ー文",
+    "a1+1=2 中文 x　y",
+]
+
+
+@pytest.mark.parametrize("hmm", [False, True])
+def test_edge_cases(small, hmm):
+    tk, o, s = small
+    for t in EDGE_TEXTS:
+        b = t.encode("utf-8") if isinstance(t, str) else t
+        gs, ge = tk.cut_spans(b, hmm)
+        os_, oe = o.cut_spans(b, hmm)
+        assert np.array_equal(gs, os_) and np.array_equal(ge, oe), repr(t)
+
+
+def test_invalid_utf8_and_doc_boundaries(small):
+    """Multi-byte sequences cut by a document boundary decode as invalid bytes
+    (each document is its own Go string)."""
+    tk, o, s = small
+    rng = random.Random(1)
+    pieces = [x.encode() for x in ("中", "文", "a", " ", "　", "𠀀", "，")] + [b"\xe4", b"\xb8\xad", b"\xf0\x9f",
+                                                                            b"\x80", b"\xc2", b"\xff"]
+    texts = [b"".join(rng.choice(pieces) for _ in range(rng.randint(0, 12))) for _ in range(400)]
+    # split a valid string at arbitrary byte positions
+    whole = "中文字符串测试abc中文𠀀𠀁".encode("utf-8")
+    for cut in range(1, len(whole)):
+        texts += [whole[:cut], whole[cut:]]
+    buf, off = _batch_of(texts)
+    for hmm in (0, 1):
+        _cmp_batch(tk, o, buf, off, hmm, "invalid/boundaries")
+
+
+def test_random_mixed_script(small):
+    tk, o, s = small
+    rng = random.Random(2)
+    alphabet = [chr(c) for c in range(0x4E00, 0x4E00 + 3000, 3)] + ["㐀", "㒐", "a", "Z", "9", " ", "，", "。",
+                                                                    "　", "ス", "한", " ", "\n", "𠀀"]
+    texts = ["".join(rng.choice(alphabet) for _ in range(rng.randint(0, 80))) for _ in range(2000)]
+    buf, off = _batch_of(texts)
+    for hmm in (0, 1):
+        _cmp_batch(tk, o, buf, off, hmm, "mixed")
+
+
+@pytest.mark.parametrize("hmm", [False, True])
+def test_s10k_sentences(full, hmm):
+    """Configs 2/3: 10k synthetic sentences (10-40 runes), HMM off/on."""
+    tk, o, s = full
+    buf, off, nr = s.corpus(synth.KIND_SENTENCES, 0, max_docs=10_000, target_bytes=1 << 30)
+    assert len(off) - 1 == 10_000
+    _cmp_batch(tk, o, buf, off, hmm, f"s10k hmm={hmm}")
+
+
+@pytest.mark.parametrize("hmm", [False, True])
+def test_docs_corpus(full, hmm):
+    tk, o, s = full
+    buf, off, nr = s.corpus(synth.KIND_DOCS, 1000, target_bytes=8 << 20)
+    _cmp_batch(tk, o, buf, off, hmm, f"docs hmm={hmm}")
+
+
+@pytest.mark.parametrize("kind", [synth.KIND_LONG_PUNCT, synth.KIND_LONG_OOV])
+def test_long_document(full, kind):
+    """Config 5: one 1M-rune document (5a punctuated, 5b long OOV runs)."""
+    tk, o, s = full
+    buf, off, nr = s.corpus(kind, 77, target_runes=1_000_000)
+    O.set_viterbi_backptr(True)  # same decisions as path copying (test_oracle_kats), O(m)
+    try:
+        for hmm in (0, 1):
+            _cmp_batch(tk, o, buf, off, hmm, f"long kind={kind} hmm={hmm}")
+    finally:
+        O.set_viterbi_backptr(False)
+
+
+def test_prefix_semantics_and_size_override(syn_small):
+    dp, ep, s = syn_small
+    tk, o = _pair(dp, ep, J.JB_DICT_PREFIX, J.JIEBA_SIZE)
+    buf, off, nr = s.corpus(synth.KIND_DOCS, 5, target_bytes=1 << 20)
+    for hmm in (0, 1):
+        _cmp_batch(tk, o, buf, off, hmm, "prefix dict")
+    tk.close()
+
+
+def test_add_word(mini_paths):
+    tk = J.Tokenizer(J.make_config(dict_path=mini_paths[0], emit_path=mini_paths[1]))
+    o = O.Oracle.from_files(*mini_paths, kind=0)
+    text = "今天天氣很好，我昨天去上海"
+    assert tk.Cut(text, False) == o.cut(text, False)
+    tk.AddWord("天氣", 500)
+    o.add_term("天氣", 500)
+    assert tk.dict_get("天氣") == 500 and tk.size == o.size
+    assert tk.Cut(text, False) == o.cut(text, False)
+    assert "天氣" in tk.Cut(text, False)
+    # freq < 1: suggestFreq (tokenizer.go:589-614)
+    pieces = o.cut("很好", False)
+    dsize = float(o.size)
+    f = 1.0
+    for p in pieces:
+        v = o.get(p)
+        f *= float(v if v is not None else 1) / dsize
+    want = max(int(f * dsize) + 1, o.get("很好") or 1)
+    tk.AddWord("很好", 0)
+    o.add_term("很好", want)
+    assert tk.dict_get("很好") == want
+    assert tk.Cut(text, True) == o.cut(text, True)
+    tk.close()
+
+
+def test_empty_batch_and_docs(small):
+    tk, o, s = small
+    buf, off = _batch_of(["", "", "中文", "", "abc", ""])
+    gs, ge, gd = tk.cut_batch(buf, off, True)
+    os_, oe, od = o.cut_batch(buf, off, True)
+    assert np.array_equal(gs, os_) and np.array_equal(ge, oe) and np.array_equal(gd, od)
+    buf, off = _batch_of([])
+    gs, ge, gd = tk.cut_batch(buf, off, True)
+    assert len(gs) == 0 and list(gd) == [0]
+
+
+def test_device_api_and_profile(small):
+    """jb_cut_device on torch-owned HBM buffers (the bench path) equals the
+    host-batch path; per-kernel event timing records every launch."""
+    import torch
+    tk, o, s = small
+    buf, off, nr = s.corpus(synth.KIND_DOCS, 9, target_bytes=2 << 20)
+    dev = torch.device("cuda:0")
+    d_text = torch.from_numpy(buf).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    tk.profile(True)
+    tk.profile_reset()
+    stream = torch.cuda.current_stream().cuda_stream
+    ps, pe, pd, pn = tk.cut_device(d_text.data_ptr(), int(off[-1]), d_off.data_ptr(), len(off) - 1, True, stream)
+    torch.cuda.synchronize()
+    prof = tk.profile_read()
+    tk.profile(False)
+    assert prof["k_zh"][1] == 1 and prof["k_zh"][0] > 0
+    n = int(J.dev_to_host(pn, 8, np.uint64)[0])
+    gs = J.dev_to_host(ps, 4 * n, np.uint32)
+    ge = J.dev_to_host(pe, 4 * n, np.uint32)
+    gd = J.dev_to_host(pd, 8 * len(off), np.uint64)
+    hs, he, hd = tk.cut_batch(buf, off, True)
+    assert np.array_equal(gs, hs) and np.array_equal(ge, he) and np.array_equal(gd, hd)

@@ -1,0 +1,145 @@
+"""CPU: the product library's host side — exports, loaders, device-image
+builder — checked against the oracle.  No kernel is launched here."""
+import math
+import os
+import random
+import re
+import struct
+
+import pytest
+
+import jiebahip as J
+import oracle as O
+from conftest import ROOT
+
+
+def _bits(x):
+    return struct.unpack("<q", struct.pack("<d", x))[0]
+
+
+def test_library_exports_every_declared_symbol():
+    L = J.lib()
+    with open(os.path.join(ROOT, "include", "jiebahip.h")) as f:
+        hdr = f.read()
+    declared = set(re.findall(r"\b(jb_[a-z_]+)\s*\(", hdr))
+    assert declared == set(J.EXPORTS)
+    for name in declared:
+        assert hasattr(L, name), name
+
+
+def test_go_log_product_equals_oracle_bitwise():
+    rng = random.Random(11)
+    xs = [1.0, 2.0, 60101967.0, 0.0, 3.5] + [float(rng.randint(1, 10 ** 12)) for _ in range(20000)]
+    for x in xs:
+        assert _bits(J.go_log(x)) == _bits(O.go_log(x)), x
+    assert math.isnan(J.go_log(-2.0))
+
+
+@pytest.mark.parametrize("kind", [J.JB_DICT_TXT, J.JB_DICT_PREFIX])
+def test_image_matches_oracle_map(syn_small, kind):
+    """Every key the reference's walk can reach is in the image with the
+    oracle's frequency and weight w = Log(freq) - Log(size); unreachable keys
+    are absent; size follows the dictionary semantics."""
+    dp, ep, s = syn_small
+    img = J.Image(J.make_config(dict_path=dp, emit_path=ep, kind=kind))
+    o = O.Oracle.from_files(dp, ep, kind)
+    st = img.stats()
+    assert st["size"] == o.size
+    total = O.go_log(o.size)
+    assert _bits(st["w_absent"]) == _bits(O.go_log(1.0) - total)
+    items = o.items()
+    rng = random.Random(5)
+    keys = rng.sample(sorted(items), 4000)
+    reach = 0
+    for k in keys:
+        runes = list(k)
+        reachable = all(0x3400 <= ord(c) <= 0x9FFF for c in runes) and \
+            all(items.get(k[:i]) is not None for i in range(1, len(k)))
+        got = img.lookup(k)
+        if not reachable:
+            assert got is None, k
+            continue
+        reach += 1
+        assert got is not None, k
+        f, w = got
+        assert f == items[k]
+        assert _bits(w) == _bits(O.go_log(float(items[k])) - total), k
+    assert reach > 1000
+    assert img.lookup("不在字典里的词语") is None or items.get("不在字典里的词语") is not None
+
+
+def test_image_txt_vs_prefix_semantics():
+    d = "甲乙丙 5 n\n甲 2\n甲 9\n乙丙 4\n"
+    e = "{}"
+    txt = J.Image(J.make_config(dict_bytes=d, emit_bytes=e, kind=J.JB_DICT_TXT))
+    pre = J.Image(J.make_config(dict_bytes=d, emit_bytes=e, kind=J.JB_DICT_PREFIX))
+    # txt: first wins, no prefixes -> 甲乙丙 unreachable (甲乙 absent)
+    assert txt.stats()["size"] == 5 + 2 + 4
+    assert txt.lookup("甲")[0] == 2
+    assert txt.lookup("甲乙丙") is None
+    # prefix: last wins, prefixes inserted with 0
+    assert pre.stats()["size"] == 5 + 2 + 9 + 4
+    assert pre.lookup("甲")[0] == 9
+    assert pre.lookup("甲乙")[0] == 0
+    assert pre.lookup("甲乙丙")[0] == 5
+    assert pre.lookup("甲乙")[1] == float("-inf")
+
+
+def test_size_override():
+    img = J.Image(J.make_config(dict_bytes="甲 3\n", emit_bytes="{}", kind=J.JB_DICT_PREFIX,
+                                size_override=J.JIEBA_SIZE))
+    assert img.stats()["size"] == 60_101_967
+    assert _bits(img.lookup("甲")[1]) == _bits(O.go_log(3.0) - O.go_log(60_101_967.0))
+
+
+def test_emission_matches_oracle(syn_small):
+    dp, ep, s = syn_small
+    img = J.Image(J.make_config(dict_path=dp, emit_path=ep))
+    o = O.Oracle.from_files(dp, ep, 0)
+    rng = random.Random(9)
+    for _ in range(5000):
+        ch = chr(rng.choice([rng.randint(0x4E00, 0x9FA5), rng.randint(0x3400, 0x4DBF)]))
+        for st in "BMES":
+            want = o.emit(st, ch)
+            got = img.emit(st, ch)
+            assert got == (want if want is not None else -3.14e100)
+
+
+def test_emission_json_edge_cases():
+    e = '{"B": {"\\u4e00": -1.5, "丁": -2}, "B": {"丁": -3.25}, "X": {"一": 1}, "S": null, "E": {"ab": -1}}'
+    img = J.Image(J.make_config(dict_bytes="", emit_bytes=e))
+    o = O.Oracle("", e, 0)
+    for st in "BMES":
+        for ch in "一丁":
+            want = o.emit(st, ch)
+            assert img.emit(st, ch) == (want if want is not None else -3.14e100)
+    assert img.emit("B", "丁") == -3.25 and img.emit("B", "一") == -3.14e100
+
+
+@pytest.mark.parametrize("bad,code", [("甲\n", J.JB_EPARSE), ("甲 x\n", J.JB_EPARSE), ("甲 1\n\n", J.JB_EPARSE)])
+def test_dictionary_parse_errors(bad, code):
+    with pytest.raises(J.JbError) as ei:
+        J.Image(J.make_config(dict_bytes=bad, emit_bytes="{}"))
+    assert ei.value.code == code
+
+
+def test_missing_files():
+    with pytest.raises(J.JbError) as ei:
+        J.Image(J.make_config(dict_path="/nonexistent/dict.txt", emit_path="/nonexistent/e.json"))
+    assert ei.value.code == J.JB_EIO
+
+
+def test_crlf_and_tags():
+    img = J.Image(J.make_config(dict_bytes="甲 3 n\r\n乙 4\r\n", emit_bytes="{}"))
+    assert img.lookup("甲")[0] == 3 and img.lookup("乙")[0] == 4
+
+
+def test_open_without_gpu_fails_loudly(syn_small):
+    """No CPU fallback: without a HIP device jb_open reports JB_EDEVICE."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    dp, ep, s = syn_small
+    with pytest.raises(J.JbError) as ei:
+        J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep))
+    assert ei.value.code == J.JB_EDEVICE
