@@ -207,6 +207,7 @@ def main():
             "input_GBps": round(tot_bytes * args.steps / elapsed / 1e9, 3),
             "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
             "gen_s": round(gen_s, 2),
+            "loaded": J.loaded_runtime(),
         }
         print(json.dumps(line), flush=True)
     tk.close()

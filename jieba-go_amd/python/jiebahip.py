@@ -59,6 +59,17 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise JbError(JB_EIO, f"{LIB_PATH} not built: run `make -C jieba-go_amd` (no CPU fallback exists)")
+        # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7
+        # (ROCm 7.0) under torch/lib.  Loading torch first makes the dynamic
+        # linker bind libjiebahip.so's libamdhip64.so.7 dependency to that same
+        # runtime, so torch tensors and this library share device pointers,
+        # streams and one HSA context.  (Loading the system ROCm 7.2 runtime and
+        # torch's side by side in one process left torch with "No HIP GPUs are
+        # available".)  Outside Python (Go / C++ callers) the system runtime is used.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         vp, cp = C.c_void_p, C.c_char_p
         L.jb_open.argtypes = [C.POINTER(jb_config), C.POINTER(vp)]
@@ -288,7 +299,8 @@ def dev_to_host(ptr, nbytes, dtype):
     """Copy nbytes of device memory at a raw pointer into a numpy array."""
     global _hip
     if _hip is None:
-        _hip = C.CDLL("libamdhip64.so")
+        lib()
+        _hip = C.CDLL("libamdhip64.so.7")  # the runtime libjiebahip.so is bound to
         _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
     out = np.empty(nbytes // np.dtype(dtype).itemsize, dtype)
     if nbytes:
@@ -296,6 +308,19 @@ def dev_to_host(ptr, nbytes, dtype):
         if rc != 0:
             raise JbError(JB_EDEVICE, f"hipMemcpy failed: {rc}")
     return out
+
+
+def loaded_runtime():
+    """Paths of the HIP runtime and of libjiebahip.so mapped into this process."""
+    out = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for l in f:
+                if "libamdhip64" in l or "libjiebahip" in l:
+                    out.add(l.split()[-1])
+    except OSError:
+        pass
+    return sorted(out)
 
 
 def go_log(x):
