@@ -67,7 +67,10 @@ def main():
     ap.add_argument("--mib", type=float, default=128.0, help="corpus MiB per GPU")
     ap.add_argument("--hmm", type=int, default=1)
     ap.add_argument("--nwords", type=int, default=350_000)
-    ap.add_argument("--cpu-sample-mib", type=float, default=24.0)
+    ap.add_argument("--dict-kind", choices=["prefix", "txt"], default="prefix",
+                    help="prefix: NewJiebaTokenizer semantics (prefix_dictionary.gob, size 60,101,967) as in the "
+                         "reference's own benchmarks; txt: NewTokenizer(dict.txt)")
+    ap.add_argument("--cpu-sample-mib", type=float, default=128.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
@@ -99,8 +102,11 @@ def main():
     hbytes = han_bytes(buf, nbytes)
     gen_s = time.time() - t0
 
-    tk = J.Tokenizer(J.make_config(dict_path=dpath, emit_path=epath, kind=J.JB_DICT_TXT, device=local))
-    d_text = torch.from_numpy(buf).to(dev)                      # nbytes + 16 zero padding bytes
+    kind = J.JB_DICT_PREFIX if args.dict_kind == "prefix" else J.JB_DICT_TXT
+    size_override = J.JIEBA_SIZE if args.dict_kind == "prefix" else 0
+    tk = J.Tokenizer(J.make_config(dict_path=dpath, emit_path=epath, kind=kind, size_override=size_override,
+                                   device=local))
+    d_text = torch.from_numpy(buf).to(dev)                      # nbytes + 64 zero padding bytes
     d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
@@ -171,7 +177,7 @@ def main():
         dend = max(1, min(dend, ndocs))
         sbytes = int(off[dend])
         s_runes = int(np.count_nonzero((buf[:sbytes] & 0xC0) != 0x80))
-        o = O.Oracle.from_files(dpath, epath, 0)
+        o = O.Oracle.from_files(dpath, epath, kind, size_override)
         threads = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
         tc = time.perf_counter()
         os_, oe, od = o.cut_batch(buf[: sbytes + 16], off[: dend + 1], bool(args.hmm), nthreads=threads)
@@ -197,7 +203,8 @@ def main():
             "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic (seeded D_syn 350k-word dict, E_syn emissions, C_syn Zipf corpus)",
             "config": {"workload": f"C_syn corpus shard {args.mib:g} MiB/GPU (1 GiB over 8 GPUs = config 4), "
-                                   f"Cut hmm={'on' if args.hmm else 'off'}",
+                                   f"Cut hmm={'on' if args.hmm else 'off'}, "
+                                   f"{'NewJiebaTokenizer (prefix dict, size 60,101,967)' if args.dict_kind == 'prefix' else 'NewTokenizer(dict.txt)'}",
                        "bytes_per_gpu": nbytes, "chars_per_gpu": nrunes, "han_bytes_per_gpu": hbytes,
                        "docs_per_gpu": ndocs, "dict_words": s.nwords, "parallelism": f"doc-shard x{world}, no collectives"},
             "roofline": roof,

@@ -74,7 +74,7 @@ class Synth:
         return dpath, epath
 
     def corpus(self, kind=KIND_DOCS, doc0=0, max_docs=1 << 62, target_bytes=1 << 20, target_runes=0,
-               pad=16):
+               pad=64):
         """Returns (buf uint8 with `pad` trailing zero bytes, doc_off uint64[ndocs+1], nrunes)."""
         if kind in (KIND_LONG_PUNCT, KIND_LONG_OOV):
             cap = target_runes * 4 + 4096

@@ -89,8 +89,8 @@ int jb_cut_batch(jb_ctx *ctx, const uint8_t *text, const uint64_t *doc_off, uint
                  jb_spans *out);
 void jb_spans_free(jb_spans *s);
 
-/* Device-resident form for pipelines and benchmarks: d_text (nbytes, plus 16
- * readable padding bytes) and d_doc_off (ndocs+1 offsets, d_doc_off[0] == 0,
+/* Device-resident form for pipelines and benchmarks: d_text (nbytes, plus 64
+ * readable padding bytes; 16-byte aligned) and d_doc_off (ndocs+1 offsets, d_doc_off[0] == 0,
  * d_doc_off[ndocs] == nbytes) are device pointers on ctx's first device; the
  * work is queued on `stream` (a hipStream_t; NULL = default stream) and the
  * call returns without synchronising.  Results stay in ctx-owned device memory

@@ -107,7 +107,7 @@ struct Device {
     hipStream_t stream = nullptr;
     // image
     uint16_t* pagemap = nullptr;
-    uint32_t* l1 = nullptr;
+    jb_l1* l1 = nullptr;
     double* emit = nullptr;
     jb_node* nodes = nullptr;
     DevImage dim{};
@@ -132,7 +132,6 @@ struct jb_ctx {
     std::unique_ptr<jb_image> im;
     std::vector<std::unique_ptr<Device>> devs;
     std::shared_mutex lock;  // prefixDictionary.lock: cuts share, AddWord excludes
-    uint32_t ring = 16;
 };
 
 // ---------------------------------------------------------------------------
@@ -227,7 +226,7 @@ extern "C" int jb_image_stats(const jb_image* img, uint64_t* nodes, uint64_t* ca
 extern "C" double jb_image_emit(const jb_image* img, int state, uint32_t rune) {
     if (!img || state < 0 || state > 3 || rune >= 0x110000u) return JB_MIN_FLOAT;
     const Image& m = img->img;
-    return m.emit[((size_t)m.pagemap[rune >> 8] * 256 + (rune & 255)) * 4 + state];
+    return m.emit[(size_t)jb_row(m.pagemap.data(), rune) * 4 + state];
 }
 
 extern "C" double jb_go_log(double x) { return go_log(x); }
@@ -235,12 +234,6 @@ extern "C" double jb_go_log(double x) { return go_log(x); }
 // ---------------------------------------------------------------------------
 // devices
 // ---------------------------------------------------------------------------
-static uint32_t ring_for(uint32_t maxlen) {
-    uint32_t r = 8;
-    while (r <= maxlen) r <<= 1;
-    return r;
-}
-
 static int upload_image(Device* d, const Image& img) {
     HIPCHK(hipSetDevice(d->ordinal));
     dfree(d->pagemap);
@@ -249,11 +242,11 @@ static int upload_image(Device* d, const Image& img) {
     dfree(d->nodes);
     d->pagemap = nullptr; d->l1 = nullptr; d->emit = nullptr; d->nodes = nullptr;
     HIPCHK(hipMalloc(&d->pagemap, img.pagemap.size() * sizeof(uint16_t)));
-    HIPCHK(hipMalloc(&d->l1, img.l1.size() * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&d->l1, img.l1.size() * sizeof(jb_l1)));
     HIPCHK(hipMalloc(&d->emit, img.emit.size() * sizeof(double)));
     HIPCHK(hipMalloc(&d->nodes, img.nodes.size() * sizeof(jb_node)));
     HIPCHK(hipMemcpy(d->pagemap, img.pagemap.data(), img.pagemap.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(d->l1, img.l1.data(), img.l1.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d->l1, img.l1.data(), img.l1.size() * sizeof(jb_l1), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d->emit, img.emit.data(), img.emit.size() * sizeof(double), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d->nodes, img.nodes.data(), img.nodes.size() * sizeof(jb_node), hipMemcpyHostToDevice));
     d->dim.pagemap = d->pagemap;
@@ -267,7 +260,8 @@ static int upload_image(Device* d, const Image& img) {
 
 static void free_work(Work* w) {
     dfree(w->docbits); dfree(w->sbits); dfree(w->ebits); dfree(w->tile_cnt); dfree(w->tile_off);
-    dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->blk); dfree(w->lists); dfree(w->scr);
+    dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->blk); dfree(w->lists); dfree(w->longq); dfree(w->gbest);
+    dfree(w->gbl);
     dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters);
     *w = Work{};
 }
@@ -291,7 +285,9 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.ttile_off, nttiles * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.blk, (nb + 4) * 4));
     HIPCHK(hipMalloc(&w.lists, (nb + 4) * 4));
-    HIPCHK(hipMalloc(&w.scr, nb + 16));
+    HIPCHK(hipMalloc(&w.longq, (nb / 4096 + 4) * 4));
+    HIPCHK(hipMalloc(&w.gbest, (nb / 3 + 4) * 8));
+    HIPCHK(hipMalloc(&w.gbl, nb / 3 + 4));
     HIPCHK(hipMalloc(&w.tok_start, (nb + 4) * 4));
     HIPCHK(hipMalloc(&w.tok_end, (nb + 4) * 4));
     HIPCHK(hipMalloc(&w.doc_tok, ((uint64_t)ndc + 2) * 8));
@@ -302,10 +298,10 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
 }
 
 static int ensure_staging(Device* d, uint64_t nbytes, uint32_t ndocs) {
-    if (nbytes + 64 > d->text_cap) {
+    if (nbytes + 128 > d->text_cap) {
         dfree(d->text);
         d->text = nullptr;
-        const uint64_t cap = std::max<uint64_t>(nbytes + 64, d->text_cap * 3 / 2);
+        const uint64_t cap = std::max<uint64_t>(nbytes + 128, d->text_cap * 3 / 2);
         HIPCHK(hipMalloc(&d->text, cap));
         d->text_cap = cap;
     }
@@ -319,13 +315,12 @@ static int ensure_staging(Device* d, uint64_t nbytes, uint32_t ndocs) {
     return JB_OK;
 }
 
-static int launch(jb_ctx* ctx, Device* d, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off,
+static int launch(jb_ctx*, Device* d, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off,
                   uint32_t ndocs, bool hmm, hipStream_t s) {
-    const uint32_t wg = zh_threads_for_ring(ctx->ring);
-    const uint32_t grid_zh = d->ncu * std::max(1u, zh_blocks_per_cu(hmm, ctx->ring, wg));
+    const uint32_t grid_zh = d->ncu * std::max(1u, zh_blocks_per_cu(hmm));
     const uint32_t grid_nz = d->ncu * std::max(1u, std::min(4u, nonzh_blocks_per_cu()));
-    const hipError_t e = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, ctx->ring, wg, grid_zh,
-                                      grid_nz, s, d->profile ? &d->timer : nullptr);
+    const hipError_t e = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, grid_zh, grid_nz, s,
+                                      d->profile ? &d->timer : nullptr);
     if (e != hipSuccess) return fail(JB_EDEVICE, "pipeline launch: %s", hipGetErrorString(e));
     return JB_OK;
 }
@@ -338,7 +333,6 @@ extern "C" int jb_open(const jb_config* cfg, jb_ctx** out) {
     if (rc) return rc;
     auto ctx = std::make_unique<jb_ctx>();
     ctx->im.reset(img);
-    ctx->ring = ring_for(img->img.maxlen);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(JB_EDEVICE, "no HIP device available");
     const int nuse = cfg->ndevices > 0 ? cfg->ndevices : 1;
@@ -403,7 +397,7 @@ static int cut_range(jb_ctx* ctx, Device* d, const uint8_t* text, const uint64_t
         off.resize(nd + 1);
         for (uint32_t k = 0; k <= nd; k++) off[k] = doc_off[a + k] - base;
         HIPCHK(hipMemcpyAsync(d->text, text + base, nbytes, hipMemcpyHostToDevice, d->stream));
-        HIPCHK(hipMemsetAsync(d->text + nbytes, 0, 16, d->stream));
+        HIPCHK(hipMemsetAsync(d->text + nbytes, 0, 64, d->stream));
         HIPCHK(hipMemcpyAsync(d->doc_off, off.data(), (nd + 1) * 8, hipMemcpyHostToDevice, d->stream));
         if ((rc = launch(ctx, d, d->text, nbytes, d->doc_off, nd, hmm, d->stream))) return rc;
         uint32_t cnt[8];
@@ -595,7 +589,6 @@ extern "C" int jb_add_word(jb_ctx* ctx, const char* word, size_t len, int64_t fr
     dict.size += freq;
     build_image(dict, ctx->im->emit, &ctx->im->img);
     if (ctx->im->img.maxlen > 255) return fail(JB_ELIMIT, "dictionary word of %u runes (max 255)", ctx->im->img.maxlen);
-    ctx->ring = ring_for(ctx->im->img.maxlen);
     for (auto& d : ctx->devs) {
         std::lock_guard<std::mutex> g(d->mu);
         (void)hipSetDevice(d->ordinal);

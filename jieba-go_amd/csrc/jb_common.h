@@ -6,8 +6,10 @@
 //   hiddenMarkovModel.emitP   map[string]map[string]float64 (tokenizer.go:616-621)
 // with flat arrays that a wavefront can probe without strings:
 //
-//   pagemap[0x110000 >> 8]  u16   rune page -> dense page id (page 0 = empty page)
-//   l1[npages * 256]        u32   single-rune key -> node id  (JB_EMPTY if absent)
+//   pagemap[0x110000 >> 8]  u16   rune page -> dense page id (page 0 = empty page;
+//                                 pages 0x34..0x9F, U+3400..U+9FFF, are always ids
+//                                 1..108 so jb_row() skips the pagemap for them)
+//   l1[npages * 256]        16 B  single-rune key -> {node id, freq class, w}
 //   emit[npages * 256][4]   f64   emitP[B|M|E|S][string(rune)], minFloat if absent
 //   nodes[cap]              16 B  open-addressing hash of trie edges:
 //                                 key (parent node id, rune) -> {freq class, w}
@@ -35,6 +37,7 @@
 #define JB_FC_ZERO 0u   // freq == 0: a prefix-only entry (e.g. "撙", tokenizer_test.go:126)
 #define JB_FC_POS 1u    // freq > 0: a DAG edge (tokenizer.go:479)
 #define JB_FC_NEG 2u    // freq < 0: present, no edge, walk continues
+#define JB_FC_ABSENT 3u // (l1 records only) the single rune is not a key
 #define JB_FC_SHIFT 24
 #define JB_RUNE_MASK 0x1FFFFFu
 
@@ -43,6 +46,24 @@ struct alignas(16) jb_node {
     uint32_t rune_fc;  // rune | (freq class << 24)
     double w;          // Log(freq) - Log(size)
 };
+
+// Level-1 record: everything the walk needs for the rune itself in one 16-byte load.
+struct alignas(16) jb_l1 {
+    uint32_t id;  // node id of the single-rune key (JB_EMPTY if absent)
+    uint32_t fc;  // JB_FC_*; JB_FC_ABSENT when the rune is not a key
+    double w;     // node w, or w_absent = Log(1.0) - Log(size) when absent (tokenizer.go:515-519)
+};
+
+// Pages U+3400..U+9FFF (CJK Ext-A + URO) sit at fixed page ids 1..108.
+#define JB_DIRECT_LO 0x3400u
+#define JB_DIRECT_N 0x6C00u
+#define JB_DIRECT_PAGES 108u
+
+// Row of rune r in l1 / emit.
+JB_HD uint32_t jb_row(const uint16_t* pagemap, uint32_t r) {
+    if (r - JB_DIRECT_LO < JB_DIRECT_N) return r - 0x3300u;  // ((r>>8) - 0x33) * 256 + (r & 255)
+    return (uint32_t)pagemap[r >> 8] * 256u + (r & 255u);
+}
 
 // 32-bit mix of (parent, rune); identical on host and device.
 JB_HD uint32_t jb_hash(uint32_t parent, uint32_t rune) {

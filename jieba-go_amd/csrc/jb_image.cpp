@@ -393,16 +393,21 @@ void build_image(const Dictionary& d, const Emission& e, Image* img) {
         for (const auto& kv : e.by_rune[s])
             if (kv.first < 0x110000u) page_used[kv.first >> 8] = 1;
     img->pagemap.assign(JB_NPAGES_MAX, 0);
-    img->npages = 1;  // page 0: the empty page
+    for (uint32_t p = 0; p < JB_DIRECT_PAGES; p++) img->pagemap[(JB_DIRECT_LO >> 8) + p] = (uint16_t)(p + 1);
+    img->npages = 1 + JB_DIRECT_PAGES;  // page 0: the empty page; then the fixed U+3400..U+9FFF pages
     for (uint32_t p = 0; p < JB_NPAGES_MAX; p++)
-        if (page_used[p]) img->pagemap[p] = (uint16_t)img->npages++;
-    img->l1.assign((size_t)img->npages * 256, JB_EMPTY);
+        if (page_used[p] && img->pagemap[p] == 0 && p != 0) img->pagemap[p] = (uint16_t)img->npages++;
+    if (page_used[0]) img->pagemap[0] = (uint16_t)img->npages++;
+    img->l1.assign((size_t)img->npages * 256, jb_l1{JB_EMPTY, JB_FC_ABSENT, img->w_absent});
     img->emit.assign((size_t)img->npages * 256 * 4, JB_MIN_FLOAT);  // not found -> minFloat (tokenizer.go:690,710)
-    for (const auto& p : level1) img->l1[(size_t)img->pagemap[p.first >> 8] * 256 + (p.first & 255)] = p.second;
+    for (const auto& p : level1) {
+        const jb_node& n = img->nodes[p.second];
+        img->l1[jb_row(img->pagemap.data(), p.first)] = jb_l1{p.second, n.rune_fc >> JB_FC_SHIFT, n.w};
+    }
     for (int s = 0; s < 4; s++)
         for (const auto& kv : e.by_rune[s]) {
             if (kv.first >= 0x110000u) continue;
-            img->emit[((size_t)img->pagemap[kv.first >> 8] * 256 + (kv.first & 255)) * 4 + s] = kv.second;
+            img->emit[(size_t)jb_row(img->pagemap.data(), kv.first) * 4 + s] = kv.second;
         }
 }
 
@@ -411,7 +416,7 @@ uint32_t image_lookup(const Image& img, const uint32_t* runes, size_t n) {
     const uint64_t mask = img.nodes.size() - 1;
     const uint32_t r0 = runes[0];
     if (r0 >= 0x110000u) return JB_EMPTY;
-    uint32_t id = img.l1[(size_t)img.pagemap[r0 >> 8] * 256 + (r0 & 255)];
+    uint32_t id = img.l1[jb_row(img.pagemap.data(), r0)].id;
     for (size_t i = 1; i < n && id != JB_EMPTY; i++) {
         uint64_t h = jb_hash(id, runes[i]) & mask;
         uint32_t found = JB_EMPTY;

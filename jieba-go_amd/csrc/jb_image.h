@@ -27,7 +27,7 @@ struct Emission {
 // Flat arrays uploaded to every device (layout: jb_common.h).
 struct Image {
     std::vector<uint16_t> pagemap;  // JB_NPAGES_MAX
-    std::vector<uint32_t> l1;       // npages * 256
+    std::vector<jb_l1> l1;          // npages * 256
     std::vector<double> emit;       // npages * 256 * 4
     std::vector<jb_node> nodes;     // hash capacity (power of two)
     uint32_t npages = 0;

@@ -6,8 +6,9 @@
 //                 block starts                  (zh regex + splitText, tokenizer.go:21,154-155,165-210)
 //   k_scan2       tile counts -> offsets
 //   k_blocks<1>   write block list (start | zh<<31), zh ids, non-zh ids
-//   k_zh          one lane per Han block: trie walk + backward max-prob DP +
-//                 forward path + BMES Viterbi on singleton runs
+//   k_zh          one lane per Han block, text staged per workgroup in LDS: trie
+//                 walk + backward max-prob DP + forward path + BMES Viterbi on
+//                 singleton runs (k_zh_long: blocks longer than an LDS window)
 //                                               (cutZh/cutDAG/buildDag/calcDagProba/
 //                                                findDagPath/maxIndexProba/viterbi/cutHMM,
 //                                                tokenizer.go:221-285,462-578,668-756)
@@ -27,8 +28,8 @@
 namespace jb {
 
 const char* const kKernelNames[K_NUM] = {"k_docbits", "k_blocks_count", "k_scan_blocks", "k_blocks_write",
-                                         "k_zh", "k_nonzh", "k_tok_count", "k_scan_tok", "k_tok_write",
-                                         "k_doc_tok"};
+                                         "k_zh", "k_zh_long", "k_nonzh", "k_tok_count", "k_scan_tok",
+                                         "k_tok_write", "k_doc_tok"};
 
 // newJiebaHMM literals (tokenizer.go:629-652)
 #define START_B (-0.26268660809250016)
@@ -50,29 +51,6 @@ const char* const kKernelNames[K_NUM] = {"k_docbits", "k_blocks_count", "k_scan_
 __device__ __forceinline__ uint32_t ld4(const uint8_t* __restrict__ t, uint64_t q) {
     const uint32_t* a = reinterpret_cast<const uint32_t*>(t + (q & ~3ull));
     return __builtin_amdgcn_alignbyte(a[1], a[0], (uint32_t)(q & 3));
-}
-
-// A Han rune at q (3- or 4-byte UTF-8, validated by k_blocks).
-__device__ __forceinline__ uint32_t han_at(const uint8_t* __restrict__ t, uint64_t q, uint32_t* w) {
-    const uint32_t x = ld4(t, q);
-    const uint32_t b0 = x & 0xFFu;
-    if (b0 < 0xF0u) {
-        *w = 3;
-        return ((b0 & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
-    }
-    *w = 4;
-    return ((b0 & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) | (((x >> 16) & 0x3Fu) << 6) | ((x >> 24) & 0x3Fu);
-}
-
-__device__ __forceinline__ uint32_t han_width(const uint8_t* __restrict__ t, uint32_t q) {
-    return t[q] < 0xF0u ? 3u : 4u;
-}
-
-// Start of the Han rune that ends at q (q > lo; runes in [lo, q) are Han).
-__device__ __forceinline__ uint32_t han_prev(const uint8_t* __restrict__ t, uint32_t q, uint32_t lo) {
-    if (q - lo < 4u) return lo;
-    const uint32_t x = ld4(t, q - 4u);
-    return ((x >> 8) & 0xF0u) == 0xE0u ? q - 3u : q - 4u;
 }
 
 // Child of `parent` labelled r in the open-addressing edge hash.
@@ -316,21 +294,26 @@ __global__ __launch_bounds__(1024) void k_scan2(const uint2* __restrict__ cnt, u
 }
 
 // ---------------------------------------------------------------------------
-// k_zh: one lane per Han block (cutZh, tokenizer.go:221-255).
+// Han blocks (cutZh, tokenizer.go:221-255).
 //
-// Backward over the block's runes (calcDagProba, :502-548): for rune i the
-// lane walks the trie forward from i (buildDag, :462-497) and folds each edge
-// (i, i+len) — in ascending len, as the DAG lists them — into maxIndexProba's
-// running state (:565-578) with pieceProba = w + best(i+len) (:519-529).
-// best(j) for the next R-1 runes lives in an LDS ring (R > longest key);
-// best(n) is the {n, 0.0} sentinel (:522-525).  The chosen piece length is
-// stored in scr[] at the rune's first byte, then the forward walk
-// (findDagPath, :552-562) emits pieces or, with HMM, collects runs of
-// single-rune pieces for the Viterbi (:228-253).
+// process_block() runs one block in one lane.  Backward over the block's runes
+// (calcDagProba, :502-548): for rune i the lane walks the trie forward from i
+// (buildDag, :462-497) and folds each edge (i, i+len) — in ascending len, as
+// the DAG lists them — into maxIndexProba's running state (:565-578) with
+// pieceProba = w + best(i+len) (:519-529); best(n) is the {n, 0.0} sentinel
+// (:522-525).  best / the chosen length live per rune at index (byte offset)/3
+// (Han runes are >= 3 bytes, so distinct runes never share an index).  The
+// forward walk (findDagPath, :552-562) then emits pieces or, with HMM,
+// gathers runs of single-rune pieces for the Viterbi (:228-253).
+//
+// A View supplies the text bytes, the per-rune slots and the token sink:
+//   LdsView    — k_zh: the workgroup's window of text staged in LDS
+//   GlobalView — k_zh_long: blocks longer than a window, straight from HBM
 // ---------------------------------------------------------------------------
+constexpr uint32_t kWin = 8192;  // k_zh window bytes (LDS)
+
 __device__ __forceinline__ void load_emit(const DevImage& im, uint32_t r, double e[4]) {
-    const uint32_t page = im.pagemap[r >> 8];
-    const double2* p = reinterpret_cast<const double2*>(im.emit) + (size_t)(page * 256u + (r & 255u)) * 2u;
+    const double2* p = reinterpret_cast<const double2*>(im.emit) + (size_t)jb_row(im.pagemap, r) * 2u;
     const double2 a = p[0], b = p[1];
     e[0] = a.x; e[1] = a.y; e[2] = b.x; e[3] = b.y;
 }
@@ -346,24 +329,94 @@ __device__ __forceinline__ void route2(double a, double b, uint32_t* code, doubl
     *p = best;
 }
 
+struct LdsEmitter {  // token bits accumulated per word, OR-ed into the LDS bitmap
+    uint32_t* ls;
+    uint32_t* le;
+    uint32_t w0, word, s, e;
+    __device__ __forceinline__ void flush() {
+        if (s) atomicOr(ls + (word - w0), s);
+        if (e) atomicOr(le + (word - w0), e);
+        s = e = 0;
+    }
+    __device__ __forceinline__ void at(uint32_t pos) {
+        const uint32_t w = pos >> 5;
+        if (w != word) {
+            flush();
+            word = w;
+        }
+    }
+    __device__ __forceinline__ void token(uint32_t a, uint32_t b) {
+        at(a);
+        s |= 1u << (a & 31u);
+        at(b - 1u);
+        e |= 1u << ((b - 1u) & 31u);
+    }
+};
+
+struct LdsView {
+    const uint8_t* tx;  // tx[k] = text[wb + k]
+    double* best;
+    uint8_t* bl;
+    uint32_t wb;
+    LdsEmitter em;
+    __device__ __forceinline__ uint32_t byte(uint32_t q) const { return tx[q - wb]; }
+    __device__ __forceinline__ uint32_t load4(uint32_t q) const {
+        const uint32_t k = q - wb;
+        const uint32_t* a = reinterpret_cast<const uint32_t*>(tx + (k & ~3u));
+        return __builtin_amdgcn_alignbyte(a[1], a[0], k & 3u);
+    }
+    __device__ __forceinline__ uint32_t slot(uint32_t q) const { return (q - wb) / 3u; }
+    __device__ __forceinline__ void token(uint32_t a, uint32_t b) { em.token(a, b); }
+};
+
+struct GlobalView {
+    const uint8_t* text;
+    double* best;  // index q / 3
+    uint8_t* bl;
+    Emitter em;
+    __device__ __forceinline__ uint32_t byte(uint32_t q) const { return text[q]; }
+    __device__ __forceinline__ uint32_t load4(uint32_t q) const { return ld4(text, q); }
+    __device__ __forceinline__ uint32_t slot(uint32_t q) const { return q / 3u; }
+    __device__ __forceinline__ void token(uint32_t a, uint32_t b) { em.token(a, b); }
+};
+
+template <class V>
+__device__ __forceinline__ uint32_t v_han(const V& v, uint32_t q, uint32_t* w) {
+    const uint32_t x = v.load4(q);
+    const uint32_t b0 = x & 0xFFu;
+    if (b0 < 0xF0u) {
+        *w = 3;
+        return ((b0 & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
+    }
+    *w = 4;
+    return ((b0 & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) | (((x >> 16) & 0x3Fu) << 6) | ((x >> 24) & 0x3Fu);
+}
+template <class V>
+__device__ __forceinline__ uint32_t v_width(const V& v, uint32_t q) { return v.byte(q) < 0xF0u ? 3u : 4u; }
+template <class V>
+__device__ __forceinline__ uint32_t v_prev(const V& v, uint32_t q, uint32_t lo) {  // rune ending at q
+    if (q - lo < 4u) return lo;
+    return (v.byte(q - 3u) & 0xF0u) == 0xE0u ? q - 3u : q - 4u;
+}
+
 // viterbi (tokenizer.go:668-730) over the m runes [rs, re) + cutHMM (:273-285).
-// Back-pointers (2 bits per state) go to scr[] at each rune's first byte; the
-// traceback stops at the first "" route: the reference's path then restarts
-// at that step (fullPath[""] is nil, :715) and cutHMM labels runes from 0.
-__device__ void viterbi_run(const uint8_t* __restrict__ text, uint8_t* __restrict__ scr, const DevImage& im,
-                            uint32_t rs, uint32_t re, uint32_t m, Emitter& em) {
+// Back-pointers (2 bits per state) go to each rune's slot; the traceback stops
+// at the first "" route: the reference's path then restarts at that step
+// (fullPath[""] is nil, :715) and cutHMM labels runes from the run's start.
+template <class V>
+__device__ void viterbi_run(V& v, const DevImage& im, uint32_t rs, uint32_t re, uint32_t m) {
     if (m == 1) {  // always "S" for a single rune (:672-674)
-        em.token(rs, re);
+        v.token(rs, re);
         return;
     }
     uint32_t w;
     double e[4];
-    uint32_t r = han_at(text, rs, &w);
+    uint32_t r = v_han(v, rs, &w);
     load_emit(im, r, e);
     double vB = START_B + e[0], vM = JB_MIN_FLOAT + e[1], vE = JB_MIN_FLOAT + e[2], vS = START_S + e[3];
     uint32_t q = rs + w;
     while (q < re) {
-        r = han_at(text, q, &w);
+        r = v_han(v, q, &w);
         load_emit(im, r, e);
         uint32_t cB, cM, cE, cS;
         double pB, pM, pE, pS;
@@ -375,135 +428,201 @@ __device__ void viterbi_run(const uint8_t* __restrict__ text, uint8_t* __restric
         vM = pM + e[1];
         vE = pE + e[2];
         vS = pS + e[3];
-        scr[q] = (uint8_t)(cB | (cM << 2) | (cE << 4) | (cS << 6));
+        v.bl[v.slot(q)] = (uint8_t)(cB | (cM << 2) | (cE << 4) | (cS << 6));
         q += w;
     }
     uint32_t st = vE > vS ? (uint32_t)JB_E : (uint32_t)JB_S;  // (:723-729)
     uint32_t t = m - 1, reset = 0;
-    uint32_t qt = han_prev(text, re, rs);
+    uint32_t qt = v_prev(v, re, rs);
     for (;;) {
+        const uint32_t sl = v.slot(qt);
         if (t == 0) {
-            scr[qt] = (uint8_t)st;
+            v.bl[sl] = (uint8_t)st;
             break;
         }
-        const uint32_t code = (scr[qt] >> (2u * st)) & 3u;
-        scr[qt] = (uint8_t)st;
+        const uint32_t code = (v.bl[sl] >> (2u * st)) & 3u;
+        v.bl[sl] = (uint8_t)st;
         if (code == 2u) {
             reset = t;
             break;
         }
-        // predecessors: B,S <- {E,S}; M,E <- {B,M}
-        st = (st == JB_B || st == JB_S) ? 2u + code : code;
+        st = (st == JB_B || st == JB_S) ? 2u + code : code;  // B,S <- {E,S}; M,E <- {B,M}
         --t;
-        qt = han_prev(text, qt, rs);
+        qt = v_prev(v, qt, rs);
     }
     uint32_t qa = rs, qb = qt, ts = rs;
     for (uint32_t k = 0; k < m - reset; k++) {
-        const uint32_t lab = scr[qb];
-        qa += han_width(text, qa);
-        qb += han_width(text, qb);
+        const uint32_t lab = v.bl[v.slot(qb)];
+        qa += v_width(v, qa);
+        qb += v_width(v, qb);
         if (lab >= (uint32_t)JB_E) {
-            em.token(ts, qa);
+            v.token(ts, qa);
             ts = qa;
         }
     }
 }
 
-template <bool HMM, uint32_t R>
-__global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, const uint32_t* __restrict__ blk,
-                                            const uint32_t* __restrict__ lists, const uint32_t* __restrict__ counters,
-                                            DevImage im, uint8_t* __restrict__ scr, uint32_t* __restrict__ sbits,
-                                            uint32_t* __restrict__ ebits, uint32_t* __restrict__ err) {
-    extern __shared__ double ring[];
-    const uint32_t bd = blockDim.x;
-    double* my = ring + threadIdx.x;
-    const uint32_t nzh = counters[CNT_NZH];
-    Emitter em(sbits, ebits);
-    for (uint32_t z = blockIdx.x * bd + threadIdx.x; z < nzh; z += gridDim.x * bd) {
-        const uint32_t g = lists[z];
-        const uint32_t bs = blk[g] & 0x7FFFFFFFu, be = blk[g + 1] & 0x7FFFFFFFu;
-        // ---- backward DP -------------------------------------------------
-        uint32_t q = be, c = 0;
-        while (q > bs) {
-            q = han_prev(text, q, bs);
-            ++c;
-            uint32_t w0;
-            const uint32_t r0 = han_at(text, q, &w0);
-            double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT;
-            uint32_t bestL = 0, lastL = 0;
-            auto edge = [&](uint32_t len, double wt) {
-                const double nb = len == c ? 0.0 : my[((c - len) & (R - 1u)) * bd];
-                const double pp = wt + nb;
-                if (pp >= prevP) {
-                    bestL = len;
-                    bestP = pp;
-                }
-                prevP = pp;
-                lastL = len;
-            };
-            uint32_t id = im.l1[(uint32_t)im.pagemap[r0 >> 8] * 256u + (r0 & 255u)];
-            if (id == JB_EMPTY) {
-                edge(1, im.w_absent);  // absent rune: single edge, tf = 1 (:468-471, :515)
-            } else {
-                const jb_node n = im.nodes[id];
-                const uint32_t fc = n.rune_fc >> JB_FC_SHIFT;
-                if (fc == JB_FC_ZERO) {
-                    edge(1, n.w);  // count == 0: single edge, Log(0) = -Inf (:469, Q4)
-                } else {
-                    if (fc == JB_FC_POS) edge(1, n.w);
-                    uint32_t qq = q + w0, len = 1;
-                    while (len < c) {
-                        uint32_t wr;
-                        const uint32_t r = han_at(text, qq, &wr);
-                        jb_node m;
-                        const uint32_t id2 = child(im.nodes, im.mask, id, r, &m);
-                        if (id2 == JB_EMPTY) break;  // (:475-478)
-                        ++len;
-                        if ((m.rune_fc >> JB_FC_SHIFT) == JB_FC_POS) edge(len, m.w);  // (:479-481)
-                        id = id2;
-                        qq += wr;
-                    }
-                }
+// One Han block [bs, be). Returns false when the reference would panic
+// (a position with no DAG edge on the chosen path: cutDAG slices with -1).
+template <bool HMM, class V>
+__device__ bool process_block(V& v, const DevImage& im, uint32_t bs, uint32_t be) {
+    // ---- backward DP ----------------------------------------------------------
+    uint32_t q = be;
+    while (q > bs) {
+        q = v_prev(v, q, bs);
+        uint32_t w0;
+        const uint32_t r0 = v_han(v, q, &w0);
+        double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT;
+        uint32_t bestL = 0, lastL = 0;
+        auto edge = [&](uint32_t len, uint32_t end, double wt) {
+            const double nb = end == be ? 0.0 : v.best[v.slot(end)];
+            const double pp = wt + nb;
+            if (pp >= prevP) {
+                bestL = len;
+                bestP = pp;
             }
-            if (bestL == 0) {  // no item qualified: the last item (or {-1, minFloat})
-                bestL = lastL;
-                bestP = prevP;
+            prevP = pp;
+            lastL = len;
+        };
+        const jb_l1 l1 = im.l1[jb_row(im.pagemap, r0)];
+        if (l1.fc == JB_FC_ABSENT || l1.fc == JB_FC_ZERO) {
+            // absent or count 0: the single edge only (:468-471); w is -Log(size) or -Inf (:515-519)
+            edge(1, q + w0, l1.w);
+        } else {
+            if (l1.fc == JB_FC_POS) edge(1, q + w0, l1.w);
+            uint32_t id = l1.id, qq = q + w0, len = 1;
+            while (qq < be) {
+                uint32_t wr;
+                const uint32_t r = v_han(v, qq, &wr);
+                jb_node m;
+                const uint32_t id2 = child(im.nodes, im.mask, id, r, &m);
+                if (id2 == JB_EMPTY) break;  // (:475-478)
+                ++len;
+                qq += wr;
+                if ((m.rune_fc >> JB_FC_SHIFT) == JB_FC_POS) edge(len, qq, m.w);  // (:479-481)
+                id = id2;
             }
-            my[(c & (R - 1u)) * bd] = bestP;
-            scr[q] = (uint8_t)bestL;
         }
-        // ---- forward walk (findDagPath) + HMM runs ----------------------------
-        uint32_t p = bs, run_s = 0, run_n = 0;
-        bool bad = false;
-        while (p < be) {
-            const uint32_t L = scr[p];
-            if (L == 0) {  // tail index -1: cutDAG's slice panics in the reference
-                bad = true;
-                break;
-            }
-            uint32_t pe = p;
-            for (uint32_t k = 0; k < L; k++) pe += han_width(text, pe);
-            if (!HMM) {
-                em.token(p, pe);
-            } else if (L == 1) {
-                if (run_n == 0) run_s = p;
-                run_n++;
-            } else {
-                if (run_n) {
-                    viterbi_run(text, scr, im, run_s, p, run_n, em);
-                    run_n = 0;
-                }
-                em.token(p, pe);
-            }
-            p = pe;
+        if (bestL == 0) {  // no item qualified: the last item (or {-1, minFloat})
+            bestL = lastL;
+            bestP = prevP;
         }
-        if (bad) {
-            atomicOr(err, 1u);
-            continue;
-        }
-        if (HMM && run_n) viterbi_run(text, scr, im, run_s, be, run_n, em);
+        const uint32_t sl = v.slot(q);
+        v.best[sl] = bestP;
+        v.bl[sl] = (uint8_t)bestL;
     }
-    em.flush();
+    // ---- forward walk (findDagPath) + HMM runs ------------------------------------
+    uint32_t p = bs, run_s = 0, run_n = 0;
+    while (p < be) {
+        const uint32_t L = v.bl[v.slot(p)];
+        if (L == 0) return false;
+        uint32_t pe = p;
+        for (uint32_t k = 0; k < L; k++) pe += v_width(v, pe);
+        if (!HMM) {
+            v.token(p, pe);
+        } else if (L == 1) {
+            if (run_n == 0) run_s = p;
+            run_n++;
+        } else {
+            if (run_n) {
+                viterbi_run(v, im, run_s, p, run_n);
+                run_n = 0;
+            }
+            v.token(p, pe);
+        }
+        p = pe;
+    }
+    if (HMM && run_n) viterbi_run(v, im, run_s, be, run_n);
+    return true;
+}
+
+// k_zh: workgroups pull 256 consecutive Han blocks at a time from a global
+// counter, stage the text window that holds them in LDS (coalesced 16-byte
+// loads), run one block per lane out of LDS, and OR the window's token bits
+// into the global bitmaps.  Blocks too long for a window go to k_zh_long.
+template <bool HMM>
+__global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, const uint32_t* __restrict__ blk,
+                                            const uint32_t* __restrict__ lists, uint32_t* __restrict__ counters,
+                                            DevImage im, uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
+                                            uint32_t* __restrict__ longq) {
+    __shared__ __attribute__((aligned(16))) uint8_t tx[kWin + 16];
+    __shared__ double best[kWin / 3 + 2];
+    __shared__ uint8_t bl[kWin / 3 + 2];
+    __shared__ uint32_t ls[kWin / 32 + 2], le[kWin / 32 + 2];
+    __shared__ uint32_t sh[4];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nzh = counters[CNT_NZH];
+    for (;;) {
+        if (tid == 0) sh[0] = atomicAdd(counters + CNT_WORK, 256u);
+        __syncthreads();
+        const uint32_t z0 = sh[0];
+        if (z0 >= nzh) break;
+        const uint32_t z = z0 + tid;
+        bool todo = z < nzh;
+        uint32_t bs = 0, be = 0;
+        if (todo) {
+            const uint32_t g = lists[z];
+            bs = blk[g] & 0x7FFFFFFFu;
+            be = blk[g + 1] & 0x7FFFFFFFu;
+            if (be - bs > kWin - 32u) {
+                longq[atomicAdd(counters + CNT_NLONG, 1u)] = z;
+                todo = false;
+            }
+        }
+        for (;;) {  // sub-rounds: the blocks whose bytes fit one window
+            if (tid == 0) {
+                sh[1] = 0xFFFFFFFFu;
+                sh[2] = 0u;
+            }
+            __syncthreads();
+            if (todo) atomicMin(&sh[1], bs);
+            __syncthreads();
+            const uint32_t first = sh[1];
+            if (first == 0xFFFFFFFFu) break;
+            const uint32_t wb = first & ~15u;
+            const bool mine = todo && be - wb <= kWin;
+            if (mine) atomicMax(&sh[2], be);
+            __syncthreads();
+            const uint32_t wend = sh[2];
+            const uint32_t nld = (wend - wb + 8u + 15u) >> 4;
+            for (uint32_t k = tid; k < nld; k += 256u)
+                reinterpret_cast<uint4*>(tx)[k] = reinterpret_cast<const uint4*>(text + wb)[k];
+            const uint32_t w0 = wb >> 5, nw = ((wend - 1u) >> 5) - w0 + 1u;
+            for (uint32_t k = tid; k < nw; k += 256u) ls[k] = le[k] = 0u;
+            __syncthreads();
+            if (mine) {
+                LdsView v{tx, best, bl, wb, LdsEmitter{ls, le, w0, 0xFFFFFFFFu, 0u, 0u}};
+                if (!process_block<HMM>(v, im, bs, be)) atomicOr(counters + CNT_ERR, 1u);
+                v.em.flush();
+                todo = false;
+            }
+            __syncthreads();
+            for (uint32_t k = tid; k < nw; k += 256u) {
+                const uint32_t a = ls[k], b = le[k];
+                if (a) atomicOr(sbits + w0 + k, a);
+                if (b) atomicOr(ebits + w0 + k, b);
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// k_zh_long: one lane per block longer than a window, text from HBM,
+// per-rune slots in global scratch (index q / 3).
+template <bool HMM>
+__global__ __launch_bounds__(64) void k_zh_long(const uint8_t* __restrict__ text, const uint32_t* __restrict__ blk,
+                                                const uint32_t* __restrict__ lists, uint32_t* __restrict__ counters,
+                                                DevImage im, const uint32_t* __restrict__ longq, double* gbest,
+                                                uint8_t* gbl, uint32_t* __restrict__ sbits,
+                                                uint32_t* __restrict__ ebits) {
+    const uint32_t n = counters[CNT_NLONG];
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t g = lists[longq[i]];
+        const uint32_t bs = blk[g] & 0x7FFFFFFFu, be = blk[g + 1] & 0x7FFFFFFFu;
+        GlobalView v{text, gbest, gbl, Emitter(sbits, ebits)};
+        if (!process_block<HMM>(v, im, bs, be)) atomicOr(counters + CNT_ERR, 1u);
+        v.em.flush();
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -626,54 +745,14 @@ __global__ void k_doc_tok(const uint64_t* __restrict__ doc_off, uint32_t ndocs, 
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-uint32_t zh_threads_for_ring(uint32_t ring) {
-    uint32_t t = 32768u / (ring * 8u);
-    if (t > 256u) t = 256u;
-    t &= ~63u;
-    return t < 64u ? 64u : t;
-}
-
-template <bool HMM, uint32_t R>
-static void launch_zh(uint32_t grid, uint32_t wg, hipStream_t s, const uint8_t* text, const Work& w,
-                      const DevImage& im) {
-    hipLaunchKernelGGL((k_zh<HMM, R>), dim3(grid), dim3(wg), (size_t)R * wg * sizeof(double), s, text, w.blk,
-                       w.lists, w.counters, im, w.scr, w.sbits, w.ebits, w.counters + CNT_ERR);
-}
-
 template <bool HMM>
-static bool dispatch_zh(uint32_t ring, uint32_t grid, uint32_t wg, hipStream_t s, const uint8_t* text,
-                        const Work& w, const DevImage& im) {
-    switch (ring) {
-        case 8: launch_zh<HMM, 8>(grid, wg, s, text, w, im); return true;
-        case 16: launch_zh<HMM, 16>(grid, wg, s, text, w, im); return true;
-        case 32: launch_zh<HMM, 32>(grid, wg, s, text, w, im); return true;
-        case 64: launch_zh<HMM, 64>(grid, wg, s, text, w, im); return true;
-        case 128: launch_zh<HMM, 128>(grid, wg, s, text, w, im); return true;
-        case 256: launch_zh<HMM, 256>(grid, wg, s, text, w, im); return true;
-        default: return false;
-    }
-}
-
-template <bool HMM>
-static uint32_t occ_zh(uint32_t ring, uint32_t wg) {
+static uint32_t occ_zh() {
     int n = 0;
-    const size_t lds = (size_t)ring * wg * sizeof(double);
-    hipError_t e = hipErrorInvalidValue;
-    switch (ring) {
-        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_zh<HMM, 8>, (int)wg, lds); break;
-        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_zh<HMM, 16>, (int)wg, lds); break;
-        case 32: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_zh<HMM, 32>, (int)wg, lds); break;
-        case 64: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_zh<HMM, 64>, (int)wg, lds); break;
-        case 128: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_zh<HMM, 128>, (int)wg, lds); break;
-        case 256: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_zh<HMM, 256>, (int)wg, lds); break;
-        default: return 0;
-    }
-    return e == hipSuccess && n > 0 ? (uint32_t)n : 1u;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_zh<HMM>, 256, 0) != hipSuccess || n <= 0) return 1;
+    return (uint32_t)n;
 }
 
-uint32_t zh_blocks_per_cu(bool hmm, uint32_t ring, uint32_t wg) {
-    return hmm ? occ_zh<true>(ring, wg) : occ_zh<false>(ring, wg);
-}
+uint32_t zh_blocks_per_cu(bool hmm) { return hmm ? occ_zh<true>() : occ_zh<false>(); }
 
 uint32_t nonzh_blocks_per_cu() {
     int n = 0;
@@ -689,8 +768,8 @@ uint32_t nonzh_blocks_per_cu() {
     } while (0)
 
 hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text, uint64_t nbytes,
-                        const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, uint32_t ring, uint32_t zh_wg,
-                        uint32_t grid_zh, uint32_t grid_nz, hipStream_t stream, KernelTimer* timer) {
+                        const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, uint32_t grid_zh, uint32_t grid_nz,
+                        hipStream_t stream, KernelTimer* timer) {
     const uint64_t nwords = (nbytes + 31) / 32;
     const uint32_t ntiles = (uint32_t)((nbytes + kTileBytes - 1) / kTileBytes);
     const uint32_t nttiles = (uint32_t)((nwords + kTokTileWords - 1) / kTokTileWords);
@@ -715,10 +794,18 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                                (uint32_t)nbytes));
     JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL((k_blocks<true>), dim3(ntiles), dim3(256), 0, stream, d_text,
                                                 nbytes, w.docbits, nullptr, w.tile_off, w.blk, w.lists, list_cap));
-    bool ok = true;
-    JB_TIMED(K_ZH, ok = hmm ? dispatch_zh<true>(ring, grid_zh, zh_wg, stream, d_text, w, im)
-                            : dispatch_zh<false>(ring, grid_zh, zh_wg, stream, d_text, w, im));
-    if (!ok) return hipErrorInvalidValue;
+    if (hmm)
+        JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, w.blk, w.lists,
+                                          w.counters, im, w.sbits, w.ebits, w.longq));
+    else
+        JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, w.blk, w.lists,
+                                          w.counters, im, w.sbits, w.ebits, w.longq));
+    if (hmm)
+        JB_TIMED(K_ZH_LONG, hipLaunchKernelGGL((k_zh_long<true>), dim3(64), dim3(64), 0, stream, d_text, w.blk,
+                                               w.lists, w.counters, im, w.longq, w.gbest, w.gbl, w.sbits, w.ebits));
+    else
+        JB_TIMED(K_ZH_LONG, hipLaunchKernelGGL((k_zh_long<false>), dim3(64), dim3(64), 0, stream, d_text, w.blk,
+                                               w.lists, w.counters, im, w.longq, w.gbest, w.gbl, w.sbits, w.ebits));
     JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3(grid_nz), dim3(256), 0, stream, d_text, w.blk, w.lists,
                                          list_cap, w.counters, w.sbits, w.ebits));
     JB_TIMED(K_TOK_COUNT, hipLaunchKernelGGL((k_tok<false>), dim3(nttiles), dim3(256), 0, stream, w.sbits, w.ebits,

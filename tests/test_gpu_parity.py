@@ -85,6 +85,8 @@ EDGE_TEXTS = [
     "⺀⺙⺛⻳⼀⿕々〇〡〩〸〻豈鶴侮頻𖿰𖿱",  # every Han range edge
     "〆ゝ中ー文",
     "a1+1=2 中文 x　y",
+    "丁" * 2719, "丁" * 2720, "丁" * 2721, "一丁" * 1400, "𠀀" * 2041,   # around the k_zh window limit
+    ("中文。" * 900) + "丁" * 3000 + ("，中文" * 900),                   # long block between short ones
 ]
 
 
