@@ -107,9 +107,10 @@ struct Device {
     hipStream_t stream = nullptr;
     // image
     uint16_t* pagemap = nullptr;
-    jb_l1* l1 = nullptr;
+    uint32_t* l1 = nullptr;
     double* emit = nullptr;
-    jb_node* nodes = nullptr;
+    uint64_t* nodes = nullptr;
+    double* wtab = nullptr;
     DevImage dim{};
     // workspace
     Work w{};
@@ -179,7 +180,7 @@ extern "C" int jb_image_build(const jb_config* cfg, jb_image** out) {
     if ((rc = parse_dictionary(d ? d : "", dl, cfg->dict_kind, &im->dict, &err))) return fail(rc, "%s", err.c_str());
     if (cfg->size_override > 0) im->dict.size = cfg->size_override;
     if ((rc = parse_emission(e, el, &im->emit, &err))) return fail(rc, "%s", err.c_str());
-    build_image(im->dict, im->emit, &im->img);
+    if ((rc = build_image(im->dict, im->emit, &im->img, &err))) return fail(rc, "%s", err.c_str());
     if (im->img.maxlen > 255) return fail(JB_ELIMIT, "dictionary word of %u runes (max 255)", im->img.maxlen);
     *out = im.release();
     return JB_OK;
@@ -199,15 +200,13 @@ extern "C" int jb_image_lookup(const jb_image* img, const char* word, size_t len
         runes.push_back(r);
         i += wd;
     }
-    const uint32_t id = image_lookup(img->img, runes.data(), runes.size());
-    if (id == JB_EMPTY) return 0;
-    const jb_node& n = img->img.nodes[id];
+    const Lookup lk = image_lookup(img->img, runes.data(), runes.size());
+    if (!lk.found) return 0;
     if (freq) {
-        const uint32_t fc = n.rune_fc >> JB_FC_SHIFT;
         auto it = img->dict.term_freq.find(std::string(word, len));
-        *freq = it != img->dict.term_freq.end() ? it->second : (fc == JB_FC_ZERO ? 0 : -1);
+        *freq = it != img->dict.term_freq.end() ? it->second : (lk.fc == JB_FC_ZERO ? 0 : -1);
     }
-    if (w) *w = n.w;
+    if (w) *w = img->img.wtab[lk.widx];
     return 1;
 }
 
@@ -234,33 +233,34 @@ extern "C" double jb_go_log(double x) { return go_log(x); }
 // ---------------------------------------------------------------------------
 // devices
 // ---------------------------------------------------------------------------
+template <class T>
+static int upload(T** dst, const std::vector<T>& src) {
+    dfree(*dst);
+    *dst = nullptr;
+    HIPCHK(hipMalloc(dst, std::max<size_t>(src.size(), 1) * sizeof(T)));
+    if (!src.empty()) HIPCHK(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    return JB_OK;
+}
+
 static int upload_image(Device* d, const Image& img) {
     HIPCHK(hipSetDevice(d->ordinal));
-    dfree(d->pagemap);
-    dfree(d->l1);
-    dfree(d->emit);
-    dfree(d->nodes);
-    d->pagemap = nullptr; d->l1 = nullptr; d->emit = nullptr; d->nodes = nullptr;
-    HIPCHK(hipMalloc(&d->pagemap, img.pagemap.size() * sizeof(uint16_t)));
-    HIPCHK(hipMalloc(&d->l1, img.l1.size() * sizeof(jb_l1)));
-    HIPCHK(hipMalloc(&d->emit, img.emit.size() * sizeof(double)));
-    HIPCHK(hipMalloc(&d->nodes, img.nodes.size() * sizeof(jb_node)));
-    HIPCHK(hipMemcpy(d->pagemap, img.pagemap.data(), img.pagemap.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(d->l1, img.l1.data(), img.l1.size() * sizeof(jb_l1), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(d->emit, img.emit.data(), img.emit.size() * sizeof(double), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(d->nodes, img.nodes.data(), img.nodes.size() * sizeof(jb_node), hipMemcpyHostToDevice));
+    int rc;
+    if ((rc = upload(&d->pagemap, img.pagemap)) || (rc = upload(&d->l1, img.l1)) || (rc = upload(&d->emit, img.emit)) ||
+        (rc = upload(&d->nodes, img.nodes)) || (rc = upload(&d->wtab, img.wtab)))
+        return rc;
     d->dim.pagemap = d->pagemap;
     d->dim.l1 = d->l1;
     d->dim.emit = d->emit;
     d->dim.nodes = d->nodes;
+    d->dim.wtab = d->wtab;
     d->dim.mask = (uint32_t)(img.nodes.size() - 1);
-    d->dim.w_absent = img.w_absent;
+    d->dim.nrows = img.nrows;
     return JB_OK;
 }
 
 static void free_work(Work* w) {
     dfree(w->docbits); dfree(w->sbits); dfree(w->ebits); dfree(w->tile_cnt); dfree(w->tile_off);
-    dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->blk); dfree(w->lists); dfree(w->longq); dfree(w->gbest);
+    dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->blk); dfree(w->lists); dfree(w->emask); dfree(w->ewidx);
     dfree(w->gbl);
     dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters);
     *w = Work{};
@@ -285,9 +285,10 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.ttile_off, nttiles * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.blk, (nb + 4) * 4));
     HIPCHK(hipMalloc(&w.lists, (nb + 4) * 4));
-    HIPCHK(hipMalloc(&w.longq, (nb / 4096 + 4) * 4));
-    HIPCHK(hipMalloc(&w.gbest, (nb / 3 + 4) * 8));
-    HIPCHK(hipMalloc(&w.gbl, nb / 3 + 4));
+    HIPCHK(hipMalloc(&w.emask, (nb / 3 + 8) * 4));
+    HIPCHK(hipMalloc(&w.ewidx, (nb / 3 + 8) * sizeof(uint2)));
+    HIPCHK(hipMalloc(&w.gbl, nb / 3 + 8));
+
     HIPCHK(hipMalloc(&w.tok_start, (nb + 4) * 4));
     HIPCHK(hipMalloc(&w.tok_end, (nb + 4) * 4));
     HIPCHK(hipMalloc(&w.doc_tok, ((uint64_t)ndc + 2) * 8));
@@ -315,11 +316,23 @@ static int ensure_staging(Device* d, uint64_t nbytes, uint32_t ndocs) {
     return JB_OK;
 }
 
-static int launch(jb_ctx*, Device* d, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off,
+static uint32_t grid_zh_override = 0;
+
+static int launch(jb_ctx* ctx, Device* d, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off,
                   uint32_t ndocs, bool hmm, hipStream_t s) {
-    const uint32_t grid_zh = d->ncu * std::max(1u, zh_blocks_per_cu(hmm));
+    const uint32_t ring = zh_ring(ctx->im->img.maxlen);
+    if (!ring) return fail(JB_ELIMIT, "dictionary word of %u runes (max 255)", ctx->im->img.maxlen);
+    const uint32_t grid_zh = d->ncu * std::max(1u, zh_blocks_per_cu(hmm, ring));
     const uint32_t grid_nz = d->ncu * std::max(1u, std::min(4u, nonzh_blocks_per_cu()));
-    const hipError_t e = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, grid_zh, grid_nz, s,
+    static const bool dbg = getenv("JB_DEBUG") != nullptr;
+    if (const char* a = getenv("JB_ABLATE")) g_ablate = (uint32_t)atoi(a);
+    if (const char* gz = getenv("JB_GRID_ZH")) grid_zh_override = (uint32_t)atoi(gz);
+    const uint32_t gzh = grid_zh_override ? grid_zh_override : grid_zh;
+    if (dbg)
+        fprintf(stderr, "[jb] nbytes=%llu ndocs=%u ring=%u zh_threads=%u grid_zh=%u (occ %u/CU) grid_nz=%u ablate=%u\n",
+                (unsigned long long)nbytes, ndocs, ring, zh_threads(ring), gzh, zh_blocks_per_cu(hmm, ring), grid_nz,
+                g_ablate);
+    const hipError_t e = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, ring, gzh, grid_nz, s,
                                       d->profile ? &d->timer : nullptr);
     if (e != hipSuccess) return fail(JB_EDEVICE, "pipeline launch: %s", hipGetErrorString(e));
     return JB_OK;
@@ -361,6 +374,7 @@ extern "C" void jb_close(jb_ctx* ctx) {
         d->timer.reset();
         free_work(&d->w);
         dfree(d->text); dfree(d->doc_off); dfree(d->pagemap); dfree(d->l1); dfree(d->emit); dfree(d->nodes);
+        dfree(d->wtab);
         (void)hipStreamDestroy(d->stream);
     }
     delete ctx;
@@ -587,7 +601,8 @@ extern "C" int jb_add_word(jb_ctx* ctx, const char* word, size_t len, int64_t fr
     Dictionary& dict = ctx->im->dict;
     dict.term_freq[std::string(word, len)] = freq;
     dict.size += freq;
-    build_image(dict, ctx->im->emit, &ctx->im->img);
+    std::string err;
+    if ((rc = build_image(dict, ctx->im->emit, &ctx->im->img, &err))) return fail(rc, "%s", err.c_str());
     if (ctx->im->img.maxlen > 255) return fail(JB_ELIMIT, "dictionary word of %u runes (max 255)", ctx->im->img.maxlen);
     for (auto& d : ctx->devs) {
         std::lock_guard<std::mutex> g(d->mu);

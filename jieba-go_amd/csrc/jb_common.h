@@ -9,16 +9,19 @@
 //   pagemap[0x110000 >> 8]  u16   rune page -> dense page id (page 0 = empty page;
 //                                 pages 0x34..0x9F, U+3400..U+9FFF, are always ids
 //                                 1..108 so jb_row() skips the pagemap for them)
-//   l1[npages * 256]        16 B  single-rune key -> {node id, freq class, w}
+//   l1[npages * 256]        u32   the single-rune key: freq class | has-children |
+//                                 weight index (its node id is its row)
 //   emit[npages * 256][4]   f64   emitP[B|M|E|S][string(rune)], minFloat if absent
-//   nodes[cap]              16 B  open-addressing hash of trie edges:
-//                                 key (parent node id, rune) -> {freq class, w}
-//                                 w = math.Log(float64(freq)) - math.Log(float64(size))
-//                                 computed on the host with Go's Log algorithm.
+//   nodes[cap]              u64   open-addressing hash of the deeper trie edges:
+//                                 key (parent id, rune) -> {freq class, has-children,
+//                                 weight index}; a node's id is nrows + its slot
+//   wtab[nw]                f64   distinct weights w = math.Log(float64(freq)) -
+//                                 math.Log(float64(size)) (Go's Log, on the host);
+//                                 wtab[0] = Log(1.0) - Log(size) for absent runes
 //
-// A node id is the index of the node's own hash slot, so walking one more rune is
-// one hash probe (usually one 16-byte load).  Only keys that the reference's walk
-// can reach are stored: keys made of valid Han runes whose every proper prefix is
+// Walking one more rune is one hash probe, usually one 8-byte load, and none at
+// all from a node without children.  Only keys that the reference's walk can
+// reach are stored: keys made of valid Han runes whose every proper prefix is
 // itself a key (buildDag breaks at the first absent string, tokenizer.go:475-478).
 #pragma once
 #include <stdint.h>
@@ -33,26 +36,33 @@
 #define JB_ROOT 0xFFFFFFFEu
 #define JB_NPAGES_MAX (0x110000u >> 8)
 
-// freq class, stored in bits 24..25 of jb_node.rune_fc
+// freq class
 #define JB_FC_ZERO 0u   // freq == 0: a prefix-only entry (e.g. "撙", tokenizer_test.go:126)
 #define JB_FC_POS 1u    // freq > 0: a DAG edge (tokenizer.go:479)
 #define JB_FC_NEG 2u    // freq < 0: present, no edge, walk continues
-#define JB_FC_ABSENT 3u // (l1 records only) the single rune is not a key
-#define JB_FC_SHIFT 24
-#define JB_RUNE_MASK 0x1FFFFFu
+#define JB_FC_ABSENT 3u // (l1 only) the single rune is not a key
+#define JB_WIDX_ABSENT 0u
 
-struct alignas(16) jb_node {
-    uint32_t parent;   // parent node id (JB_ROOT for single runes), JB_EMPTY = free slot
-    uint32_t rune_fc;  // rune | (freq class << 24)
-    double w;          // Log(freq) - Log(size)
-};
+// u64 node: rune[0,21) fc[21,23) has_child[23] widx[24,41) parent[41,64); empty slot = ~0
+#define JB_NODE_EMPTY 0xFFFFFFFFFFFFFFFFull
+#define JB_MAX_IDS (1u << 23)
+#define JB_MAX_WIDX (1u << 17)
+JB_HD uint64_t jb_node_make(uint32_t parent, uint32_t rune, uint32_t fc, uint32_t hc, uint32_t widx) {
+    return (uint64_t)rune | ((uint64_t)fc << 21) | ((uint64_t)hc << 23) | ((uint64_t)widx << 24) |
+           ((uint64_t)parent << 41);
+}
+JB_HD uint32_t jb_node_rune(uint64_t n) { return (uint32_t)n & 0x1FFFFFu; }
+JB_HD uint32_t jb_node_fc(uint64_t n) { return (uint32_t)(n >> 21) & 3u; }
+JB_HD uint32_t jb_node_hc(uint64_t n) { return (uint32_t)(n >> 23) & 1u; }
+JB_HD uint32_t jb_node_widx(uint64_t n) { return (uint32_t)(n >> 24) & 0x1FFFFu; }
+JB_HD uint32_t jb_node_parent(uint64_t n) { return (uint32_t)(n >> 41); }
+// match of a probed slot against (parent, rune): the low 21 and high 23 bits
+JB_HD bool jb_node_is(uint64_t n, uint32_t parent, uint32_t rune) {
+    return ((n ^ ((uint64_t)parent << 41) ^ rune) & 0xFFFFFE00001FFFFFull) == 0;
+}
 
-// Level-1 record: everything the walk needs for the rune itself in one 16-byte load.
-struct alignas(16) jb_l1 {
-    uint32_t id;  // node id of the single-rune key (JB_EMPTY if absent)
-    uint32_t fc;  // JB_FC_*; JB_FC_ABSENT when the rune is not a key
-    double w;     // node w, or w_absent = Log(1.0) - Log(size) when absent (tokenizer.go:515-519)
-};
+// u32 level-1 record: fc[0,2) has_child[2] widx[3,20)
+JB_HD uint32_t jb_l1_make(uint32_t fc, uint32_t hc, uint32_t widx) { return fc | (hc << 2) | (widx << 3); }
 
 // Pages U+3400..U+9FFF (CJK Ext-A + URO) sit at fixed page ids 1..108.
 #define JB_DIRECT_LO 0x3400u
@@ -65,7 +75,7 @@ JB_HD uint32_t jb_row(const uint16_t* pagemap, uint32_t r) {
     return (uint32_t)pagemap[r >> 8] * 256u + (r & 255u);
 }
 
-// 32-bit mix of (parent, rune); identical on host and device.
+// Slot hash of the edge (parent, rune); identical on host and device.
 JB_HD uint32_t jb_hash(uint32_t parent, uint32_t rune) {
     uint32_t h = parent * 0x9E3779B1u ^ (rune * 0x85EBCA77u + 0x165667B1u);
     h ^= h >> 16;

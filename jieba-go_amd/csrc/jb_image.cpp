@@ -326,13 +326,12 @@ int parse_emission(const char* buf, size_t len, Emission* out, std::string* err)
 // ---------------------------------------------------------------------------
 static uint32_t freq_class(int64_t f) { return f > 0 ? JB_FC_POS : (f == 0 ? JB_FC_ZERO : JB_FC_NEG); }
 
-void build_image(const Dictionary& d, const Emission& e, Image* img) {
+int build_image(const Dictionary& d, const Emission& e, Image* img, std::string* err) {
     img->size = d.size;
     img->total = go_log((double)d.size);       // calcDagProba: total := math.Log(float64(pd.size))
     img->w_absent = go_log(1.0) - img->total;  // tf := 1.0 when the piece is absent (tokenizer.go:515)
 
-    // Reachable keys: valid Han runes, every proper prefix a key.  Insert level
-    // by level so that a parent's node id exists before its children.
+    // Keys a walk can spell: valid UTF-8, every rune Han.
     struct Key { std::vector<uint32_t> r; int64_t f; };
     std::vector<Key> keys;
     keys.reserve(d.term_freq.size());
@@ -348,87 +347,134 @@ void build_image(const Dictionary& d, const Emission& e, Image* img) {
         if (a.r.size() != b.r.size()) return a.r.size() < b.r.size();
         return a.r < b.r;
     });
-    uint64_t cap = 1024;
-    while (cap < keys.size() * 2) cap <<= 1;
-    img->nodes.assign(cap, jb_node{JB_EMPTY, 0, 0.0});
-    img->maxlen = 0;
-    img->nnodes = 0;
 
+    // pages: single-rune keys and emission runes
     std::vector<uint8_t> page_used(JB_NPAGES_MAX, 0);
-    std::vector<std::pair<uint32_t, uint32_t>> level1;  // rune -> node id
-    const uint64_t mask = cap - 1;
-    auto find = [&](uint32_t parent, uint32_t r) -> uint32_t {
-        uint64_t h = jb_hash(parent, r) & mask;
-        for (;;) {
-            const jb_node& n = img->nodes[h];
-            if (n.parent == JB_EMPTY) return JB_EMPTY;
-            if (n.parent == parent && (n.rune_fc & JB_RUNE_MASK) == r) return (uint32_t)h;
-            h = (h + 1) & mask;
-        }
-    };
-    // node id by key prefix: resolve through the table itself
-    for (const Key& k : keys) {
-        uint32_t parent = JB_ROOT;
-        bool ok = true;
-        for (size_t i = 0; i + 1 < k.r.size() && ok; i++) {
-            parent = find(parent, k.r[i]);
-            ok = parent != JB_EMPTY;
-        }
-        if (!ok) continue;  // a proper prefix is not a key: unreachable (tokenizer.go:475-478)
-        const uint32_t r = k.r.back();
-        uint64_t h = jb_hash(parent, r) & mask;
-        while (img->nodes[h].parent != JB_EMPTY) h = (h + 1) & mask;
-        jb_node& n = img->nodes[h];
-        n.parent = parent;
-        n.rune_fc = r | (freq_class(k.f) << JB_FC_SHIFT);
-        n.w = go_log((double)k.f) - img->total;  // pieceFreq := math.Log(tf) - total (tokenizer.go:519)
-        img->nnodes++;
-        img->maxlen = std::max<uint32_t>(img->maxlen, (uint32_t)k.r.size());
-        if (parent == JB_ROOT) {
-            level1.emplace_back(r, (uint32_t)h);
-            page_used[r >> 8] = 1;
-        }
-    }
+    for (const Key& k : keys)
+        if (k.r.size() == 1) page_used[k.r[0] >> 8] = 1;
     for (int s = 0; s < 4; s++)
         for (const auto& kv : e.by_rune[s])
             if (kv.first < 0x110000u) page_used[kv.first >> 8] = 1;
     img->pagemap.assign(JB_NPAGES_MAX, 0);
     for (uint32_t p = 0; p < JB_DIRECT_PAGES; p++) img->pagemap[(JB_DIRECT_LO >> 8) + p] = (uint16_t)(p + 1);
     img->npages = 1 + JB_DIRECT_PAGES;  // page 0: the empty page; then the fixed U+3400..U+9FFF pages
-    for (uint32_t p = 0; p < JB_NPAGES_MAX; p++)
-        if (page_used[p] && img->pagemap[p] == 0 && p != 0) img->pagemap[p] = (uint16_t)img->npages++;
+    for (uint32_t p = 1; p < JB_NPAGES_MAX; p++)
+        if (page_used[p] && img->pagemap[p] == 0) img->pagemap[p] = (uint16_t)img->npages++;
     if (page_used[0]) img->pagemap[0] = (uint16_t)img->npages++;
-    img->l1.assign((size_t)img->npages * 256, jb_l1{JB_EMPTY, JB_FC_ABSENT, img->w_absent});
-    img->emit.assign((size_t)img->npages * 256 * 4, JB_MIN_FLOAT);  // not found -> minFloat (tokenizer.go:690,710)
-    for (const auto& p : level1) {
-        const jb_node& n = img->nodes[p.second];
-        img->l1[jb_row(img->pagemap.data(), p.first)] = jb_l1{p.second, n.rune_fc >> JB_FC_SHIFT, n.w};
+    img->nrows = img->npages * 256u;
+    const uint16_t* pm = img->pagemap.data();
+
+    // distinct weights: pieceFreq := math.Log(tf) - total (tokenizer.go:519)
+    img->wtab.assign(1, img->w_absent);
+    std::unordered_map<uint64_t, uint32_t> widx_of;
+    auto widx = [&](int64_t f) -> uint32_t {
+        const double w = go_log((double)f) - img->total;
+        uint64_t bits;
+        memcpy(&bits, &w, 8);
+        auto it = widx_of.find(bits);
+        if (it != widx_of.end()) return it->second;
+        const uint32_t i = (uint32_t)img->wtab.size();
+        img->wtab.push_back(w);
+        widx_of.emplace(bits, i);
+        return i;
+    };
+
+    size_t deep = 0;
+    for (const Key& k : keys) deep += k.r.size() > 1;
+    uint64_t cap = 1024;
+    while (cap < deep * 2) cap <<= 1;
+    if (img->nrows + cap >= JB_MAX_IDS - 1) {
+        *err = "dictionary too large for the packed trie (" + std::to_string(deep) + " multi-rune keys)";
+        return JB_ELIMIT;
     }
+    img->nodes.assign(cap, JB_NODE_EMPTY);
+    img->l1.assign(img->nrows, jb_l1_make(JB_FC_ABSENT, 0, JB_WIDX_ABSENT));
+    img->maxlen = 0;
+    img->nnodes = 0;
+    const uint64_t mask = cap - 1;
+    auto find = [&](uint32_t parent, uint32_t r) -> uint64_t {  // slot or ~0
+        uint64_t h = jb_hash(parent, r) & mask;
+        for (;;) {
+            const uint64_t n = img->nodes[h];
+            if (n == JB_NODE_EMPTY) return ~0ull;
+            if (jb_node_is(n, parent, r)) return h;
+            h = (h + 1) & mask;
+        }
+    };
+    std::vector<uint32_t> parents;  // parent id of every stored deeper node
+    for (const Key& k : keys) {
+        const uint32_t fc = freq_class(k.f);
+        const uint32_t wi = widx(k.f);
+        if (wi >= JB_MAX_WIDX) {
+            *err = "more than " + std::to_string(JB_MAX_WIDX) + " distinct frequencies";
+            return JB_ELIMIT;
+        }
+        if (k.r.size() == 1) {
+            img->l1[jb_row(pm, k.r[0])] = jb_l1_make(fc, 0, wi);
+            img->nnodes++;
+            img->maxlen = std::max<uint32_t>(img->maxlen, 1);
+            continue;
+        }
+        // parent id: level-1 row, then nrows + slot for each deeper prefix
+        const uint32_t row0 = jb_row(pm, k.r[0]);
+        if ((img->l1[row0] & 3u) == JB_FC_ABSENT) continue;  // unreachable (tokenizer.go:475-478)
+        uint32_t parent = row0;
+        bool ok = true;
+        for (size_t i = 1; i + 1 < k.r.size() && ok; i++) {
+            const uint64_t sl = find(parent, k.r[i]);
+            ok = sl != ~0ull;
+            if (ok) parent = img->nrows + (uint32_t)sl;
+        }
+        if (!ok) continue;
+        const uint32_t r = k.r.back();
+        uint64_t h = jb_hash(parent, r) & mask;
+        while (img->nodes[h] != JB_NODE_EMPTY) h = (h + 1) & mask;
+        img->nodes[h] = jb_node_make(parent, r, fc, 0, wi);
+        parents.push_back(parent);
+        img->nnodes++;
+        img->maxlen = std::max<uint32_t>(img->maxlen, (uint32_t)k.r.size());
+    }
+    // has-children flags: a walk stops at a node without children, no probe
+    for (uint32_t p : parents) {
+        if (p < img->nrows) img->l1[p] |= 1u << 2;
+        else img->nodes[p - img->nrows] |= 1ull << 23;
+    }
+    img->emit.assign((size_t)img->npages * 256 * 4, JB_MIN_FLOAT);  // not found -> minFloat (tokenizer.go:690,710)
     for (int s = 0; s < 4; s++)
         for (const auto& kv : e.by_rune[s]) {
             if (kv.first >= 0x110000u) continue;
-            img->emit[(size_t)jb_row(img->pagemap.data(), kv.first) * 4 + s] = kv.second;
+            img->emit[(size_t)jb_row(pm, kv.first) * 4 + s] = kv.second;
         }
+    return JB_OK;
 }
 
-uint32_t image_lookup(const Image& img, const uint32_t* runes, size_t n) {
-    if (n == 0) return JB_EMPTY;
+Lookup image_lookup(const Image& img, const uint32_t* runes, size_t n) {
+    Lookup out;
+    if (n == 0 || runes[0] >= 0x110000u) return out;
+    const uint32_t row = jb_row(img.pagemap.data(), runes[0]);
+    const uint32_t rec = img.l1[row];
+    if ((rec & 3u) == JB_FC_ABSENT) return out;
+    uint32_t id = row, fc = rec & 3u, wi = rec >> 3;
     const uint64_t mask = img.nodes.size() - 1;
-    const uint32_t r0 = runes[0];
-    if (r0 >= 0x110000u) return JB_EMPTY;
-    uint32_t id = img.l1[jb_row(img.pagemap.data(), r0)].id;
-    for (size_t i = 1; i < n && id != JB_EMPTY; i++) {
+    for (size_t i = 1; i < n; i++) {
         uint64_t h = jb_hash(id, runes[i]) & mask;
-        uint32_t found = JB_EMPTY;
         for (;;) {
-            const jb_node& nd = img.nodes[h];
-            if (nd.parent == JB_EMPTY) break;
-            if (nd.parent == id && (nd.rune_fc & JB_RUNE_MASK) == runes[i]) { found = (uint32_t)h; break; }
+            const uint64_t nd = img.nodes[h];
+            if (nd == JB_NODE_EMPTY) return Lookup{};
+            if (jb_node_is(nd, id, runes[i])) {
+                id = img.nrows + (uint32_t)h;
+                fc = jb_node_fc(nd);
+                wi = jb_node_widx(nd);
+                break;
+            }
             h = (h + 1) & mask;
         }
-        id = found;
     }
-    return id;
+    out.found = true;
+    out.fc = fc;
+    out.widx = wi;
+    out.id = id;
+    return out;
 }
 
 }  // namespace jb

@@ -27,15 +27,24 @@ struct Emission {
 // Flat arrays uploaded to every device (layout: jb_common.h).
 struct Image {
     std::vector<uint16_t> pagemap;  // JB_NPAGES_MAX
-    std::vector<jb_l1> l1;          // npages * 256
+    std::vector<uint32_t> l1;       // npages * 256 level-1 records
     std::vector<double> emit;       // npages * 256 * 4
-    std::vector<jb_node> nodes;     // hash capacity (power of two)
+    std::vector<uint64_t> nodes;    // hash capacity (power of two), deeper trie edges
+    std::vector<double> wtab;       // distinct weights; [0] = w_absent
     uint32_t npages = 0;
+    uint32_t nrows = 0;             // npages * 256: ids of level-1 nodes; deeper ids = nrows + slot
     uint32_t maxlen = 0;            // longest reachable key, runes
-    uint64_t nnodes = 0;
+    uint64_t nnodes = 0;            // reachable keys (all levels)
     double total = 0;               // math.Log(float64(size))
     double w_absent = 0;            // math.Log(1.0) - total
     int64_t size = 0;
+};
+
+struct Lookup {
+    bool found = false;
+    uint32_t fc = JB_FC_ABSENT;
+    uint32_t widx = 0;
+    uint32_t id = JB_EMPTY;
 };
 
 double go_log(double x);
@@ -45,9 +54,10 @@ double go_log(double x);
 // Returns 0 or a negative JB_E* code; err receives a message.
 int parse_dictionary(const char* buf, size_t len, int kind, Dictionary* out, std::string* err);
 int parse_emission(const char* buf, size_t len, Emission* out, std::string* err);
-void build_image(const Dictionary& d, const Emission& e, Image* img);
+// Returns 0 or JB_ELIMIT (too many trie nodes / distinct weights for the packed layout).
+int build_image(const Dictionary& d, const Emission& e, Image* img, std::string* err);
 
-// Walk the image like the kernel does: returns node id or JB_EMPTY.
-uint32_t image_lookup(const Image& img, const uint32_t* runes, size_t n);
+// Walk the image like the kernels do.
+Lookup image_lookup(const Image& img, const uint32_t* runes, size_t n);
 
 }  // namespace jb

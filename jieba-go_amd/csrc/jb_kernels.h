@@ -10,11 +10,12 @@ namespace jb {
 // Device copy of the image (jb_common.h), passed by value to kernels.
 struct DevImage {
     const uint16_t* pagemap;
-    const jb_l1* l1;
+    const uint32_t* l1;
     const double* emit;
-    const jb_node* nodes;
+    const uint64_t* nodes;
+    const double* wtab;
     uint32_t mask;     // hash capacity - 1
-    double w_absent;   // math.Log(1.0) - math.Log(size)
+    uint32_t nrows;    // deeper node id = nrows + slot
 };
 
 // Device counters (u32 slots unless noted)
@@ -24,8 +25,7 @@ enum {
     CNT_NTOK = 2,   // token starts
     CNT_NTOKE = 3,  // token ends (== CNT_NTOK when consistent)
     CNT_ERR = 4,    // bit 0: a zh block reached a tail index -1 (the reference panics)
-    CNT_WORK = 5,   // k_zh work counter (next zh block to hand out)
-    CNT_NLONG = 6,  // zh blocks deferred to k_zh_long
+    CNT_WORK = 5,   // k_zh work counter: next chunk of 64 zh blocks
     CNT_NWORDS = 8  // u32 slots reserved; u64 token count lives at byte offset 32
 };
 
@@ -43,9 +43,9 @@ struct Work {
     uint2* ttile_off;
     uint32_t* blk;         // block start | zh << 31, then sentinel nbytes
     uint32_t* lists;       // zh block ids from the front, non-zh block ids from the back
-    uint32_t* longq;       // zh list positions of blocks longer than a k_zh window
-    double* gbest;         // k_zh_long per-rune best proba, index byte / 3
-    uint8_t* gbl;          // k_zh_long per-rune piece length / Viterbi back-pointers, index byte / 3
+    uint32_t* emask;       // per Han rune (slot = byte / 3): bit L-1 = DAG edge of L runes; bit 31 overflow
+    uint2* ewidx;          // per Han rune: weight indices of its first 4 edges (u16 each)
+    uint8_t* gbl;          // per Han rune: chosen piece length, then Viterbi back-pointers / labels
     uint32_t* tok_start;
     uint32_t* tok_end;
     uint64_t* doc_tok;
@@ -56,7 +56,7 @@ struct Work {
 
 // Kernel ids for per-launch timing.
 enum KernelId {
-    K_DOCBITS = 0, K_BLOCKS_COUNT, K_SCAN_BLOCKS, K_BLOCKS_WRITE, K_ZH, K_ZH_LONG, K_NONZH,
+    K_DOCBITS = 0, K_BLOCKS_COUNT, K_SCAN_BLOCKS, K_BLOCKS_WRITE, K_WALK, K_ZH, K_NONZH,
     K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_NUM
 };
 extern const char* const kKernelNames[K_NUM];
@@ -72,11 +72,15 @@ struct KernelTimer {
 // launch error.  grid_zh / grid_nz: persistent grids of k_zh / k_nonzh.
 // d_text must be readable 64 bytes past nbytes.
 hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text, uint64_t nbytes,
-                        const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, uint32_t grid_zh, uint32_t grid_nz,
-                        hipStream_t stream, KernelTimer* timer);
+                        const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, uint32_t ring, uint32_t grid_zh,
+                        uint32_t grid_nz, hipStream_t stream, KernelTimer* timer);
 
-// Resident k_zh workgroups per CU (occupancy API).
-uint32_t zh_blocks_per_cu(bool hmm);
+// k_zh's best-proba ring: a power of two > the longest reachable key (runes),
+// LDS ring * threads * 8 bytes <= 32 KiB.  0 if the key is too long.
+uint32_t zh_ring(uint32_t maxlen);
+uint32_t zh_threads(uint32_t ring);
+uint32_t zh_blocks_per_cu(bool hmm, uint32_t ring);
+extern uint32_t g_ablate;  // diagnostic ablations from JB_ABLATE (results are wrong when non-zero)
 uint32_t nonzh_blocks_per_cu();
 
 }  // namespace jb

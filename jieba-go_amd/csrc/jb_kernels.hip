@@ -6,9 +6,10 @@
 //                 block starts                  (zh regex + splitText, tokenizer.go:21,154-155,165-210)
 //   k_scan2       tile counts -> offsets
 //   k_blocks<1>   write block list (start | zh<<31), zh ids, non-zh ids
-//   k_zh          one lane per Han block, text staged per workgroup in LDS: trie
-//                 walk + backward max-prob DP + forward path + BMES Viterbi on
-//                 singleton runs (k_zh_long: blocks longer than an LDS window)
+//   k_walk        one thread per 16 bytes: the trie walk (DAG edges) of every Han
+//                 rune, several walks in flight per thread
+//   k_zh          one lane per Han block: backward max-prob DP over those edges +
+//                 forward path + BMES Viterbi on singleton runs
 //                                               (cutZh/cutDAG/buildDag/calcDagProba/
 //                                                findDagPath/maxIndexProba/viterbi/cutHMM,
 //                                                tokenizer.go:221-285,462-578,668-756)
@@ -28,7 +29,7 @@
 namespace jb {
 
 const char* const kKernelNames[K_NUM] = {"k_docbits", "k_blocks_count", "k_scan_blocks", "k_blocks_write",
-                                         "k_zh", "k_zh_long", "k_nonzh", "k_tok_count", "k_scan_tok",
+                                         "k_walk", "k_zh", "k_nonzh", "k_tok_count", "k_scan_tok",
                                          "k_tok_write", "k_doc_tok"};
 
 // newJiebaHMM literals (tokenizer.go:629-652)
@@ -51,21 +52,6 @@ const char* const kKernelNames[K_NUM] = {"k_docbits", "k_blocks_count", "k_scan_
 __device__ __forceinline__ uint32_t ld4(const uint8_t* __restrict__ t, uint64_t q) {
     const uint32_t* a = reinterpret_cast<const uint32_t*>(t + (q & ~3ull));
     return __builtin_amdgcn_alignbyte(a[1], a[0], (uint32_t)(q & 3));
-}
-
-// Child of `parent` labelled r in the open-addressing edge hash.
-__device__ __forceinline__ uint32_t child(const jb_node* __restrict__ nodes, uint32_t mask, uint32_t parent,
-                                          uint32_t r, jb_node* out) {
-    uint32_t h = jb_hash(parent, r) & mask;
-    for (;;) {
-        const jb_node n = nodes[h];
-        if (n.parent == JB_EMPTY) return JB_EMPTY;
-        if (n.parent == parent && (n.rune_fc & JB_RUNE_MASK) == r) {
-            *out = n;
-            return h;
-        }
-        h = (h + 1) & mask;
-    }
 }
 
 // Token bitmaps: bits are accumulated per 32-byte word in registers and
@@ -294,24 +280,246 @@ __global__ __launch_bounds__(1024) void k_scan2(const uint2* __restrict__ cnt, u
 }
 
 // ---------------------------------------------------------------------------
-// Han blocks (cutZh, tokenizer.go:221-255).
+// k_walk: the DAG edges of every Han rune (buildDag, tokenizer.go:462-497).
 //
-// process_block() runs one block in one lane.  Backward over the block's runes
-// (calcDagProba, :502-548): for rune i the lane walks the trie forward from i
-// (buildDag, :462-497) and folds each edge (i, i+len) — in ascending len, as
-// the DAG lists them — into maxIndexProba's running state (:565-578) with
-// pieceProba = w + best(i+len) (:519-529); best(n) is the {n, 0.0} sentinel
-// (:522-525).  best / the chosen length live per rune at index (byte offset)/3
-// (Han runes are >= 3 bytes, so distinct runes never share an index).  The
-// forward walk (findDagPath, :552-562) then emits pieces or, with HMM,
-// gathers runs of single-rune pieces for the Viterbi (:228-253).
+// Each wave owns 1 KiB of text.  It stages those bytes (plus 192 bytes of
+// look-ahead) and their document-start bits in LDS, finds the Han rune starts
+// (16 bytes per lane) and compacts them into a wave-local queue.  Then every
+// lane runs one walk at a time as a small state machine — one trie probe per
+// loop trip — and takes the next queued start as soon as its walk ends, so
+// the 64 lanes stay busy however long the individual walks are.  A walk
+// starts at the rune's l1 record (level 1) and follows one (parent id, rune)
+// probe per further rune.  It stops at the first string that is not a key
+// (:475-478), at a node without children, or at the end of the Han run (next
+// rune not Han, invalid, or in the next document).
 //
-// A View supplies the text bytes, the per-rune slots and the token sink:
-//   LdsView    — k_zh: the workgroup's window of text staged in LDS
-//   GlobalView — k_zh_long: blocks longer than a window, straight from HBM
+// Output per rune, slot = byte offset / 3 (Han runes are >= 3 bytes, so slots
+// never collide):
+//   emask[slot]  bit L-1 set for an edge of L runes (L <= 31) (:479-481)
+//   ewidx[slot]  weight indices of the first 4 edges in ascending L (u16 x 4)
+//   bit 31 of emask: more than 4 edges or an edge longer than 31 runes; k_zh
+//   then walks that rune itself.
+// A rune that is absent or has count 0 gets the single edge L = 1 (:468-471)
+// with weight index 0 (Log(1) - Log(size)) or that of Log(0) - Log(size) = -Inf.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kWin = 8192;  // k_zh window bytes (LDS)
+#define JB_EDGE_OVF 0x80000000u
+constexpr uint32_t kWalkSpan = 1024;                  // text bytes per wave
+constexpr uint32_t kWalkWin = kWalkSpan + 192;        // staged bytes (span + look-ahead)
+constexpr uint32_t kWalkQ = 64 * 6;                   // <= 6 Han starts per 16 bytes
 
+// 4 bytes at window offset k of a wave's staged text.
+__device__ __forceinline__ uint32_t lds4(const uint8_t* tx, uint32_t k) {
+    const uint32_t* a = reinterpret_cast<const uint32_t*>(tx + (k & ~3u));
+    return __builtin_amdgcn_alignbyte(a[1], a[0], k & 3u);
+}
+
+// The Han rune encoded by x (Go-valid, within `lim` bytes), or 0.  A 3-byte
+// form with a Han value cannot be overlong (E0) or a surrogate (ED), and a
+// 4-byte form with a Han value is >= U+16FF0, so the bit patterns suffice.
+__device__ __forceinline__ uint32_t han_rune(uint32_t x, uint32_t lim, uint32_t* w) {
+    const uint32_t b0 = x & 0xFFu;
+    if ((x & 0x00C0C0F0u) == 0x008080E0u) {
+        const uint32_t r = ((b0 & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
+        if (lim < 3u || !jb_is_han(r)) return 0u;
+        *w = 3u;
+        return r;
+    }
+    if ((x & 0xC0C0C0F8u) == 0x808080F0u) {
+        const uint32_t r =
+            ((b0 & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) | (((x >> 16) & 0x3Fu) << 6) | ((x >> 24) & 0x3Fu);
+        if (lim < 4u || !jb_is_han(r)) return 0u;
+        *w = 4u;
+        return r;
+    }
+    return 0u;
+}
+
+__global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ text, uint64_t nbytes,
+                                              const uint32_t* __restrict__ docbits, DevImage im,
+                                              uint32_t* __restrict__ emask, uint2* __restrict__ ewidx,
+                                              uint32_t ablate) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_tx[4][kWalkWin + 16];
+    __shared__ uint32_t s_db[4][kWalkWin / 32 + 4];
+    __shared__ uint16_t s_q[4][kWalkQ];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t base = ((uint64_t)blockIdx.x * 4u + wv) * kWalkSpan;
+    if (base >= nbytes) return;  // whole wave
+    uint8_t* tx = s_tx[wv];
+    uint32_t* db = s_db[wv];
+    uint16_t* queue = s_q[wv];
+    // ---- stage text and document-start bits ------------------------------------
+    for (uint32_t k = lane; k < kWalkWin / 16; k += 64) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (base + 16u * k < nbytes + 48u) v = *reinterpret_cast<const uint4*>(text + base + 16u * k);
+        reinterpret_cast<uint4*>(tx)[k] = v;
+    }
+    const uint64_t lastw = (nbytes + 31) >> 5;
+    if (lane < kWalkWin / 32 + 4) {
+        const uint64_t wi = (base >> 5) + lane;
+        db[lane] = wi < lastw ? docbits[wi] : 0u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t avail_all = nbytes - base;  // bytes of text from the window start
+    // bytes available for a rune at window offset k: up to the next document start or the end
+    auto lim_at = [&](uint32_t k, bool* docstart) -> uint32_t {
+        const uint32_t w = k >> 5, sh = k & 31u;
+        const uint64_t v = ((((uint64_t)db[w + 1]) << 32) | db[w]) >> sh;
+        *docstart = (v & 1ull) != 0;
+        uint32_t lim = 1u + (uint32_t)__builtin_ctzll(((v >> 1) & 7ull) | 8ull);
+        if ((uint64_t)k + lim > avail_all) lim = (uint32_t)(avail_all > k ? avail_all - k : 0);
+        return lim;
+    };
+    // ---- Han rune starts of this lane's 16 bytes -> wave queue --------------------
+    uint32_t hs = 0;
+    {
+        const uint32_t k0 = 16u * lane;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint32_t x = lds4(tx, k0 + k);
+            if ((x & 0xFFu) >= 0xE2u) {
+                bool ds;
+                const uint32_t lim = lim_at(k0 + k, &ds);
+                uint32_t w;
+                if (han_rune(x, lim, &w)) hs |= 1u << k;
+            }
+        }
+        if (avail_all < k0 + 16u) hs &= avail_all > k0 ? (1u << (uint32_t)(avail_all - k0)) - 1u : 0u;
+    }
+    const uint32_t cnt = __popc(hs);
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += y;
+    }
+    const uint32_t nq = __shfl(incl, 63, 64);
+    {
+        uint32_t o = incl - cnt, m = hs;
+        while (m) {
+            queue[o++] = (uint16_t)(16u * lane + (uint32_t)__builtin_ctz(m));
+            m &= m - 1u;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- walks -------------------------------------------------------------------------
+    bool act = false;
+    uint32_t q = 0, id = 0, qq = 0, len = 0, emk = 0, w01 = 0, w23 = 0, ne = 0;
+    auto edge = [&](uint32_t L, uint32_t wi) {
+        if (L > 31u || ne >= 4u) {
+            emk |= JB_EDGE_OVF;
+            return;
+        }
+        emk |= 1u << (L - 1u);
+        if (ne == 0u) w01 = wi;
+        else if (ne == 1u) w01 |= wi << 16;
+        else if (ne == 2u) w23 = wi;
+        else w23 |= wi << 16;
+        ne++;
+    };
+    auto finish = [&]() {
+        const uint32_t sl = (uint32_t)((base + q) / 3u);
+        emask[sl] = emk;
+        ewidx[sl] = make_uint2(w01, w23);
+        act = false;
+    };
+    uint32_t head = 0;
+    for (;;) {
+        const bool stepping = act;
+        // refill idle lanes from the queue
+        const uint64_t need = __ballot(!act);
+        const uint32_t rank =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+        const bool fresh = !act && head + rank < nq;
+        uint32_t rec = 0, r0 = 0, w0 = 0, row = 0;
+        if (fresh) {
+            q = queue[head + rank];
+            const uint32_t x = lds4(tx, q);
+            w0 = (x & 0xFFu) < 0xF0u ? 3u : 4u;
+            r0 = w0 == 3u ? ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu)
+                          : ((x & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) | (((x >> 16) & 0x3Fu) << 6) |
+                                ((x >> 24) & 0x3Fu);
+            row = jb_row(im.pagemap, r0);
+            rec = (ablate & 2u) ? jb_l1_make(JB_FC_ABSENT, 0u, 0u) : im.l1[row];
+        }
+        head = min(nq, head + (uint32_t)__popcll(need));
+        // one probe step for the walks already under way
+        uint32_t r = 0, wr = 0, h = 0;
+        uint64_t nd = JB_NODE_EMPTY;
+        bool go = false;
+        if (stepping) {
+            bool ds = false;
+            uint32_t x, lim;
+            if (qq + 4u <= kWalkWin) {
+                x = lds4(tx, qq);
+                lim = lim_at(qq, &ds);
+            } else {  // beyond the staged look-ahead (long keys): global text and bits
+                const uint64_t p = base + qq;
+                const uint64_t wi = p >> 5;
+                const uint32_t sh = (uint32_t)p & 31u;
+                const uint64_t v = ((((uint64_t)docbits[wi + 1]) << 32) | docbits[wi]) >> sh;
+                ds = (v & 1ull) != 0;
+                lim = 1u + (uint32_t)__builtin_ctzll(((v >> 1) & 7ull) | 8ull);
+                if (p + lim > nbytes) lim = p < nbytes ? (uint32_t)(nbytes - p) : 0u;
+                x = ld4(text, p);
+            }
+            r = ds ? 0u : han_rune(x, lim, &wr);
+            if (r) {
+                h = jb_hash(id, r) & im.mask;
+                nd = im.nodes[h];
+                go = true;
+            } else {
+                finish();
+            }
+        }
+        if (fresh) {
+            len = 1u;
+            emk = w01 = w23 = ne = 0u;
+            const uint32_t fc = rec & 3u;
+            if (fc == JB_FC_ABSENT || fc == JB_FC_ZERO) {
+                edge(1u, rec >> 3);  // the single edge only (:468-471)
+                finish();
+            } else {
+                if (fc == JB_FC_POS) edge(1u, rec >> 3);
+                id = row;
+                qq = q + w0;
+                act = ((rec >> 2) & 1u) != 0u && !(ablate & 1u);
+                if (!act) finish();
+            }
+        }
+        if (go) {
+            while (nd != JB_NODE_EMPTY && !jb_node_is(nd, id, r)) {
+                h = (h + 1u) & im.mask;
+                nd = im.nodes[h];
+            }
+            if (nd == JB_NODE_EMPTY) {
+                finish();  // (:475-478)
+            } else {
+                len++;
+                qq += wr;
+                if (jb_node_fc(nd) == JB_FC_POS) edge(len, jb_node_widx(nd));
+                id = im.nrows + h;
+                if (!jb_node_hc(nd) || (emk & JB_EDGE_OVF)) finish();
+            }
+        }
+        if (!__any(act) && head >= nq) break;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_zh: one lane per Han block (cutZh, tokenizer.go:221-255).
+//
+// Backward over the block's runes (calcDagProba, :502-548): each rune's edges
+// (i, i+L), ascending in L as the DAG lists them, fold into maxIndexProba's
+// running state (:565-578) with pieceProba = w + best(i+L) (:519-529); best(n)
+// is the {n, 0.0} sentinel (:522-525).  best(j) for the next R-1 runes lives
+// in an LDS ring (R > longest key).  The chosen length goes to gbl[slot]; the
+// forward walk (findDagPath, :552-562) then emits pieces or, with HMM, gathers
+// runs of single-rune pieces for the Viterbi (:228-253).
+// ---------------------------------------------------------------------------
 __device__ __forceinline__ void load_emit(const DevImage& im, uint32_t r, double e[4]) {
     const double2* p = reinterpret_cast<const double2*>(im.emit) + (size_t)jb_row(im.pagemap, r) * 2u;
     const double2 a = p[0], b = p[1];
@@ -329,60 +537,8 @@ __device__ __forceinline__ void route2(double a, double b, uint32_t* code, doubl
     *p = best;
 }
 
-struct LdsEmitter {  // token bits accumulated per word, OR-ed into the LDS bitmap
-    uint32_t* ls;
-    uint32_t* le;
-    uint32_t w0, word, s, e;
-    __device__ __forceinline__ void flush() {
-        if (s) atomicOr(ls + (word - w0), s);
-        if (e) atomicOr(le + (word - w0), e);
-        s = e = 0;
-    }
-    __device__ __forceinline__ void at(uint32_t pos) {
-        const uint32_t w = pos >> 5;
-        if (w != word) {
-            flush();
-            word = w;
-        }
-    }
-    __device__ __forceinline__ void token(uint32_t a, uint32_t b) {
-        at(a);
-        s |= 1u << (a & 31u);
-        at(b - 1u);
-        e |= 1u << ((b - 1u) & 31u);
-    }
-};
-
-struct LdsView {
-    const uint8_t* tx;  // tx[k] = text[wb + k]
-    double* best;
-    uint8_t* bl;
-    uint32_t wb;
-    LdsEmitter em;
-    __device__ __forceinline__ uint32_t byte(uint32_t q) const { return tx[q - wb]; }
-    __device__ __forceinline__ uint32_t load4(uint32_t q) const {
-        const uint32_t k = q - wb;
-        const uint32_t* a = reinterpret_cast<const uint32_t*>(tx + (k & ~3u));
-        return __builtin_amdgcn_alignbyte(a[1], a[0], k & 3u);
-    }
-    __device__ __forceinline__ uint32_t slot(uint32_t q) const { return (q - wb) / 3u; }
-    __device__ __forceinline__ void token(uint32_t a, uint32_t b) { em.token(a, b); }
-};
-
-struct GlobalView {
-    const uint8_t* text;
-    double* best;  // index q / 3
-    uint8_t* bl;
-    Emitter em;
-    __device__ __forceinline__ uint32_t byte(uint32_t q) const { return text[q]; }
-    __device__ __forceinline__ uint32_t load4(uint32_t q) const { return ld4(text, q); }
-    __device__ __forceinline__ uint32_t slot(uint32_t q) const { return q / 3u; }
-    __device__ __forceinline__ void token(uint32_t a, uint32_t b) { em.token(a, b); }
-};
-
-template <class V>
-__device__ __forceinline__ uint32_t v_han(const V& v, uint32_t q, uint32_t* w) {
-    const uint32_t x = v.load4(q);
+__device__ __forceinline__ uint32_t han_dec(const uint8_t* __restrict__ t, uint32_t q, uint32_t* w) {
+    const uint32_t x = ld4(t, q);
     const uint32_t b0 = x & 0xFFu;
     if (b0 < 0xF0u) {
         *w = 3;
@@ -391,33 +547,34 @@ __device__ __forceinline__ uint32_t v_han(const V& v, uint32_t q, uint32_t* w) {
     *w = 4;
     return ((b0 & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) | (((x >> 16) & 0x3Fu) << 6) | ((x >> 24) & 0x3Fu);
 }
-template <class V>
-__device__ __forceinline__ uint32_t v_width(const V& v, uint32_t q) { return v.byte(q) < 0xF0u ? 3u : 4u; }
-template <class V>
-__device__ __forceinline__ uint32_t v_prev(const V& v, uint32_t q, uint32_t lo) {  // rune ending at q
+__device__ __forceinline__ uint32_t han_w(const uint8_t* __restrict__ t, uint32_t q) { return t[q] < 0xF0u ? 3u : 4u; }
+// start of the Han rune that ends at q (runes in [lo, q) are Han)
+__device__ __forceinline__ uint32_t han_prev(const uint8_t* __restrict__ t, uint32_t q, uint32_t lo) {
     if (q - lo < 4u) return lo;
-    return (v.byte(q - 3u) & 0xF0u) == 0xE0u ? q - 3u : q - 4u;
+    return (t[q - 3u] & 0xF0u) == 0xE0u ? q - 3u : q - 4u;
 }
 
 // viterbi (tokenizer.go:668-730) over the m runes [rs, re) + cutHMM (:273-285).
-// Back-pointers (2 bits per state) go to each rune's slot; the traceback stops
-// at the first "" route: the reference's path then restarts at that step
-// (fullPath[""] is nil, :715) and cutHMM labels runes from the run's start.
-template <class V>
-__device__ void viterbi_run(V& v, const DevImage& im, uint32_t rs, uint32_t re, uint32_t m) {
+// Back-pointers (2 bits per state) go to each rune's gbl slot; the traceback
+// stops at the first "" route: the reference's path then restarts at that
+// step (fullPath[""] is nil, :715) and cutHMM labels runes from the run start.
+__device__ void viterbi_run(const uint8_t* __restrict__ text, uint8_t* __restrict__ bl, const DevImage& im,
+                            uint32_t rs, uint32_t re, uint32_t m, Emitter& em) {
     if (m == 1) {  // always "S" for a single rune (:672-674)
-        v.token(rs, re);
+        em.token(rs, re);
         return;
     }
     uint32_t w;
-    double e[4];
-    uint32_t r = v_han(v, rs, &w);
+    double e[4], en[4];
+    uint32_t r = han_dec(text, rs, &w);
     load_emit(im, r, e);
     double vB = START_B + e[0], vM = JB_MIN_FLOAT + e[1], vE = JB_MIN_FLOAT + e[2], vS = START_S + e[3];
     uint32_t q = rs + w;
+    if (q < re) load_emit(im, han_dec(text, q, &w), e);
     while (q < re) {
-        r = v_han(v, q, &w);
-        load_emit(im, r, e);
+        const uint32_t qn = q + w;
+        uint32_t wn = 0;
+        if (qn < re) load_emit(im, han_dec(text, qn, &wn), en);  // next rune's emissions, in flight
         uint32_t cB, cM, cE, cS;
         double pB, pM, pE, pS;
         route2(vE + T_EB, vS + T_SB, &cB, &pB);  // B <- E, S
@@ -428,201 +585,169 @@ __device__ void viterbi_run(V& v, const DevImage& im, uint32_t rs, uint32_t re, 
         vM = pM + e[1];
         vE = pE + e[2];
         vS = pS + e[3];
-        v.bl[v.slot(q)] = (uint8_t)(cB | (cM << 2) | (cE << 4) | (cS << 6));
-        q += w;
+        bl[q / 3u] = (uint8_t)(cB | (cM << 2) | (cE << 4) | (cS << 6));
+        q = qn;
+        w = wn;
+        e[0] = en[0]; e[1] = en[1]; e[2] = en[2]; e[3] = en[3];
     }
     uint32_t st = vE > vS ? (uint32_t)JB_E : (uint32_t)JB_S;  // (:723-729)
     uint32_t t = m - 1, reset = 0;
-    uint32_t qt = v_prev(v, re, rs);
+    uint32_t qt = han_prev(text, re, rs);
     for (;;) {
-        const uint32_t sl = v.slot(qt);
+        const uint32_t sl = qt / 3u;
         if (t == 0) {
-            v.bl[sl] = (uint8_t)st;
+            bl[sl] = (uint8_t)st;
             break;
         }
-        const uint32_t code = (v.bl[sl] >> (2u * st)) & 3u;
-        v.bl[sl] = (uint8_t)st;
+        const uint32_t code = (bl[sl] >> (2u * st)) & 3u;
+        bl[sl] = (uint8_t)st;
         if (code == 2u) {
             reset = t;
             break;
         }
         st = (st == JB_B || st == JB_S) ? 2u + code : code;  // B,S <- {E,S}; M,E <- {B,M}
         --t;
-        qt = v_prev(v, qt, rs);
+        qt = han_prev(text, qt, rs);
     }
     uint32_t qa = rs, qb = qt, ts = rs;
     for (uint32_t k = 0; k < m - reset; k++) {
-        const uint32_t lab = v.bl[v.slot(qb)];
-        qa += v_width(v, qa);
-        qb += v_width(v, qb);
+        const uint32_t lab = bl[qb / 3u];
+        qa += han_w(text, qa);
+        qb += han_w(text, qb);
         if (lab >= (uint32_t)JB_E) {
-            v.token(ts, qa);
+            em.token(ts, qa);
             ts = qa;
         }
     }
 }
 
-// One Han block [bs, be). Returns false when the reference would panic
-// (a position with no DAG edge on the chosen path: cutDAG slices with -1).
-template <bool HMM, class V>
-__device__ bool process_block(V& v, const DevImage& im, uint32_t bs, uint32_t be) {
-    // ---- backward DP ----------------------------------------------------------
-    uint32_t q = be;
-    while (q > bs) {
-        q = v_prev(v, q, bs);
-        uint32_t w0;
-        const uint32_t r0 = v_han(v, q, &w0);
-        double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT;
-        uint32_t bestL = 0, lastL = 0;
-        auto edge = [&](uint32_t len, uint32_t end, double wt) {
-            const double nb = end == be ? 0.0 : v.best[v.slot(end)];
-            const double pp = wt + nb;
-            if (pp >= prevP) {
-                bestL = len;
-                bestP = pp;
-            }
-            prevP = pp;
-            lastL = len;
-        };
-        const jb_l1 l1 = im.l1[jb_row(im.pagemap, r0)];
-        if (l1.fc == JB_FC_ABSENT || l1.fc == JB_FC_ZERO) {
-            // absent or count 0: the single edge only (:468-471); w is -Log(size) or -Inf (:515-519)
-            edge(1, q + w0, l1.w);
-        } else {
-            if (l1.fc == JB_FC_POS) edge(1, q + w0, l1.w);
-            uint32_t id = l1.id, qq = q + w0, len = 1;
-            while (qq < be) {
-                uint32_t wr;
-                const uint32_t r = v_han(v, qq, &wr);
-                jb_node m;
-                const uint32_t id2 = child(im.nodes, im.mask, id, r, &m);
-                if (id2 == JB_EMPTY) break;  // (:475-478)
-                ++len;
-                qq += wr;
-                if ((m.rune_fc >> JB_FC_SHIFT) == JB_FC_POS) edge(len, qq, m.w);  // (:479-481)
-                id = id2;
-            }
-        }
-        if (bestL == 0) {  // no item qualified: the last item (or {-1, minFloat})
-            bestL = lastL;
-            bestP = prevP;
-        }
-        const uint32_t sl = v.slot(q);
-        v.best[sl] = bestP;
-        v.bl[sl] = (uint8_t)bestL;
-    }
-    // ---- forward walk (findDagPath) + HMM runs ------------------------------------
-    uint32_t p = bs, run_s = 0, run_n = 0;
-    while (p < be) {
-        const uint32_t L = v.bl[v.slot(p)];
-        if (L == 0) return false;
-        uint32_t pe = p;
-        for (uint32_t k = 0; k < L; k++) pe += v_width(v, pe);
-        if (!HMM) {
-            v.token(p, pe);
-        } else if (L == 1) {
-            if (run_n == 0) run_s = p;
-            run_n++;
-        } else {
-            if (run_n) {
-                viterbi_run(v, im, run_s, p, run_n);
-                run_n = 0;
-            }
-            v.token(p, pe);
-        }
-        p = pe;
-    }
-    if (HMM && run_n) viterbi_run(v, im, run_s, be, run_n);
-    return true;
-}
-
-// k_zh: workgroups pull 256 consecutive Han blocks at a time from a global
-// counter, stage the text window that holds them in LDS (coalesced 16-byte
-// loads), run one block per lane out of LDS, and OR the window's token bits
-// into the global bitmaps.  Blocks too long for a window go to k_zh_long.
-template <bool HMM>
+template <bool HMM, uint32_t R>
 __global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, const uint32_t* __restrict__ blk,
-                                            const uint32_t* __restrict__ lists, uint32_t* __restrict__ counters,
-                                            DevImage im, uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
-                                            uint32_t* __restrict__ longq) {
-    __shared__ __attribute__((aligned(16))) uint8_t tx[kWin + 16];
-    __shared__ double best[kWin / 3 + 2];
-    __shared__ uint8_t bl[kWin / 3 + 2];
-    __shared__ uint32_t ls[kWin / 32 + 2], le[kWin / 32 + 2];
-    __shared__ uint32_t sh[4];
-    const uint32_t tid = threadIdx.x;
+                                            const uint32_t* __restrict__ order, uint32_t* __restrict__ counters,
+                                            DevImage im, const uint32_t* __restrict__ emask,
+                                            const uint2* __restrict__ ewidx, uint8_t* __restrict__ bl,
+                                            uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
+                                            uint32_t ablate) {
+    extern __shared__ double ring[];
+    const uint32_t bd = blockDim.x;
+    double* my = ring + threadIdx.x;
     const uint32_t nzh = counters[CNT_NZH];
+    const uint32_t lane = threadIdx.x & 63u;
+    Emitter em(sbits, ebits);
+    // Waves pull 64 consecutive blocks at a time: neighbouring lanes work on
+    // neighbouring text (shared cache lines), and fast waves take more chunks.
     for (;;) {
-        if (tid == 0) sh[0] = atomicAdd(counters + CNT_WORK, 256u);
-        __syncthreads();
-        const uint32_t z0 = sh[0];
-        if (z0 >= nzh) break;
-        const uint32_t z = z0 + tid;
-        bool todo = z < nzh;
-        uint32_t bs = 0, be = 0;
-        if (todo) {
-            const uint32_t g = lists[z];
-            bs = blk[g] & 0x7FFFFFFFu;
-            be = blk[g + 1] & 0x7FFFFFFFu;
-            if (be - bs > kWin - 32u) {
-                longq[atomicAdd(counters + CNT_NLONG, 1u)] = z;
-                todo = false;
-            }
-        }
-        for (;;) {  // sub-rounds: the blocks whose bytes fit one window
-            if (tid == 0) {
-                sh[1] = 0xFFFFFFFFu;
-                sh[2] = 0u;
-            }
-            __syncthreads();
-            if (todo) atomicMin(&sh[1], bs);
-            __syncthreads();
-            const uint32_t first = sh[1];
-            if (first == 0xFFFFFFFFu) break;
-            const uint32_t wb = first & ~15u;
-            const bool mine = todo && be - wb <= kWin;
-            if (mine) atomicMax(&sh[2], be);
-            __syncthreads();
-            const uint32_t wend = sh[2];
-            const uint32_t nld = (wend - wb + 8u + 15u) >> 4;
-            for (uint32_t k = tid; k < nld; k += 256u)
-                reinterpret_cast<uint4*>(tx)[k] = reinterpret_cast<const uint4*>(text + wb)[k];
-            const uint32_t w0 = wb >> 5, nw = ((wend - 1u) >> 5) - w0 + 1u;
-            for (uint32_t k = tid; k < nw; k += 256u) ls[k] = le[k] = 0u;
-            __syncthreads();
-            if (mine) {
-                LdsView v{tx, best, bl, wb, LdsEmitter{ls, le, w0, 0xFFFFFFFFu, 0u, 0u}};
-                if (!process_block<HMM>(v, im, bs, be)) atomicOr(counters + CNT_ERR, 1u);
-                v.em.flush();
-                todo = false;
-            }
-            __syncthreads();
-            for (uint32_t k = tid; k < nw; k += 256u) {
-                const uint32_t a = ls[k], b = le[k];
-                if (a) atomicOr(sbits + w0 + k, a);
-                if (b) atomicOr(ebits + w0 + k, b);
-            }
-            __syncthreads();
-        }
-    }
-}
-
-// k_zh_long: one lane per block longer than a window, text from HBM,
-// per-rune slots in global scratch (index q / 3).
-template <bool HMM>
-__global__ __launch_bounds__(64) void k_zh_long(const uint8_t* __restrict__ text, const uint32_t* __restrict__ blk,
-                                                const uint32_t* __restrict__ lists, uint32_t* __restrict__ counters,
-                                                DevImage im, const uint32_t* __restrict__ longq, double* gbest,
-                                                uint8_t* gbl, uint32_t* __restrict__ sbits,
-                                                uint32_t* __restrict__ ebits) {
-    const uint32_t n = counters[CNT_NLONG];
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t g = lists[longq[i]];
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(counters + CNT_WORK, 64u);
+        base = __shfl(base, 0, 64);
+        if (base >= nzh) break;
+        const uint32_t z = base + lane;
+        if (z >= nzh) continue;
+        const uint32_t g = order[z];
         const uint32_t bs = blk[g] & 0x7FFFFFFFu, be = blk[g + 1] & 0x7FFFFFFFu;
-        GlobalView v{text, gbest, gbl, Emitter(sbits, ebits)};
-        if (!process_block<HMM>(v, im, bs, be)) atomicOr(counters + CNT_ERR, 1u);
-        v.em.flush();
+        // ---- backward DP ------------------------------------------------------
+        uint32_t q = be, c = 0;
+        while (q > bs) {
+            q = han_prev(text, q, bs);
+            ++c;
+            const uint32_t sl = q / 3u;
+            double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT;
+            uint32_t bestL = 0, lastL = 0;
+            auto fold = [&](uint32_t L, double wt) {
+                const double nb = L == c ? 0.0 : my[((c - L) & (R - 1u)) * bd];
+                const double pp = wt + nb;
+                if (pp >= prevP) {
+                    bestL = L;
+                    bestP = pp;
+                }
+                prevP = pp;
+                lastL = L;
+            };
+            uint32_t m = emask[sl];
+            if (!(m & JB_EDGE_OVF)) {
+                const uint2 wi = ewidx[sl];
+                double w4[4];
+                uint32_t L4[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {  // weight loads of all edges first (independent)
+                    L4[k] = m ? (uint32_t)__builtin_ctz(m) + 1u : 0u;
+                    m &= m - 1u;
+                    const uint32_t idx = ((k < 2 ? wi.x : wi.y) >> (16 * (k & 1))) & 0xFFFFu;
+                    w4[k] = L4[k] ? im.wtab[idx] : 0.0;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (L4[k]) fold(L4[k], w4[k]);
+            } else {  // many or long edges: walk this rune here (same rules as k_walk)
+                uint32_t w0;
+                const uint32_t r0 = han_dec(text, q, &w0);
+                const uint32_t row = jb_row(im.pagemap, r0);
+                const uint32_t rec = im.l1[row];
+                const uint32_t fc = rec & 3u;
+                if (fc == JB_FC_ABSENT || fc == JB_FC_ZERO) {
+                    fold(1u, im.wtab[rec >> 3]);
+                } else {
+                    if (fc == JB_FC_POS) fold(1u, im.wtab[rec >> 3]);
+                    uint32_t id = row, qq = q + w0, len = 1;
+                    bool more = ((rec >> 2) & 1u) != 0u;
+                    while (more && qq < be) {
+                        uint32_t wr;
+                        const uint32_t r = han_dec(text, qq, &wr);
+                        uint32_t h = jb_hash(id, r) & im.mask;
+                        uint64_t nd = im.nodes[h];
+                        while (nd != JB_NODE_EMPTY && !jb_node_is(nd, id, r)) {
+                            h = (h + 1u) & im.mask;
+                            nd = im.nodes[h];
+                        }
+                        if (nd == JB_NODE_EMPTY) break;
+                        ++len;
+                        qq += wr;
+                        if (jb_node_fc(nd) == JB_FC_POS) fold(len, im.wtab[jb_node_widx(nd)]);
+                        more = jb_node_hc(nd) != 0u;
+                        id = im.nrows + h;
+                    }
+                }
+            }
+            if (bestL == 0) {  // no item qualified: the last item (or {-1, minFloat})
+                bestL = lastL;
+                bestP = prevP;
+            }
+            my[(c & (R - 1u)) * bd] = bestP;
+            bl[sl] = (uint8_t)bestL;
+        }
+        if (ablate & 4u) continue;  // diagnostic only: DP without the forward walk
+        // ---- forward walk (findDagPath) + HMM runs ------------------------------
+        uint32_t p = bs, run_s = 0, run_n = 0;
+        bool bad = false;
+        while (p < be) {
+            const uint32_t L = bl[p / 3u];
+            if (L == 0) {  // tail index -1: cutDAG's slice panics in the reference
+                bad = true;
+                break;
+            }
+            uint32_t pe = p;
+            for (uint32_t k = 0; k < L; k++) pe += han_w(text, pe);
+            if (!HMM) {
+                em.token(p, pe);
+            } else if (L == 1) {
+                if (run_n == 0) run_s = p;
+                run_n++;
+            } else {
+                if (run_n) {
+                    viterbi_run(text, bl, im, run_s, p, run_n, em);
+                    run_n = 0;
+                }
+                em.token(p, pe);
+            }
+            p = pe;
+        }
+        if (bad) {
+            atomicOr(counters + CNT_ERR, 1u);
+            continue;
+        }
+        if (HMM && run_n) viterbi_run(text, bl, im, run_s, be, run_n, em);
     }
+    em.flush();
 }
 
 // ---------------------------------------------------------------------------
@@ -745,14 +870,64 @@ __global__ void k_doc_tok(const uint64_t* __restrict__ doc_off, uint32_t ndocs, 
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-template <bool HMM>
-static uint32_t occ_zh() {
+uint32_t g_ablate = 0;  // diagnostic ablations (JB_ABLATE); results are wrong when non-zero
+
+uint32_t zh_ring(uint32_t maxlen) {
+    uint32_t r = 8;
+    while (r <= maxlen) r <<= 1;
+    return r <= 256 ? r : 0;
+}
+
+uint32_t zh_threads(uint32_t ring) {
+    uint32_t t = 32768u / (ring * 8u);
+    if (t > 256u) t = 256u;
+    t &= ~63u;
+    return t < 64u ? 64u : t;
+}
+
+template <bool HMM, uint32_t R>
+static uint32_t occ_zh_r() {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_zh<HMM>, 256, 0) != hipSuccess || n <= 0) return 1;
+    const uint32_t wg = zh_threads(R);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_zh<HMM, R>, (int)wg, (size_t)R * wg * 8) != hipSuccess ||
+        n <= 0)
+        return 1;
     return (uint32_t)n;
 }
 
-uint32_t zh_blocks_per_cu(bool hmm) { return hmm ? occ_zh<true>() : occ_zh<false>(); }
+template <bool HMM>
+static uint32_t occ_zh(uint32_t ring) {
+    switch (ring) {
+        case 8: return occ_zh_r<HMM, 8>();
+        case 16: return occ_zh_r<HMM, 16>();
+        case 32: return occ_zh_r<HMM, 32>();
+        case 64: return occ_zh_r<HMM, 64>();
+        case 128: return occ_zh_r<HMM, 128>();
+        default: return occ_zh_r<HMM, 256>();
+    }
+}
+
+uint32_t zh_blocks_per_cu(bool hmm, uint32_t ring) { return hmm ? occ_zh<true>(ring) : occ_zh<false>(ring); }
+
+template <bool HMM, uint32_t R>
+static void launch_zh(uint32_t grid, hipStream_t s, const uint8_t* text, const Work& w, const DevImage& im) {
+    const uint32_t wg = zh_threads(R);
+    hipLaunchKernelGGL((k_zh<HMM, R>), dim3(grid), dim3(wg), (size_t)R * wg * sizeof(double), s, text, w.blk,
+                       w.lists, w.counters, im, w.emask, w.ewidx, w.gbl, w.sbits, w.ebits, g_ablate);
+}
+
+template <bool HMM>
+static void dispatch_zh(uint32_t ring, uint32_t grid, hipStream_t s, const uint8_t* text, const Work& w,
+                        const DevImage& im) {
+    switch (ring) {
+        case 8: launch_zh<HMM, 8>(grid, s, text, w, im); break;
+        case 16: launch_zh<HMM, 16>(grid, s, text, w, im); break;
+        case 32: launch_zh<HMM, 32>(grid, s, text, w, im); break;
+        case 64: launch_zh<HMM, 64>(grid, s, text, w, im); break;
+        case 128: launch_zh<HMM, 128>(grid, s, text, w, im); break;
+        default: launch_zh<HMM, 256>(grid, s, text, w, im); break;
+    }
+}
 
 uint32_t nonzh_blocks_per_cu() {
     int n = 0;
@@ -768,8 +943,8 @@ uint32_t nonzh_blocks_per_cu() {
     } while (0)
 
 hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text, uint64_t nbytes,
-                        const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, uint32_t grid_zh, uint32_t grid_nz,
-                        hipStream_t stream, KernelTimer* timer) {
+                        const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, uint32_t ring, uint32_t grid_zh,
+                        uint32_t grid_nz, hipStream_t stream, KernelTimer* timer) {
     const uint64_t nwords = (nbytes + 31) / 32;
     const uint32_t ntiles = (uint32_t)((nbytes + kTileBytes - 1) / kTileBytes);
     const uint32_t nttiles = (uint32_t)((nwords + kTokTileWords - 1) / kTokTileWords);
@@ -794,18 +969,10 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                                (uint32_t)nbytes));
     JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL((k_blocks<true>), dim3(ntiles), dim3(256), 0, stream, d_text,
                                                 nbytes, w.docbits, nullptr, w.tile_off, w.blk, w.lists, list_cap));
-    if (hmm)
-        JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, w.blk, w.lists,
-                                          w.counters, im, w.sbits, w.ebits, w.longq));
-    else
-        JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, w.blk, w.lists,
-                                          w.counters, im, w.sbits, w.ebits, w.longq));
-    if (hmm)
-        JB_TIMED(K_ZH_LONG, hipLaunchKernelGGL((k_zh_long<true>), dim3(64), dim3(64), 0, stream, d_text, w.blk,
-                                               w.lists, w.counters, im, w.longq, w.gbest, w.gbl, w.sbits, w.ebits));
-    else
-        JB_TIMED(K_ZH_LONG, hipLaunchKernelGGL((k_zh_long<false>), dim3(64), dim3(64), 0, stream, d_text, w.blk,
-                                               w.lists, w.counters, im, w.longq, w.gbest, w.gbl, w.sbits, w.ebits));
+    JB_TIMED(K_WALK, hipLaunchKernelGGL(k_walk, dim3((uint32_t)((nbytes + 4 * 1024 - 1) / (4 * 1024))), dim3(256), 0, stream,
+                                        d_text, nbytes, w.docbits, im, w.emask, w.ewidx, g_ablate));
+    JB_TIMED(K_ZH, hmm ? dispatch_zh<true>(ring, grid_zh, stream, d_text, w, im)
+                       : dispatch_zh<false>(ring, grid_zh, stream, d_text, w, im));
     JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3(grid_nz), dim3(256), 0, stream, d_text, w.blk, w.lists,
                                          list_cap, w.counters, w.sbits, w.ebits));
     JB_TIMED(K_TOK_COUNT, hipLaunchKernelGGL((k_tok<false>), dim3(nttiles), dim3(256), 0, stream, w.sbits, w.ebits,
