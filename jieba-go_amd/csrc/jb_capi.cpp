@@ -261,7 +261,7 @@ static int upload_image(Device* d, const Image& img) {
 static void free_work(Work* w) {
     dfree(w->docbits); dfree(w->sbits); dfree(w->ebits); dfree(w->tile_cnt); dfree(w->tile_off);
     dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->blk); dfree(w->lists); dfree(w->emask); dfree(w->ewidx);
-    dfree(w->gbl);
+    dfree(w->gbl); dfree(w->gbest);
     dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters);
     *w = Work{};
 }
@@ -288,6 +288,7 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.emask, (nb / 3 + 8) * 4));
     HIPCHK(hipMalloc(&w.ewidx, (nb / 3 + 8) * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.gbl, nb / 3 + 8));
+    HIPCHK(hipMalloc(&w.gbest, (nb / 3 + 8) * sizeof(double)));
 
     HIPCHK(hipMalloc(&w.tok_start, (nb + 4) * 4));
     HIPCHK(hipMalloc(&w.tok_end, (nb + 4) * 4));
@@ -320,19 +321,16 @@ static uint32_t grid_zh_override = 0;
 
 static int launch(jb_ctx* ctx, Device* d, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off,
                   uint32_t ndocs, bool hmm, hipStream_t s) {
-    const uint32_t ring = zh_ring(ctx->im->img.maxlen);
-    if (!ring) return fail(JB_ELIMIT, "dictionary word of %u runes (max 255)", ctx->im->img.maxlen);
-    const uint32_t grid_zh = d->ncu * std::max(1u, zh_blocks_per_cu(hmm, ring));
+    const uint32_t grid_zh = d->ncu * std::max(1u, zh_blocks_per_cu(hmm));
     const uint32_t grid_nz = d->ncu * std::max(1u, std::min(4u, nonzh_blocks_per_cu()));
     static const bool dbg = getenv("JB_DEBUG") != nullptr;
     if (const char* a = getenv("JB_ABLATE")) g_ablate = (uint32_t)atoi(a);
     if (const char* gz = getenv("JB_GRID_ZH")) grid_zh_override = (uint32_t)atoi(gz);
     const uint32_t gzh = grid_zh_override ? grid_zh_override : grid_zh;
     if (dbg)
-        fprintf(stderr, "[jb] nbytes=%llu ndocs=%u ring=%u zh_threads=%u grid_zh=%u (occ %u/CU) grid_nz=%u ablate=%u\n",
-                (unsigned long long)nbytes, ndocs, ring, zh_threads(ring), gzh, zh_blocks_per_cu(hmm, ring), grid_nz,
-                g_ablate);
-    const hipError_t e = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, ring, gzh, grid_nz, s,
+        fprintf(stderr, "[jb] nbytes=%llu ndocs=%u grid_zh=%u (occ %u/CU) grid_nz=%u ablate=%u\n",
+                (unsigned long long)nbytes, ndocs, gzh, zh_blocks_per_cu(hmm), grid_nz, g_ablate);
+    const hipError_t e = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, gzh, grid_nz, s,
                                       d->profile ? &d->timer : nullptr);
     if (e != hipSuccess) return fail(JB_EDEVICE, "pipeline launch: %s", hipGetErrorString(e));
     return JB_OK;

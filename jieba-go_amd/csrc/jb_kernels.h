@@ -46,6 +46,7 @@ struct Work {
     uint32_t* emask;       // per Han rune (slot = byte / 3): bit L-1 = DAG edge of L runes; bit 31 overflow
     uint2* ewidx;          // per Han rune: weight indices of its first 4 edges (u16 each)
     uint8_t* gbl;          // per Han rune: chosen piece length, then Viterbi back-pointers / labels
+    double* gbest;         // per Han rune: best proba (index be/3 - c inside each block)
     uint32_t* tok_start;
     uint32_t* tok_end;
     uint64_t* doc_tok;
@@ -72,14 +73,11 @@ struct KernelTimer {
 // launch error.  grid_zh / grid_nz: persistent grids of k_zh / k_nonzh.
 // d_text must be readable 64 bytes past nbytes.
 hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text, uint64_t nbytes,
-                        const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, uint32_t ring, uint32_t grid_zh,
-                        uint32_t grid_nz, hipStream_t stream, KernelTimer* timer);
+                        const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, uint32_t grid_zh, uint32_t grid_nz,
+                        hipStream_t stream, KernelTimer* timer);
 
-// k_zh's best-proba ring: a power of two > the longest reachable key (runes),
-// LDS ring * threads * 8 bytes <= 32 KiB.  0 if the key is too long.
-uint32_t zh_ring(uint32_t maxlen);
-uint32_t zh_threads(uint32_t ring);
-uint32_t zh_blocks_per_cu(bool hmm, uint32_t ring);
+// Resident k_zh workgroups per CU (occupancy API).
+uint32_t zh_blocks_per_cu(bool hmm);
 extern uint32_t g_ablate;  // diagnostic ablations from JB_ABLATE (results are wrong when non-zero)
 uint32_t nonzh_blocks_per_cu();
 

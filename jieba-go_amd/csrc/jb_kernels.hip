@@ -512,14 +512,58 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ text, 
 // ---------------------------------------------------------------------------
 // k_zh: one lane per Han block (cutZh, tokenizer.go:221-255).
 //
-// Backward over the block's runes (calcDagProba, :502-548): each rune's edges
-// (i, i+L), ascending in L as the DAG lists them, fold into maxIndexProba's
-// running state (:565-578) with pieceProba = w + best(i+L) (:519-529); best(n)
-// is the {n, 0.0} sentinel (:522-525).  best(j) for the next R-1 runes lives
-// in an LDS ring (R > longest key).  The chosen length goes to gbl[slot]; the
-// forward walk (findDagPath, :552-562) then emits pieces or, with HMM, gathers
-// runs of single-rune pieces for the Viterbi (:228-253).
+// Waves pull 64 consecutive blocks at a time (one per lane; fast waves take
+// more) and stage the text span that holds them in LDS, so rune stepping,
+// decoding and the per-rune scratch run out of LDS.  Per block, backward over
+// its runes (calcDagProba, :502-548): the rune's edges (i, i+L) from k_walk,
+// ascending in L as the DAG lists them, fold into maxIndexProba's running
+// state (:565-578) with pieceProba = w + best(i+L) (:519-529); best(n) is the
+// {n, 0.0} sentinel (:522-525).  best(i+L) for L < 8 comes from an 8-entry
+// LDS ring, longer edges read gbest (every rune's best is also stored there,
+// at index be/3 - c, which stays inside the block's slot range).  The chosen
+// piece length goes to the rune's slot; the forward walk (findDagPath,
+// :552-562) then emits pieces or, with HMM, gathers runs of single-rune pieces
+// for the Viterbi (:228-253).  Blocks that do not fit the staged span run the
+// same code on global memory.
 // ---------------------------------------------------------------------------
+constexpr uint32_t kZhCap = 2560;  // staged text bytes per wave
+constexpr uint32_t kZhRing = 8;    // LDS best ring per lane (runes)
+
+struct LdsZv {  // text and slots of the wave's staged span
+    const uint8_t* tx;
+    uint8_t* bls;
+    uint32_t wb;
+    __device__ __forceinline__ uint32_t b(uint32_t q) const { return tx[q - wb]; }
+    __device__ __forceinline__ uint32_t x4(uint32_t q) const { return lds4(tx, q - wb); }
+    __device__ __forceinline__ uint8_t& bl(uint32_t q) const { return bls[(q - wb) / 3u]; }
+};
+struct GlbZv {  // the same, straight from HBM
+    const uint8_t* text;
+    uint8_t* gbl;
+    __device__ __forceinline__ uint32_t b(uint32_t q) const { return text[q]; }
+    __device__ __forceinline__ uint32_t x4(uint32_t q) const { return ld4(text, q); }
+    __device__ __forceinline__ uint8_t& bl(uint32_t q) const { return gbl[q / 3u]; }
+};
+
+template <class V>
+__device__ __forceinline__ uint32_t z_dec(const V& v, uint32_t q, uint32_t* w) {  // Han rune at q
+    const uint32_t x = v.x4(q);
+    const uint32_t b0 = x & 0xFFu;
+    if (b0 < 0xF0u) {
+        *w = 3;
+        return ((b0 & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
+    }
+    *w = 4;
+    return ((b0 & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) | (((x >> 16) & 0x3Fu) << 6) | ((x >> 24) & 0x3Fu);
+}
+template <class V>
+__device__ __forceinline__ uint32_t z_w(const V& v, uint32_t q) { return v.b(q) < 0xF0u ? 3u : 4u; }
+template <class V>
+__device__ __forceinline__ uint32_t z_prev(const V& v, uint32_t q, uint32_t lo) {  // rune that ends at q
+    if (q - lo < 4u) return lo;
+    return (v.b(q - 3u) & 0xF0u) == 0xE0u ? q - 3u : q - 4u;
+}
+
 __device__ __forceinline__ void load_emit(const DevImage& im, uint32_t r, double e[4]) {
     const double2* p = reinterpret_cast<const double2*>(im.emit) + (size_t)jb_row(im.pagemap, r) * 2u;
     const double2 a = p[0], b = p[1];
@@ -537,44 +581,27 @@ __device__ __forceinline__ void route2(double a, double b, uint32_t* code, doubl
     *p = best;
 }
 
-__device__ __forceinline__ uint32_t han_dec(const uint8_t* __restrict__ t, uint32_t q, uint32_t* w) {
-    const uint32_t x = ld4(t, q);
-    const uint32_t b0 = x & 0xFFu;
-    if (b0 < 0xF0u) {
-        *w = 3;
-        return ((b0 & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
-    }
-    *w = 4;
-    return ((b0 & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) | (((x >> 16) & 0x3Fu) << 6) | ((x >> 24) & 0x3Fu);
-}
-__device__ __forceinline__ uint32_t han_w(const uint8_t* __restrict__ t, uint32_t q) { return t[q] < 0xF0u ? 3u : 4u; }
-// start of the Han rune that ends at q (runes in [lo, q) are Han)
-__device__ __forceinline__ uint32_t han_prev(const uint8_t* __restrict__ t, uint32_t q, uint32_t lo) {
-    if (q - lo < 4u) return lo;
-    return (t[q - 3u] & 0xF0u) == 0xE0u ? q - 3u : q - 4u;
-}
-
 // viterbi (tokenizer.go:668-730) over the m runes [rs, re) + cutHMM (:273-285).
-// Back-pointers (2 bits per state) go to each rune's gbl slot; the traceback
+// Back-pointers (2 bits per state) go to each rune's slot; the traceback
 // stops at the first "" route: the reference's path then restarts at that
 // step (fullPath[""] is nil, :715) and cutHMM labels runes from the run start.
-__device__ void viterbi_run(const uint8_t* __restrict__ text, uint8_t* __restrict__ bl, const DevImage& im,
-                            uint32_t rs, uint32_t re, uint32_t m, Emitter& em) {
+template <class V>
+__device__ void viterbi_run(const V& v, const DevImage& im, uint32_t rs, uint32_t re, uint32_t m, Emitter& em) {
     if (m == 1) {  // always "S" for a single rune (:672-674)
         em.token(rs, re);
         return;
     }
     uint32_t w;
     double e[4], en[4];
-    uint32_t r = han_dec(text, rs, &w);
+    uint32_t r = z_dec(v, rs, &w);
     load_emit(im, r, e);
     double vB = START_B + e[0], vM = JB_MIN_FLOAT + e[1], vE = JB_MIN_FLOAT + e[2], vS = START_S + e[3];
     uint32_t q = rs + w;
-    if (q < re) load_emit(im, han_dec(text, q, &w), e);
+    if (q < re) load_emit(im, z_dec(v, q, &w), e);
     while (q < re) {
         const uint32_t qn = q + w;
         uint32_t wn = 0;
-        if (qn < re) load_emit(im, han_dec(text, qn, &wn), en);  // next rune's emissions, in flight
+        if (qn < re) load_emit(im, z_dec(v, qn, &wn), en);  // next rune's emissions, in flight
         uint32_t cB, cM, cE, cS;
         double pB, pM, pE, pS;
         route2(vE + T_EB, vS + T_SB, &cB, &pB);  // B <- E, S
@@ -585,35 +612,34 @@ __device__ void viterbi_run(const uint8_t* __restrict__ text, uint8_t* __restric
         vM = pM + e[1];
         vE = pE + e[2];
         vS = pS + e[3];
-        bl[q / 3u] = (uint8_t)(cB | (cM << 2) | (cE << 4) | (cS << 6));
+        v.bl(q) = (uint8_t)(cB | (cM << 2) | (cE << 4) | (cS << 6));
         q = qn;
         w = wn;
         e[0] = en[0]; e[1] = en[1]; e[2] = en[2]; e[3] = en[3];
     }
     uint32_t st = vE > vS ? (uint32_t)JB_E : (uint32_t)JB_S;  // (:723-729)
     uint32_t t = m - 1, reset = 0;
-    uint32_t qt = han_prev(text, re, rs);
+    uint32_t qt = z_prev(v, re, rs);
     for (;;) {
-        const uint32_t sl = qt / 3u;
         if (t == 0) {
-            bl[sl] = (uint8_t)st;
+            v.bl(qt) = (uint8_t)st;
             break;
         }
-        const uint32_t code = (bl[sl] >> (2u * st)) & 3u;
-        bl[sl] = (uint8_t)st;
+        const uint32_t code = (v.bl(qt) >> (2u * st)) & 3u;
+        v.bl(qt) = (uint8_t)st;
         if (code == 2u) {
             reset = t;
             break;
         }
         st = (st == JB_B || st == JB_S) ? 2u + code : code;  // B,S <- {E,S}; M,E <- {B,M}
         --t;
-        qt = han_prev(text, qt, rs);
+        qt = z_prev(v, qt, rs);
     }
     uint32_t qa = rs, qb = qt, ts = rs;
     for (uint32_t k = 0; k < m - reset; k++) {
-        const uint32_t lab = bl[qb / 3u];
-        qa += han_w(text, qa);
-        qb += han_w(text, qb);
+        const uint32_t lab = v.bl(qb);
+        qa += z_w(v, qa);
+        qb += z_w(v, qb);
         if (lab >= (uint32_t)JB_E) {
             em.token(ts, qa);
             ts = qa;
@@ -621,131 +647,171 @@ __device__ void viterbi_run(const uint8_t* __restrict__ text, uint8_t* __restric
     }
 }
 
-template <bool HMM, uint32_t R>
-__global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, const uint32_t* __restrict__ blk,
-                                            const uint32_t* __restrict__ order, uint32_t* __restrict__ counters,
-                                            DevImage im, const uint32_t* __restrict__ emask,
-                                            const uint2* __restrict__ ewidx, uint8_t* __restrict__ bl,
+// One Han block [bs, be).  Returns false where the reference panics (a rune
+// on the chosen path with no DAG edge: cutDAG slices with tail index -1).
+template <bool HMM, class V>
+__device__ bool zh_block(const V& v, const DevImage& im, const uint32_t* __restrict__ emask,
+                         const uint2* __restrict__ ewidx, double* __restrict__ gbest, double* ring, uint32_t bs,
+                         uint32_t be, Emitter& em, uint32_t ablate) {
+    const uint32_t key0 = be / 3u;
+    uint32_t q = z_prev(v, be, bs), c = 1;
+    uint32_t m = emask[q / 3u];
+    uint2 wi = ewidx[q / 3u];
+    for (;;) {
+        const bool more = q > bs;
+        uint32_t qn = 0, mn = 0;
+        uint2 win = make_uint2(0, 0);
+        if (more) {  // next rune's edge record, in flight while this rune folds
+            qn = z_prev(v, q, bs);
+            mn = emask[qn / 3u];
+            win = ewidx[qn / 3u];
+        }
+        double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT;
+        uint32_t bestL = 0, lastL = 0;
+        auto fold = [&](uint32_t L, double wt) {
+            double nb;
+            if (L == c) nb = 0.0;
+            else if (L < kZhRing) nb = ring[((c - L) & (kZhRing - 1u)) * 64u];
+            else nb = gbest[key0 - (c - L)];
+            const double pp = wt + nb;
+            if (pp >= prevP) {
+                bestL = L;
+                bestP = pp;
+            }
+            prevP = pp;
+            lastL = L;
+        };
+        if (!(m & JB_EDGE_OVF)) {
+            double w4[4];
+            uint32_t L4[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {  // weight loads of all edges first (independent)
+                L4[k] = m ? (uint32_t)__builtin_ctz(m) + 1u : 0u;
+                m &= m - 1u;
+                const uint32_t idx = ((k < 2 ? wi.x : wi.y) >> (16 * (k & 1))) & 0xFFFFu;
+                w4[k] = L4[k] ? im.wtab[idx] : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (L4[k]) fold(L4[k], w4[k]);
+        } else {  // many or long edges: walk this rune here (the rules of k_walk)
+            uint32_t w0;
+            const uint32_t r0 = z_dec(v, q, &w0);
+            const uint32_t row = jb_row(im.pagemap, r0);
+            const uint32_t rec = im.l1[row];
+            const uint32_t fc = rec & 3u;
+            if (fc == JB_FC_ABSENT || fc == JB_FC_ZERO) {
+                fold(1u, im.wtab[rec >> 3]);
+            } else {
+                if (fc == JB_FC_POS) fold(1u, im.wtab[rec >> 3]);
+                uint32_t id = row, qq = q + w0, len = 1;
+                bool go = ((rec >> 2) & 1u) != 0u;
+                while (go && qq < be) {
+                    uint32_t wr;
+                    const uint32_t r = z_dec(v, qq, &wr);
+                    uint32_t h = jb_hash(id, r) & im.mask;
+                    uint64_t nd = im.nodes[h];
+                    while (nd != JB_NODE_EMPTY && !jb_node_is(nd, id, r)) {
+                        h = (h + 1u) & im.mask;
+                        nd = im.nodes[h];
+                    }
+                    if (nd == JB_NODE_EMPTY) break;
+                    ++len;
+                    qq += wr;
+                    if (jb_node_fc(nd) == JB_FC_POS) fold(len, im.wtab[jb_node_widx(nd)]);
+                    go = jb_node_hc(nd) != 0u;
+                    id = im.nrows + h;
+                }
+            }
+        }
+        if (bestL == 0) {  // no item qualified: the last item (or {-1, minFloat})
+            bestL = lastL;
+            bestP = prevP;
+        }
+        ring[(c & (kZhRing - 1u)) * 64u] = bestP;
+        gbest[key0 - c] = bestP;
+        v.bl(q) = (uint8_t)bestL;
+        if (!more) break;
+        q = qn;
+        m = mn;
+        wi = win;
+        ++c;
+    }
+    if (ablate & 4u) return true;  // diagnostic only: DP without the forward walk
+    // ---- forward walk (findDagPath) + HMM runs ---------------------------------------
+    uint32_t p = bs, run_s = 0, run_n = 0;
+    while (p < be) {
+        const uint32_t L = v.bl(p);
+        if (L == 0) return false;  // tail index -1: cutDAG's slice panics in the reference
+        uint32_t pe = p;
+        for (uint32_t k = 0; k < L; k++) pe += z_w(v, pe);
+        if (!HMM) {
+            em.token(p, pe);
+        } else if (L == 1) {
+            if (run_n == 0) run_s = p;
+            run_n++;
+        } else {
+            if (run_n) {
+                viterbi_run(v, im, run_s, p, run_n, em);
+                run_n = 0;
+            }
+            em.token(p, pe);
+        }
+        p = pe;
+    }
+    if (HMM && run_n) viterbi_run(v, im, run_s, be, run_n, em);
+    return true;
+}
+
+template <bool HMM>
+__global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, uint64_t nbytes,
+                                            const uint32_t* __restrict__ blk, const uint32_t* __restrict__ lists,
+                                            uint32_t* __restrict__ counters, DevImage im,
+                                            const uint32_t* __restrict__ emask, const uint2* __restrict__ ewidx,
+                                            uint8_t* __restrict__ gbl, double* __restrict__ gbest,
                                             uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
                                             uint32_t ablate) {
-    extern __shared__ double ring[];
-    const uint32_t bd = blockDim.x;
-    double* my = ring + threadIdx.x;
+    __shared__ __attribute__((aligned(16))) uint8_t s_tx[4][kZhCap + 32];
+    __shared__ uint8_t s_bl[4][kZhCap / 3 + 4];
+    __shared__ double s_ring[4][kZhRing * 64];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint8_t* tx = s_tx[wv];
+    double* ring = s_ring[wv] + lane;
     const uint32_t nzh = counters[CNT_NZH];
-    const uint32_t lane = threadIdx.x & 63u;
     Emitter em(sbits, ebits);
-    // Waves pull 64 consecutive blocks at a time: neighbouring lanes work on
-    // neighbouring text (shared cache lines), and fast waves take more chunks.
     for (;;) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(counters + CNT_WORK, 64u);
         base = __shfl(base, 0, 64);
         if (base >= nzh) break;
         const uint32_t z = base + lane;
-        if (z >= nzh) continue;
-        const uint32_t g = order[z];
-        const uint32_t bs = blk[g] & 0x7FFFFFFFu, be = blk[g + 1] & 0x7FFFFFFFu;
-        // ---- backward DP ------------------------------------------------------
-        uint32_t q = be, c = 0;
-        while (q > bs) {
-            q = han_prev(text, q, bs);
-            ++c;
-            const uint32_t sl = q / 3u;
-            double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT;
-            uint32_t bestL = 0, lastL = 0;
-            auto fold = [&](uint32_t L, double wt) {
-                const double nb = L == c ? 0.0 : my[((c - L) & (R - 1u)) * bd];
-                const double pp = wt + nb;
-                if (pp >= prevP) {
-                    bestL = L;
-                    bestP = pp;
-                }
-                prevP = pp;
-                lastL = L;
-            };
-            uint32_t m = emask[sl];
-            if (!(m & JB_EDGE_OVF)) {
-                const uint2 wi = ewidx[sl];
-                double w4[4];
-                uint32_t L4[4];
-#pragma unroll
-                for (int k = 0; k < 4; k++) {  // weight loads of all edges first (independent)
-                    L4[k] = m ? (uint32_t)__builtin_ctz(m) + 1u : 0u;
-                    m &= m - 1u;
-                    const uint32_t idx = ((k < 2 ? wi.x : wi.y) >> (16 * (k & 1))) & 0xFFFFu;
-                    w4[k] = L4[k] ? im.wtab[idx] : 0.0;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    if (L4[k]) fold(L4[k], w4[k]);
-            } else {  // many or long edges: walk this rune here (same rules as k_walk)
-                uint32_t w0;
-                const uint32_t r0 = han_dec(text, q, &w0);
-                const uint32_t row = jb_row(im.pagemap, r0);
-                const uint32_t rec = im.l1[row];
-                const uint32_t fc = rec & 3u;
-                if (fc == JB_FC_ABSENT || fc == JB_FC_ZERO) {
-                    fold(1u, im.wtab[rec >> 3]);
-                } else {
-                    if (fc == JB_FC_POS) fold(1u, im.wtab[rec >> 3]);
-                    uint32_t id = row, qq = q + w0, len = 1;
-                    bool more = ((rec >> 2) & 1u) != 0u;
-                    while (more && qq < be) {
-                        uint32_t wr;
-                        const uint32_t r = han_dec(text, qq, &wr);
-                        uint32_t h = jb_hash(id, r) & im.mask;
-                        uint64_t nd = im.nodes[h];
-                        while (nd != JB_NODE_EMPTY && !jb_node_is(nd, id, r)) {
-                            h = (h + 1u) & im.mask;
-                            nd = im.nodes[h];
-                        }
-                        if (nd == JB_NODE_EMPTY) break;
-                        ++len;
-                        qq += wr;
-                        if (jb_node_fc(nd) == JB_FC_POS) fold(len, im.wtab[jb_node_widx(nd)]);
-                        more = jb_node_hc(nd) != 0u;
-                        id = im.nrows + h;
-                    }
-                }
-            }
-            if (bestL == 0) {  // no item qualified: the last item (or {-1, minFloat})
-                bestL = lastL;
-                bestP = prevP;
-            }
-            my[(c & (R - 1u)) * bd] = bestP;
-            bl[sl] = (uint8_t)bestL;
+        const bool valid = z < nzh;
+        uint32_t bs = 0, be = 0;
+        if (valid) {
+            const uint32_t g = lists[z];
+            bs = blk[g] & 0x7FFFFFFFu;
+            be = blk[g + 1] & 0x7FFFFFFFu;
         }
-        if (ablate & 4u) continue;  // diagnostic only: DP without the forward walk
-        // ---- forward walk (findDagPath) + HMM runs ------------------------------
-        uint32_t p = bs, run_s = 0, run_n = 0;
-        bool bad = false;
-        while (p < be) {
-            const uint32_t L = bl[p / 3u];
-            if (L == 0) {  // tail index -1: cutDAG's slice panics in the reference
-                bad = true;
-                break;
-            }
-            uint32_t pe = p;
-            for (uint32_t k = 0; k < L; k++) pe += han_w(text, pe);
-            if (!HMM) {
-                em.token(p, pe);
-            } else if (L == 1) {
-                if (run_n == 0) run_s = p;
-                run_n++;
-            } else {
-                if (run_n) {
-                    viterbi_run(text, bl, im, run_s, p, run_n, em);
-                    run_n = 0;
-                }
-                em.token(p, pe);
-            }
-            p = pe;
+        const uint32_t lastl = min(63u, nzh - 1u - base);
+        const uint32_t first = __shfl(bs, 0, 64), last_be = __shfl(be, lastl, 64);
+        const uint32_t wb = first & ~15u;
+        const uint32_t wend = min(last_be, wb + kZhCap);
+        // stage [wb, wend + 16) (the text buffer is padded 64 bytes past its end)
+        const uint32_t n16 = (wend - wb + 16u + 15u) >> 4;
+        for (uint32_t k = lane; k < n16; k += 64u)
+            reinterpret_cast<uint4*>(tx)[k] = reinterpret_cast<const uint4*>(text + wb)[k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (valid) {
+            bool ok;
+            if (be <= wend) ok = zh_block<HMM>(LdsZv{tx, s_bl[wv], wb}, im, emask, ewidx, gbest, ring, bs, be, em, ablate);
+            else ok = zh_block<HMM>(GlbZv{text, gbl}, im, emask, ewidx, gbest, ring, bs, be, em, ablate);
+            if (!ok) atomicOr(counters + CNT_ERR, 1u);
         }
-        if (bad) {
-            atomicOr(counters + CNT_ERR, 1u);
-            continue;
-        }
-        if (HMM && run_n) viterbi_run(text, bl, im, run_s, be, run_n, em);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     em.flush();
 }
@@ -872,62 +938,14 @@ __global__ void k_doc_tok(const uint64_t* __restrict__ doc_off, uint32_t ndocs, 
 // ---------------------------------------------------------------------------
 uint32_t g_ablate = 0;  // diagnostic ablations (JB_ABLATE); results are wrong when non-zero
 
-uint32_t zh_ring(uint32_t maxlen) {
-    uint32_t r = 8;
-    while (r <= maxlen) r <<= 1;
-    return r <= 256 ? r : 0;
-}
-
-uint32_t zh_threads(uint32_t ring) {
-    uint32_t t = 32768u / (ring * 8u);
-    if (t > 256u) t = 256u;
-    t &= ~63u;
-    return t < 64u ? 64u : t;
-}
-
-template <bool HMM, uint32_t R>
-static uint32_t occ_zh_r() {
+template <bool HMM>
+static uint32_t occ_zh() {
     int n = 0;
-    const uint32_t wg = zh_threads(R);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_zh<HMM, R>, (int)wg, (size_t)R * wg * 8) != hipSuccess ||
-        n <= 0)
-        return 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_zh<HMM>, 256, 0) != hipSuccess || n <= 0) return 1;
     return (uint32_t)n;
 }
 
-template <bool HMM>
-static uint32_t occ_zh(uint32_t ring) {
-    switch (ring) {
-        case 8: return occ_zh_r<HMM, 8>();
-        case 16: return occ_zh_r<HMM, 16>();
-        case 32: return occ_zh_r<HMM, 32>();
-        case 64: return occ_zh_r<HMM, 64>();
-        case 128: return occ_zh_r<HMM, 128>();
-        default: return occ_zh_r<HMM, 256>();
-    }
-}
-
-uint32_t zh_blocks_per_cu(bool hmm, uint32_t ring) { return hmm ? occ_zh<true>(ring) : occ_zh<false>(ring); }
-
-template <bool HMM, uint32_t R>
-static void launch_zh(uint32_t grid, hipStream_t s, const uint8_t* text, const Work& w, const DevImage& im) {
-    const uint32_t wg = zh_threads(R);
-    hipLaunchKernelGGL((k_zh<HMM, R>), dim3(grid), dim3(wg), (size_t)R * wg * sizeof(double), s, text, w.blk,
-                       w.lists, w.counters, im, w.emask, w.ewidx, w.gbl, w.sbits, w.ebits, g_ablate);
-}
-
-template <bool HMM>
-static void dispatch_zh(uint32_t ring, uint32_t grid, hipStream_t s, const uint8_t* text, const Work& w,
-                        const DevImage& im) {
-    switch (ring) {
-        case 8: launch_zh<HMM, 8>(grid, s, text, w, im); break;
-        case 16: launch_zh<HMM, 16>(grid, s, text, w, im); break;
-        case 32: launch_zh<HMM, 32>(grid, s, text, w, im); break;
-        case 64: launch_zh<HMM, 64>(grid, s, text, w, im); break;
-        case 128: launch_zh<HMM, 128>(grid, s, text, w, im); break;
-        default: launch_zh<HMM, 256>(grid, s, text, w, im); break;
-    }
-}
+uint32_t zh_blocks_per_cu(bool hmm) { return hmm ? occ_zh<true>() : occ_zh<false>(); }
 
 uint32_t nonzh_blocks_per_cu() {
     int n = 0;
@@ -943,8 +961,8 @@ uint32_t nonzh_blocks_per_cu() {
     } while (0)
 
 hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text, uint64_t nbytes,
-                        const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, uint32_t ring, uint32_t grid_zh,
-                        uint32_t grid_nz, hipStream_t stream, KernelTimer* timer) {
+                        const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, uint32_t grid_zh, uint32_t grid_nz,
+                        hipStream_t stream, KernelTimer* timer) {
     const uint64_t nwords = (nbytes + 31) / 32;
     const uint32_t ntiles = (uint32_t)((nbytes + kTileBytes - 1) / kTileBytes);
     const uint32_t nttiles = (uint32_t)((nwords + kTokTileWords - 1) / kTokTileWords);
@@ -971,8 +989,14 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                                 nbytes, w.docbits, nullptr, w.tile_off, w.blk, w.lists, list_cap));
     JB_TIMED(K_WALK, hipLaunchKernelGGL(k_walk, dim3((uint32_t)((nbytes + 4 * 1024 - 1) / (4 * 1024))), dim3(256), 0, stream,
                                         d_text, nbytes, w.docbits, im, w.emask, w.ewidx, g_ablate));
-    JB_TIMED(K_ZH, hmm ? dispatch_zh<true>(ring, grid_zh, stream, d_text, w, im)
-                       : dispatch_zh<false>(ring, grid_zh, stream, d_text, w, im));
+    if (hmm)
+        JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
+                                          w.lists, w.counters, im, w.emask, w.ewidx, w.gbl, w.gbest, w.sbits, w.ebits,
+                                          g_ablate));
+    else
+        JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
+                                          w.lists, w.counters, im, w.emask, w.ewidx, w.gbl, w.gbest, w.sbits, w.ebits,
+                                          g_ablate));
     JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3(grid_nz), dim3(256), 0, stream, d_text, w.blk, w.lists,
                                          list_cap, w.counters, w.sbits, w.ebits));
     JB_TIMED(K_TOK_COUNT, hipLaunchKernelGGL((k_tok<false>), dim3(nttiles), dim3(256), 0, stream, w.sbits, w.ebits,
