@@ -285,7 +285,8 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.ttile_off, nttiles * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.blk, (nb + 4) * 4));
     HIPCHK(hipMalloc(&w.lists, (nb + 4) * 4));
-    HIPCHK(hipMalloc(&w.emask, (nb / 3 + 8) * 4));
+    // emask also holds k_blocks' lane masks (ntiles * 256 u32) before k_walk runs
+    HIPCHK(hipMalloc(&w.emask, std::max<uint64_t>(nb / 3 + 8, ntiles * 256) * 4));
     HIPCHK(hipMalloc(&w.ewidx, (nb / 3 + 8) * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.gbl, nb / 3 + 8));
     HIPCHK(hipMalloc(&w.gbest, (nb / 3 + 8) * sizeof(double)));

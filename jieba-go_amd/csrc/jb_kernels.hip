@@ -2,10 +2,11 @@
 //
 // Pipeline for one batch of documents (all in HBM, one stream):
 //   k_docbits     document starts -> 1 bit per byte
-//   k_blocks<0>   per 4 KiB tile: UTF-8 decode (Go rules), \p{Han} runs, count
-//                 block starts                  (zh regex + splitText, tokenizer.go:21,154-155,165-210)
+//   k_blocks_mark per 4 KiB tile: UTF-8 decode at lead bytes (Go rules), \p{Han}
+//                 runs -> block-start masks + counts (zh regex + splitText,
+//                                               tokenizer.go:21,154-155,165-210)
 //   k_scan2       tile counts -> offsets
-//   k_blocks<1>   write block list (start | zh<<31), zh ids, non-zh ids
+//   k_blocks_write  block list (start | zh<<31), zh ids, non-zh ids
 //   k_walk        one thread per 16 bytes: the trie walk (DAG edges) of every Han
 //                 rune, several walks in flight per thread
 //   k_zh          one lane per Han block: backward max-prob DP over those edges +
@@ -28,7 +29,7 @@
 
 namespace jb {
 
-const char* const kKernelNames[K_NUM] = {"k_docbits", "k_blocks_count", "k_scan_blocks", "k_blocks_write",
+const char* const kKernelNames[K_NUM] = {"k_docbits", "k_blocks_mark", "k_scan_blocks", "k_blocks_write",
                                          "k_walk", "k_zh", "k_nonzh", "k_tok_count", "k_scan_tok",
                                          "k_tok_write", "k_doc_tok"};
 
@@ -52,6 +53,12 @@ const char* const kKernelNames[K_NUM] = {"k_docbits", "k_blocks_count", "k_scan_
 __device__ __forceinline__ uint32_t ld4(const uint8_t* __restrict__ t, uint64_t q) {
     const uint32_t* a = reinterpret_cast<const uint32_t*>(t + (q & ~3ull));
     return __builtin_amdgcn_alignbyte(a[1], a[0], (uint32_t)(q & 3));
+}
+
+// 4 bytes at window offset k of staged text (k + 8 readable).
+__device__ __forceinline__ uint32_t lds4(const uint8_t* tx, uint32_t k) {
+    const uint32_t* a = reinterpret_cast<const uint32_t*>(tx + (k & ~3u));
+    return __builtin_amdgcn_alignbyte(a[1], a[0], k & 3u);
 }
 
 // Token bitmaps: bits are accumulated per 32-byte word in registers and
@@ -122,22 +129,41 @@ __device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t* lds, ui
     return base + x - v;
 }
 
-template <bool WRITE>
-__global__ __launch_bounds__(256) void k_blocks(const uint8_t* __restrict__ text, uint64_t nbytes,
-                                                const uint32_t* __restrict__ docbits, uint2* __restrict__ tile_cnt,
-                                                const uint2* __restrict__ tile_off, uint32_t* __restrict__ blk,
-                                                uint32_t* __restrict__ lists, uint32_t list_cap) {
+// \p{Han} (unicode.Han, Unicode 13) with the common ranges first: the two
+// big BMP blocks, a bitmask for U+3000-303F (CJK punctuation: only 3005,
+// 3007, 3021-3029, 3038-303B are Han), and the full table only for the rare
+// rest (radicals, compatibility ideographs, the supplementary planes).
+__device__ __forceinline__ bool han_cp(uint32_t r) {
+    constexpr uint64_t k3000 = (1ull << 5) | (1ull << 7) | (0x1FFull << 0x21) | (0xFull << 0x38);
+    bool h = (r - 0x4E00u <= 0x9FFCu - 0x4E00u) | (r - 0x3400u <= 0x4DBFu - 0x3400u);
+    const uint32_t o = r - 0x3000u;
+    h |= o < 64u && ((k3000 >> (o & 63u)) & 1ull);
+    const bool rare = (r - 0x2E80u < 0x180u) | (r - 0xF900u < 0x200u) | (r >= 0x16FF0u);
+    if (rare) h = jb_is_han(r);
+    return h;
+}
+
+// k_blocks_mark: 16 bytes per lane, 4 KiB per workgroup, staged in LDS.
+// The lane's window is [p0-4, p0+20).  Only lead bytes (>= 0xC0) can start a
+// multi-byte rune, so the lane decodes (Go utf8.DecodeRune, bounded by the
+// document end) at its lead bytes only; a valid sequence covers its
+// continuation bytes, every other byte is a rune of its own (Go's range loop
+// takes an invalid byte as one U+FFFD).  A block starts at a rune start that
+// is a document start or changes Han-ness (splitText's regexp runs).
+// Output per lane: bits 0-15 block starts, bits 16-31 of those the Han ones.
+__global__ __launch_bounds__(256) void k_blocks_mark(const uint8_t* __restrict__ text, uint64_t nbytes,
+                                                     const uint32_t* __restrict__ docbits,
+                                                     uint32_t* __restrict__ lanemask, uint2* __restrict__ tile_cnt) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_t[kTileBytes + 32];  // bytes [t0-16, t0+4096+16)
     __shared__ uint32_t lds[8];
-    const uint64_t p0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 16u;
-    uint32_t wv[6];
-    wv[0] = p0 >= 4 ? *reinterpret_cast<const uint32_t*>(text + p0 - 4) : 0u;
-    if (p0 < nbytes) {
-        const uint4 m = *reinterpret_cast<const uint4*>(text + p0);
-        wv[1] = m.x; wv[2] = m.y; wv[3] = m.z; wv[4] = m.w;
-    } else {
-        wv[1] = wv[2] = wv[3] = wv[4] = 0u;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kTileBytes;
+    for (uint32_t k = threadIdx.x; k < kTileBytes / 16 + 2; k += 256) {
+        const int64_t g = (int64_t)t0 - 16 + 16 * (int64_t)k;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (g >= 0 && (uint64_t)g + 16 <= nbytes + 64) v = *reinterpret_cast<const uint4*>(text + g);
+        reinterpret_cast<uint4*>(s_t)[k] = v;
     }
-    wv[5] = p0 + 16 < nbytes ? *reinterpret_cast<const uint32_t*>(text + p0 + 16) : 0u;
+    const uint64_t p0 = t0 + threadIdx.x * 16u;
     // doc-start / past-the-end mask, bit k <-> byte p0 - 4 + k (k < 24)
     uint64_t M;
     {
@@ -150,83 +176,71 @@ __global__ __launch_bounds__(256) void k_blocks(const uint8_t* __restrict__ text
             const uint64_t hi = wi + 1 < lastw ? docbits[wi + 1] : 0u;
             M = ((hi << 32) | lo) >> off;
         } else {
-            M = (uint64_t)docbits[0] << 4;  // p0 == 0: window bytes -4..-1 do not exist
+            M = (uint64_t)docbits[0] << 4;  // p0 == 0: window bytes -4..-1 do not exist (zeros)
         }
-        // bytes at or past the end stop every decode
-        if (nbytes < p0 + 20) {
-            const int64_t endk = (int64_t)nbytes - base;  // first window index past the end
+        if (nbytes < p0 + 20) {  // bytes at or past the end stop every decode
+            const int64_t endk = (int64_t)nbytes - base;
             if (endk <= 0) M = ~0ull;
             else M |= ~0ull << endk;
         }
     }
-    // decode at window indices 0..19
-    uint32_t dw[20];
-    bool dv[20], dh[20], cont[20];
+    __syncthreads();
+    const uint8_t* win = s_t + 12 + threadIdx.x * 16u;  // window index 0
+    // lead bytes (>= 0xC0) at window indices 0..19
+    uint32_t lead = 0;
 #pragma unroll
-    for (int k = 0; k < 20; k++) {
-        const int wi = k >> 2, sh = (k & 3) * 8;
-        const uint32_t x = sh ? (wv[wi] >> sh) | (wv[wi + 1] << (32 - sh)) : wv[wi];
+    for (int j = 0; j < 5; j++) {
+        const uint32_t x = reinterpret_cast<const uint32_t*>(win)[j];
+        const uint32_t f = (x & (x << 1) & 0x80808080u) >> 7;  // bit 0/8/16/24
+        lead |= ((f * 0x204081u) >> 21 & 0xFu) << (4 * j);
+    }
+    uint32_t covered = 0, hanb = 0;
+    while (lead) {
+        const uint32_t k = __builtin_ctz(lead);
+        lead &= lead - 1u;
         const uint32_t lim = 1u + (uint32_t)__builtin_ctzll(((M >> (k + 1)) & 7ull) | 8ull);
         uint32_t r;
-        const uint32_t w = jb_decode(x, lim, &r);
-        dw[k] = w;
-        dv[k] = !(w == 1 && r == 0xFFFDu);
-        dh[k] = dv[k] && jb_is_han(r);
-        cont[k] = (x & 0xC0u) == 0x80u;
-    }
-    // covering rune for window indices 3..19 (byte p0-1 .. p0+15)
-    bool han[20], start[20];
-#pragma unroll
-    for (int k = 3; k < 20; k++) {
-        int c = k;
-#pragma unroll
-        for (int d = 1; d <= 3; d++) {
-            const int q = k - d;
-            if (dv[q]) {
-                if ((int)dw[q] > d) c = q;
-                break;
-            }
-            if (!cont[q]) break;
-        }
-        // (c is a compile-time-unknown index; select through a small unrolled mux)
-        bool h = dh[k];
-#pragma unroll
-        for (int d = 1; d <= 3; d++)
-            if (c == k - d) h = dh[k - d];
-        han[k] = h;
-        start[k] = c == k;
-    }
-    if (p0 == 0) han[3] = false;
-    uint32_t na = 0, nz = 0, bmask = 0;
-#pragma unroll
-    for (int k = 4; k < 20; k++) {
-        const uint64_t p = p0 + (uint64_t)(k - 4);
-        const bool bs = p < nbytes && start[k] && ((((M >> k) & 1ull) != 0) || han[k] != han[k - 1]);
-        if (bs) {
-            bmask |= 1u << (k - 4);
-            na++;
-            nz += han[k] ? 1u : 0u;
+        const uint32_t w = jb_decode(lds4(win, k), lim, &r);
+        if (w > 1u) {
+            covered |= ((1u << (w - 1u)) - 1u) << (k + 1u);
+            if (w >= 3u && han_cp(r)) hanb |= ((1u << w) - 1u) << k;
         }
     }
+    if (p0 == 0) hanb &= ~0xFu;
+    uint32_t valid = 0xFFFF0u;  // window indices 4..19 that are inside the batch
+    if (nbytes < p0 + 16) valid = nbytes > p0 ? ((1u << (uint32_t)(nbytes - p0)) - 1u) << 4 : 0u;
+    const uint32_t bs = ~covered & valid & ((uint32_t)M | (hanb ^ (hanb << 1)));
+    const uint32_t bmask = (bs >> 4) & 0xFFFFu, zmask = ((bs & hanb) >> 4) & 0xFFFFu;
+    lanemask[blockIdx.x * 256u + threadIdx.x] = bmask | (zmask << 16);
     uint32_t tot;
-    const uint32_t ex = block_scan_u32(na | (nz << 16), lds, &tot);
-    if (!WRITE) {
-        if (threadIdx.x == 0) tile_cnt[blockIdx.x] = make_uint2(tot & 0xFFFFu, tot >> 16);
-        return;
-    }
+    block_scan_u32(__popc(bmask) | (__popc(zmask) << 16), lds, &tot);
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = make_uint2(tot & 0xFFFFu, tot >> 16);
+}
+
+// k_blocks_write: the lane masks -> block list (start | zh<<31), zh block ids
+// (ascending) and non-zh block ids (from the end of `lists`, descending).
+__global__ __launch_bounds__(256) void k_blocks_write(const uint32_t* __restrict__ lanemask,
+                                                      const uint2* __restrict__ tile_off, uint32_t* __restrict__ blk,
+                                                      uint32_t* __restrict__ lists, uint32_t list_cap) {
+    __shared__ uint32_t lds[8];
+    uint32_t m = lanemask[blockIdx.x * 256u + threadIdx.x];
+    const uint32_t bmask = m & 0xFFFFu, zmask = m >> 16;
+    uint32_t tot;
+    const uint32_t ex = block_scan_u32(__popc(bmask) | (__popc(zmask) << 16), lds, &tot);
     if (!bmask) return;
     const uint2 to = tile_off[blockIdx.x];
     uint32_t ga = to.x + (ex & 0xFFFFu);  // global block rank
     uint32_t gz = to.y + (ex >> 16);      // global zh rank
-#pragma unroll
-    for (int k = 4; k < 20; k++) {
-        if (bmask & (1u << (k - 4))) {
-            const uint32_t p = (uint32_t)(p0 + (uint64_t)(k - 4));
-            blk[ga] = p | (han[k] ? 0x80000000u : 0u);
-            if (han[k]) lists[gz++] = ga;
-            else lists[list_cap - 1u - (ga - gz)] = ga;
-            ga++;
-        }
+    const uint32_t p0 = (blockIdx.x * 256u + threadIdx.x) * 16u;
+    uint32_t b = bmask;
+    while (b) {
+        const uint32_t k = __builtin_ctz(b);
+        b &= b - 1u;
+        const bool h = (zmask >> k) & 1u;
+        blk[ga] = (p0 + k) | (h ? 0x80000000u : 0u);
+        if (h) lists[gz++] = ga;
+        else lists[list_cap - 1u - (ga - gz)] = ga;
+        ga++;
     }
 }
 
@@ -307,11 +321,6 @@ constexpr uint32_t kWalkSpan = 1024;                  // text bytes per wave
 constexpr uint32_t kWalkWin = kWalkSpan + 192;        // staged bytes (span + look-ahead)
 constexpr uint32_t kWalkQ = 64 * 6;                   // <= 6 Han starts per 16 bytes
 
-// 4 bytes at window offset k of a wave's staged text.
-__device__ __forceinline__ uint32_t lds4(const uint8_t* tx, uint32_t k) {
-    const uint32_t* a = reinterpret_cast<const uint32_t*>(tx + (k & ~3u));
-    return __builtin_amdgcn_alignbyte(a[1], a[0], k & 3u);
-}
 
 // The Han rune encoded by x (Go-valid, within `lim` bytes), or 0.  A 3-byte
 // form with a Han value cannot be overlong (E0) or a surrogate (ED), and a
@@ -320,14 +329,14 @@ __device__ __forceinline__ uint32_t han_rune(uint32_t x, uint32_t lim, uint32_t*
     const uint32_t b0 = x & 0xFFu;
     if ((x & 0x00C0C0F0u) == 0x008080E0u) {
         const uint32_t r = ((b0 & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
-        if (lim < 3u || !jb_is_han(r)) return 0u;
+        if (lim < 3u || !han_cp(r)) return 0u;
         *w = 3u;
         return r;
     }
     if ((x & 0xC0C0C0F8u) == 0x808080F0u) {
         const uint32_t r =
             ((b0 & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) | (((x >> 16) & 0x3Fu) << 6) | ((x >> 24) & 0x3Fu);
-        if (lim < 4u || !jb_is_han(r)) return 0u;
+        if (lim < 4u || !han_cp(r)) return 0u;
         *w = 4u;
         return r;
     }
@@ -980,13 +989,14 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     if (ndocs)
         JB_TIMED(K_DOCBITS, hipLaunchKernelGGL(k_docbits, dim3((ndocs + 255) / 256), dim3(256), 0, stream,
                                                d_doc_off, ndocs, nbytes, w.docbits));
-    JB_TIMED(K_BLOCKS_COUNT, hipLaunchKernelGGL((k_blocks<false>), dim3(ntiles), dim3(256), 0, stream, d_text,
-                                                nbytes, w.docbits, w.tile_cnt, nullptr, nullptr, nullptr, 0u));
+    // lane masks live in emask until k_walk overwrites it
+    JB_TIMED(K_BLOCKS_COUNT, hipLaunchKernelGGL(k_blocks_mark, dim3(ntiles), dim3(256), 0, stream, d_text, nbytes,
+                                                w.docbits, w.emask, w.tile_cnt));
     JB_TIMED(K_SCAN_BLOCKS, hipLaunchKernelGGL(k_scan2, dim3(1), dim3(1024), 0, stream, w.tile_cnt, ntiles,
                                                w.tile_off, w.counters + CNT_NBLK, nullptr, w.blk,
                                                (uint32_t)nbytes));
-    JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL((k_blocks<true>), dim3(ntiles), dim3(256), 0, stream, d_text,
-                                                nbytes, w.docbits, nullptr, w.tile_off, w.blk, w.lists, list_cap));
+    JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL(k_blocks_write, dim3(ntiles), dim3(256), 0, stream, w.emask,
+                                                w.tile_off, w.blk, w.lists, list_cap));
     JB_TIMED(K_WALK, hipLaunchKernelGGL(k_walk, dim3((uint32_t)((nbytes + 4 * 1024 - 1) / (4 * 1024))), dim3(256), 0, stream,
                                         d_text, nbytes, w.docbits, im, w.emask, w.ewidx, g_ablate));
     if (hmm)
