@@ -260,7 +260,7 @@ static int upload_image(Device* d, const Image& img) {
 
 static void free_work(Work* w) {
     dfree(w->docbits); dfree(w->sbits); dfree(w->ebits); dfree(w->tile_cnt); dfree(w->tile_off);
-    dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->blk); dfree(w->lists); dfree(w->emask); dfree(w->ewidx);
+    dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->blk); dfree(w->lists); dfree(w->erec);
     dfree(w->gbl); dfree(w->gbest);
     dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters);
     *w = Work{};
@@ -285,9 +285,8 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.ttile_off, nttiles * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.blk, (nb + 4) * 4));
     HIPCHK(hipMalloc(&w.lists, (nb + 4) * 4));
-    // emask also holds k_blocks' lane masks (ntiles * 256 u32) before k_walk runs
-    HIPCHK(hipMalloc(&w.emask, std::max<uint64_t>(nb / 3 + 8, ntiles * 256) * 4));
-    HIPCHK(hipMalloc(&w.ewidx, (nb / 3 + 8) * sizeof(uint2)));
+    // erec also holds k_blocks' lane masks (ntiles * 256 u32) before k_walk runs
+    HIPCHK(hipMalloc(&w.erec, std::max<uint64_t>(nb / 3 + 8, ntiles * 128) * 8));
     HIPCHK(hipMalloc(&w.gbl, nb / 3 + 8));
     HIPCHK(hipMalloc(&w.gbest, (nb / 3 + 8) * sizeof(double)));
 

@@ -364,20 +364,33 @@ int build_image(const Dictionary& d, const Emission& e, Image* img, std::string*
     img->nrows = img->npages * 256u;
     const uint16_t* pm = img->pagemap.data();
 
-    // distinct weights: pieceFreq := math.Log(tf) - total (tokenizer.go:519)
+    // distinct weights: pieceFreq := math.Log(tf) - total (tokenizer.go:519).  Indices go to
+    // the weights in order of how many keys use them (ties by value bits), so the
+    // common ones get small indices (k_walk packs 14-bit indices).
     img->wtab.assign(1, img->w_absent);
     std::unordered_map<uint64_t, uint32_t> widx_of;
-    auto widx = [&](int64_t f) -> uint32_t {
+    auto wbits = [&](int64_t f) -> uint64_t {
         const double w = go_log((double)f) - img->total;
         uint64_t bits;
         memcpy(&bits, &w, 8);
-        auto it = widx_of.find(bits);
-        if (it != widx_of.end()) return it->second;
-        const uint32_t i = (uint32_t)img->wtab.size();
-        img->wtab.push_back(w);
-        widx_of.emplace(bits, i);
-        return i;
+        return bits;
     };
+    {
+        std::unordered_map<uint64_t, uint64_t> uses;
+        for (const Key& k : keys) uses[wbits(k.f)]++;
+        std::vector<std::pair<uint64_t, uint64_t>> order(uses.begin(), uses.end());
+        std::sort(order.begin(), order.end(), [](const std::pair<uint64_t, uint64_t>& a,
+                                                 const std::pair<uint64_t, uint64_t>& b) {
+            return a.second != b.second ? a.second > b.second : a.first < b.first;
+        });
+        for (const auto& o : order) {
+            double w;
+            memcpy(&w, &o.first, 8);
+            widx_of.emplace(o.first, (uint32_t)img->wtab.size());
+            img->wtab.push_back(w);
+        }
+    }
+    auto widx = [&](int64_t f) -> uint32_t { return widx_of.at(wbits(f)); };
 
     size_t deep = 0;
     for (const Key& k : keys) deep += k.r.size() > 1;

@@ -43,10 +43,10 @@ struct Work {
     uint2* ttile_off;
     uint32_t* blk;         // block start | zh << 31, then sentinel nbytes
     uint32_t* lists;       // zh block ids from the front, non-zh block ids from the back
-    uint32_t* emask;       // per Han rune (slot = byte / 3): bit L-1 = DAG edge of L runes; bit 31 overflow
-    uint2* ewidx;          // per Han rune: weight indices of its first 4 edges (u16 each)
+    uint64_t* erec;        // per Han rune (slot = byte / 3): packed DAG edges (k_walk -> k_zh); its
+                           // memory first holds k_blocks' lane masks (u32 per 16 bytes)
     uint8_t* gbl;          // per Han rune: chosen piece length, then Viterbi back-pointers / labels
-    double* gbest;         // per Han rune: best proba (index be/3 - c inside each block)
+    double* gbest;         // per Han rune: best proba, kept only for blocks with an edge > 8 runes
     uint32_t* tok_start;
     uint32_t* tok_end;
     uint64_t* doc_tok;

@@ -308,15 +308,17 @@ __global__ __launch_bounds__(1024) void k_scan2(const uint2* __restrict__ cnt, u
 // rune not Han, invalid, or in the next document).
 //
 // Output per rune, slot = byte offset / 3 (Han runes are >= 3 bytes, so slots
-// never collide):
-//   emask[slot]  bit L-1 set for an edge of L runes (L <= 31) (:479-481)
-//   ewidx[slot]  weight indices of the first 4 edges in ascending L (u16 x 4)
-//   bit 31 of emask: more than 4 edges or an edge longer than 31 runes; k_zh
-//   then walks that rune itself.
+// never collide), one u64 record erec[slot]:
+//   bits 0-7    bit L-1 set for an edge of L runes (:479-481)
+//   bits 8-63   weight indices of the edges in ascending L, 14 bits each
+// A rune with more than 4 edges, an edge longer than 8 runes or a weight index
+// >= 2^14 gets the record 0 (a Han rune always has at least one edge); k_zh
+// then walks that rune itself.
 // A rune that is absent or has count 0 gets the single edge L = 1 (:468-471)
 // with weight index 0 (Log(1) - Log(size)) or that of Log(0) - Log(size) = -Inf.
 // ---------------------------------------------------------------------------
-#define JB_EDGE_OVF 0x80000000u
+constexpr uint32_t kEdgeMaxL = 8;     // edge lengths a record holds
+constexpr uint32_t kEdgeIdxBits = 14;
 constexpr uint32_t kWalkSpan = 1024;                  // text bytes per wave
 constexpr uint32_t kWalkWin = kWalkSpan + 192;        // staged bytes (span + look-ahead)
 constexpr uint32_t kWalkQ = 64 * 6;                   // <= 6 Han starts per 16 bytes
@@ -345,8 +347,7 @@ __device__ __forceinline__ uint32_t han_rune(uint32_t x, uint32_t lim, uint32_t*
 
 __global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ text, uint64_t nbytes,
                                               const uint32_t* __restrict__ docbits, DevImage im,
-                                              uint32_t* __restrict__ emask, uint2* __restrict__ ewidx,
-                                              uint32_t ablate) {
+                                              uint64_t* __restrict__ erec, uint32_t ablate) {
     __shared__ __attribute__((aligned(16))) uint8_t s_tx[4][kWalkWin + 16];
     __shared__ uint32_t s_db[4][kWalkWin / 32 + 4];
     __shared__ uint16_t s_q[4][kWalkQ];
@@ -415,24 +416,19 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ text, 
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // ---- walks -------------------------------------------------------------------------
-    bool act = false;
-    uint32_t q = 0, id = 0, qq = 0, len = 0, emk = 0, w01 = 0, w23 = 0, ne = 0;
+    bool act = false, ovf = false;
+    uint32_t q = 0, id = 0, qq = 0, len = 0, ne = 0;
+    uint64_t rc = 0;
     auto edge = [&](uint32_t L, uint32_t wi) {
-        if (L > 31u || ne >= 4u) {
-            emk |= JB_EDGE_OVF;
+        if (L > kEdgeMaxL || ne >= 4u || wi >= (1u << kEdgeIdxBits)) {
+            ovf = true;
             return;
         }
-        emk |= 1u << (L - 1u);
-        if (ne == 0u) w01 = wi;
-        else if (ne == 1u) w01 |= wi << 16;
-        else if (ne == 2u) w23 = wi;
-        else w23 |= wi << 16;
+        rc |= (1ull << (L - 1u)) | ((uint64_t)wi << (8u + kEdgeIdxBits * ne));
         ne++;
     };
     auto finish = [&]() {
-        const uint32_t sl = (uint32_t)((base + q) / 3u);
-        emask[sl] = emk;
-        ewidx[sl] = make_uint2(w01, w23);
+        erec[(base + q) / 3u] = ovf ? 0ull : rc;
         act = false;
     };
     uint32_t head = 0;
@@ -486,7 +482,9 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ text, 
         }
         if (fresh) {
             len = 1u;
-            emk = w01 = w23 = ne = 0u;
+            ne = 0u;
+            rc = 0ull;
+            ovf = false;
             const uint32_t fc = rec & 3u;
             if (fc == JB_FC_ABSENT || fc == JB_FC_ZERO) {
                 edge(1u, rec >> 3);  // the single edge only (:468-471)
@@ -511,7 +509,7 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ text, 
                 qq += wr;
                 if (jb_node_fc(nd) == JB_FC_POS) edge(len, jb_node_widx(nd));
                 id = im.nrows + h;
-                if (!jb_node_hc(nd) || (emk & JB_EDGE_OVF)) finish();
+                if (!jb_node_hc(nd) || ovf) finish();
             }
         }
         if (!__any(act) && head >= nq) break;
@@ -527,10 +525,10 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ text, 
 // its runes (calcDagProba, :502-548): the rune's edges (i, i+L) from k_walk,
 // ascending in L as the DAG lists them, fold into maxIndexProba's running
 // state (:565-578) with pieceProba = w + best(i+L) (:519-529); best(n) is the
-// {n, 0.0} sentinel (:522-525).  best(i+L) for L < 8 comes from an 8-entry
-// LDS ring, longer edges read gbest (every rune's best is also stored there,
-// at index be/3 - c, which stays inside the block's slot range).  The chosen
-// piece length goes to the rune's slot; the forward walk (findDagPath,
+// {n, 0.0} sentinel (:522-525).  best(i+L) for L <= 8 comes from an 8-entry
+// LDS ring; a block with a longer edge (rare) is redone with every best value
+// also stored in gbest (index be/3 - c, inside the block's slot range).  The
+// chosen piece length goes to the rune's slot; the forward walk (findDagPath,
 // :552-562) then emits pieces or, with HMM, gathers runs of single-rune pieces
 // for the Viterbi (:228-253).  Blocks that do not fit the staged span run the
 // same code on global memory.
@@ -659,92 +657,104 @@ __device__ void viterbi_run(const V& v, const DevImage& im, uint32_t rs, uint32_
 // One Han block [bs, be).  Returns false where the reference panics (a rune
 // on the chosen path with no DAG edge: cutDAG slices with tail index -1).
 template <bool HMM, class V>
-__device__ bool zh_block(const V& v, const DevImage& im, const uint32_t* __restrict__ emask,
-                         const uint2* __restrict__ ewidx, double* __restrict__ gbest, double* ring, uint32_t bs,
-                         uint32_t be, Emitter& em, uint32_t ablate) {
+__device__ bool zh_block(const V& v, const DevImage& im, const uint64_t* __restrict__ erec,
+                         double* __restrict__ gbest, double* ring, uint32_t bs, uint32_t be, Emitter& em,
+                         uint32_t ablate) {
     const uint32_t key0 = be / 3u;
-    uint32_t q = z_prev(v, be, bs), c = 1;
-    uint32_t m = emask[q / 3u];
-    uint2 wi = ewidx[q / 3u];
-    for (;;) {
-        const bool more = q > bs;
-        uint32_t qn = 0, mn = 0;
-        uint2 win = make_uint2(0, 0);
-        if (more) {  // next rune's edge record, in flight while this rune folds
-            qn = z_prev(v, q, bs);
-            mn = emask[qn / 3u];
-            win = ewidx[qn / 3u];
-        }
-        double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT;
-        uint32_t bestL = 0, lastL = 0;
-        auto fold = [&](uint32_t L, double wt) {
-            double nb;
-            if (L == c) nb = 0.0;
-            else if (L < kZhRing) nb = ring[((c - L) & (kZhRing - 1u)) * 64u];
-            else nb = gbest[key0 - (c - L)];
-            const double pp = wt + nb;
-            if (pp >= prevP) {
-                bestL = L;
-                bestP = pp;
-            }
-            prevP = pp;
-            lastL = L;
-        };
-        if (!(m & JB_EDGE_OVF)) {
-            double w4[4];
-            uint32_t L4[4];
+    // The best values of the last kZhRing runes live in the LDS ring.  A block
+    // with a longer edge is redone with every best value also kept in gbest.
+    for (bool longm = false;; longm = true) {
+        bool redo = false;
+        uint32_t q = z_prev(v, be, bs), c = 1;
+        uint64_t rc = erec[q / 3u];
+        for (;;) {
+            const bool more = q > bs;
+            double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT;
+            uint32_t bestL = 0, lastL = 0;
+            auto fold = [&](uint32_t L, double wt) {
+                double nb;
+                if (L == c) nb = 0.0;
+                else if (L <= kZhRing) nb = ring[((c - L) & (kZhRing - 1u)) * 64u];
+                else if (longm) nb = gbest[key0 - (c - L)];
+                else {
+                    redo = true;
+                    nb = 0.0;
+                }
+                const double pp = wt + nb;
+                if (pp >= prevP) {
+                    bestL = L;
+                    bestP = pp;
+                }
+                prevP = pp;
+                lastL = L;
+            };
+            uint32_t qn = 0;
+            uint64_t rn = 0;
+            if ((uint32_t)rc & 0xFFu) {
+                double w4[4];
+                uint32_t L4[4];
+                uint32_t m = (uint32_t)rc & 0xFFu;
 #pragma unroll
-            for (int k = 0; k < 4; k++) {  // weight loads of all edges first (independent)
-                L4[k] = m ? (uint32_t)__builtin_ctz(m) + 1u : 0u;
-                m &= m - 1u;
-                const uint32_t idx = ((k < 2 ? wi.x : wi.y) >> (16 * (k & 1))) & 0xFFFFu;
-                w4[k] = L4[k] ? im.wtab[idx] : 0.0;
-            }
+                for (int k = 0; k < 4; k++) {  // weight loads of all edges first (independent)
+                    L4[k] = m ? (uint32_t)__builtin_ctz(m) + 1u : 0u;
+                    m &= m - 1u;
+                    const uint32_t idx = (uint32_t)(rc >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u);
+                    w4[k] = L4[k] ? im.wtab[idx] : 0.0;
+                }
+                if (more) {  // next rune's record, in flight while this rune folds
+                    qn = z_prev(v, q, bs);
+                    rn = (ablate & 64u) ? 1ull : erec[qn / 3u];
+                }
 #pragma unroll
-            for (int k = 0; k < 4; k++)
-                if (L4[k]) fold(L4[k], w4[k]);
-        } else {  // many or long edges: walk this rune here (the rules of k_walk)
-            uint32_t w0;
-            const uint32_t r0 = z_dec(v, q, &w0);
-            const uint32_t row = jb_row(im.pagemap, r0);
-            const uint32_t rec = im.l1[row];
-            const uint32_t fc = rec & 3u;
-            if (fc == JB_FC_ABSENT || fc == JB_FC_ZERO) {
-                fold(1u, im.wtab[rec >> 3]);
-            } else {
-                if (fc == JB_FC_POS) fold(1u, im.wtab[rec >> 3]);
-                uint32_t id = row, qq = q + w0, len = 1;
-                bool go = ((rec >> 2) & 1u) != 0u;
-                while (go && qq < be) {
-                    uint32_t wr;
-                    const uint32_t r = z_dec(v, qq, &wr);
-                    uint32_t h = jb_hash(id, r) & im.mask;
-                    uint64_t nd = im.nodes[h];
-                    while (nd != JB_NODE_EMPTY && !jb_node_is(nd, id, r)) {
-                        h = (h + 1u) & im.mask;
-                        nd = im.nodes[h];
+                for (int k = 0; k < 4; k++)
+                    if (L4[k]) fold(L4[k], w4[k]);
+            } else {  // many or long edges: walk this rune here (the rules of k_walk)
+                if (more) {
+                    qn = z_prev(v, q, bs);
+                    rn = erec[qn / 3u];
+                }
+                uint32_t w0;
+                const uint32_t r0 = z_dec(v, q, &w0);
+                const uint32_t row = jb_row(im.pagemap, r0);
+                const uint32_t rec = im.l1[row];
+                const uint32_t fc = rec & 3u;
+                if (fc == JB_FC_ABSENT || fc == JB_FC_ZERO) {
+                    fold(1u, im.wtab[rec >> 3]);
+                } else {
+                    if (fc == JB_FC_POS) fold(1u, im.wtab[rec >> 3]);
+                    uint32_t id = row, qq = q + w0, len = 1;
+                    bool go = ((rec >> 2) & 1u) != 0u;
+                    while (go && qq < be) {
+                        uint32_t wr;
+                        const uint32_t r = z_dec(v, qq, &wr);
+                        uint32_t h = jb_hash(id, r) & im.mask;
+                        uint64_t nd = im.nodes[h];
+                        while (nd != JB_NODE_EMPTY && !jb_node_is(nd, id, r)) {
+                            h = (h + 1u) & im.mask;
+                            nd = im.nodes[h];
+                        }
+                        if (nd == JB_NODE_EMPTY) break;
+                        ++len;
+                        qq += wr;
+                        if (jb_node_fc(nd) == JB_FC_POS) fold(len, im.wtab[jb_node_widx(nd)]);
+                        go = jb_node_hc(nd) != 0u;
+                        id = im.nrows + h;
                     }
-                    if (nd == JB_NODE_EMPTY) break;
-                    ++len;
-                    qq += wr;
-                    if (jb_node_fc(nd) == JB_FC_POS) fold(len, im.wtab[jb_node_widx(nd)]);
-                    go = jb_node_hc(nd) != 0u;
-                    id = im.nrows + h;
                 }
             }
+            if (bestL == 0) {  // no item qualified: the last item (or {-1, minFloat})
+                bestL = lastL;
+                bestP = prevP;
+            }
+            ring[(c & (kZhRing - 1u)) * 64u] = bestP;
+            if (longm) gbest[key0 - c] = bestP;
+            v.bl(q) = (uint8_t)bestL;
+            if (redo || !more) break;
+            q = qn;
+            rc = rn;
+            ++c;
         }
-        if (bestL == 0) {  // no item qualified: the last item (or {-1, minFloat})
-            bestL = lastL;
-            bestP = prevP;
-        }
-        ring[(c & (kZhRing - 1u)) * 64u] = bestP;
-        gbest[key0 - c] = bestP;
-        v.bl(q) = (uint8_t)bestL;
-        if (!more) break;
-        q = qn;
-        m = mn;
-        wi = win;
-        ++c;
+        if (!redo) break;
     }
     if (ablate & 4u) return true;  // diagnostic only: DP without the forward walk
     // ---- forward walk (findDagPath) + HMM runs ---------------------------------------
@@ -761,14 +771,18 @@ __device__ bool zh_block(const V& v, const DevImage& im, const uint32_t* __restr
             run_n++;
         } else {
             if (run_n) {
-                viterbi_run(v, im, run_s, p, run_n, em);
+                if (ablate & 32u) em.token(run_s, p);
+                else viterbi_run(v, im, run_s, p, run_n, em);
                 run_n = 0;
             }
             em.token(p, pe);
         }
         p = pe;
     }
-    if (HMM && run_n) viterbi_run(v, im, run_s, be, run_n, em);
+    if (HMM && run_n) {
+        if (ablate & 32u) em.token(run_s, be);
+        else viterbi_run(v, im, run_s, be, run_n, em);
+    }
     return true;
 }
 
@@ -776,8 +790,8 @@ template <bool HMM>
 __global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, uint64_t nbytes,
                                             const uint32_t* __restrict__ blk, const uint32_t* __restrict__ lists,
                                             uint32_t* __restrict__ counters, DevImage im,
-                                            const uint32_t* __restrict__ emask, const uint2* __restrict__ ewidx,
-                                            uint8_t* __restrict__ gbl, double* __restrict__ gbest,
+                                            const uint64_t* __restrict__ erec, uint8_t* __restrict__ gbl,
+                                            double* __restrict__ gbest,
                                             uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
                                             uint32_t ablate) {
     __shared__ __attribute__((aligned(16))) uint8_t s_tx[4][kZhCap + 32];
@@ -814,8 +828,8 @@ __global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, ui
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (valid) {
             bool ok;
-            if (be <= wend) ok = zh_block<HMM>(LdsZv{tx, s_bl[wv], wb}, im, emask, ewidx, gbest, ring, bs, be, em, ablate);
-            else ok = zh_block<HMM>(GlbZv{text, gbl}, im, emask, ewidx, gbest, ring, bs, be, em, ablate);
+            if (be <= wend) ok = zh_block<HMM>(LdsZv{tx, s_bl[wv], wb}, im, erec, gbest, ring, bs, be, em, ablate);
+            else ok = zh_block<HMM>(GlbZv{text, gbl}, im, erec, gbest, ring, bs, be, em, ablate);
             if (!ok) atomicOr(counters + CNT_ERR, 1u);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -989,23 +1003,24 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     if (ndocs)
         JB_TIMED(K_DOCBITS, hipLaunchKernelGGL(k_docbits, dim3((ndocs + 255) / 256), dim3(256), 0, stream,
                                                d_doc_off, ndocs, nbytes, w.docbits));
-    // lane masks live in emask until k_walk overwrites it
+    // lane masks live in erec's memory until k_walk overwrites it
     JB_TIMED(K_BLOCKS_COUNT, hipLaunchKernelGGL(k_blocks_mark, dim3(ntiles), dim3(256), 0, stream, d_text, nbytes,
-                                                w.docbits, w.emask, w.tile_cnt));
+                                                w.docbits, reinterpret_cast<uint32_t*>(w.erec), w.tile_cnt));
     JB_TIMED(K_SCAN_BLOCKS, hipLaunchKernelGGL(k_scan2, dim3(1), dim3(1024), 0, stream, w.tile_cnt, ntiles,
                                                w.tile_off, w.counters + CNT_NBLK, nullptr, w.blk,
                                                (uint32_t)nbytes));
-    JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL(k_blocks_write, dim3(ntiles), dim3(256), 0, stream, w.emask,
+    JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL(k_blocks_write, dim3(ntiles), dim3(256), 0, stream,
+                                                reinterpret_cast<const uint32_t*>(w.erec),
                                                 w.tile_off, w.blk, w.lists, list_cap));
     JB_TIMED(K_WALK, hipLaunchKernelGGL(k_walk, dim3((uint32_t)((nbytes + 4 * 1024 - 1) / (4 * 1024))), dim3(256), 0, stream,
-                                        d_text, nbytes, w.docbits, im, w.emask, w.ewidx, g_ablate));
+                                        d_text, nbytes, w.docbits, im, w.erec, g_ablate));
     if (hmm)
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
-                                          w.lists, w.counters, im, w.emask, w.ewidx, w.gbl, w.gbest, w.sbits, w.ebits,
+                                          w.lists, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,
                                           g_ablate));
     else
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
-                                          w.lists, w.counters, im, w.emask, w.ewidx, w.gbl, w.gbest, w.sbits, w.ebits,
+                                          w.lists, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,
                                           g_ablate));
     JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3(grid_nz), dim3(256), 0, stream, d_text, w.blk, w.lists,
                                          list_cap, w.counters, w.sbits, w.ebits));
