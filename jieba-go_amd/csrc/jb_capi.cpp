@@ -253,14 +253,15 @@ static int upload_image(Device* d, const Image& img) {
     d->dim.emit = d->emit;
     d->dim.nodes = d->nodes;
     d->dim.wtab = d->wtab;
-    d->dim.mask = (uint32_t)(img.nodes.size() - 1);
+    d->dim.mask = (uint32_t)(img.nodes.size() / JB_BUCKET - 1);  // bucket mask
+    d->dim.seed = img.seed;
     d->dim.nrows = img.nrows;
     return JB_OK;
 }
 
 static void free_work(Work* w) {
     dfree(w->docbits); dfree(w->sbits); dfree(w->ebits); dfree(w->tile_cnt); dfree(w->tile_off);
-    dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->blk); dfree(w->lists); dfree(w->erec);
+    dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->blk); dfree(w->lists); dfree(w->erec); dfree(w->lanemask);
     dfree(w->gbl); dfree(w->gbest);
     dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters);
     *w = Work{};
@@ -285,8 +286,8 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.ttile_off, nttiles * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.blk, (nb + 4) * 4));
     HIPCHK(hipMalloc(&w.lists, (nb + 4) * 4));
-    // erec also holds k_blocks' lane masks (ntiles * 256 u32) before k_walk runs
-    HIPCHK(hipMalloc(&w.erec, std::max<uint64_t>(nb / 3 + 8, ntiles * 128) * 8));
+    HIPCHK(hipMalloc(&w.erec, (nb / 3 + 8) * 8));
+    HIPCHK(hipMalloc(&w.lanemask, ntiles * 256 * 4));
     HIPCHK(hipMalloc(&w.gbl, nb / 3 + 8));
     HIPCHK(hipMalloc(&w.gbest, (nb / 3 + 8) * sizeof(double)));
 

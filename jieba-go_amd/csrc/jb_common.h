@@ -12,9 +12,10 @@
 //   l1[npages * 256]        u32   the single-rune key: freq class | has-children |
 //                                 weight index (its node id is its row)
 //   emit[npages * 256][4]   f64   emitP[B|M|E|S][string(rune)], minFloat if absent
-//   nodes[cap]              u64   open-addressing hash of the deeper trie edges:
-//                                 key (parent id, rune) -> {freq class, has-children,
-//                                 weight index}; a node's id is nrows + its slot
+//   nodes[cap]              u64   bucketed cuckoo hash of the deeper trie edges
+//                                 (2 candidate buckets of 4 slots): key (parent id,
+//                                 rune) -> {freq class, has-children, weight index};
+//                                 a node's id is nrows + its slot
 //   wtab[nw]                f64   distinct weights w = math.Log(float64(freq)) -
 //                                 math.Log(float64(size)) (Go's Log, on the host);
 //                                 wtab[0] = Log(1.0) - Log(size) for absent runes
@@ -75,15 +76,17 @@ JB_HD uint32_t jb_row(const uint16_t* pagemap, uint32_t r) {
     return (uint32_t)pagemap[r >> 8] * 256u + (r & 255u);
 }
 
-// Slot hash of the edge (parent, rune); identical on host and device.
-JB_HD uint32_t jb_hash(uint32_t parent, uint32_t rune) {
-    uint32_t h = parent * 0x9E3779B1u ^ (rune * 0x85EBCA77u + 0x165667B1u);
-    h ^= h >> 16;
-    h *= 0x7FEB352Du;
-    h ^= h >> 15;
-    h *= 0x846CA68Bu;
-    h ^= h >> 16;
-    return h;
+// The two candidate buckets (JB_BUCKET slots = 32 bytes each) of the edge
+// (parent, rune) in the bucketed cuckoo hash; identical on host and device.
+#define JB_BUCKET 4
+JB_HD void jb_buckets(uint32_t parent, uint32_t rune, uint32_t bmask, uint32_t seed, uint32_t* b1, uint32_t* b2) {
+    const uint32_t t = (parent * 0x9E3779B1u + rune * 0x85EBCA77u) ^ seed;
+    uint32_t h1 = (t ^ (t >> 15)) * 0x2C1B3C6Du;
+    uint32_t h2 = (t ^ (t >> 13)) * 0x297A2D39u;
+    h1 ^= h1 >> 13;
+    h2 ^= h2 >> 16;
+    *b1 = h1 & bmask;
+    *b2 = (h2 & bmask) == *b1 ? *b1 ^ 1u : h2 & bmask;
 }
 
 // tokenizer.go:19

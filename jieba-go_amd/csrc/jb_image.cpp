@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <unordered_set>
 #include <cstdlib>
 
 #include "../../include/jiebahip.h"
@@ -324,6 +325,8 @@ int parse_emission(const char* buf, size_t len, Emission* out, std::string* err)
 // ---------------------------------------------------------------------------
 // Device image
 // ---------------------------------------------------------------------------
+static uint32_t jb_buckets_seed(uint32_t attempt) { return attempt * 0x7F4A7C15u + 0x2545F491u; }
+
 static uint32_t freq_class(int64_t f) { return f > 0 ? JB_FC_POS : (f == 0 ? JB_FC_ZERO : JB_FC_NEG); }
 
 int build_image(const Dictionary& d, const Emission& e, Image* img, std::string* err) {
@@ -366,7 +369,7 @@ int build_image(const Dictionary& d, const Emission& e, Image* img, std::string*
 
     // distinct weights: pieceFreq := math.Log(tf) - total (tokenizer.go:519).  Indices go to
     // the weights in order of how many keys use them (ties by value bits), so the
-    // common ones get small indices (k_walk packs 14-bit indices).
+    // common ones get small indices (k_mark_walk packs 14-bit indices).
     img->wtab.assign(1, img->w_absent);
     std::unordered_map<uint64_t, uint32_t> widx_of;
     auto wbits = [&](int64_t f) -> uint64_t {
@@ -394,63 +397,144 @@ int build_image(const Dictionary& d, const Emission& e, Image* img, std::string*
 
     size_t deep = 0;
     for (const Key& k : keys) deep += k.r.size() > 1;
-    uint64_t cap = 1024;
-    while (cap < deep * 2) cap <<= 1;
-    if (img->nrows + cap >= JB_MAX_IDS - 1) {
-        *err = "dictionary too large for the packed trie (" + std::to_string(deep) + " multi-rune keys)";
-        return JB_ELIMIT;
-    }
-    img->nodes.assign(cap, JB_NODE_EMPTY);
     img->l1.assign(img->nrows, jb_l1_make(JB_FC_ABSENT, 0, JB_WIDX_ABSENT));
     img->maxlen = 0;
     img->nnodes = 0;
-    const uint64_t mask = cap - 1;
-    auto find = [&](uint32_t parent, uint32_t r) -> uint64_t {  // slot or ~0
-        uint64_t h = jb_hash(parent, r) & mask;
-        for (;;) {
-            const uint64_t n = img->nodes[h];
-            if (n == JB_NODE_EMPTY) return ~0ull;
-            if (jb_node_is(n, parent, r)) return h;
-            h = (h + 1) & mask;
-        }
-    };
-    std::vector<uint32_t> parents;  // parent id of every stored deeper node
-    for (const Key& k : keys) {
-        const uint32_t fc = freq_class(k.f);
+    for (const Key& k : keys) {  // level 1: the l1 rows
+        if (k.r.size() != 1) continue;
         const uint32_t wi = widx(k.f);
         if (wi >= JB_MAX_WIDX) {
             *err = "more than " + std::to_string(JB_MAX_WIDX) + " distinct frequencies";
             return JB_ELIMIT;
         }
-        if (k.r.size() == 1) {
-            img->l1[jb_row(pm, k.r[0])] = jb_l1_make(fc, 0, wi);
-            img->nnodes++;
-            img->maxlen = std::max<uint32_t>(img->maxlen, 1);
-            continue;
-        }
-        // parent id: level-1 row, then nrows + slot for each deeper prefix
-        const uint32_t row0 = jb_row(pm, k.r[0]);
-        if ((img->l1[row0] & 3u) == JB_FC_ABSENT) continue;  // unreachable (tokenizer.go:475-478)
-        uint32_t parent = row0;
-        bool ok = true;
-        for (size_t i = 1; i + 1 < k.r.size() && ok; i++) {
-            const uint64_t sl = find(parent, k.r[i]);
-            ok = sl != ~0ull;
-            if (ok) parent = img->nrows + (uint32_t)sl;
-        }
-        if (!ok) continue;
-        const uint32_t r = k.r.back();
-        uint64_t h = jb_hash(parent, r) & mask;
-        while (img->nodes[h] != JB_NODE_EMPTY) h = (h + 1) & mask;
-        img->nodes[h] = jb_node_make(parent, r, fc, 0, wi);
-        parents.push_back(parent);
+        img->l1[jb_row(pm, k.r[0])] = jb_l1_make(freq_class(k.f), 0, wi);
         img->nnodes++;
-        img->maxlen = std::max<uint32_t>(img->maxlen, (uint32_t)k.r.size());
+        img->maxlen = 1;
     }
-    // has-children flags: a walk stops at a node without children, no probe
-    for (uint32_t p : parents) {
-        if (p < img->nrows) img->l1[p] |= 1u << 2;
-        else img->nodes[p - img->nrows] |= 1ull << 23;
+    const std::vector<uint32_t> l1_base = img->l1;
+    const uint64_t nnodes1 = img->nnodes;
+    // Deeper levels: bucketed cuckoo hash, placed level by level.  A node's slot
+    // is its id, so a placement may not move a node that is already a parent:
+    // it moves leaves (keys no longer key extends) and nodes of the level being
+    // placed.  Load <= 2/3; a placement that gets stuck retries with another
+    // hash seed, and the table doubles after 16 seeds.
+    std::unordered_set<std::string> internal;  // keys that a longer key extends by one rune
+    auto rkey = [](const std::vector<uint32_t>& r, size_t n) {
+        return std::string(reinterpret_cast<const char*>(r.data()), n * sizeof(uint32_t));
+    };
+    for (const Key& k : keys)
+        if (k.r.size() >= 3) internal.insert(rkey(k.r, k.r.size() - 1));
+    uint64_t cap = 1024;
+    while (cap * 2 < deep * 3) cap <<= 1;  // load <= 2/3
+    for (uint32_t attempt = 0;; attempt++) {
+        if (attempt && attempt % 16 == 0) cap <<= 1;
+        img->seed = attempt ? jb_buckets_seed(attempt) : 0u;
+        if (img->nrows + cap >= JB_MAX_IDS - 1) {
+            *err = "dictionary too large for the packed trie (" + std::to_string(deep) + " multi-rune keys)";
+            return JB_ELIMIT;
+        }
+        img->nodes.assign(cap, JB_NODE_EMPTY);
+        img->l1 = l1_base;
+        img->nnodes = nnodes1;
+        std::vector<uint8_t> lvl(cap, 0);  // level of the node in each slot; 0 = free to move
+        const uint32_t bmask = (uint32_t)(cap / JB_BUCKET - 1);
+        auto find = [&](uint32_t parent, uint32_t r) -> uint64_t {  // slot or ~0
+            uint32_t b[2];
+            jb_buckets(parent, r, bmask, img->seed, &b[0], &b[1]);
+            for (int i = 0; i < 2 * JB_BUCKET; i++) {
+                const uint64_t sl = (uint64_t)JB_BUCKET * b[i / JB_BUCKET] + (i % JB_BUCKET);
+                if (jb_node_is(img->nodes[sl], parent, r)) return sl;
+            }
+            return ~0ull;
+        };
+        uint64_t rng = 0x9E3779B97F4A7C15ull;
+        // level: the level being placed; a node is stored with its level, or 0 if it is a leaf
+        auto place = [&](uint64_t node, uint8_t nlvl, uint8_t level) -> bool {
+            for (int kick = 0; kick < 512; kick++) {
+                uint32_t b[2];
+                jb_buckets(jb_node_parent(node), jb_node_rune(node), bmask, img->seed, &b[0], &b[1]);
+                // the emptier of the two buckets first (keeps buckets evenly filled)
+                int fill[2] = {0, 0};
+                for (int i = 0; i < 2 * JB_BUCKET; i++)
+                    fill[i / JB_BUCKET] += img->nodes[(uint64_t)JB_BUCKET * b[i / JB_BUCKET] + (i % JB_BUCKET)] !=
+                                           JB_NODE_EMPTY;
+                const int first = fill[1] < fill[0] ? 1 : 0;
+                uint64_t movable[2 * JB_BUCKET];
+                int nm = 0;
+                for (int i0 = 0; i0 < 2 * JB_BUCKET; i0++) {
+                    const int i = (i0 + first * JB_BUCKET) % (2 * JB_BUCKET);
+                    const uint64_t sl = (uint64_t)JB_BUCKET * b[i / JB_BUCKET] + (i % JB_BUCKET);
+                    if (img->nodes[sl] == JB_NODE_EMPTY) {
+                        img->nodes[sl] = node;
+                        lvl[sl] = nlvl;
+                        return true;
+                    }
+                    if (lvl[sl] == level || lvl[sl] == 0) movable[nm++] = sl;
+                }
+                if (nm == 0) {
+                    if (getenv("JB_DEBUG_BUILD")) {
+                        fprintf(stderr, "stuck kick %d:", kick);
+                        for (int i = 0; i < 2 * JB_BUCKET; i++)
+                            fprintf(stderr, " %u", (unsigned)lvl[(uint64_t)JB_BUCKET * b[i / JB_BUCKET] + (i % JB_BUCKET)]);
+                        fprintf(stderr, " b=%u,%u\n", b[0], b[1]);
+                    }
+                    return false;
+                }
+                rng ^= rng << 13;
+                rng ^= rng >> 7;
+                rng ^= rng << 17;
+                const uint64_t v = movable[rng % (uint64_t)nm];
+                std::swap(node, img->nodes[v]);
+                std::swap(nlvl, lvl[v]);
+            }
+            return false;
+        };
+        std::vector<uint32_t> parents;  // parent id of every stored deeper node
+        bool ok_all = true;
+        for (size_t i0 = 0; i0 < keys.size() && ok_all;) {
+            const size_t n = keys[i0].r.size();
+            size_t i1 = i0;
+            while (i1 < keys.size() && keys[i1].r.size() == n) i1++;
+            if (n >= 2) {
+                for (size_t i = i0; i < i1 && ok_all; i++) {
+                    const Key& k = keys[i];
+                    // parent id: level-1 row, then nrows + slot for each deeper prefix
+                    const uint32_t row0 = jb_row(pm, k.r[0]);
+                    if ((img->l1[row0] & 3u) == JB_FC_ABSENT) continue;  // unreachable (tokenizer.go:475-478)
+                    uint32_t parent = row0;
+                    bool ok = true;
+                    for (size_t j = 1; j + 1 < n && ok; j++) {
+                        const uint64_t sl = find(parent, k.r[j]);
+                        ok = sl != ~0ull;
+                        if (ok) parent = img->nrows + (uint32_t)sl;
+                    }
+                    if (!ok) continue;
+                    const uint32_t wi = widx(k.f);
+                    if (wi >= JB_MAX_WIDX) {
+                        *err = "more than " + std::to_string(JB_MAX_WIDX) + " distinct frequencies";
+                        return JB_ELIMIT;
+                    }
+                    const uint8_t nl = internal.count(rkey(k.r, n)) ? (uint8_t)std::min<size_t>(n, 255) : 0;
+                    if (!place(jb_node_make(parent, k.r.back(), freq_class(k.f), 0, wi), nl,
+                               (uint8_t)std::min<size_t>(n, 255))) {
+                        if (getenv("JB_DEBUG_BUILD")) fprintf(stderr, "cap %llu: placement failed at key %zu (len %zu) nnodes %llu\n", (unsigned long long)cap, i, n, (unsigned long long)img->nnodes);
+                        ok_all = false;
+                        break;
+                    }
+                    parents.push_back(parent);
+                    img->nnodes++;
+                    img->maxlen = std::max<uint32_t>(img->maxlen, (uint32_t)n);
+                }
+            }
+            i0 = i1;
+        }
+        if (!ok_all) continue;  // another seed / a bigger table
+        // has-children flags: a walk stops at a node without children, no probe
+        for (uint32_t p : parents) {
+            if (p < img->nrows) img->l1[p] |= 1u << 2;
+            else img->nodes[p - img->nrows] |= 1ull << 23;
+        }
+        break;
     }
     img->emit.assign((size_t)img->npages * 256 * 4, JB_MIN_FLOAT);  // not found -> minFloat (tokenizer.go:690,710)
     for (int s = 0; s < 4; s++)
@@ -468,20 +552,20 @@ Lookup image_lookup(const Image& img, const uint32_t* runes, size_t n) {
     const uint32_t rec = img.l1[row];
     if ((rec & 3u) == JB_FC_ABSENT) return out;
     uint32_t id = row, fc = rec & 3u, wi = rec >> 3;
-    const uint64_t mask = img.nodes.size() - 1;
+    const uint32_t bmask = (uint32_t)(img.nodes.size() / JB_BUCKET - 1);
     for (size_t i = 1; i < n; i++) {
-        uint64_t h = jb_hash(id, runes[i]) & mask;
-        for (;;) {
-            const uint64_t nd = img.nodes[h];
-            if (nd == JB_NODE_EMPTY) return Lookup{};
-            if (jb_node_is(nd, id, runes[i])) {
-                id = img.nrows + (uint32_t)h;
-                fc = jb_node_fc(nd);
-                wi = jb_node_widx(nd);
-                break;
-            }
-            h = (h + 1) & mask;
+        uint32_t b[2];
+        jb_buckets(id, runes[i], bmask, img.seed, &b[0], &b[1]);
+        uint64_t hit = ~0ull;
+        for (int k = 0; k < 2 * JB_BUCKET && hit == ~0ull; k++) {
+            const uint64_t sl = (uint64_t)JB_BUCKET * b[k / JB_BUCKET] + (k % JB_BUCKET);
+            if (jb_node_is(img.nodes[sl], id, runes[i])) hit = sl;
         }
+        if (hit == ~0ull) return Lookup{};
+        const uint64_t nd = img.nodes[hit];
+        id = img.nrows + (uint32_t)hit;
+        fc = jb_node_fc(nd);
+        wi = jb_node_widx(nd);
     }
     out.found = true;
     out.fc = fc;

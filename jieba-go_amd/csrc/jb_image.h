@@ -31,6 +31,7 @@ struct Image {
     std::vector<double> emit;       // npages * 256 * 4
     std::vector<uint64_t> nodes;    // hash capacity (power of two), deeper trie edges
     std::vector<double> wtab;       // distinct weights; [0] = w_absent
+    uint32_t seed = 0;              // cuckoo hash seed (jb_buckets)
     uint32_t npages = 0;
     uint32_t nrows = 0;             // npages * 256: ids of level-1 nodes; deeper ids = nrows + slot
     uint32_t maxlen = 0;            // longest reachable key, runes

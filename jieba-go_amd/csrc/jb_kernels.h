@@ -14,7 +14,8 @@ struct DevImage {
     const double* emit;
     const uint64_t* nodes;
     const double* wtab;
-    uint32_t mask;     // hash capacity - 1
+    uint32_t mask;     // cuckoo buckets - 1 (JB_BUCKET slots per bucket)
+    uint32_t seed;     // cuckoo hash seed
     uint32_t nrows;    // deeper node id = nrows + slot
 };
 
@@ -43,8 +44,8 @@ struct Work {
     uint2* ttile_off;
     uint32_t* blk;         // block start | zh << 31, then sentinel nbytes
     uint32_t* lists;       // zh block ids from the front, non-zh block ids from the back
-    uint64_t* erec;        // per Han rune (slot = byte / 3): packed DAG edges (k_walk -> k_zh); its
-                           // memory first holds k_blocks' lane masks (u32 per 16 bytes)
+    uint64_t* erec;        // per Han rune (slot = byte / 3): packed DAG edges (k_mark_walk -> k_zh)
+    uint32_t* lanemask;    // per 16 bytes: block starts | Han block starts << 16
     uint8_t* gbl;          // per Han rune: chosen piece length, then Viterbi back-pointers / labels
     double* gbest;         // per Han rune: best proba, kept only for blocks with an edge > 8 runes
     uint32_t* tok_start;
@@ -57,7 +58,7 @@ struct Work {
 
 // Kernel ids for per-launch timing.
 enum KernelId {
-    K_DOCBITS = 0, K_BLOCKS_COUNT, K_SCAN_BLOCKS, K_BLOCKS_WRITE, K_WALK, K_ZH, K_NONZH,
+    K_DOCBITS = 0, K_MARK_WALK, K_SCAN_BLOCKS, K_BLOCKS_WRITE, K_ZH, K_NONZH,
     K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_NUM
 };
 extern const char* const kKernelNames[K_NUM];

@@ -2,13 +2,13 @@
 //
 // Pipeline for one batch of documents (all in HBM, one stream):
 //   k_docbits     document starts -> 1 bit per byte
-//   k_blocks_mark per 4 KiB tile: UTF-8 decode at lead bytes (Go rules), \p{Han}
+//   k_mark_walk   per 4 KiB tile: UTF-8 decode at lead bytes (Go rules), \p{Han}
 //                 runs -> block-start masks + counts (zh regex + splitText,
-//                                               tokenizer.go:21,154-155,165-210)
+//                 tokenizer.go:21,154-155,165-210); then the trie walk (DAG
+//                 edges) of every Han rune of the tile, one walk per lane at a
+//                 time from an LDS entry list (buildDag, :462-497)
 //   k_scan2       tile counts -> offsets
 //   k_blocks_write  block list (start | zh<<31), zh ids, non-zh ids
-//   k_walk        one thread per 16 bytes: the trie walk (DAG edges) of every Han
-//                 rune, several walks in flight per thread
 //   k_zh          one lane per Han block: backward max-prob DP over those edges +
 //                 forward path + BMES Viterbi on singleton runs
 //                                               (cutZh/cutDAG/buildDag/calcDagProba/
@@ -29,8 +29,8 @@
 
 namespace jb {
 
-const char* const kKernelNames[K_NUM] = {"k_docbits", "k_blocks_mark", "k_scan_blocks", "k_blocks_write",
-                                         "k_walk", "k_zh", "k_nonzh", "k_tok_count", "k_scan_tok",
+const char* const kKernelNames[K_NUM] = {"k_docbits", "k_mark_walk", "k_scan_blocks", "k_blocks_write",
+                                         "k_zh", "k_nonzh", "k_tok_count", "k_scan_tok",
                                          "k_tok_write", "k_doc_tok"};
 
 // newJiebaHMM literals (tokenizer.go:629-652)
@@ -143,19 +143,107 @@ __device__ __forceinline__ bool han_cp(uint32_t r) {
     return h;
 }
 
-// k_blocks_mark: 16 bytes per lane, 4 KiB per workgroup, staged in LDS.
-// The lane's window is [p0-4, p0+20).  Only lead bytes (>= 0xC0) can start a
-// multi-byte rune, so the lane decodes (Go utf8.DecodeRune, bounded by the
-// document end) at its lead bytes only; a valid sequence covers its
-// continuation bytes, every other byte is a rune of its own (Go's range loop
-// takes an invalid byte as one U+FFFD).  A block starts at a rune start that
-// is a document start or changes Han-ness (splitText's regexp runs).
-// Output per lane: bits 0-15 block starts, bits 16-31 of those the Han ones.
-__global__ __launch_bounds__(256) void k_blocks_mark(const uint8_t* __restrict__ text, uint64_t nbytes,
-                                                     const uint32_t* __restrict__ docbits,
-                                                     uint32_t* __restrict__ lanemask, uint2* __restrict__ tile_cnt) {
+constexpr uint32_t kEdgeMaxL = 8;     // edge lengths a record holds
+constexpr uint32_t kEdgeIdxBits = 14;
+constexpr uint32_t kTileE = kTileBytes / 3 + 2;  // Han rune entries of a tile (>= 3 bytes each)
+// entry: rune (bits 0-17; Han runes are < 0x40000) | tile offset (bits 18-29)
+constexpr uint32_t kEntCont = 0x40000000u;  // the next entry continues the run
+constexpr uint32_t kEntEdge = 0x80000000u;  // the run may continue past the tile
+__device__ __forceinline__ uint32_t ent_rune(uint32_t e) { return e & 0x3FFFFu; }
+__device__ __forceinline__ uint32_t ent_pos(uint32_t e) { return (e >> 18) & 0xFFFu; }
+__device__ __forceinline__ uint32_t ent_w(uint32_t e) { return ent_rune(e) >= 0x10000u ? 4u : 3u; }
+
+// The Han rune encoded by x (Go-valid, within `lim` bytes), or 0.  A 3-byte
+// form with a Han value cannot be overlong (E0) or a surrogate (ED), and a
+// 4-byte form with a Han value is >= U+16FF0, so the bit patterns suffice.
+__device__ __forceinline__ uint32_t han_rune(uint32_t x, uint32_t lim, uint32_t* w) {
+    const uint32_t b0 = x & 0xFFu;
+    if ((x & 0x00C0C0F0u) == 0x008080E0u) {
+        const uint32_t r = ((b0 & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
+        if (lim < 3u || !han_cp(r)) return 0u;
+        *w = 3u;
+        return r;
+    }
+    if ((x & 0xC0C0C0F8u) == 0x808080F0u) {
+        const uint32_t r =
+            ((b0 & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) | (((x >> 16) & 0x3Fu) << 6) | ((x >> 24) & 0x3Fu);
+        if (lim < 4u || !han_cp(r)) return 0u;
+        *w = 4u;
+        return r;
+    }
+    return 0u;
+}
+
+// Cuckoo lookup of the trie edge (parent, r): both candidate buckets are
+// loaded at once (2 x 32 bytes, one round trip); slot or ~0u.
+struct Probe {
+    ulonglong2 x0, x1, y0, y1;
+    uint32_t b1, b2;
+};
+__device__ __forceinline__ void probe_issue(const DevImage& im, uint32_t parent, uint32_t r, Probe* p) {
+    jb_buckets(parent, r, im.mask, im.seed, &p->b1, &p->b2);
+    const ulonglong2* n2 = reinterpret_cast<const ulonglong2*>(im.nodes);
+    p->x0 = n2[2u * p->b1];
+    p->x1 = n2[2u * p->b1 + 1u];
+    p->y0 = n2[2u * p->b2];
+    p->y1 = n2[2u * p->b2 + 1u];
+}
+__device__ __forceinline__ uint32_t probe_match(const Probe& p, uint32_t parent, uint32_t r, uint64_t* nd) {
+    const uint64_t c[8] = {p.x0.x, p.x0.y, p.x1.x, p.x1.y, p.y0.x, p.y0.y, p.y1.x, p.y1.y};
+    uint32_t sl = ~0u;
+#pragma unroll
+    for (int k = 7; k >= 0; k--)
+        if (jb_node_is(c[k], parent, r)) {
+            sl = (k < 4 ? p.b1 : p.b2) * 4u + (uint32_t)(k & 3);
+            *nd = c[k];
+        }
+    return sl;
+}
+
+// k_mark_walk: one workgroup per 4 KiB tile, staged in LDS, two phases.
+//
+// (1) Blocks (zh regex + splitText, tokenizer.go:21,154-155,165-210): 16
+// bytes per lane; the lane's window is [p0-4, p0+20).  Only lead bytes
+// (>= 0xC0) can start a multi-byte rune, so the lane decodes (Go
+// utf8.DecodeRune, bounded by the document end) at its lead bytes only; a
+// valid sequence covers its continuation bytes, every other byte is a rune of
+// its own (Go's range loop takes an invalid byte as one U+FFFD).  A block
+// starts at a rune start that is a document start or changes Han-ness.
+// Output per lane: bits 0-15 block starts, bits 16-31 of those the Han ones,
+// and the tile's (blocks, Han blocks) counts.
+//
+// (2) DAG edges of every Han rune of the tile (buildDag, tokenizer.go:462-497).
+// The tile's Han runes go to an LDS entry list in text order: rune value,
+// tile offset, and whether the next entry is the next rune of the same Han
+// run (adjacent, same document).  Every lane runs one walk at a time as a
+// small state machine — one trie probe per loop trip, the next rune read from
+// the entry list — and takes the next walk start from the tile's queue as soon
+// as its walk ends, so lanes stay busy however long the walks are.  A walk
+// starts at the rune's l1 record (level 1); the probe of its second rune goes
+// out with that load.  It follows one (parent id, rune) probe per further
+// rune and stops at the first string that is not a key (:475-478), at a node
+// without children, or at the end of the Han run.  A run that goes past the
+// tile is walked again at the end, from global memory.
+//
+// Output per rune, slot = byte offset / 3 (Han runes are >= 3 bytes, so slots
+// never collide), one u64 record erec[slot]:
+//   bits 0-7    bit L-1 set for an edge of L runes (:479-481)
+//   bits 8-63   weight indices of the edges in ascending L, 14 bits each
+// A rune with more than 4 edges, an edge longer than 8 runes or a weight index
+// >= 2^14 gets the record 0 (a Han rune always has at least one edge); k_zh
+// then walks that rune itself.  A rune that is absent or has count 0 gets the
+// single edge L = 1 (:468-471) with weight index 0 (Log(1) - Log(size)) or
+// that of Log(0) - Log(size) = -Inf.
+__global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ text, uint64_t nbytes,
+                                                   const uint32_t* __restrict__ docbits, DevImage im,
+                                                   uint32_t* __restrict__ lanemask, uint2* __restrict__ tile_cnt,
+                                                   uint64_t* __restrict__ erec, uint32_t ablate) {
     __shared__ __attribute__((aligned(16))) uint8_t s_t[kTileBytes + 32];  // bytes [t0-16, t0+4096+16)
+    __shared__ uint32_t s_db[kTileBytes / 32 + 2];                        // document starts of the tile
+    __shared__ uint32_t s_e[kTileE];
     __shared__ uint32_t lds[8];
+    __shared__ uint16_t s_def[256];  // walk starts whose run goes past the tile
+    __shared__ uint32_t s_ndef;
     const uint64_t t0 = (uint64_t)blockIdx.x * kTileBytes;
     for (uint32_t k = threadIdx.x; k < kTileBytes / 16 + 2; k += 256) {
         const int64_t g = (int64_t)t0 - 16 + 16 * (int64_t)k;
@@ -163,6 +251,12 @@ __global__ __launch_bounds__(256) void k_blocks_mark(const uint8_t* __restrict__
         if (g >= 0 && (uint64_t)g + 16 <= nbytes + 64) v = *reinterpret_cast<const uint4*>(text + g);
         reinterpret_cast<uint4*>(s_t)[k] = v;
     }
+    const uint64_t lastw = (nbytes + 31) >> 5;
+    if (threadIdx.x < kTileBytes / 32 + 2) {
+        const uint64_t wi = (t0 >> 5) + threadIdx.x;
+        s_db[threadIdx.x] = wi < lastw ? docbits[wi] : 0u;
+    }
+    if (threadIdx.x == 0) s_ndef = 0;
     const uint64_t p0 = t0 + threadIdx.x * 16u;
     // doc-start / past-the-end mask, bit k <-> byte p0 - 4 + k (k < 24)
     uint64_t M;
@@ -171,7 +265,6 @@ __global__ __launch_bounds__(256) void k_blocks_mark(const uint8_t* __restrict__
         if (base >= 0) {
             const uint64_t wi = (uint64_t)base >> 5;
             const uint32_t off = (uint32_t)base & 31u;
-            const uint64_t lastw = (nbytes + 31) >> 5;
             const uint64_t lo = wi < lastw ? docbits[wi] : 0u;
             const uint64_t hi = wi + 1 < lastw ? docbits[wi + 1] : 0u;
             M = ((hi << 32) | lo) >> off;
@@ -215,6 +308,168 @@ __global__ __launch_bounds__(256) void k_blocks_mark(const uint8_t* __restrict__
     uint32_t tot;
     block_scan_u32(__popc(bmask) | (__popc(zmask) << 16), lds, &tot);
     if (threadIdx.x == 0) tile_cnt[blockIdx.x] = make_uint2(tot & 0xFFFFu, tot >> 16);
+
+    // ---- (2) Han rune entries of the tile, in text order ---------------------------
+    uint32_t hs = ((hanb & ~covered & valid) >> 4) & 0xFFFFu;  // Han rune starts of the lane's bytes
+    uint32_t nent;
+    uint32_t o = block_scan_u32(__popc(hs), lds, &nent);
+    while (hs) {
+        const uint32_t k = (uint32_t)__builtin_ctz(hs);
+        hs &= hs - 1u;
+        const uint32_t x = lds4(win, k + 4u);
+        const uint32_t r = (x & 0xF0u) == 0xE0u
+                               ? ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu)
+                               : ((x & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) | (((x >> 16) & 0x3Fu) << 6) |
+                                     ((x >> 24) & 0x3Fu);
+        s_e[o++] = r | ((threadIdx.x * 16u + k) << 18);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nent; i += 256u) {  // run links
+        const uint32_t e = s_e[i];
+        const uint32_t nxt = ent_pos(e) + ent_w(e);
+        uint32_t f = 0;
+        if (nxt >= kTileBytes) f = kEntEdge;
+        else if (i + 1u < nent && ent_pos(s_e[i + 1u]) == nxt && !((s_db[nxt >> 5] >> (nxt & 31u)) & 1u)) f = kEntCont;
+        s_e[i] = e | f;
+    }
+    __syncthreads();
+    // ---- walks: wave w takes the walk starts [lo, hi) of the tile ---------------------
+    const uint32_t* ent = s_e;
+    const uint32_t wv = threadIdx.x >> 6;
+    uint32_t head = (nent * wv) >> 2;
+    const uint32_t hi = (nent * (wv + 1u)) >> 2;
+    const uint32_t elast = nent ? nent - 1u : 0u;
+    bool act = false, ovf = false;
+    uint32_t q = 0, j = 0, ecur = 0, id = 0, len = 0, nedge = 0;
+    uint64_t rc = 0;
+    auto edge = [&](uint32_t L, uint32_t wi) {
+        if (L > kEdgeMaxL || nedge >= 4u || wi >= (1u << kEdgeIdxBits)) {
+            ovf = true;
+            return;
+        }
+        rc |= (1ull << (L - 1u)) | ((uint64_t)wi << (8u + kEdgeIdxBits * nedge));
+        nedge++;
+    };
+    auto finish = [&]() {
+        erec[(t0 + q) / 3u] = ovf ? 0ull : rc;
+        act = false;
+    };
+    auto defer = [&]() {  // the run goes on past the tile: walked again from global memory below
+        s_def[atomicAdd(&s_ndef, 1u)] = (uint16_t)q;
+        act = false;
+    };
+    for (;;) {
+        const uint64_t need = __ballot(!act);
+        const uint32_t rank =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+        const uint32_t j0 = head + rank;
+        const bool fresh = !act && j0 < hi;
+        head = min(hi, head + (uint32_t)__popcll(need));
+        const bool cont = act && (ecur & kEntCont);
+        // LDS: a fresh walk's first two runes, or the next rune of a walk under way
+        const uint32_t ea = ent[min(fresh ? j0 : j + 1u, elast)];
+        const uint32_t eb = ent[min(j0 + 1u, elast)];
+        const uint32_t row = jb_row(im.pagemap, ent_rune(ea));
+        // one round trip: the l1 record of a fresh walk and the probe of its second
+        // rune (speculative), or the probe of the next rune of a walk under way
+        const bool spec = fresh && (ea & kEntCont);
+        const bool probing = spec || cont;
+        const uint32_t pid = probing ? (fresh ? row : id) : 0u;
+        const uint32_t r = probing ? ent_rune(fresh ? eb : ea) : 0u;
+        const uint32_t rec = (ablate & 2u) ? jb_l1_make(JB_FC_ABSENT, 0u, 0u) : im.l1[fresh ? row : 0u];
+        Probe pr;
+        probe_issue(im, pid, r, &pr);
+        bool use = cont;  // does this trip's probe extend the lane's walk?
+        if (act && !cont) {  // the run ended at the last rune
+            if (ecur & kEntEdge) defer();
+            else finish();
+        }
+        if (cont) {
+            ++j;
+            ecur = ea;
+        }
+        if (fresh) {
+            q = ent_pos(ea);
+            j = j0;
+            ecur = ea;
+            len = 1u;
+            nedge = 0u;
+            rc = 0ull;
+            ovf = false;
+            const uint32_t fc = rec & 3u;
+            if (fc == JB_FC_ABSENT || fc == JB_FC_ZERO) {
+                edge(1u, rec >> 3);  // the single edge only (:468-471)
+                finish();
+            } else {
+                if (fc == JB_FC_POS) edge(1u, rec >> 3);
+                id = row;
+                act = ((rec >> 2) & 1u) != 0u && !(ablate & 1u);
+                if (!act) {
+                    finish();
+                } else if (spec) {  // the speculative probe is this walk's first step
+                    j = j0 + 1u;
+                    ecur = eb;
+                    use = true;
+                } else if (!(ea & kEntEdge)) {
+                    finish();  // a one-rune run
+                }  // else: the next trip defers it
+            }
+        }
+        if (use) {
+            uint64_t nd = 0;
+            const uint32_t sl = probe_match(pr, pid, r, &nd);
+            if (sl == ~0u) {
+                finish();  // (:475-478)
+            } else {
+                len++;
+                if (jb_node_fc(nd) == JB_FC_POS) edge(len, jb_node_widx(nd));
+                id = im.nrows + sl;
+                if (!jb_node_hc(nd) || ovf) finish();
+            }
+        }
+        if (!__any(act) && head >= hi) break;
+    }
+    __syncthreads();
+    // ---- walks whose Han run goes past the tile: from global memory (rare) ------------
+    const uint32_t ndef = s_ndef;
+    for (uint32_t i = threadIdx.x; i < ndef; i += 256u) {
+        const uint64_t p = t0 + s_def[i];
+        uint32_t wr;
+        const uint32_t r0 = han_rune(ld4(text, p), 4u, &wr);  // a Han rune of this tile (checked above)
+        const uint32_t row = jb_row(im.pagemap, r0);
+        const uint32_t rec = im.l1[row];
+        const uint32_t fc = rec & 3u;
+        rc = 0ull;
+        nedge = 0u;
+        ovf = false;
+        if (fc == JB_FC_POS) edge(1u, rec >> 3);
+        uint32_t pid = row, n = 1u;
+        uint64_t pp = p + wr;
+        bool go = ((rec >> 2) & 1u) != 0u;  // (fc is POS or NEG here: the walk went on)
+        while (go) {
+            const uint64_t wi = pp >> 5;
+            const uint32_t sh = (uint32_t)pp & 31u;
+            const uint64_t v = ((((uint64_t)docbits[wi + 1]) << 32) | docbits[wi]) >> sh;
+            if (v & 1ull) break;  // next document
+            uint32_t lim = 1u + (uint32_t)__builtin_ctzll(((v >> 1) & 7ull) | 8ull);
+            if (pp + lim > nbytes) lim = pp < nbytes ? (uint32_t)(nbytes - pp) : 0u;
+            uint32_t w2;
+            const uint32_t r2 = han_rune(ld4(text, pp), lim, &w2);
+            if (!r2) break;  // end of the Han run
+            Probe p2;
+            probe_issue(im, pid, r2, &p2);
+            uint64_t nd = 0;
+            const uint32_t sl = probe_match(p2, pid, r2, &nd);
+            if (sl == ~0u) break;  // (:475-478)
+            n++;
+            if (jb_node_fc(nd) == JB_FC_POS) edge(n, jb_node_widx(nd));
+            if (ovf) break;
+            pid = im.nrows + sl;
+            pp += w2;
+            go = jb_node_hc(nd) != 0u;
+        }
+        erec[p / 3u] = ovf ? 0ull : rc;
+    }
 }
 
 // k_blocks_write: the lane masks -> block list (start | zh<<31), zh block ids
@@ -294,235 +549,12 @@ __global__ __launch_bounds__(1024) void k_scan2(const uint2* __restrict__ cnt, u
 }
 
 // ---------------------------------------------------------------------------
-// k_walk: the DAG edges of every Han rune (buildDag, tokenizer.go:462-497).
-//
-// Each wave owns 1 KiB of text.  It stages those bytes (plus 192 bytes of
-// look-ahead) and their document-start bits in LDS, finds the Han rune starts
-// (16 bytes per lane) and compacts them into a wave-local queue.  Then every
-// lane runs one walk at a time as a small state machine — one trie probe per
-// loop trip — and takes the next queued start as soon as its walk ends, so
-// the 64 lanes stay busy however long the individual walks are.  A walk
-// starts at the rune's l1 record (level 1) and follows one (parent id, rune)
-// probe per further rune.  It stops at the first string that is not a key
-// (:475-478), at a node without children, or at the end of the Han run (next
-// rune not Han, invalid, or in the next document).
-//
-// Output per rune, slot = byte offset / 3 (Han runes are >= 3 bytes, so slots
-// never collide), one u64 record erec[slot]:
-//   bits 0-7    bit L-1 set for an edge of L runes (:479-481)
-//   bits 8-63   weight indices of the edges in ascending L, 14 bits each
-// A rune with more than 4 edges, an edge longer than 8 runes or a weight index
-// >= 2^14 gets the record 0 (a Han rune always has at least one edge); k_zh
-// then walks that rune itself.
-// A rune that is absent or has count 0 gets the single edge L = 1 (:468-471)
-// with weight index 0 (Log(1) - Log(size)) or that of Log(0) - Log(size) = -Inf.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kEdgeMaxL = 8;     // edge lengths a record holds
-constexpr uint32_t kEdgeIdxBits = 14;
-constexpr uint32_t kWalkSpan = 1024;                  // text bytes per wave
-constexpr uint32_t kWalkWin = kWalkSpan + 192;        // staged bytes (span + look-ahead)
-constexpr uint32_t kWalkQ = 64 * 6;                   // <= 6 Han starts per 16 bytes
-
-
-// The Han rune encoded by x (Go-valid, within `lim` bytes), or 0.  A 3-byte
-// form with a Han value cannot be overlong (E0) or a surrogate (ED), and a
-// 4-byte form with a Han value is >= U+16FF0, so the bit patterns suffice.
-__device__ __forceinline__ uint32_t han_rune(uint32_t x, uint32_t lim, uint32_t* w) {
-    const uint32_t b0 = x & 0xFFu;
-    if ((x & 0x00C0C0F0u) == 0x008080E0u) {
-        const uint32_t r = ((b0 & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
-        if (lim < 3u || !han_cp(r)) return 0u;
-        *w = 3u;
-        return r;
-    }
-    if ((x & 0xC0C0C0F8u) == 0x808080F0u) {
-        const uint32_t r =
-            ((b0 & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) | (((x >> 16) & 0x3Fu) << 6) | ((x >> 24) & 0x3Fu);
-        if (lim < 4u || !han_cp(r)) return 0u;
-        *w = 4u;
-        return r;
-    }
-    return 0u;
-}
-
-__global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ text, uint64_t nbytes,
-                                              const uint32_t* __restrict__ docbits, DevImage im,
-                                              uint64_t* __restrict__ erec, uint32_t ablate) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_tx[4][kWalkWin + 16];
-    __shared__ uint32_t s_db[4][kWalkWin / 32 + 4];
-    __shared__ uint16_t s_q[4][kWalkQ];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint64_t base = ((uint64_t)blockIdx.x * 4u + wv) * kWalkSpan;
-    if (base >= nbytes) return;  // whole wave
-    uint8_t* tx = s_tx[wv];
-    uint32_t* db = s_db[wv];
-    uint16_t* queue = s_q[wv];
-    // ---- stage text and document-start bits ------------------------------------
-    for (uint32_t k = lane; k < kWalkWin / 16; k += 64) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (base + 16u * k < nbytes + 48u) v = *reinterpret_cast<const uint4*>(text + base + 16u * k);
-        reinterpret_cast<uint4*>(tx)[k] = v;
-    }
-    const uint64_t lastw = (nbytes + 31) >> 5;
-    if (lane < kWalkWin / 32 + 4) {
-        const uint64_t wi = (base >> 5) + lane;
-        db[lane] = wi < lastw ? docbits[wi] : 0u;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint64_t avail_all = nbytes - base;  // bytes of text from the window start
-    // bytes available for a rune at window offset k: up to the next document start or the end
-    auto lim_at = [&](uint32_t k, bool* docstart) -> uint32_t {
-        const uint32_t w = k >> 5, sh = k & 31u;
-        const uint64_t v = ((((uint64_t)db[w + 1]) << 32) | db[w]) >> sh;
-        *docstart = (v & 1ull) != 0;
-        uint32_t lim = 1u + (uint32_t)__builtin_ctzll(((v >> 1) & 7ull) | 8ull);
-        if ((uint64_t)k + lim > avail_all) lim = (uint32_t)(avail_all > k ? avail_all - k : 0);
-        return lim;
-    };
-    // ---- Han rune starts of this lane's 16 bytes -> wave queue --------------------
-    uint32_t hs = 0;
-    {
-        const uint32_t k0 = 16u * lane;
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const uint32_t x = lds4(tx, k0 + k);
-            if ((x & 0xFFu) >= 0xE2u) {
-                bool ds;
-                const uint32_t lim = lim_at(k0 + k, &ds);
-                uint32_t w;
-                if (han_rune(x, lim, &w)) hs |= 1u << k;
-            }
-        }
-        if (avail_all < k0 + 16u) hs &= avail_all > k0 ? (1u << (uint32_t)(avail_all - k0)) - 1u : 0u;
-    }
-    const uint32_t cnt = __popc(hs);
-    uint32_t incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(incl, d, 64);
-        if (lane >= (uint32_t)d) incl += y;
-    }
-    const uint32_t nq = __shfl(incl, 63, 64);
-    {
-        uint32_t o = incl - cnt, m = hs;
-        while (m) {
-            queue[o++] = (uint16_t)(16u * lane + (uint32_t)__builtin_ctz(m));
-            m &= m - 1u;
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- walks -------------------------------------------------------------------------
-    bool act = false, ovf = false;
-    uint32_t q = 0, id = 0, qq = 0, len = 0, ne = 0;
-    uint64_t rc = 0;
-    auto edge = [&](uint32_t L, uint32_t wi) {
-        if (L > kEdgeMaxL || ne >= 4u || wi >= (1u << kEdgeIdxBits)) {
-            ovf = true;
-            return;
-        }
-        rc |= (1ull << (L - 1u)) | ((uint64_t)wi << (8u + kEdgeIdxBits * ne));
-        ne++;
-    };
-    auto finish = [&]() {
-        erec[(base + q) / 3u] = ovf ? 0ull : rc;
-        act = false;
-    };
-    uint32_t head = 0;
-    for (;;) {
-        const bool stepping = act;
-        // refill idle lanes from the queue
-        const uint64_t need = __ballot(!act);
-        const uint32_t rank =
-            __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-        const bool fresh = !act && head + rank < nq;
-        uint32_t rec = 0, r0 = 0, w0 = 0, row = 0;
-        if (fresh) {
-            q = queue[head + rank];
-            const uint32_t x = lds4(tx, q);
-            w0 = (x & 0xFFu) < 0xF0u ? 3u : 4u;
-            r0 = w0 == 3u ? ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu)
-                          : ((x & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) | (((x >> 16) & 0x3Fu) << 6) |
-                                ((x >> 24) & 0x3Fu);
-            row = jb_row(im.pagemap, r0);
-            rec = (ablate & 2u) ? jb_l1_make(JB_FC_ABSENT, 0u, 0u) : im.l1[row];
-        }
-        head = min(nq, head + (uint32_t)__popcll(need));
-        // one probe step for the walks already under way
-        uint32_t r = 0, wr = 0, h = 0;
-        uint64_t nd = JB_NODE_EMPTY;
-        bool go = false;
-        if (stepping) {
-            bool ds = false;
-            uint32_t x, lim;
-            if (qq + 4u <= kWalkWin) {
-                x = lds4(tx, qq);
-                lim = lim_at(qq, &ds);
-            } else {  // beyond the staged look-ahead (long keys): global text and bits
-                const uint64_t p = base + qq;
-                const uint64_t wi = p >> 5;
-                const uint32_t sh = (uint32_t)p & 31u;
-                const uint64_t v = ((((uint64_t)docbits[wi + 1]) << 32) | docbits[wi]) >> sh;
-                ds = (v & 1ull) != 0;
-                lim = 1u + (uint32_t)__builtin_ctzll(((v >> 1) & 7ull) | 8ull);
-                if (p + lim > nbytes) lim = p < nbytes ? (uint32_t)(nbytes - p) : 0u;
-                x = ld4(text, p);
-            }
-            r = ds ? 0u : han_rune(x, lim, &wr);
-            if (r) {
-                h = jb_hash(id, r) & im.mask;
-                nd = im.nodes[h];
-                go = true;
-            } else {
-                finish();
-            }
-        }
-        if (fresh) {
-            len = 1u;
-            ne = 0u;
-            rc = 0ull;
-            ovf = false;
-            const uint32_t fc = rec & 3u;
-            if (fc == JB_FC_ABSENT || fc == JB_FC_ZERO) {
-                edge(1u, rec >> 3);  // the single edge only (:468-471)
-                finish();
-            } else {
-                if (fc == JB_FC_POS) edge(1u, rec >> 3);
-                id = row;
-                qq = q + w0;
-                act = ((rec >> 2) & 1u) != 0u && !(ablate & 1u);
-                if (!act) finish();
-            }
-        }
-        if (go) {
-            while (nd != JB_NODE_EMPTY && !jb_node_is(nd, id, r)) {
-                h = (h + 1u) & im.mask;
-                nd = im.nodes[h];
-            }
-            if (nd == JB_NODE_EMPTY) {
-                finish();  // (:475-478)
-            } else {
-                len++;
-                qq += wr;
-                if (jb_node_fc(nd) == JB_FC_POS) edge(len, jb_node_widx(nd));
-                id = im.nrows + h;
-                if (!jb_node_hc(nd) || ovf) finish();
-            }
-        }
-        if (!__any(act) && head >= nq) break;
-    }
-}
-
-// ---------------------------------------------------------------------------
 // k_zh: one lane per Han block (cutZh, tokenizer.go:221-255).
 //
 // Waves pull 64 consecutive blocks at a time (one per lane; fast waves take
 // more) and stage the text span that holds them in LDS, so rune stepping,
 // decoding and the per-rune scratch run out of LDS.  Per block, backward over
-// its runes (calcDagProba, :502-548): the rune's edges (i, i+L) from k_walk,
+// its runes (calcDagProba, :502-548): the rune's edges (i, i+L) from k_mark_walk,
 // ascending in L as the DAG lists them, fold into maxIndexProba's running
 // state (:565-578) with pieceProba = w + best(i+L) (:519-529); best(n) is the
 // {n, 0.0} sentinel (:522-525).  best(i+L) for L <= 8 comes from an 8-entry
@@ -708,7 +740,7 @@ __device__ bool zh_block(const V& v, const DevImage& im, const uint64_t* __restr
 #pragma unroll
                 for (int k = 0; k < 4; k++)
                     if (L4[k]) fold(L4[k], w4[k]);
-            } else {  // many or long edges: walk this rune here (the rules of k_walk)
+            } else {  // many or long edges: walk this rune here (the rules of k_mark_walk)
                 if (more) {
                     qn = z_prev(v, q, bs);
                     rn = erec[qn / 3u];
@@ -727,18 +759,16 @@ __device__ bool zh_block(const V& v, const DevImage& im, const uint64_t* __restr
                     while (go && qq < be) {
                         uint32_t wr;
                         const uint32_t r = z_dec(v, qq, &wr);
-                        uint32_t h = jb_hash(id, r) & im.mask;
-                        uint64_t nd = im.nodes[h];
-                        while (nd != JB_NODE_EMPTY && !jb_node_is(nd, id, r)) {
-                            h = (h + 1u) & im.mask;
-                            nd = im.nodes[h];
-                        }
-                        if (nd == JB_NODE_EMPTY) break;
+                        Probe pr;
+                        probe_issue(im, id, r, &pr);
+                        uint64_t nd = 0;
+                        const uint32_t sl = probe_match(pr, id, r, &nd);
+                        if (sl == ~0u) break;
                         ++len;
                         qq += wr;
                         if (jb_node_fc(nd) == JB_FC_POS) fold(len, im.wtab[jb_node_widx(nd)]);
                         go = jb_node_hc(nd) != 0u;
-                        id = im.nrows + h;
+                        id = im.nrows + sl;
                     }
                 }
             }
@@ -1003,17 +1033,13 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     if (ndocs)
         JB_TIMED(K_DOCBITS, hipLaunchKernelGGL(k_docbits, dim3((ndocs + 255) / 256), dim3(256), 0, stream,
                                                d_doc_off, ndocs, nbytes, w.docbits));
-    // lane masks live in erec's memory until k_walk overwrites it
-    JB_TIMED(K_BLOCKS_COUNT, hipLaunchKernelGGL(k_blocks_mark, dim3(ntiles), dim3(256), 0, stream, d_text, nbytes,
-                                                w.docbits, reinterpret_cast<uint32_t*>(w.erec), w.tile_cnt));
+    JB_TIMED(K_MARK_WALK, hipLaunchKernelGGL(k_mark_walk, dim3(ntiles), dim3(256), 0, stream, d_text, nbytes,
+                                             w.docbits, im, w.lanemask, w.tile_cnt, w.erec, g_ablate));
     JB_TIMED(K_SCAN_BLOCKS, hipLaunchKernelGGL(k_scan2, dim3(1), dim3(1024), 0, stream, w.tile_cnt, ntiles,
                                                w.tile_off, w.counters + CNT_NBLK, nullptr, w.blk,
                                                (uint32_t)nbytes));
-    JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL(k_blocks_write, dim3(ntiles), dim3(256), 0, stream,
-                                                reinterpret_cast<const uint32_t*>(w.erec),
+    JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL(k_blocks_write, dim3(ntiles), dim3(256), 0, stream, w.lanemask,
                                                 w.tile_off, w.blk, w.lists, list_cap));
-    JB_TIMED(K_WALK, hipLaunchKernelGGL(k_walk, dim3((uint32_t)((nbytes + 4 * 1024 - 1) / (4 * 1024))), dim3(256), 0, stream,
-                                        d_text, nbytes, w.docbits, im, w.erec, g_ablate));
     if (hmm)
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
                                           w.lists, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,

@@ -225,3 +225,52 @@ def test_device_api_and_profile(small):
     gd = J.dev_to_host(pd, 8 * len(off), np.uint64)
     hs, he, hd = tk.cut_batch(buf, off, True)
     assert np.array_equal(gs, hs) and np.array_equal(ge, he) and np.array_equal(gd, hd)
+
+
+@pytest.mark.parametrize("kind", [J.JB_DICT_TXT, J.JB_DICT_PREFIX])
+def test_record_overflow_paths(tmp_path, syn_small, kind):
+    """Dictionaries that push k_walk's packed records past their limits: runes
+    with more than 4 edges, edges longer than 8 runes (k_zh's redo with the
+    global best array) and more than 2^14 distinct weights (14-bit indices)."""
+    _, ep, _ = syn_small
+    rng = random.Random(11)
+    pool = [chr(c) for c in range(0x4E00, 0x4E00 + 600)]
+    lines, seqs = [], []
+    f = 7
+    for _ in range(40):  # nested chains: every prefix of a 6..24-rune string is a word
+        s = "".join(rng.choice(pool) for _ in range(rng.randint(6, 24)))
+        seqs.append(s)
+        for k in range(1, len(s) + 1):
+            if rng.random() < 0.8:
+                f += rng.randint(1, 5)
+                lines.append(f"{s[:k]} {f}")
+    fill = []
+    for i in range(20000):  # distinct frequencies -> > 2^14 weights
+        w = rng.choice(pool) + rng.choice(pool) + (rng.choice(pool) if i % 3 == 0 else "")
+        fill.append(w)
+        lines.append(f"{w} {1000 + 3 * i}")
+    dp = tmp_path / "dict.txt"
+    dp.write_text("\n".join(lines) + "\n", encoding="utf-8")
+    tk, o = _pair(str(dp), ep, kind=kind, size_override=60101967 if kind == J.JB_DICT_PREFIX else 0)
+    try:
+        texts = []
+        for _ in range(400):
+            parts = []
+            for _ in range(rng.randint(1, 12)):
+                r = rng.random()
+                if r < 0.35:
+                    s = rng.choice(seqs)
+                    parts.append(s[: rng.randint(1, len(s))])
+                elif r < 0.7:
+                    parts.append(rng.choice(fill))
+                elif r < 0.9:
+                    parts.append("".join(rng.choice(pool) for _ in range(rng.randint(1, 6))))
+                else:
+                    parts.append(rng.choice(["，", "。", " ab12 ", "\n"]))
+            texts.append("".join(parts))
+        texts.append("".join(seqs))  # one long block through every chain
+        buf, off = _batch_of(texts)
+        for hmm in (False, True):
+            _cmp_batch(tk, o, buf, off, hmm, f"overflow kind={kind} hmm={hmm}")
+    finally:
+        tk.close()
