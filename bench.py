@@ -72,7 +72,9 @@ def main():
                          "reference's own benchmarks; txt: NewTokenizer(dict.txt)")
     ap.add_argument("--cpu-sample-mib", type=float, default=128.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu1-sample-mib", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
 
@@ -195,6 +197,28 @@ def main():
         ge = J.dev_to_host(pe, 4 * k1, np.uint32)
         ok = bool(np.array_equal(gs, os_) and np.array_equal(ge, oe) and np.array_equal(gd[: dend + 1], od))
         parity = {"docs": dend, "tokens": int(len(os_)), "bit_exact": ok, "gpu_tokens_total": ntok}
+        # one-thread oracle on a smaller sample (SURVEY.md §8d asks for 1 and n threads)
+        d1 = max(1, min(ndocs, int(np.searchsorted(off, min(int(args.cpu1_sample_mib * (1 << 20)), nbytes),
+                                                   side="right")) - 1))
+        b1 = int(off[d1])
+        r1 = int(np.count_nonzero((buf[:b1] & 0xC0) != 0x80))
+        tc = time.perf_counter()
+        o.cut_batch(buf[: b1 + 16], off[: d1 + 1], bool(args.hmm), nthreads=1)
+        c1 = time.perf_counter() - tc
+        cpu["value_1thread"] = round(r1 / c1, 1)
+        cpu["sample_1thread"] = f"first {d1} documents ({b1 / 2**20:.1f} MiB, {r1} chars), 1 thread, {c1:.2f} s"
+        del o
+
+    # ---- end to end from host memory (PCIe in and out; rank 0, N = 1) -------
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        tk.cut_batch(buf, off, bool(args.hmm))  # warm the host-side staging
+        te = time.perf_counter()
+        for _ in range(2):
+            tk.cut_batch(buf, off, bool(args.hmm))
+        e2e_s = (time.perf_counter() - te) / 2
+        e2e = {"value": round(nrunes / e2e_s, 1), "unit": "chars/s", "ms": round(e2e_s * 1e3, 2),
+               "what": "jb_cut_batch on host buffers: H2D text + offsets, all kernels, D2H spans as u64"}
 
     if rank == 0:
         line = {
@@ -210,6 +234,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity_sample": parity,
+            "end_to_end_host": e2e,
             "han_chars_per_s": round(tot_han / 3 * args.steps / elapsed, 1),
             "input_GBps": round(tot_bytes * args.steps / elapsed / 1e9, 3),
             "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},

@@ -1,0 +1,170 @@
+// Package jiebahip is the drop-in Go front end of the MI355X segmentation path:
+// the API of github.com/ericlingit/jieba-go's Tokenizer (tokenizer.go:52-162,
+// 372-379) over the C ABI of libjiebahip.so (include/jiebahip.h).
+//
+// Not built in the development image (no Go toolchain there); see
+// INTEGRATION.md for how a maintainer wires it into the reference module.
+package jiebahip
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../include
+#cgo LDFLAGS: -L${SRCDIR}/../lib -ljiebahip -Wl,-rpath,${SRCDIR}/../lib
+#include <stdlib.h>
+#include "jiebahip.h"
+*/
+import "C"
+
+import (
+	"log"
+	"runtime"
+	"sync"
+	"unsafe"
+)
+
+// JiebaSize is the total count NewJiebaTokenizer uses (tokenizer.go:454).
+const JiebaSize = 60101967
+
+// Tokenizer mirrors the reference's Tokenizer: safe for concurrent Cut calls,
+// AddWord takes the exclusive lock (tokenizer.go:82-83,152-153,376).
+type Tokenizer struct {
+	mu  sync.RWMutex
+	ctx *C.jb_ctx
+}
+
+func lastError() string { return C.GoString(C.jb_last_error()) }
+
+func open(dictPath, emitPath string, kind C.int, size int64) *Tokenizer {
+	cd := C.CString(dictPath)
+	ce := C.CString(emitPath)
+	defer C.free(unsafe.Pointer(cd))
+	defer C.free(unsafe.Pointer(ce))
+	var cfg C.jb_config
+	cfg.dict_path = cd
+	cfg.emit_path = ce
+	cfg.dict_kind = kind
+	cfg.size_override = C.int64_t(size)
+	cfg.device = 0
+	cfg.ndevices = 1
+	var ctx *C.jb_ctx
+	if rc := C.jb_open(&cfg, &ctx); rc != C.JB_OK {
+		// the reference stops the process on load errors (tokenizer.go:397,443,656)
+		log.Fatal("jiebahip: ", lastError())
+	}
+	t := &Tokenizer{ctx: ctx}
+	runtime.SetFinalizer(t, (*Tokenizer).Close)
+	return t
+}
+
+// NewTokenizer loads a dict.txt-format dictionary (tokenizer.go:61).
+func NewTokenizer(dictionaryFile string) *Tokenizer {
+	return open(dictionaryFile, "prob_emit.json", C.JB_DICT_TXT, 0)
+}
+
+// NewJiebaTokenizer is the reference's default tokenizer (tokenizer.go:69).
+// The reference decodes prefix_dictionary.gob; this reads dict.txt with the
+// same semantics (prefix entries, last value wins, size 60,101,967).
+func NewJiebaTokenizer() *Tokenizer {
+	return open("dict.txt", "prob_emit.json", C.JB_DICT_PREFIX, JiebaSize)
+}
+
+// Close releases the device context.
+func (t *Tokenizer) Close() {
+	t.mu.Lock()
+	defer t.mu.Unlock()
+	if t.ctx != nil {
+		C.jb_close(t.ctx)
+		t.ctx = nil
+	}
+}
+
+func spansToTokens(text string, s *C.jb_spans, doc int) []string {
+	n := int(s.ntokens)
+	starts := unsafe.Slice((*uint64)(unsafe.Pointer(s.start)), n)
+	ends := unsafe.Slice((*uint64)(unsafe.Pointer(s.end)), n)
+	docTok := unsafe.Slice((*uint64)(unsafe.Pointer(s.doc_tok)), int(s.ndocs)+1)
+	a, b := int(docTok[doc]), int(docTok[doc+1])
+	out := make([]string, 0, b-a)
+	for k := a; k < b; k++ {
+		st, en := int(starts[k]), int(ends[k])
+		if en-st == 1 && text[st] >= 0x80 {
+			out = append(out, "�") // invalid UTF-8 byte (tokenizer.go:301-306)
+		} else {
+			out = append(out, text[st:en])
+		}
+	}
+	return out
+}
+
+// Cut segments one text (tokenizer.go:151).  Never returns nil.
+func (t *Tokenizer) Cut(text string, useHmm bool) []string {
+	t.mu.RLock()
+	defer t.mu.RUnlock()
+	if len(text) == 0 {
+		return []string{}
+	}
+	b := []byte(text)
+	hmm := C.int(0)
+	if useHmm {
+		hmm = 1
+	}
+	var s C.jb_spans
+	if rc := C.jb_cut(t.ctx, (*C.uint8_t)(unsafe.Pointer(&b[0])), C.size_t(len(b)), hmm, &s); rc != C.JB_OK {
+		// JB_EPANIC: the reference panics on this input (cutDAG slice with tail -1)
+		panic("jiebahip: " + lastError())
+	}
+	defer C.jb_spans_free(&s)
+	return spansToTokens(text, &s, 0)
+}
+
+// CutParallel (tokenizer.go:81) returns the tokens of Cut in document order;
+// the device splits the work itself, numWorkers is accepted for API parity.
+// ordered=false allows any block order in the reference; this order is one of them.
+func (t *Tokenizer) CutParallel(text string, hmm bool, numWorkers int, ordered bool) []string {
+	return t.Cut(text, hmm)
+}
+
+// CutBatch segments many documents in one device call (the batched form of Cut).
+func (t *Tokenizer) CutBatch(docs []string, useHmm bool) [][]string {
+	t.mu.RLock()
+	defer t.mu.RUnlock()
+	total := 0
+	for _, d := range docs {
+		total += len(d)
+	}
+	buf := make([]byte, 0, total+1)
+	off := make([]uint64, len(docs)+1)
+	for i, d := range docs {
+		buf = append(buf, d...)
+		off[i+1] = uint64(len(buf))
+	}
+	buf = append(buf, 0)
+	hmm := C.int(0)
+	if useHmm {
+		hmm = 1
+	}
+	var s C.jb_spans
+	if rc := C.jb_cut_batch(t.ctx, (*C.uint8_t)(unsafe.Pointer(&buf[0])), (*C.uint64_t)(unsafe.Pointer(&off[0])),
+		C.uint32_t(len(docs)), hmm, &s); rc != C.JB_OK {
+		panic("jiebahip: " + lastError())
+	}
+	defer C.jb_spans_free(&s)
+	all := string(buf[:total])
+	out := make([][]string, len(docs))
+	for i := range docs {
+		out[i] = spansToTokens(all, &s, i) // tokens share one copy of the batch text
+	}
+	return out
+}
+
+// AddWord adds or updates a word (tokenizer.go:372).  freq < 1 takes
+// suggestFreq's value (tokenizer.go:589-614).  Unlike the reference it does
+// not deadlock.
+func (t *Tokenizer) AddWord(word string, freq int) {
+	t.mu.Lock()
+	defer t.mu.Unlock()
+	cw := C.CString(word)
+	defer C.free(unsafe.Pointer(cw))
+	if rc := C.jb_add_word(t.ctx, cw, C.size_t(len(word)), C.int64_t(freq)); rc != C.JB_OK {
+		log.Fatal("jiebahip: ", lastError())
+	}
+}

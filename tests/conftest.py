@@ -71,3 +71,19 @@ def real_data_dir():
             if hashlib.sha256(f.read()).hexdigest() != want[name]:
                 return None
     return d
+
+
+@pytest.fixture(scope="session")
+def syn_golden(tmp_path_factory):
+    """Committed golden vectors (tests/golden/syn_golden.json) and the regenerated
+    synthetic data files they were made on (checked by sha256)."""
+    import base64
+    import hashlib
+    with open(os.path.join(GOLDEN, "syn_golden.json")) as f:
+        g = json.load(f)
+    dp, ep, _ = _syn_files(tmp_path_factory, g["nwords"], "syn_golden")
+    for name, p in (("dict.txt", dp), ("prob_emit.json", ep)):
+        with open(p, "rb") as f:
+            assert hashlib.sha256(f.read()).hexdigest() == g["sha256"][name], f"generator output changed: {name}"
+    docs = [base64.b64decode(d) for d in g["docs_b64"]]
+    return g, docs, dp, ep

@@ -274,3 +274,24 @@ def test_record_overflow_paths(tmp_path, syn_small, kind):
             _cmp_batch(tk, o, buf, off, hmm, f"overflow kind={kind} hmm={hmm}")
     finally:
         tk.close()
+
+
+def test_synthetic_golden_vectors(syn_golden):
+    """The GPU path reproduces the committed golden vectors (oracle output frozen in tests/golden)."""
+    g, docs, dp, ep = syn_golden
+    buf, off = _batch_of(docs)
+    for kind, size in ((J.JB_DICT_TXT, 0), (J.JB_DICT_PREFIX, 60101967)):
+        tk = J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep, kind=kind, size_override=size))
+        try:
+            for hmm in (False, True):
+                gs, ge, gd = tk.cut_batch(buf, off, hmm)
+                for c in g["cases"]:
+                    if c["kind"] != kind or c["hmm"] != hmm:
+                        continue
+                    d = c["doc"]
+                    a, b = int(gd[d]), int(gd[d + 1])
+                    base = int(off[d])
+                    assert (gs[a:b] - base).tolist() == c["starts"], (kind, hmm, d)
+                    assert (ge[a:b] - base).tolist() == c["ends"], (kind, hmm, d)
+        finally:
+            tk.close()

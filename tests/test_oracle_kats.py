@@ -195,3 +195,15 @@ def test_batch_equals_per_doc(syn_small):
             s1, e1 = o.cut_spans(bytes(buf[a:b]), hmm)
             k0, k1 = int(tdo[d]), int(tdo[d + 1])
             assert np.array_equal(st[k0:k1], s1 + a) and np.array_equal(en[k0:k1], e1 + a)
+
+
+def test_oracle_reproduces_synthetic_golden(syn_golden):
+    """The oracle still produces the committed golden spans (tests/golden/make_golden.py)."""
+    g, docs, dp, ep = syn_golden
+    oracles = {}
+    for c in g["cases"]:
+        key = (c["kind"], c["size"])
+        if key not in oracles:
+            oracles[key] = O.Oracle.from_files(dp, ep, c["kind"], c["size"])
+        s, e = oracles[key].cut_spans(docs[c["doc"]], c["hmm"])
+        assert s.tolist() == c["starts"] and e.tolist() == c["ends"], (c["kind"], c["hmm"], c["doc"])

@@ -25,6 +25,6 @@ done
 if [ "${PROF:-1}" = "1" ]; then
   echo "== rocprofv3"
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-      python3 bench.py --steps 5 --warmup 1 --no-cpu ${BENCH_ARGS:-} > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+      python3 bench.py --steps 5 --warmup 1 --no-cpu --no-e2e ${BENCH_ARGS:-} > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
 fi
 echo "== done"
