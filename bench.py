@@ -54,7 +54,10 @@ def load_pmc_traffic(kernel):
     try:
         with open(p) as f:
             d = json.load(f)
-        return d["kernels"][kernel]["hbm_bytes_per_launch"]
+        for name, e in d["kernels"].items():  # e.g. "k_zh<true>" for kernel "k_zh"
+            if name == kernel or name.startswith(kernel + "<"):
+                return e["hbm_bytes_per_launch"]
+        return None
     except Exception:
         return None
 
