@@ -89,6 +89,14 @@ int jb_cut_batch(jb_ctx *ctx, const uint8_t *text, const uint64_t *doc_off, uint
                  jb_spans *out);
 void jb_spans_free(jb_spans *s);
 
+/* jb_cut_batch into caller-owned arrays (no library allocation; what a Go
+ * caller passes as slices): start/end hold up to `cap` tokens, doc_tok ndocs+1
+ * entries.  *ntokens receives the token count; when it exceeds cap the call
+ * returns JB_ELIMIT with *ntokens set and the caller retries with bigger arrays
+ * (a batch of n bytes never has more than n tokens). */
+int jb_cut_batch_into(jb_ctx *ctx, const uint8_t *text, const uint64_t *doc_off, uint32_t ndocs, int hmm,
+                      uint64_t *start, uint64_t *end, uint64_t cap, uint64_t *doc_tok, uint64_t *ntokens);
+
 /* Device-resident form for pipelines and benchmarks: d_text (nbytes, plus 64
  * readable padding bytes; 16-byte aligned) and d_doc_off (ndocs+1 offsets, d_doc_off[0] == 0,
  * d_doc_off[ndocs] == nbytes) are device pointers on ctx's first device; the

@@ -118,6 +118,14 @@ struct Device {
     uint64_t* doc_off = nullptr;
     uint64_t text_cap = 0;
     uint32_t doc_cap = 0;
+    // pinned host staging for host batches (full-speed DMA both ways)
+    uint8_t* h_text = nullptr;
+    uint64_t h_text_cap = 0;
+    uint32_t* h_span = nullptr;  // starts then ends, u32
+    uint64_t h_span_cap = 0;     // tokens
+    uint64_t* h_misc = nullptr;  // doc offsets in / doc_tok out (u64)
+    uint64_t h_misc_cap = 0;
+    uint32_t* h_cnt = nullptr;   // counters (64 u32)
     uint32_t ncu = 0;
     EventTimer timer;
     bool profile = false;
@@ -126,6 +134,77 @@ struct Device {
 void dfree(void* p) {
     if (p) (void)hipFree(p);
 }
+void hfree(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+// memcpy with a few host threads for large copies (staging into pinned memory)
+void par_copy(void* dst, const void* src, size_t n) {
+    const size_t kMin = 8u << 20;
+    const unsigned nt = (unsigned)std::min<size_t>(8, std::max<size_t>(1, n / kMin));
+    if (nt <= 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (n + nt - 1) / nt;
+    for (unsigned k = 0; k < nt; k++) {
+        const size_t a = k * per, b = std::min(n, a + per);
+        if (a < b) th.emplace_back([=] { memcpy((char*)dst + a, (const char*)src + a, b - a); });
+    }
+    for (auto& t : th) t.join();
+}
+
+// out[k] = base + in[k] (u32 device spans -> u64 batch offsets), a few threads when large
+void par_widen(uint64_t* out, const uint32_t* in, size_t n, uint64_t base) {
+    const size_t kMin = 2u << 20;
+    const unsigned nt = (unsigned)std::min<size_t>(8, std::max<size_t>(1, n / kMin));
+    auto run = [=](size_t a, size_t b) {
+        for (size_t k = a; k < b; k++) out[k] = base + in[k];
+    };
+    if (nt <= 1) {
+        run(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (n + nt - 1) / nt;
+    for (unsigned k = 0; k < nt; k++) {
+        const size_t a = k * per, b = std::min(n, a + per);
+        if (a < b) th.emplace_back(run, a, b);
+    }
+    for (auto& t : th) t.join();
+}
+
+// growable malloc'd span arrays (handed to the caller as jb_spans)
+struct SpanBuf {
+    uint64_t* s = nullptr;
+    uint64_t* e = nullptr;
+    size_t n = 0, cap = 0;
+    bool external = false;          // caller-owned arrays of fixed capacity
+    size_t needed = 0;              // tokens that did not fit an external buffer
+    std::vector<uint64_t> per_doc;  // tokens per document
+    bool reserve(size_t want) {
+        if (want <= cap) return true;
+        if (external) return false;
+        const size_t nc = std::max(want, cap * 3 / 2 + 1024);
+        uint64_t* ns = (uint64_t*)realloc(s, nc * 8);
+        if (!ns) return false;
+        s = ns;
+        uint64_t* ne = (uint64_t*)realloc(e, nc * 8);
+        if (!ne) return false;
+        e = ne;
+        cap = nc;
+        return true;
+    }
+    void release() {
+        if (!external) {
+            free(s);
+            free(e);
+        }
+        s = e = nullptr;
+        n = cap = 0;
+    }
+};
 
 }  // namespace
 
@@ -315,6 +394,31 @@ static int ensure_staging(Device* d, uint64_t nbytes, uint32_t ndocs) {
         HIPCHK(hipMalloc(&d->doc_off, (uint64_t)cap * 8));
         d->doc_cap = cap;
     }
+    if (nbytes + 64 > d->h_text_cap) {
+        hfree(d->h_text);
+        d->h_text = nullptr;
+        const uint64_t cap = std::max<uint64_t>(nbytes + 64, d->h_text_cap * 3 / 2);
+        HIPCHK(hipHostMalloc(&d->h_text, cap, hipHostMallocDefault));
+        d->h_text_cap = cap;
+    }
+    if (ndocs + 2 > d->h_misc_cap) {
+        hfree(d->h_misc);
+        d->h_misc = nullptr;
+        const uint64_t cap = std::max<uint64_t>(ndocs + 2, d->h_misc_cap * 3 / 2);
+        HIPCHK(hipHostMalloc(&d->h_misc, cap * 8, hipHostMallocDefault));
+        d->h_misc_cap = cap;
+    }
+    if (!d->h_cnt) HIPCHK(hipHostMalloc(&d->h_cnt, 64 * 4, hipHostMallocDefault));
+    return JB_OK;
+}
+
+static int ensure_span_staging(Device* d, uint64_t ntok) {
+    if (ntok <= d->h_span_cap) return JB_OK;
+    hfree(d->h_span);
+    d->h_span = nullptr;
+    const uint64_t cap = std::max<uint64_t>(ntok, d->h_span_cap * 3 / 2);
+    HIPCHK(hipHostMalloc(&d->h_span, cap * 8, hipHostMallocDefault));
+    d->h_span_cap = cap;
     return JB_OK;
 }
 
@@ -374,6 +478,7 @@ extern "C" void jb_close(jb_ctx* ctx) {
         free_work(&d->w);
         dfree(d->text); dfree(d->doc_off); dfree(d->pagemap); dfree(d->l1); dfree(d->emit); dfree(d->nodes);
         dfree(d->wtab);
+        hfree(d->h_text); hfree(d->h_span); hfree(d->h_misc); hfree(d->h_cnt);
         (void)hipStreamDestroy(d->stream);
     }
     delete ctx;
@@ -386,15 +491,14 @@ extern "C" const char* jb_last_error(void) { return g_err.c_str(); }
 // ---------------------------------------------------------------------------
 static const uint64_t kChunkBytes = 1ull << 30;  // device offsets are u32 with a zh flag bit
 
-// Cut documents [d0, d1) of a host batch on one device; appends spans.
+// Cut documents [d0, d1) of a host batch on one device; appends spans to `out`.
+// Host text goes through pinned staging (full-speed DMA), spans come back into
+// pinned memory and are widened to u64 batch offsets in place in `out`.
 static int cut_range(jb_ctx* ctx, Device* d, const uint8_t* text, const uint64_t* doc_off, uint32_t d0, uint32_t d1,
-                     bool hmm, std::vector<uint64_t>* st, std::vector<uint64_t>* en, std::vector<uint64_t>* per_doc) {
+                     bool hmm, SpanBuf* out) {
     std::lock_guard<std::mutex> g(d->mu);
     HIPCHK(hipSetDevice(d->ordinal));
     uint32_t a = d0;
-    std::vector<uint64_t> off;
-    std::vector<uint32_t> hs, he;
-    std::vector<uint64_t> hdt;
     while (a < d1) {
         // whole documents up to kChunkBytes (a single larger document is an error)
         uint32_t b = a + 1;
@@ -407,51 +511,54 @@ static int cut_range(jb_ctx* ctx, Device* d, const uint8_t* text, const uint64_t
         int rc;
         if ((rc = ensure_staging(d, nbytes, nd))) return rc;
         if ((rc = ensure_work(d, nbytes, nd))) return rc;
-        off.resize(nd + 1);
-        for (uint32_t k = 0; k <= nd; k++) off[k] = doc_off[a + k] - base;
-        HIPCHK(hipMemcpyAsync(d->text, text + base, nbytes, hipMemcpyHostToDevice, d->stream));
-        HIPCHK(hipMemsetAsync(d->text + nbytes, 0, 64, d->stream));
-        HIPCHK(hipMemcpyAsync(d->doc_off, off.data(), (nd + 1) * 8, hipMemcpyHostToDevice, d->stream));
+        par_copy(d->h_text, text + base, nbytes);
+        memset(d->h_text + nbytes, 0, 64);
+        for (uint32_t k = 0; k <= nd; k++) d->h_misc[k] = doc_off[a + k] - base;
+        HIPCHK(hipMemcpyAsync(d->text, d->h_text, nbytes + 64, hipMemcpyHostToDevice, d->stream));
+        HIPCHK(hipMemcpyAsync(d->doc_off, d->h_misc, (nd + 1) * 8, hipMemcpyHostToDevice, d->stream));
         if ((rc = launch(ctx, d, d->text, nbytes, d->doc_off, nd, hmm, d->stream))) return rc;
-        uint32_t cnt[8];
-        HIPCHK(hipMemcpyAsync(cnt, d->w.counters, sizeof cnt, hipMemcpyDeviceToHost, d->stream));
+        HIPCHK(hipMemcpyAsync(d->h_cnt, d->w.counters, 8 * 4, hipMemcpyDeviceToHost, d->stream));
         HIPCHK(hipStreamSynchronize(d->stream));
-        if (cnt[CNT_ERR]) return fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)");
-        if (cnt[CNT_NTOK] != cnt[CNT_NTOKE])
-            return fail(JB_EDEVICE, "internal: %u token starts vs %u ends", cnt[CNT_NTOK], cnt[CNT_NTOKE]);
-        const uint32_t nt = cnt[CNT_NTOK];
-        hs.resize(nt);
-        he.resize(nt);
-        hdt.resize(nd + 1);
+        if (d->h_cnt[CNT_ERR]) return fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)");
+        if (d->h_cnt[CNT_NTOK] != d->h_cnt[CNT_NTOKE])
+            return fail(JB_EDEVICE, "internal: %u token starts vs %u ends", d->h_cnt[CNT_NTOK], d->h_cnt[CNT_NTOKE]);
+        const uint32_t nt = d->h_cnt[CNT_NTOK];
+        if ((rc = ensure_span_staging(d, nt))) return rc;
         if (nt) {
-            HIPCHK(hipMemcpyAsync(hs.data(), d->w.tok_start, (uint64_t)nt * 4, hipMemcpyDeviceToHost, d->stream));
-            HIPCHK(hipMemcpyAsync(he.data(), d->w.tok_end, (uint64_t)nt * 4, hipMemcpyDeviceToHost, d->stream));
+            HIPCHK(hipMemcpyAsync(d->h_span, d->w.tok_start, (uint64_t)nt * 4, hipMemcpyDeviceToHost, d->stream));
+            HIPCHK(hipMemcpyAsync(d->h_span + nt, d->w.tok_end, (uint64_t)nt * 4, hipMemcpyDeviceToHost, d->stream));
         }
-        HIPCHK(hipMemcpyAsync(hdt.data(), d->w.doc_tok, (uint64_t)(nd + 1) * 8, hipMemcpyDeviceToHost, d->stream));
+        HIPCHK(hipMemcpyAsync(d->h_misc, d->w.doc_tok, (uint64_t)(nd + 1) * 8, hipMemcpyDeviceToHost, d->stream));
         HIPCHK(hipStreamSynchronize(d->stream));
-        const size_t o = st->size();
-        st->resize(o + nt);
-        en->resize(o + nt);
-        for (uint32_t k = 0; k < nt; k++) {
-            (*st)[o + k] = base + hs[k];
-            (*en)[o + k] = base + he[k];
+        if (!out->reserve(out->n + nt)) {
+            if (out->external) {  // count the rest, write nothing more
+                out->needed = out->n + nt;
+                out->n += nt;
+                out->cap = 0;
+                a = b;
+                continue;
+            }
+            return fail(JB_ENOMEM, "out of host memory for %u tokens", nt);
         }
-        for (uint32_t k = 0; k < nd; k++) per_doc->push_back(hdt[k + 1] - hdt[k]);
+        par_widen(out->s + out->n, d->h_span, nt, base);
+        par_widen(out->e + out->n, d->h_span + nt, nt, base);
+        out->n += nt;
+        for (uint32_t k = 0; k < nd; k++) out->per_doc.push_back(d->h_misc[k + 1] - d->h_misc[k]);
         a = b;
     }
     return JB_OK;
 }
 
-extern "C" int jb_cut_batch(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off, uint32_t ndocs, int hmm,
-                            jb_spans* out) {
-    if (!ctx || !out || (!doc_off && ndocs)) return fail(JB_EINVAL, "jb_cut_batch: null argument");
-    memset(out, 0, sizeof *out);
+// Shard [0, ndocs) over the devices (contiguous byte-balanced ranges) and cut.
+// sb[k] receives device k's spans; ext (optional) makes device 0 write into
+// caller-owned arrays when there is a single device.
+static int cut_sharded(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off, uint32_t ndocs, int hmm,
+                       std::vector<SpanBuf>* sbp) {
     for (uint32_t k = 0; k < ndocs; k++)
         if (doc_off[k + 1] < doc_off[k]) return fail(JB_EINVAL, "doc_off not monotonic at %u", k);
     if (ndocs && !text && doc_off[ndocs] > doc_off[0]) return fail(JB_EINVAL, "null text");
-    std::shared_lock<std::shared_mutex> rl(ctx->lock);
+    std::vector<SpanBuf>& sb = *sbp;
     const size_t nd = ctx->devs.size();
-    // contiguous byte-balanced document ranges, one per device
     std::vector<uint32_t> cut(nd + 1, ndocs);
     cut[0] = 0;
     const uint64_t total = ndocs ? doc_off[ndocs] - doc_off[0] : 0;
@@ -461,13 +568,11 @@ extern "C" int jb_cut_batch(jb_ctx* ctx, const uint8_t* text, const uint64_t* do
         while (lo < ndocs && doc_off[lo + 1] <= target) lo++;
         cut[k] = lo;
     }
-    std::vector<std::vector<uint64_t>> st(nd), en(nd), pd(nd);
     std::vector<int> rcs(nd, JB_OK);
     std::vector<std::string> errs(nd);
     auto work = [&](size_t k) {
         if (cut[k] < cut[k + 1]) {
-            rcs[k] = cut_range(ctx, ctx->devs[k].get(), text, doc_off, cut[k], cut[k + 1], hmm != 0, &st[k], &en[k],
-                               &pd[k]);
+            rcs[k] = cut_range(ctx, ctx->devs[k].get(), text, doc_off, cut[k], cut[k + 1], hmm != 0, &sb[k]);
             if (rcs[k]) errs[k] = g_err;
         }
     };
@@ -480,32 +585,114 @@ extern "C" int jb_cut_batch(jb_ctx* ctx, const uint8_t* text, const uint64_t* do
     }
     for (size_t k = 0; k < nd; k++)
         if (rcs[k]) return fail(rcs[k], "%s", errs[k].c_str());
+    return JB_OK;
+}
+
+static void fill_doc_tok(const std::vector<SpanBuf>& sb, uint32_t ndocs, uint64_t* doc_tok) {
+    uint64_t w = 0, di = 0;
+    doc_tok[0] = 0;
+    for (const auto& b : sb) {
+        uint64_t acc = w;
+        for (uint64_t c : b.per_doc) {
+            acc += c;
+            doc_tok[++di] = acc;
+        }
+        w += b.n;
+    }
+    while (di < ndocs) doc_tok[++di] = w;
+}
+
+extern "C" int jb_cut_batch(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off, uint32_t ndocs, int hmm,
+                            jb_spans* out) {
+    if (!ctx || !out || (!doc_off && ndocs)) return fail(JB_EINVAL, "jb_cut_batch: null argument");
+    memset(out, 0, sizeof *out);
+    std::shared_lock<std::shared_mutex> rl(ctx->lock);
+    const size_t nd = ctx->devs.size();
+    std::vector<SpanBuf> sb(nd);
+    auto release_all = [&] {
+        for (auto& b : sb) b.release();
+    };
+    int rc = cut_sharded(ctx, text, doc_off, ndocs, hmm, &sb);
+    if (rc) {
+        release_all();
+        return rc;
+    }
     uint64_t nt = 0;
-    for (size_t k = 0; k < nd; k++) nt += st[k].size();
+    for (size_t k = 0; k < nd; k++) nt += sb[k].n;
     out->ntokens = nt;
     out->ndocs = ndocs;
-    out->start = (uint64_t*)malloc(std::max<uint64_t>(nt, 1) * 8);
-    out->end = (uint64_t*)malloc(std::max<uint64_t>(nt, 1) * 8);
     out->doc_tok = (uint64_t*)malloc(((uint64_t)ndocs + 1) * 8);
+    if (nd == 1 || nt == sb[0].n) {  // one device's buffers are the result
+        out->start = sb[0].s ? sb[0].s : (uint64_t*)malloc(8);
+        out->end = sb[0].e ? sb[0].e : (uint64_t*)malloc(8);
+        sb[0].s = sb[0].e = nullptr;
+    } else {
+        out->start = (uint64_t*)malloc(std::max<uint64_t>(nt, 1) * 8);
+        out->end = (uint64_t*)malloc(std::max<uint64_t>(nt, 1) * 8);
+        if (out->start && out->end) {
+            uint64_t w = 0;
+            for (size_t k = 0; k < nd; k++) {
+                if (sb[k].n) {
+                    memcpy(out->start + w, sb[k].s, sb[k].n * 8);
+                    memcpy(out->end + w, sb[k].e, sb[k].n * 8);
+                }
+                w += sb[k].n;
+            }
+        }
+    }
     if (!out->start || !out->end || !out->doc_tok) {
+        release_all();
         jb_spans_free(out);
         return fail(JB_ENOMEM, "out of host memory for %llu tokens", (unsigned long long)nt);
     }
-    uint64_t w = 0, di = 0;
-    out->doc_tok[0] = 0;
-    for (size_t k = 0; k < nd; k++) {
-        if (!st[k].empty()) {
-            memcpy(out->start + w, st[k].data(), st[k].size() * 8);
-            memcpy(out->end + w, en[k].data(), en[k].size() * 8);
-        }
-        uint64_t acc = w;
-        for (uint64_t c : pd[k]) {
-            acc += c;
-            out->doc_tok[++di] = acc;
-        }
-        w += st[k].size();
+    fill_doc_tok(sb, ndocs, out->doc_tok);
+    release_all();
+    return JB_OK;
+}
+
+extern "C" int jb_cut_batch_into(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off, uint32_t ndocs,
+                                 int hmm, uint64_t* start, uint64_t* end, uint64_t cap, uint64_t* doc_tok,
+                                 uint64_t* ntokens) {
+    if (!ctx || !ntokens || !doc_tok || (!doc_off && ndocs) || (cap && (!start || !end)))
+        return fail(JB_EINVAL, "jb_cut_batch_into: null argument");
+    *ntokens = 0;
+    std::shared_lock<std::shared_mutex> rl(ctx->lock);
+    const size_t nd = ctx->devs.size();
+    std::vector<SpanBuf> sb(nd);
+    if (nd == 1) {  // the device writes straight into the caller's arrays
+        sb[0].s = start;
+        sb[0].e = end;
+        sb[0].cap = cap;
+        sb[0].external = true;
     }
-    while (di < ndocs) out->doc_tok[++di] = w;
+    auto release_all = [&] {
+        for (auto& b : sb) b.release();
+    };
+    int rc = cut_sharded(ctx, text, doc_off, ndocs, hmm, &sb);
+    if (rc) {
+        release_all();
+        return rc;
+    }
+    uint64_t nt = 0;
+    for (size_t k = 0; k < nd; k++) nt += sb[k].n;
+    *ntokens = nt;
+    if (nt > cap) {
+        release_all();
+        return fail(JB_ELIMIT, "%llu tokens do not fit the %llu-token output arrays", (unsigned long long)nt,
+                    (unsigned long long)cap);
+    }
+    if (nd > 1) {
+        uint64_t w = 0;
+        for (size_t k = 0; k < nd; k++) {
+            if (sb[k].n) {
+                memcpy(start + w, sb[k].s, sb[k].n * 8);
+                memcpy(end + w, sb[k].e, sb[k].n * 8);
+            }
+            w += sb[k].n;
+        }
+    }
+    fill_doc_tok(sb, ndocs, doc_tok);
+    release_all();
     return JB_OK;
 }
 

@@ -24,7 +24,8 @@ JIEBA_SIZE = 60_101_967  # tokenizer.go:454
 
 # Every symbol include/jiebahip.h declares.
 EXPORTS = [
-    "jb_open", "jb_close", "jb_last_error", "jb_cut", "jb_cut_batch", "jb_spans_free", "jb_cut_device",
+    "jb_open", "jb_close", "jb_last_error", "jb_cut", "jb_cut_batch", "jb_cut_batch_into", "jb_spans_free",
+    "jb_cut_device",
     "jb_add_word", "jb_dict_get", "jb_dict_size", "jb_profile_enable", "jb_profile_read", "jb_profile_reset",
     "jb_image_build", "jb_image_free", "jb_image_lookup", "jb_image_stats", "jb_image_emit", "jb_go_log",
 ]
@@ -78,6 +79,8 @@ def lib():
         L.jb_last_error.restype = cp
         L.jb_cut.argtypes = [vp, vp, C.c_size_t, C.c_int, C.POINTER(jb_spans)]
         L.jb_cut_batch.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, C.POINTER(jb_spans)]
+        L.jb_cut_batch_into.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, vp, vp, C.c_uint64, vp,
+                                        C.POINTER(C.c_uint64)]
         L.jb_spans_free.argtypes = [C.POINTER(jb_spans)]
         L.jb_spans_free.restype = None
         L.jb_cut_device.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_int, vp, C.POINTER(vp), C.POINTER(vp),
@@ -254,6 +257,29 @@ class Tokenizer:
         finally:
             lib().jb_spans_free(C.byref(sp))
         return s, e, d
+
+    def cut_batch_into(self, buf, doc_off, hmm, out=None):
+        """Host batch into caller-owned arrays (jb_cut_batch_into).  `out` =
+        (starts u64, ends u64, doc_tok u64[ndocs+1]) to reuse; grown when too
+        small.  Returns (starts[:n], ends[:n], doc_tok, out)."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
+        nd = len(doc_off) - 1
+        if out is None or len(out[2]) != nd + 1:
+            cap = max(1024, int(doc_off[-1] - doc_off[0]) // 2)
+            out = (np.empty(cap, np.uint64), np.empty(cap, np.uint64), np.empty(nd + 1, np.uint64))
+        n = C.c_uint64()
+        for _ in range(2):
+            rc = lib().jb_cut_batch_into(self.h, buf.ctypes.data, doc_off.ctypes.data, nd, int(hmm),
+                                         out[0].ctypes.data, out[1].ctypes.data, len(out[0]), out[2].ctypes.data,
+                                         C.byref(n))
+            if rc == JB_ELIMIT and n.value > len(out[0]):
+                out = (np.empty(n.value, np.uint64), np.empty(n.value, np.uint64), out[2])
+                continue
+            _check(rc)
+            break
+        k = n.value
+        return out[0][:k], out[1][:k], out[2], out
 
     def cut_device(self, d_text_ptr, nbytes, d_doc_off_ptr, ndocs, hmm, stream_ptr=0):
         """Device-resident cut; returns device pointers (start, end, doc_tok, ntok)."""

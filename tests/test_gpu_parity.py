@@ -295,3 +295,18 @@ def test_synthetic_golden_vectors(syn_golden):
                     assert (ge[a:b] - base).tolist() == c["ends"], (kind, hmm, d)
         finally:
             tk.close()
+
+
+def test_cut_batch_into_caller_arrays(small):
+    """jb_cut_batch_into: same spans as jb_cut_batch; too-small arrays give
+    JB_ELIMIT with the needed count, and the binding retries."""
+    tk, o, s = small
+    buf, off, _ = s.corpus(synth.KIND_SENTENCES, 40, max_docs=300, target_bytes=1 << 20)
+    for hmm in (False, True):
+        gs, ge, gd = tk.cut_batch(buf, off, hmm)
+        tiny = (np.empty(3, np.uint64), np.empty(3, np.uint64), np.empty(len(off), np.uint64))
+        ts, te, td, out = tk.cut_batch_into(buf, off, hmm, tiny)
+        assert len(out[0]) >= len(gs)
+        assert np.array_equal(ts, gs) and np.array_equal(te, ge) and np.array_equal(td, gd)
+        ts2, te2, td2, _ = tk.cut_batch_into(buf, off, hmm, out)  # reuse
+        assert np.array_equal(ts2, gs) and np.array_equal(td2, gd)
