@@ -342,7 +342,7 @@ static void free_work(Work* w) {
     dfree(w->docbits); dfree(w->sbits); dfree(w->ebits); dfree(w->tile_cnt); dfree(w->tile_off);
     dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->blk); dfree(w->lists); dfree(w->erec); dfree(w->lanemask);
     dfree(w->gbl); dfree(w->gbest);
-    dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters);
+    dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters); dfree(w->dbg);
     *w = Work{};
 }
 
@@ -374,6 +374,7 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.tok_end, (nb + 4) * 4));
     HIPCHK(hipMalloc(&w.doc_tok, ((uint64_t)ndc + 2) * 8));
     HIPCHK(hipMalloc(&w.counters, 64 * 4));
+    if (getenv("JB_ABLATE") && (atoi(getenv("JB_ABLATE")) & 0x100)) HIPCHK(hipMalloc(&w.dbg, 65536 * 8 * 8));
     w.cap_bytes = nb;
     w.cap_docs = ndc;
     return JB_OK;
@@ -438,6 +439,25 @@ static int launch(jb_ctx* ctx, Device* d, const uint8_t* d_text, uint64_t nbytes
     const hipError_t e = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, gzh, grid_nz, s,
                                       d->profile ? &d->timer : nullptr);
     if (e != hipSuccess) return fail(JB_EDEVICE, "pipeline launch: %s", hipGetErrorString(e));
+    if ((g_ablate & 0x100u) && d->w.dbg) {  // diagnostic: per-wave clocks of k_zh (JB_ABLATE bit 8)
+        const uint32_t nwv = std::min<uint32_t>(gzh * 4u, 65536u);
+        std::vector<uint64_t> st((size_t)nwv * 8);
+        HIPCHK(hipMemcpyAsync(st.data(), d->w.dbg, st.size() * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        double n = 0;
+        for (uint32_t i = 0; i < nwv; i++)
+            if (st[i * 8 + 3]) {
+                for (int k = 0; k < 8; k++) a[k] += (double)st[i * 8 + k];
+                n++;
+            }
+        if (n == 0) n = 1;
+        fprintf(stderr, "[jb] k_zh clocks/wave: staging %.0f dp %.0f fwd+vit %.0f total %.0f; groups/wave %.1f; "
+                        "lane DP runes %.0f vs 64*max %.0f (DP lane use %.2f); lanes outside the window %.3f\n",
+                a[0] / n, a[1] / n, a[2] / n, a[6] / n, a[3] / n, a[4] / n, 64.0 * a[5] / n,
+                a[4] / (64.0 * a[5] + 1e-9), a[7] / (64.0 * a[3] + 1e-9));
+        HIPCHK(hipMemsetAsync(d->w.dbg, 0, (size_t)nwv * 64, s));
+    }
     return JB_OK;
 }
 

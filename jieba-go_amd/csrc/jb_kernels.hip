@@ -27,6 +27,13 @@
 
 #include "jb_kernels.h"
 
+#ifndef JB_STAMPS
+#define JB_STAMPS 0
+#endif
+#ifndef JB_ZH_CAP
+#define JB_ZH_CAP 3584  // k_zh window: text bytes staged per wave
+#endif
+
 namespace jb {
 
 const char* const kKernelNames[K_NUM] = {"k_docbits", "k_mark_walk", "k_scan_blocks", "k_blocks_write",
@@ -67,10 +74,13 @@ struct Emitter {
     uint32_t* sb;
     uint32_t* eb;
     uint32_t word, s, e;
+    bool off = false;  // diagnostic (JB_ABLATE bit 7): drop the bits instead of flushing them
     __device__ Emitter(uint32_t* s_, uint32_t* e_) : sb(s_), eb(e_), word(0xFFFFFFFFu), s(0), e(0) {}
     __device__ __forceinline__ void flush() {
-        if (s) atomicOr(sb + word, s);
-        if (e) atomicOr(eb + word, e);
+        if (!off) {
+            if (s) atomicOr(sb + word, s);
+            if (e) atomicOr(eb + word, e);
+        }
         s = e = 0;
     }
     __device__ __forceinline__ void at(uint32_t pos) {
@@ -81,6 +91,34 @@ struct Emitter {
         }
     }
     // token = bytes [a, b)
+    __device__ __forceinline__ void token(uint32_t a, uint32_t b) {
+        at(a);
+        s |= 1u << (a & 31u);
+        at(b - 1u);
+        e |= 1u << ((b - 1u) & 31u);
+    }
+};
+
+// The same for a wave's LDS token bitmaps: word index = global word - w0.
+struct LdsEmitter {
+    uint32_t* sb;
+    uint32_t* eb;
+    uint32_t w0;
+    uint32_t word, s, e;
+    __device__ LdsEmitter(uint32_t* s_, uint32_t* e_, uint32_t w0_)
+        : sb(s_), eb(e_), w0(w0_), word(0xFFFFFFFFu), s(0), e(0) {}
+    __device__ __forceinline__ void flush() {
+        if (s) atomicOr(sb + (word - w0), s);
+        if (e) atomicOr(eb + (word - w0), e);
+        s = e = 0;
+    }
+    __device__ __forceinline__ void at(uint32_t pos) {
+        const uint32_t w = pos >> 5;
+        if (w != word) {
+            flush();
+            word = w;
+        }
+    }
     __device__ __forceinline__ void token(uint32_t a, uint32_t b) {
         at(a);
         s |= 1u << (a & 31u);
@@ -565,7 +603,7 @@ __global__ __launch_bounds__(1024) void k_scan2(const uint2* __restrict__ cnt, u
 // for the Viterbi (:228-253).  Blocks that do not fit the staged span run the
 // same code on global memory.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kZhCap = 2560;  // staged text bytes per wave
+constexpr uint32_t kZhCap = JB_ZH_CAP;  // staged text bytes per wave
 constexpr uint32_t kZhRing = 8;    // LDS best ring per lane (runes)
 
 struct LdsZv {  // text and slots of the wave's staged span
@@ -624,8 +662,8 @@ __device__ __forceinline__ void route2(double a, double b, uint32_t* code, doubl
 // Back-pointers (2 bits per state) go to each rune's slot; the traceback
 // stops at the first "" route: the reference's path then restarts at that
 // step (fullPath[""] is nil, :715) and cutHMM labels runes from the run start.
-template <class V>
-__device__ void viterbi_run(const V& v, const DevImage& im, uint32_t rs, uint32_t re, uint32_t m, Emitter& em) {
+template <class V, class E>
+__device__ void viterbi_run(const V& v, const DevImage& im, uint32_t rs, uint32_t re, uint32_t m, E& em) {
     if (m == 1) {  // always "S" for a single rune (:672-674)
         em.token(rs, re);
         return;
@@ -688,11 +726,12 @@ __device__ void viterbi_run(const V& v, const DevImage& im, uint32_t rs, uint32_
 
 // One Han block [bs, be).  Returns false where the reference panics (a rune
 // on the chosen path with no DAG edge: cutDAG slices with tail index -1).
-template <bool HMM, class V>
+template <bool HMM, class V, class E>
 __device__ bool zh_block(const V& v, const DevImage& im, const uint64_t* __restrict__ erec,
-                         double* __restrict__ gbest, double* ring, uint32_t bs, uint32_t be, Emitter& em,
-                         uint32_t ablate) {
+                         double* __restrict__ gbest, double* ring, uint32_t bs, uint32_t be, E& em,
+                         uint32_t ablate, uint64_t* st) {
     const uint32_t key0 = be / 3u;
+    uint32_t c_done = 0;
     // The best values of the last kZhRing runes live in the LDS ring.  A block
     // with a longer edge is redone with every best value also kept in gbest.
     for (bool longm = false;; longm = true) {
@@ -779,12 +818,19 @@ __device__ bool zh_block(const V& v, const DevImage& im, const uint64_t* __restr
             ring[(c & (kZhRing - 1u)) * 64u] = bestP;
             if (longm) gbest[key0 - c] = bestP;
             v.bl(q) = (uint8_t)bestL;
+            c_done = c;
             if (redo || !more) break;
             q = qn;
             rc = rn;
             ++c;
         }
         if (!redo) break;
+    }
+    if (st) {  // diagnostic phase clocks (wave-uniform point: every lane has left the DP)
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        st[1] += t - st[7];
+        st[7] = t;
+        st[4] += c_done;
     }
     if (ablate & 4u) return true;  // diagnostic only: DP without the forward walk
     // ---- forward walk (findDagPath) + HMM runs ---------------------------------------
@@ -823,16 +869,29 @@ __global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, ui
                                             const uint64_t* __restrict__ erec, uint8_t* __restrict__ gbl,
                                             double* __restrict__ gbest,
                                             uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
-                                            uint32_t ablate) {
+                                            uint32_t ablate, uint64_t* __restrict__ dbg) {
     __shared__ __attribute__((aligned(16))) uint8_t s_tx[4][kZhCap + 32];
     __shared__ uint8_t s_bl[4][kZhCap / 3 + 4];
     __shared__ double s_ring[4][kZhRing * 64];
+    __shared__ uint32_t s_sb[4][kZhCap / 32 + 4], s_eb[4][kZhCap / 32 + 4];  // token bits of the window
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint8_t* tx = s_tx[wv];
     double* ring = s_ring[wv] + lane;
     const uint32_t nzh = counters[CNT_NZH];
     Emitter em(sbits, ebits);
+    em.off = (ablate & 128u) != 0;
+    // diagnostic per-wave clocks (JB_ABLATE bit 8): [0] staging [1] DP [2] forward+Viterbi [3] groups
+    // [4] sum of lane DP runes [5] sum of per-group max lane runes [6] total (out) / lanes outside the
+    // window (running) [7] scratch (running) / lanes outside the window (out)
+    uint64_t stv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#if JB_STAMPS
+    uint64_t* st = (ablate & 0x100u) ? stv : nullptr;
+#else
+    uint64_t* const st = nullptr;  // built without the diagnostic clocks (make STAMPS=1)
+#endif
+    const uint64_t tk0 = st ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
+        if (st) stv[7] = __builtin_amdgcn_s_memtime();
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(counters + CNT_WORK, 64u);
         base = __shfl(base, 0, 64);
@@ -853,20 +912,80 @@ __global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, ui
         const uint32_t n16 = (wend - wb + 16u + 15u) >> 4;
         for (uint32_t k = lane; k < n16; k += 64u)
             reinterpret_cast<uint4*>(tx)[k] = reinterpret_cast<const uint4*>(text + wb)[k];
+        // token bits of blocks inside the window collect in LDS words [wb >> 5, wend >> 5]
+        const uint32_t w0 = wb >> 5, nw = (wend >> 5) - w0 + 1u;
+        for (uint32_t k = lane; k < nw; k += 64u) {
+            s_sb[wv][k] = 0u;
+            s_eb[wv][k] = 0u;
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (st) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            stv[0] += t - stv[7];
+            stv[7] = t;
+            stv[3]++;
+            stv[6] += __popcll(__ballot(valid && be > wend));  // lanes outside the window
+            // lane rune estimate for the max-lane statistic
+            uint32_t est = valid ? (be - bs) / 3u : 0u;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) est = max(est, (uint32_t)__shfl_xor((int)est, d, 64));
+            stv[5] += est;
+        }
         if (valid) {
             bool ok;
-            if (be <= wend) ok = zh_block<HMM>(LdsZv{tx, s_bl[wv], wb}, im, erec, gbest, ring, bs, be, em, ablate);
-            else ok = zh_block<HMM>(GlbZv{text, gbl}, im, erec, gbest, ring, bs, be, em, ablate);
+            if (be <= wend) {
+                LdsEmitter le(s_sb[wv], s_eb[wv], w0);
+                ok = zh_block<HMM>(LdsZv{tx, s_bl[wv], wb}, im, erec, gbest, ring, bs, be, le, ablate, st);
+                le.flush();
+            } else {
+                ok = zh_block<HMM>(GlbZv{text, gbl}, im, erec, gbest, ring, bs, be, em, ablate, st);
+            }
             if (!ok) atomicOr(counters + CNT_ERR, 1u);
         }
+        if (st) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            stv[2] += t - stv[7];
+            stv[7] = t;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the window's token words: consecutive words per lane, one OR each (edge
+        // words are shared with neighbouring waves and with k_nonzh)
+        if (!em.off)
+            for (uint32_t k = lane; k < nw; k += 64u) {
+                const uint32_t a = s_sb[wv][k], b = s_eb[wv][k];
+                if (a) atomicOr(sbits + w0 + k, a);
+                if (b) atomicOr(ebits + w0 + k, b);
+            }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     em.flush();
+    if (st) {
+        // lane DP runes summed over the wave
+        uint64_t sum = stv[4];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)sum, d, 64);
+            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(sum >> 32), d, 64);
+            sum += ((uint64_t)hi << 32) | lo;
+        }
+        if (lane == 0) {
+            uint64_t* o = dbg + (blockIdx.x * 4u + wv) * 8u;
+            o[0] = stv[0];
+            o[1] = stv[1];
+            o[2] = stv[2];
+            o[3] = stv[3];
+            o[4] = sum;
+            o[5] = stv[5];
+            o[6] = __builtin_amdgcn_s_memtime() - tk0;
+            o[7] = stv[6];
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1043,11 +1162,11 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     if (hmm)
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
                                           w.lists, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,
-                                          g_ablate));
+                                          g_ablate, w.dbg));
     else
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
                                           w.lists, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,
-                                          g_ablate));
+                                          g_ablate, w.dbg));
     JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3(grid_nz), dim3(256), 0, stream, d_text, w.blk, w.lists,
                                          list_cap, w.counters, w.sbits, w.ebits));
     JB_TIMED(K_TOK_COUNT, hipLaunchKernelGGL((k_tok<false>), dim3(nttiles), dim3(256), 0, stream, w.sbits, w.ebits,
