@@ -107,9 +107,9 @@ struct Device {
     hipStream_t stream = nullptr;
     // image
     uint16_t* pagemap = nullptr;
-    uint32_t* l1 = nullptr;
     double* emit = nullptr;
-    uint64_t* nodes = nullptr;
+    uint64_t* cells = nullptr;
+    uint32_t* code = nullptr;
     double* wtab = nullptr;
     DevImage dim{};
     // workspace
@@ -293,7 +293,7 @@ extern "C" int jb_image_stats(const jb_image* img, uint64_t* nodes, uint64_t* ca
                               uint32_t* maxlen, int64_t* size, double* w_absent) {
     if (!img) return fail(JB_EINVAL, "null image");
     if (nodes) *nodes = img->img.nnodes;
-    if (cap) *cap = img->img.nodes.size();
+    if (cap) *cap = img->img.cells.size();
     if (npages) *npages = img->img.npages;
     if (maxlen) *maxlen = img->img.maxlen;
     if (size) *size = img->img.size;
@@ -324,16 +324,14 @@ static int upload(T** dst, const std::vector<T>& src) {
 static int upload_image(Device* d, const Image& img) {
     HIPCHK(hipSetDevice(d->ordinal));
     int rc;
-    if ((rc = upload(&d->pagemap, img.pagemap)) || (rc = upload(&d->l1, img.l1)) || (rc = upload(&d->emit, img.emit)) ||
-        (rc = upload(&d->nodes, img.nodes)) || (rc = upload(&d->wtab, img.wtab)))
+    if ((rc = upload(&d->pagemap, img.pagemap)) || (rc = upload(&d->emit, img.emit)) ||
+        (rc = upload(&d->cells, img.cells)) || (rc = upload(&d->code, img.code)) || (rc = upload(&d->wtab, img.wtab)))
         return rc;
     d->dim.pagemap = d->pagemap;
-    d->dim.l1 = d->l1;
     d->dim.emit = d->emit;
-    d->dim.nodes = d->nodes;
+    d->dim.cells = d->cells;
+    d->dim.code = d->code;
     d->dim.wtab = d->wtab;
-    d->dim.mask = (uint32_t)(img.nodes.size() / JB_BUCKET - 1);  // bucket mask
-    d->dim.seed = img.seed;
     d->dim.nrows = img.nrows;
     return JB_OK;
 }
@@ -496,7 +494,7 @@ extern "C" void jb_close(jb_ctx* ctx) {
         (void)hipStreamSynchronize(d->stream);
         d->timer.reset();
         free_work(&d->w);
-        dfree(d->text); dfree(d->doc_off); dfree(d->pagemap); dfree(d->l1); dfree(d->emit); dfree(d->nodes);
+        dfree(d->text); dfree(d->doc_off); dfree(d->pagemap); dfree(d->emit); dfree(d->cells); dfree(d->code);
         dfree(d->wtab);
         hfree(d->h_text); hfree(d->h_span); hfree(d->h_misc); hfree(d->h_cnt);
         (void)hipStreamDestroy(d->stream);

@@ -9,21 +9,25 @@
 //   pagemap[0x110000 >> 8]  u16   rune page -> dense page id (page 0 = empty page;
 //                                 pages 0x34..0x9F, U+3400..U+9FFF, are always ids
 //                                 1..108 so jb_row() skips the pagemap for them)
-//   l1[npages * 256]        u32   the single-rune key: freq class | has-children |
-//                                 weight index (its node id is its row)
+//   code[npages * 256]     u32   dense rune code, in order of occurrence in the
+//                                 keys (0: the rune is in no key)
+//   cells[ncells]           u64   the trie as a double array over rune codes: the
+//                                 node of rune r under node s is cell base(s) +
+//                                 code(r) when that cell's check is s; level-1
+//                                 nodes (single-rune keys) are the cells at their
+//                                 codes.
+//                                 A cell holds {check, base, freq class,
+//                                 has-children, weight index}; a node's id is its
+//                                 cell index.
 //   emit[npages * 256][4]   f64   emitP[B|M|E|S][string(rune)], minFloat if absent
-//   nodes[cap]              u64   bucketed cuckoo hash of the deeper trie edges
-//                                 (2 candidate buckets of 4 slots): key (parent id,
-//                                 rune) -> {freq class, has-children, weight index};
-//                                 a node's id is nrows + its slot
 //   wtab[nw]                f64   distinct weights w = math.Log(float64(freq)) -
 //                                 math.Log(float64(size)) (Go's Log, on the host);
 //                                 wtab[0] = Log(1.0) - Log(size) for absent runes
 //
-// Walking one more rune is one hash probe, usually one 8-byte load, and none at
-// all from a node without children.  Only keys that the reference's walk can
-// reach are stored: keys made of valid Han runes whose every proper prefix is
-// itself a key (buildDag breaks at the first absent string, tokenizer.go:475-478).
+// Walking one more rune is one 8-byte load (none from a node without
+// children).  Only keys that the reference's walk can reach are stored: keys
+// made of valid Han runes whose every proper prefix is itself a key (buildDag
+// breaks at the first absent string, tokenizer.go:475-478).
 #pragma once
 #include <stdint.h>
 
@@ -44,26 +48,20 @@
 #define JB_FC_ABSENT 3u // (l1 only) the single rune is not a key
 #define JB_WIDX_ABSENT 0u
 
-// u64 node: rune[0,21) fc[21,23) has_child[23] widx[24,41) parent[41,64); empty slot = ~0
-#define JB_NODE_EMPTY 0xFFFFFFFFFFFFFFFFull
-#define JB_MAX_IDS (1u << 23)
+// u64 cell: check[0,22) base[22,44) fc[44,46) has_child[46] widx[47,64).
+// check = parent id + 1 (0: free cell), JB_CHECK_ROOT for level-1 nodes.
+#define JB_CHECK_ROOT 0x3FFFFFu
+#define JB_MAX_CELLS (JB_CHECK_ROOT - 2u)
 #define JB_MAX_WIDX (1u << 17)
-JB_HD uint64_t jb_node_make(uint32_t parent, uint32_t rune, uint32_t fc, uint32_t hc, uint32_t widx) {
-    return (uint64_t)rune | ((uint64_t)fc << 21) | ((uint64_t)hc << 23) | ((uint64_t)widx << 24) |
-           ((uint64_t)parent << 41);
+JB_HD uint64_t jb_cell_make(uint32_t check, uint32_t base, uint32_t fc, uint32_t hc, uint32_t widx) {
+    return (uint64_t)check | ((uint64_t)base << 22) | ((uint64_t)fc << 44) | ((uint64_t)hc << 46) |
+           ((uint64_t)widx << 47);
 }
-JB_HD uint32_t jb_node_rune(uint64_t n) { return (uint32_t)n & 0x1FFFFFu; }
-JB_HD uint32_t jb_node_fc(uint64_t n) { return (uint32_t)(n >> 21) & 3u; }
-JB_HD uint32_t jb_node_hc(uint64_t n) { return (uint32_t)(n >> 23) & 1u; }
-JB_HD uint32_t jb_node_widx(uint64_t n) { return (uint32_t)(n >> 24) & 0x1FFFFu; }
-JB_HD uint32_t jb_node_parent(uint64_t n) { return (uint32_t)(n >> 41); }
-// match of a probed slot against (parent, rune): the low 21 and high 23 bits
-JB_HD bool jb_node_is(uint64_t n, uint32_t parent, uint32_t rune) {
-    return ((n ^ ((uint64_t)parent << 41) ^ rune) & 0xFFFFFE00001FFFFFull) == 0;
-}
-
-// u32 level-1 record: fc[0,2) has_child[2] widx[3,20)
-JB_HD uint32_t jb_l1_make(uint32_t fc, uint32_t hc, uint32_t widx) { return fc | (hc << 2) | (widx << 3); }
+JB_HD uint32_t jb_cell_check(uint64_t c) { return (uint32_t)c & 0x3FFFFFu; }
+JB_HD uint32_t jb_cell_base(uint64_t c) { return (uint32_t)(c >> 22) & 0x3FFFFFu; }
+JB_HD uint32_t jb_cell_fc(uint64_t c) { return (uint32_t)(c >> 44) & 3u; }
+JB_HD uint32_t jb_cell_hc(uint64_t c) { return (uint32_t)(c >> 46) & 1u; }
+JB_HD uint32_t jb_cell_widx(uint64_t c) { return (uint32_t)(c >> 47); }
 
 // Pages U+3400..U+9FFF (CJK Ext-A + URO) sit at fixed page ids 1..108.
 #define JB_DIRECT_LO 0x3400u
@@ -76,18 +74,6 @@ JB_HD uint32_t jb_row(const uint16_t* pagemap, uint32_t r) {
     return (uint32_t)pagemap[r >> 8] * 256u + (r & 255u);
 }
 
-// The two candidate buckets (JB_BUCKET slots = 32 bytes each) of the edge
-// (parent, rune) in the bucketed cuckoo hash; identical on host and device.
-#define JB_BUCKET 4
-JB_HD void jb_buckets(uint32_t parent, uint32_t rune, uint32_t bmask, uint32_t seed, uint32_t* b1, uint32_t* b2) {
-    const uint32_t t = (parent * 0x9E3779B1u + rune * 0x85EBCA77u) ^ seed;
-    uint32_t h1 = (t ^ (t >> 15)) * 0x2C1B3C6Du;
-    uint32_t h2 = (t ^ (t >> 13)) * 0x297A2D39u;
-    h1 ^= h1 >> 13;
-    h2 ^= h2 >> 16;
-    *b1 = h1 & bmask;
-    *b2 = (h2 & bmask) == *b1 ? *b1 ^ 1u : h2 & bmask;
-}
 
 // tokenizer.go:19
 #define JB_MIN_FLOAT (-3.14e100)

@@ -11,6 +11,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <unordered_set>
 #include <cstdlib>
 
@@ -325,8 +327,6 @@ int parse_emission(const char* buf, size_t len, Emission* out, std::string* err)
 // ---------------------------------------------------------------------------
 // Device image
 // ---------------------------------------------------------------------------
-static uint32_t jb_buckets_seed(uint32_t attempt) { return attempt * 0x7F4A7C15u + 0x2545F491u; }
-
 static uint32_t freq_class(int64_t f) { return f > 0 ? JB_FC_POS : (f == 0 ? JB_FC_ZERO : JB_FC_NEG); }
 
 int build_image(const Dictionary& d, const Emission& e, Image* img, std::string* err) {
@@ -395,147 +395,133 @@ int build_image(const Dictionary& d, const Emission& e, Image* img, std::string*
     }
     auto widx = [&](int64_t f) -> uint32_t { return widx_of.at(wbits(f)); };
 
-    size_t deep = 0;
-    for (const Key& k : keys) deep += k.r.size() > 1;
-    img->l1.assign(img->nrows, jb_l1_make(JB_FC_ABSENT, 0, JB_WIDX_ABSENT));
+    // ---- the trie as a double array over rune codes ----------------------------------
+    // Codes are dense, in order of how often a rune occurs in the keys, so a
+    // node's children sit close together.  Level-1 nodes are the cells at their
+    // codes; deeper levels are placed level by level (a node's cell index is its
+    // id, which its children's check holds): every node with children gets the
+    // first base at which base + code(child) is free for all of them, nodes with
+    // the most children first.
+    {
+        std::unordered_map<uint32_t, uint64_t> occ;
+        for (const Key& k : keys)
+            for (uint32_t r : k.r) occ[r]++;
+        std::vector<std::pair<uint32_t, uint64_t>> ord(occ.begin(), occ.end());
+        std::sort(ord.begin(), ord.end(), [](const auto& a, const auto& b) {
+            return a.second != b.second ? a.second > b.second : a.first < b.first;
+        });
+        img->code.assign(img->nrows, 0u);
+        for (size_t i = 0; i < ord.size(); i++) img->code[jb_row(pm, ord[i].first)] = (uint32_t)i + 1u;
+        img->ncodes = (uint32_t)ord.size() + 1u;
+    }
+    auto code_of = [&](uint32_t r) { return img->code[jb_row(pm, r)]; };
+    std::vector<uint64_t>& cells = img->cells;
+    std::vector<uint64_t> used;  // bitmap of occupied cells (cell 0: the absent rune, never a node)
+    auto is_used = [&](uint64_t i) { return i < used.size() * 64 && ((used[i >> 6] >> (i & 63)) & 1ull); };
+    auto set_used = [&](uint64_t i) {
+        if (i >= used.size() * 64) used.resize(i / 64 + 4096, 0ull);
+        used[i >> 6] |= 1ull << (i & 63);
+        if (i >= cells.size()) cells.resize(i + 4096, 0ull);
+    };
+    cells.assign(img->ncodes, 0ull);
+    used.assign(img->ncodes / 64 + 4096, 0ull);
+    set_used(0);
     img->maxlen = 0;
     img->nnodes = 0;
-    for (const Key& k : keys) {  // level 1: the l1 rows
+    std::unordered_map<std::string, uint32_t> id_of;  // key (runes) -> cell id
+    auto rkey = [](const std::vector<uint32_t>& r, size_t n) {
+        return std::string(reinterpret_cast<const char*>(r.data()), n * sizeof(uint32_t));
+    };
+    for (size_t i = 0; i < keys.size(); i++) {  // level 1: the cells at the codes
+        const Key& k = keys[i];
         if (k.r.size() != 1) continue;
         const uint32_t wi = widx(k.f);
         if (wi >= JB_MAX_WIDX) {
             *err = "more than " + std::to_string(JB_MAX_WIDX) + " distinct frequencies";
             return JB_ELIMIT;
         }
-        img->l1[jb_row(pm, k.r[0])] = jb_l1_make(freq_class(k.f), 0, wi);
+        const uint32_t c = code_of(k.r[0]);
+        cells[c] = jb_cell_make(JB_CHECK_ROOT, 0, freq_class(k.f), 0, wi);
+        set_used(c);
+        id_of.emplace(rkey(k.r, 1), c);
         img->nnodes++;
         img->maxlen = 1;
     }
-    const std::vector<uint32_t> l1_base = img->l1;
-    const uint64_t nnodes1 = img->nnodes;
-    // Deeper levels: bucketed cuckoo hash, placed level by level.  A node's slot
-    // is its id, so a placement may not move a node that is already a parent:
-    // it moves leaves (keys no longer key extends) and nodes of the level being
-    // placed.  Load <= 2/3; a placement that gets stuck retries with another
-    // hash seed, and the table doubles after 16 seeds.
-    std::unordered_set<std::string> internal;  // keys that a longer key extends by one rune
-    auto rkey = [](const std::vector<uint32_t>& r, size_t n) {
-        return std::string(reinterpret_cast<const char*>(r.data()), n * sizeof(uint32_t));
-    };
-    for (const Key& k : keys)
-        if (k.r.size() >= 3) internal.insert(rkey(k.r, k.r.size() - 1));
-    uint64_t cap = 1024;
-    while (cap * 2 < deep * 3) cap <<= 1;  // load <= 2/3
-    for (uint32_t attempt = 0;; attempt++) {
-        if (attempt && attempt % 16 == 0) cap <<= 1;
-        img->seed = attempt ? jb_buckets_seed(attempt) : 0u;
-        if (img->nrows + cap >= JB_MAX_IDS - 1) {
-            *err = "dictionary too large for the packed trie (" + std::to_string(deep) + " multi-rune keys)";
-            return JB_ELIMIT;
-        }
-        img->nodes.assign(cap, JB_NODE_EMPTY);
-        img->l1 = l1_base;
-        img->nnodes = nnodes1;
-        std::vector<uint8_t> lvl(cap, 0);  // level of the node in each slot; 0 = free to move
-        const uint32_t bmask = (uint32_t)(cap / JB_BUCKET - 1);
-        auto find = [&](uint32_t parent, uint32_t r) -> uint64_t {  // slot or ~0
-            uint32_t b[2];
-            jb_buckets(parent, r, bmask, img->seed, &b[0], &b[1]);
-            for (int i = 0; i < 2 * JB_BUCKET; i++) {
-                const uint64_t sl = (uint64_t)JB_BUCKET * b[i / JB_BUCKET] + (i % JB_BUCKET);
-                if (jb_node_is(img->nodes[sl], parent, r)) return sl;
+    uint64_t first_free = 1;
+    uint64_t probes = 0;
+    // search start per child count: the base found last for that count (a node with
+    // k children rarely fits below where the previous k-child node fitted)
+    std::vector<uint64_t> start_k(65, 1);
+    const auto tp0 = std::chrono::steady_clock::now();
+    for (size_t i0 = 0; i0 < keys.size();) {
+        const size_t n = keys[i0].r.size();
+        size_t i1 = i0;
+        while (i1 < keys.size() && keys[i1].r.size() == n) i1++;
+        if (n >= 2) {
+            // children of each level-(n-1) node among the reachable keys of length n
+            std::unordered_map<uint32_t, std::vector<uint32_t>> kids;  // parent id -> key indices
+            for (size_t i = i0; i < i1; i++) {
+                auto it = id_of.find(rkey(keys[i].r, n - 1));
+                if (it == id_of.end()) continue;  // unreachable (tokenizer.go:475-478)
+                kids[it->second].push_back((uint32_t)i);
             }
-            return ~0ull;
-        };
-        uint64_t rng = 0x9E3779B97F4A7C15ull;
-        // level: the level being placed; a node is stored with its level, or 0 if it is a leaf
-        auto place = [&](uint64_t node, uint8_t nlvl, uint8_t level) -> bool {
-            for (int kick = 0; kick < 512; kick++) {
-                uint32_t b[2];
-                jb_buckets(jb_node_parent(node), jb_node_rune(node), bmask, img->seed, &b[0], &b[1]);
-                // the emptier of the two buckets first (keeps buckets evenly filled)
-                int fill[2] = {0, 0};
-                for (int i = 0; i < 2 * JB_BUCKET; i++)
-                    fill[i / JB_BUCKET] += img->nodes[(uint64_t)JB_BUCKET * b[i / JB_BUCKET] + (i % JB_BUCKET)] !=
-                                           JB_NODE_EMPTY;
-                const int first = fill[1] < fill[0] ? 1 : 0;
-                uint64_t movable[2 * JB_BUCKET];
-                int nm = 0;
-                for (int i0 = 0; i0 < 2 * JB_BUCKET; i0++) {
-                    const int i = (i0 + first * JB_BUCKET) % (2 * JB_BUCKET);
-                    const uint64_t sl = (uint64_t)JB_BUCKET * b[i / JB_BUCKET] + (i % JB_BUCKET);
-                    if (img->nodes[sl] == JB_NODE_EMPTY) {
-                        img->nodes[sl] = node;
-                        lvl[sl] = nlvl;
-                        return true;
-                    }
-                    if (lvl[sl] == level || lvl[sl] == 0) movable[nm++] = sl;
-                }
-                if (nm == 0) {
-                    if (getenv("JB_DEBUG_BUILD")) {
-                        fprintf(stderr, "stuck kick %d:", kick);
-                        for (int i = 0; i < 2 * JB_BUCKET; i++)
-                            fprintf(stderr, " %u", (unsigned)lvl[(uint64_t)JB_BUCKET * b[i / JB_BUCKET] + (i % JB_BUCKET)]);
-                        fprintf(stderr, " b=%u,%u\n", b[0], b[1]);
-                    }
-                    return false;
-                }
-                rng ^= rng << 13;
-                rng ^= rng >> 7;
-                rng ^= rng << 17;
-                const uint64_t v = movable[rng % (uint64_t)nm];
-                std::swap(node, img->nodes[v]);
-                std::swap(nlvl, lvl[v]);
-            }
-            return false;
-        };
-        std::vector<uint32_t> parents;  // parent id of every stored deeper node
-        bool ok_all = true;
-        for (size_t i0 = 0; i0 < keys.size() && ok_all;) {
-            const size_t n = keys[i0].r.size();
-            size_t i1 = i0;
-            while (i1 < keys.size() && keys[i1].r.size() == n) i1++;
-            if (n >= 2) {
-                for (size_t i = i0; i < i1 && ok_all; i++) {
-                    const Key& k = keys[i];
-                    // parent id: level-1 row, then nrows + slot for each deeper prefix
-                    const uint32_t row0 = jb_row(pm, k.r[0]);
-                    if ((img->l1[row0] & 3u) == JB_FC_ABSENT) continue;  // unreachable (tokenizer.go:475-478)
-                    uint32_t parent = row0;
+            std::vector<std::pair<uint32_t, std::vector<uint32_t>>> order(kids.begin(), kids.end());
+            std::sort(order.begin(), order.end(), [](const auto& a, const auto& b) {
+                return a.second.size() != b.second.size() ? a.second.size() > b.second.size() : a.first < b.first;
+            });
+            std::vector<uint32_t> cs, srt;
+            for (auto& pk : order) {
+                const uint32_t parent = pk.first;
+                cs.clear();
+                for (uint32_t ki : pk.second) cs.push_back(code_of(keys[ki].r[n - 1]));
+                srt = cs;
+                std::sort(srt.begin(), srt.end());
+                while (is_used(first_free)) first_free++;
+                const size_t kc = std::min<size_t>(srt.size(), 64);
+                uint64_t f = std::max<uint64_t>(std::max<uint64_t>(first_free, start_k[kc]), (uint64_t)srt[0] + 1);
+                uint64_t base = 0;
+                for (;; f++) {
+                    if (is_used(f)) continue;
+                    probes++;
+                    base = f - srt[0];
                     bool ok = true;
-                    for (size_t j = 1; j + 1 < n && ok; j++) {
-                        const uint64_t sl = find(parent, k.r[j]);
-                        ok = sl != ~0ull;
-                        if (ok) parent = img->nrows + (uint32_t)sl;
-                    }
-                    if (!ok) continue;
+                    for (size_t j = 1; j < srt.size() && ok; j++) ok = !is_used(base + srt[j]);
+                    if (ok) break;
+                }
+                start_k[kc] = f;
+                if (base + srt.back() >= JB_MAX_CELLS) {
+                    *err = "dictionary too large for the double-array trie (" + std::to_string(img->nnodes) +
+                           " keys placed)";
+                    return JB_ELIMIT;
+                }
+                cells[parent] |= jb_cell_make(0, (uint32_t)base, 0, 1, 0);  // base, has-children
+                for (size_t j = 0; j < pk.second.size(); j++) {
+                    const Key& k = keys[pk.second[j]];
                     const uint32_t wi = widx(k.f);
                     if (wi >= JB_MAX_WIDX) {
                         *err = "more than " + std::to_string(JB_MAX_WIDX) + " distinct frequencies";
                         return JB_ELIMIT;
                     }
-                    const uint8_t nl = internal.count(rkey(k.r, n)) ? (uint8_t)std::min<size_t>(n, 255) : 0;
-                    if (!place(jb_node_make(parent, k.r.back(), freq_class(k.f), 0, wi), nl,
-                               (uint8_t)std::min<size_t>(n, 255))) {
-                        if (getenv("JB_DEBUG_BUILD")) fprintf(stderr, "cap %llu: placement failed at key %zu (len %zu) nnodes %llu\n", (unsigned long long)cap, i, n, (unsigned long long)img->nnodes);
-                        ok_all = false;
-                        break;
-                    }
-                    parents.push_back(parent);
+                    const uint64_t c = base + cs[j];
+                    set_used(c);
+                    cells[c] = jb_cell_make(parent + 1u, 0, freq_class(k.f), 0, wi);
+                    id_of.emplace(rkey(k.r, n), (uint32_t)c);
                     img->nnodes++;
                     img->maxlen = std::max<uint32_t>(img->maxlen, (uint32_t)n);
                 }
             }
-            i0 = i1;
         }
-        if (!ok_all) continue;  // another seed / a bigger table
-        // has-children flags: a walk stops at a node without children, no probe
-        for (uint32_t p : parents) {
-            if (p < img->nrows) img->l1[p] |= 1u << 2;
-            else img->nodes[p - img->nrows] |= 1ull << 23;
-        }
-        break;
+        i0 = i1;
     }
+    if (getenv("JB_DEBUG_BUILD"))
+        fprintf(stderr, "[jb] trie placement %.3f s, %llu candidate bases\n",
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - tp0).count(),
+                (unsigned long long)probes);
+    // room for base + code of any rune under any node: probes never leave the array
+    uint64_t top = cells.size();
+    while (top > img->ncodes && cells[top - 1] == 0ull) top--;
+    cells.resize(top + img->ncodes + 1, 0ull);
+    img->ncells = (uint32_t)cells.size();
     img->emit.assign((size_t)img->npages * 256 * 4, JB_MIN_FLOAT);  // not found -> minFloat (tokenizer.go:690,710)
     for (int s = 0; s < 4; s++)
         for (const auto& kv : e.by_rune[s]) {
@@ -548,28 +534,20 @@ int build_image(const Dictionary& d, const Emission& e, Image* img, std::string*
 Lookup image_lookup(const Image& img, const uint32_t* runes, size_t n) {
     Lookup out;
     if (n == 0 || runes[0] >= 0x110000u) return out;
-    const uint32_t row = jb_row(img.pagemap.data(), runes[0]);
-    const uint32_t rec = img.l1[row];
-    if ((rec & 3u) == JB_FC_ABSENT) return out;
-    uint32_t id = row, fc = rec & 3u, wi = rec >> 3;
-    const uint32_t bmask = (uint32_t)(img.nodes.size() / JB_BUCKET - 1);
+    const uint16_t* pm = img.pagemap.data();
+    uint32_t id = img.code[jb_row(pm, runes[0])];
+    uint64_t c = img.cells[id];
+    if (jb_cell_check(c) != JB_CHECK_ROOT) return out;
     for (size_t i = 1; i < n; i++) {
-        uint32_t b[2];
-        jb_buckets(id, runes[i], bmask, img.seed, &b[0], &b[1]);
-        uint64_t hit = ~0ull;
-        for (int k = 0; k < 2 * JB_BUCKET && hit == ~0ull; k++) {
-            const uint64_t sl = (uint64_t)JB_BUCKET * b[k / JB_BUCKET] + (k % JB_BUCKET);
-            if (jb_node_is(img.nodes[sl], id, runes[i])) hit = sl;
-        }
-        if (hit == ~0ull) return Lookup{};
-        const uint64_t nd = img.nodes[hit];
-        id = img.nrows + (uint32_t)hit;
-        fc = jb_node_fc(nd);
-        wi = jb_node_widx(nd);
+        if (runes[i] >= 0x110000u || !jb_cell_hc(c)) return Lookup{};
+        const uint64_t t = (uint64_t)jb_cell_base(c) + img.code[jb_row(pm, runes[i])];
+        if (t >= img.cells.size() || jb_cell_check(img.cells[t]) != id + 1u) return Lookup{};
+        id = (uint32_t)t;
+        c = img.cells[t];
     }
     out.found = true;
-    out.fc = fc;
-    out.widx = wi;
+    out.fc = jb_cell_fc(c);
+    out.widx = jb_cell_widx(c);
     out.id = id;
     return out;
 }

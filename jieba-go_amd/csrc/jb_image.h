@@ -27,13 +27,15 @@ struct Emission {
 // Flat arrays uploaded to every device (layout: jb_common.h).
 struct Image {
     std::vector<uint16_t> pagemap;  // JB_NPAGES_MAX
-    std::vector<uint32_t> l1;       // npages * 256 level-1 records
+
     std::vector<double> emit;       // npages * 256 * 4
-    std::vector<uint64_t> nodes;    // hash capacity (power of two), deeper trie edges
+    std::vector<uint32_t> code;     // npages * 256: dense rune code (0: in no key), by key occurrence
+    std::vector<uint64_t> cells;    // double-array trie over codes (level-1 nodes at their codes)
     std::vector<double> wtab;       // distinct weights; [0] = w_absent
-    uint32_t seed = 0;              // cuckoo hash seed (jb_buckets)
     uint32_t npages = 0;
-    uint32_t nrows = 0;             // npages * 256: ids of level-1 nodes; deeper ids = nrows + slot
+    uint32_t nrows = 0;             // npages * 256: ids of level-1 nodes are their rows
+    uint32_t ncells = 0;
+    uint32_t ncodes = 0;
     uint32_t maxlen = 0;            // longest reachable key, runes
     uint64_t nnodes = 0;            // reachable keys (all levels)
     double total = 0;               // math.Log(float64(size))

@@ -10,13 +10,11 @@ namespace jb {
 // Device copy of the image (jb_common.h), passed by value to kernels.
 struct DevImage {
     const uint16_t* pagemap;
-    const uint32_t* l1;
     const double* emit;
-    const uint64_t* nodes;
+    const uint32_t* code;   // dense rune code per row (0: in no key)
+    const uint64_t* cells;  // double-array trie over codes; level-1 nodes at their codes
     const double* wtab;
-    uint32_t mask;     // cuckoo buckets - 1 (JB_BUCKET slots per bucket)
-    uint32_t seed;     // cuckoo hash seed
-    uint32_t nrows;    // deeper node id = nrows + slot
+    uint32_t nrows;
 };
 
 // Device counters (u32 slots unless noted)

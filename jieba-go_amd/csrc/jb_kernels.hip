@@ -212,31 +212,16 @@ __device__ __forceinline__ uint32_t han_rune(uint32_t x, uint32_t lim, uint32_t*
     return 0u;
 }
 
-// Cuckoo lookup of the trie edge (parent, r): both candidate buckets are
-// loaded at once (2 x 32 bytes, one round trip); slot or ~0u.
-struct Probe {
-    ulonglong2 x0, x1, y0, y1;
-    uint32_t b1, b2;
-};
-__device__ __forceinline__ void probe_issue(const DevImage& im, uint32_t parent, uint32_t r, Probe* p) {
-    jb_buckets(parent, r, im.mask, im.seed, &p->b1, &p->b2);
-    const ulonglong2* n2 = reinterpret_cast<const ulonglong2*>(im.nodes);
-    p->x0 = n2[2u * p->b1];
-    p->x1 = n2[2u * p->b1 + 1u];
-    p->y0 = n2[2u * p->b2];
-    p->y1 = n2[2u * p->b2 + 1u];
+// One trie step in the double array: the cell that holds rune r (code k) under
+// the node whose cell is c; a hit when its check names that node.
+__device__ __forceinline__ uint32_t rune_code(const DevImage& im, uint32_t r) {
+    return im.code[jb_row(im.pagemap, r)];
 }
-__device__ __forceinline__ uint32_t probe_match(const Probe& p, uint32_t parent, uint32_t r, uint64_t* nd) {
-    const uint64_t c[8] = {p.x0.x, p.x0.y, p.x1.x, p.x1.y, p.y0.x, p.y0.y, p.y1.x, p.y1.y};
-    uint32_t sl = ~0u;
-#pragma unroll
-    for (int k = 7; k >= 0; k--)
-        if (jb_node_is(c[k], parent, r)) {
-            sl = (k < 4 ? p.b1 : p.b2) * 4u + (uint32_t)(k & 3);
-            *nd = c[k];
-        }
-    return sl;
+__device__ __forceinline__ uint32_t dat_slot_k(uint64_t c, uint32_t k) { return jb_cell_base(c) + k; }
+__device__ __forceinline__ uint32_t dat_slot(const DevImage& im, uint64_t c, uint32_t r) {
+    return dat_slot_k(c, rune_code(im, r));
 }
+__device__ __forceinline__ bool dat_hit(uint64_t child, uint32_t id) { return jb_cell_check(child) == id + 1u; }
 
 // k_mark_walk: one workgroup per 4 KiB tile, staged in LDS, two phases.
 //
@@ -256,10 +241,11 @@ __device__ __forceinline__ uint32_t probe_match(const Probe& p, uint32_t parent,
 // run (adjacent, same document).  Every lane runs one walk at a time as a
 // small state machine — one trie probe per loop trip, the next rune read from
 // the entry list — and takes the next walk start from the tile's queue as soon
-// as its walk ends, so lanes stay busy however long the walks are.  A walk
-// starts at the rune's l1 record (level 1); the probe of its second rune goes
-// out with that load.  It follows one (parent id, rune) probe per further
-// rune and stops at the first string that is not a key (:475-478), at a node
+// as its walk ends, so lanes stay busy however long the walks are.  The trie
+// is a double array: a walk starts at its rune's level-1 cell (loaded for
+// every entry while the list is built) and each further rune is one 8-byte
+// load, cell base + row(rune), a hit when that cell's check names the current
+// node.  It stops at the first string that is not a key (:475-478), at a node
 // without children, or at the end of the Han run.  A run that goes past the
 // tile is walked again at the end, from global memory.
 //
@@ -279,6 +265,7 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
     __shared__ __attribute__((aligned(16))) uint8_t s_t[kTileBytes + 32];  // bytes [t0-16, t0+4096+16)
     __shared__ uint32_t s_db[kTileBytes / 32 + 2];                        // document starts of the tile
     __shared__ uint32_t s_e[kTileE];
+    __shared__ uint64_t s_c[kTileE];  // the level-1 cell of each entry's rune
     __shared__ uint32_t lds[8];
     __shared__ uint16_t s_def[256];  // walk starts whose run goes past the tile
     __shared__ uint32_t s_ndef;
@@ -359,16 +346,17 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
                                ? ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu)
                                : ((x & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) | (((x >> 16) & 0x3Fu) << 6) |
                                      ((x >> 24) & 0x3Fu);
+        s_c[o] = (ablate & 2u) ? 0ull : im.cells[rune_code(im, r)];
         s_e[o++] = r | ((threadIdx.x * 16u + k) << 18);
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nent; i += 256u) {  // run links
+    for (uint32_t i = threadIdx.x; i < nent; i += 256u) {  // run links; the rune field becomes its code
         const uint32_t e = s_e[i];
         const uint32_t nxt = ent_pos(e) + ent_w(e);
         uint32_t f = 0;
         if (nxt >= kTileBytes) f = kEntEdge;
         else if (i + 1u < nent && ent_pos(s_e[i + 1u]) == nxt && !((s_db[nxt >> 5] >> (nxt & 31u)) & 1u)) f = kEntCont;
-        s_e[i] = e | f;
+        s_e[i] = rune_code(im, ent_rune(e)) | (e & 0x3FFC0000u) | f;  // (position bits never change)
     }
     __syncthreads();
     // ---- walks: wave w takes the walk starts [lo, hi) of the tile ---------------------
@@ -379,6 +367,7 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
     const uint32_t elast = nent ? nent - 1u : 0u;
     bool act = false, ovf = false;
     uint32_t q = 0, j = 0, ecur = 0, id = 0, len = 0, nedge = 0;
+    uint64_t cur = 0;  // the cell of the walk's current node
     uint64_t rc = 0;
     auto edge = [&](uint32_t L, uint32_t wi) {
         if (L > kEdgeMaxL || nedge >= 4u || wi >= (1u << kEdgeIdxBits)) {
@@ -396,6 +385,13 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
         s_def[atomicAdd(&s_ndef, 1u)] = (uint16_t)q;
         act = false;
     };
+    // after a hit on node `id` (cell `cur`) whose rune is entry ecur: go on, defer or stop
+    auto next_or_stop = [&]() {
+        if (!jb_cell_hc(cur) || ovf) finish();
+        else if (ecur & kEntCont) act = true;
+        else if (ecur & kEntEdge) defer();
+        else finish();  // the Han run ends
+    };
     for (;;) {
         const uint64_t need = __ballot(!act);
         const uint32_t rank =
@@ -403,66 +399,46 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
         const uint32_t j0 = head + rank;
         const bool fresh = !act && j0 < hi;
         head = min(hi, head + (uint32_t)__popcll(need));
-        const bool cont = act && (ecur & kEntCont);
-        // LDS: a fresh walk's first two runes, or the next rune of a walk under way
-        const uint32_t ea = ent[min(fresh ? j0 : j + 1u, elast)];
-        const uint32_t eb = ent[min(j0 + 1u, elast)];
-        const uint32_t row = jb_row(im.pagemap, ent_rune(ea));
-        // one round trip: the l1 record of a fresh walk and the probe of its second
-        // rune (speculative), or the probe of the next rune of a walk under way
-        const bool spec = fresh && (ea & kEntCont);
-        const bool probing = spec || cont;
-        const uint32_t pid = probing ? (fresh ? row : id) : 0u;
-        const uint32_t r = probing ? ent_rune(fresh ? eb : ea) : 0u;
-        const uint32_t rec = (ablate & 2u) ? jb_l1_make(JB_FC_ABSENT, 0u, 0u) : im.l1[fresh ? row : 0u];
-        Probe pr;
-        probe_issue(im, pid, r, &pr);
-        bool use = cont;  // does this trip's probe extend the lane's walk?
-        if (act && !cont) {  // the run ended at the last rune
-            if (ecur & kEntEdge) defer();
-            else finish();
-        }
-        if (cont) {
-            ++j;
-            ecur = ea;
-        }
-        if (fresh) {
-            q = ent_pos(ea);
+        if (fresh) {  // level 1 from LDS; the walk goes on only with children and a next rune
             j = j0;
-            ecur = ea;
+            ecur = ent[j0];
+            cur = s_c[j0];
+            q = ent_pos(ecur);
+            id = ent_rune(ecur);  // the rune's code: its level-1 cell
             len = 1u;
             nedge = 0u;
             rc = 0ull;
             ovf = false;
-            const uint32_t fc = rec & 3u;
-            if (fc == JB_FC_ABSENT || fc == JB_FC_ZERO) {
-                edge(1u, rec >> 3);  // the single edge only (:468-471)
+            const uint32_t fc = jb_cell_fc(cur);
+            if (jb_cell_check(cur) != JB_CHECK_ROOT) {
+                edge(1u, JB_WIDX_ABSENT);  // absent: the single edge only, Log(1) (:468-471)
+                finish();
+            } else if (fc == JB_FC_ZERO) {
+                edge(1u, jb_cell_widx(cur));  // count 0: the single edge only, Log(0) = -Inf
                 finish();
             } else {
-                if (fc == JB_FC_POS) edge(1u, rec >> 3);
-                id = row;
-                act = ((rec >> 2) & 1u) != 0u && !(ablate & 1u);
-                if (!act) {
-                    finish();
-                } else if (spec) {  // the speculative probe is this walk's first step
-                    j = j0 + 1u;
-                    ecur = eb;
-                    use = true;
-                } else if (!(ea & kEntEdge)) {
-                    finish();  // a one-rune run
-                }  // else: the next trip defers it
+                if (fc == JB_FC_POS) edge(1u, jb_cell_widx(cur));  // (a negative count has no edge)
+                if (ablate & 1u) finish();
+                else next_or_stop();
             }
         }
-        if (use) {
-            uint64_t nd = 0;
-            const uint32_t sl = probe_match(pr, pid, r, &nd);
-            if (sl == ~0u) {
-                finish();  // (:475-478)
-            } else {
+        // one round trip: the next rune's cell for every walk under way
+        uint64_t child = 0;
+        uint32_t t = 0;
+        if (act) {
+            const uint32_t en = ent[min(j + 1u, elast)];
+            t = dat_slot_k(cur, ent_rune(en));
+            child = im.cells[t];
+            if (dat_hit(child, id)) {
+                ++j;
+                ecur = en;
+                id = t;
+                cur = child;
                 len++;
-                if (jb_node_fc(nd) == JB_FC_POS) edge(len, jb_node_widx(nd));
-                id = im.nrows + sl;
-                if (!jb_node_hc(nd) || ovf) finish();
+                if (jb_cell_fc(child) == JB_FC_POS) edge(len, jb_cell_widx(child));
+                next_or_stop();
+            } else {
+                finish();  // (:475-478)
             }
         }
         if (!__any(act) && head >= hi) break;
@@ -474,16 +450,15 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
         const uint64_t p = t0 + s_def[i];
         uint32_t wr;
         const uint32_t r0 = han_rune(ld4(text, p), 4u, &wr);  // a Han rune of this tile (checked above)
-        const uint32_t row = jb_row(im.pagemap, r0);
-        const uint32_t rec = im.l1[row];
-        const uint32_t fc = rec & 3u;
+        uint32_t nid = rune_code(im, r0);
+        uint64_t c = im.cells[nid];
         rc = 0ull;
         nedge = 0u;
         ovf = false;
-        if (fc == JB_FC_POS) edge(1u, rec >> 3);
-        uint32_t pid = row, n = 1u;
+        if (jb_cell_fc(c) == JB_FC_POS) edge(1u, jb_cell_widx(c));
+        uint32_t n = 1u;
         uint64_t pp = p + wr;
-        bool go = ((rec >> 2) & 1u) != 0u;  // (fc is POS or NEG here: the walk went on)
+        bool go = jb_cell_hc(c) != 0u;  // (present with children: the walk went on)
         while (go) {
             const uint64_t wi = pp >> 5;
             const uint32_t sh = (uint32_t)pp & 31u;
@@ -494,17 +469,16 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
             uint32_t w2;
             const uint32_t r2 = han_rune(ld4(text, pp), lim, &w2);
             if (!r2) break;  // end of the Han run
-            Probe p2;
-            probe_issue(im, pid, r2, &p2);
-            uint64_t nd = 0;
-            const uint32_t sl = probe_match(p2, pid, r2, &nd);
-            if (sl == ~0u) break;  // (:475-478)
+            const uint32_t tt = dat_slot(im, c, r2);
+            const uint64_t ch = im.cells[tt];
+            if (!dat_hit(ch, nid)) break;  // (:475-478)
             n++;
-            if (jb_node_fc(nd) == JB_FC_POS) edge(n, jb_node_widx(nd));
+            if (jb_cell_fc(ch) == JB_FC_POS) edge(n, jb_cell_widx(ch));
             if (ovf) break;
-            pid = im.nrows + sl;
+            nid = tt;
+            c = ch;
             pp += w2;
-            go = jb_node_hc(nd) != 0u;
+            go = jb_cell_hc(ch) != 0u;
         }
         erec[p / 3u] = ovf ? 0ull : rc;
     }
@@ -786,28 +760,28 @@ __device__ bool zh_block(const V& v, const DevImage& im, const uint64_t* __restr
                 }
                 uint32_t w0;
                 const uint32_t r0 = z_dec(v, q, &w0);
-                const uint32_t row = jb_row(im.pagemap, r0);
-                const uint32_t rec = im.l1[row];
-                const uint32_t fc = rec & 3u;
-                if (fc == JB_FC_ABSENT || fc == JB_FC_ZERO) {
-                    fold(1u, im.wtab[rec >> 3]);
+                uint32_t id = rune_code(im, r0);
+                uint64_t cc = im.cells[id];
+                if (jb_cell_check(cc) != JB_CHECK_ROOT) {
+                    fold(1u, im.wtab[JB_WIDX_ABSENT]);
+                } else if (jb_cell_fc(cc) == JB_FC_ZERO) {
+                    fold(1u, im.wtab[jb_cell_widx(cc)]);
                 } else {
-                    if (fc == JB_FC_POS) fold(1u, im.wtab[rec >> 3]);
-                    uint32_t id = row, qq = q + w0, len = 1;
-                    bool go = ((rec >> 2) & 1u) != 0u;
+                    if (jb_cell_fc(cc) == JB_FC_POS) fold(1u, im.wtab[jb_cell_widx(cc)]);
+                    uint32_t qq = q + w0, len = 1;
+                    bool go = jb_cell_hc(cc) != 0u;
                     while (go && qq < be) {
                         uint32_t wr;
                         const uint32_t r = z_dec(v, qq, &wr);
-                        Probe pr;
-                        probe_issue(im, id, r, &pr);
-                        uint64_t nd = 0;
-                        const uint32_t sl = probe_match(pr, id, r, &nd);
-                        if (sl == ~0u) break;
+                        const uint32_t tt = dat_slot(im, cc, r);
+                        const uint64_t ch = im.cells[tt];
+                        if (!dat_hit(ch, id)) break;
                         ++len;
                         qq += wr;
-                        if (jb_node_fc(nd) == JB_FC_POS) fold(len, im.wtab[jb_node_widx(nd)]);
-                        go = jb_node_hc(nd) != 0u;
-                        id = im.nrows + sl;
+                        if (jb_cell_fc(ch) == JB_FC_POS) fold(len, im.wtab[jb_cell_widx(ch)]);
+                        go = jb_cell_hc(ch) != 0u;
+                        id = tt;
+                        cc = ch;
                     }
                 }
             }
