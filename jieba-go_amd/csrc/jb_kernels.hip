@@ -580,7 +580,11 @@ __global__ __launch_bounds__(1024) void k_scan2(const uint2* __restrict__ cnt, u
 constexpr uint32_t kZhCap = JB_ZH_CAP;  // staged text bytes per wave
 constexpr uint32_t kZhRing = 8;    // LDS best ring per lane (runes)
 
-struct LdsZv {  // text and slots of the wave's staged span
+// A3: every rune of the block is 3 bytes (no 4-byte Han), so rune steps are
+// plain arithmetic instead of dependent byte reads.
+template <bool A3>
+struct LdsZvT {  // text and slots of the wave's staged span
+    static constexpr bool all3 = A3;
     const uint8_t* tx;
     uint8_t* bls;
     uint32_t wb;
@@ -588,7 +592,9 @@ struct LdsZv {  // text and slots of the wave's staged span
     __device__ __forceinline__ uint32_t x4(uint32_t q) const { return lds4(tx, q - wb); }
     __device__ __forceinline__ uint8_t& bl(uint32_t q) const { return bls[(q - wb) / 3u]; }
 };
+using LdsZv = LdsZvT<false>;
 struct GlbZv {  // the same, straight from HBM
+    static constexpr bool all3 = false;
     const uint8_t* text;
     uint8_t* gbl;
     __device__ __forceinline__ uint32_t b(uint32_t q) const { return text[q]; }
@@ -600,7 +606,7 @@ template <class V>
 __device__ __forceinline__ uint32_t z_dec(const V& v, uint32_t q, uint32_t* w) {  // Han rune at q
     const uint32_t x = v.x4(q);
     const uint32_t b0 = x & 0xFFu;
-    if (b0 < 0xF0u) {
+    if (V::all3 || b0 < 0xF0u) {
         *w = 3;
         return ((b0 & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
     }
@@ -608,9 +614,13 @@ __device__ __forceinline__ uint32_t z_dec(const V& v, uint32_t q, uint32_t* w) {
     return ((b0 & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) | (((x >> 16) & 0x3Fu) << 6) | ((x >> 24) & 0x3Fu);
 }
 template <class V>
-__device__ __forceinline__ uint32_t z_w(const V& v, uint32_t q) { return v.b(q) < 0xF0u ? 3u : 4u; }
+__device__ __forceinline__ uint32_t z_w(const V& v, uint32_t q) {
+    if (V::all3) return 3u;
+    return v.b(q) < 0xF0u ? 3u : 4u;
+}
 template <class V>
 __device__ __forceinline__ uint32_t z_prev(const V& v, uint32_t q, uint32_t lo) {  // rune that ends at q
+    if (V::all3) return q - 3u;  // (q > lo: a whole rune lies before q)
     if (q - lo < 4u) return lo;
     return (v.b(q - 3u) & 0xF0u) == 0xE0u ? q - 3u : q - 4u;
 }
@@ -813,7 +823,9 @@ __device__ bool zh_block(const V& v, const DevImage& im, const uint64_t* __restr
         const uint32_t L = v.bl(p);
         if (L == 0) return false;  // tail index -1: cutDAG's slice panics in the reference
         uint32_t pe = p;
-        for (uint32_t k = 0; k < L; k++) pe += z_w(v, pe);
+        if (V::all3) pe += 3u * L;
+        else
+            for (uint32_t k = 0; k < L; k++) pe += z_w(v, pe);
         if (!HMM) {
             em.token(p, pe);
         } else if (L == 1) {
@@ -910,8 +922,17 @@ __global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, ui
         if (valid) {
             bool ok;
             if (be <= wend) {
+                // any 4-byte rune (lead byte >= 0xF0) among the words that hold the block?
+                bool has4 = false;
+                for (uint32_t a = (bs & ~3u); a < be; a += 4u) {
+                    const uint32_t x = *reinterpret_cast<const uint32_t*>(tx + (a - wb));
+                    has4 |= (x & (x << 1) & (x << 2) & (x << 3) & 0x80808080u) != 0u;
+                }
                 LdsEmitter le(s_sb[wv], s_eb[wv], w0);
-                ok = zh_block<HMM>(LdsZv{tx, s_bl[wv], wb}, im, erec, gbest, ring, bs, be, le, ablate, st);
+                if (!has4)
+                    ok = zh_block<HMM>(LdsZvT<true>{tx, s_bl[wv], wb}, im, erec, gbest, ring, bs, be, le, ablate, st);
+                else
+                    ok = zh_block<HMM>(LdsZv{tx, s_bl[wv], wb}, im, erec, gbest, ring, bs, be, le, ablate, st);
                 le.flush();
             } else {
                 ok = zh_block<HMM>(GlbZv{text, gbl}, im, erec, gbest, ring, bs, be, em, ablate, st);
