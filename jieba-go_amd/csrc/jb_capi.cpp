@@ -340,7 +340,7 @@ static void free_work(Work* w) {
     dfree(w->docbits); dfree(w->sbits); dfree(w->ebits); dfree(w->tile_cnt); dfree(w->tile_off);
     dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->blk); dfree(w->lists); dfree(w->erec); dfree(w->lanemask);
     dfree(w->gbl); dfree(w->gbest);
-    dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters); dfree(w->dbg);
+    dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters); dfree(w->dbg); dfree(w->dbg_walk);
     *w = Work{};
 }
 
@@ -372,7 +372,11 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.tok_end, (nb + 4) * 4));
     HIPCHK(hipMalloc(&w.doc_tok, ((uint64_t)ndc + 2) * 8));
     HIPCHK(hipMalloc(&w.counters, 64 * 4));
-    if (getenv("JB_ABLATE") && (atoi(getenv("JB_ABLATE")) & 0x100)) HIPCHK(hipMalloc(&w.dbg, 65536 * 8 * 8));
+    if (getenv("JB_ABLATE") && (atoi(getenv("JB_ABLATE")) & 0x100)) {
+        HIPCHK(hipMalloc(&w.dbg, 65536 * 8 * 8));
+        HIPCHK(hipMalloc(&w.dbg_walk, ntiles * 4 * 8 * 8));
+        HIPCHK(hipMemset(w.dbg_walk, 0, ntiles * 4 * 8 * 8));
+    }
     w.cap_bytes = nb;
     w.cap_docs = ndc;
     return JB_OK;
@@ -455,6 +459,19 @@ static int launch(jb_ctx* ctx, Device* d, const uint8_t* d_text, uint64_t nbytes
                 a[0] / n, a[1] / n, a[2] / n, a[6] / n, a[3] / n, a[4] / n, 64.0 * a[5] / n,
                 a[4] / (64.0 * a[5] + 1e-9), a[7] / (64.0 * a[3] + 1e-9));
         HIPCHK(hipMemsetAsync(d->w.dbg, 0, (size_t)nwv * 64, s));
+        const uint64_t nww = (nbytes + kTileBytes - 1) / kTileBytes * 4;
+        std::vector<uint64_t> sw(nww * 8);
+        HIPCHK(hipMemcpyAsync(sw.data(), d->w.dbg_walk, sw.size() * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        double b[5] = {0, 0, 0, 0, 0}, m = 0;
+        for (uint64_t i = 0; i < nww; i++)
+            if (sw[i * 8 + 5] == 1) {
+                for (int k = 0; k < 5; k++) b[k] += (double)sw[i * 8 + k];
+                m++;
+            }
+        if (m == 0) m = 1;
+        fprintf(stderr, "[jb] k_mark_walk clocks/wave: mark %.0f entries %.0f walk %.0f deferred %.0f; trips/wave %.2f\n",
+                b[0] / m, b[1] / m, b[2] / m, b[3] / m, b[4] / m);
     }
     return JB_OK;
 }

@@ -50,7 +50,8 @@ struct Work {
     uint32_t* tok_end;
     uint64_t* doc_tok;
     uint32_t* counters;    // CNT_* (+ u64 ntok at counters + 8)
-    uint64_t* dbg = nullptr;  // diagnostic per-wave clocks of k_zh (JB_ABLATE bit 8), 8 u64 per wave
+    uint64_t* dbg = nullptr;       // diagnostic per-wave clocks of k_zh (JB_ABLATE bit 8), 8 u64 per wave
+    uint64_t* dbg_walk = nullptr;  // the same for k_mark_walk
     uint64_t cap_bytes = 0;
     uint32_t cap_docs = 0;
 };

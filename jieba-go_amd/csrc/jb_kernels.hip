@@ -261,7 +261,8 @@ __device__ __forceinline__ bool dat_hit(uint64_t child, uint32_t id) { return jb
 __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                    const uint32_t* __restrict__ docbits, DevImage im,
                                                    uint32_t* __restrict__ lanemask, uint2* __restrict__ tile_cnt,
-                                                   uint64_t* __restrict__ erec, uint32_t ablate) {
+                                                   uint64_t* __restrict__ erec, uint32_t ablate,
+                                                   uint64_t* __restrict__ dbg) {
     __shared__ __attribute__((aligned(16))) uint8_t s_t[kTileBytes + 32];  // bytes [t0-16, t0+4096+16)
     __shared__ uint32_t s_db[kTileBytes / 32 + 2];                        // document starts of the tile
     __shared__ uint32_t s_e[kTileE];
@@ -269,6 +270,13 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
     __shared__ uint32_t lds[8];
     __shared__ uint16_t s_def[256];  // walk starts whose run goes past the tile
     __shared__ uint32_t s_ndef;
+#if JB_STAMPS
+    const bool stamps = (ablate & 0x100u) != 0;  // diagnostic per-wave phase clocks (make STAMPS=1)
+#else
+    const bool stamps = false;
+#endif
+    uint64_t c0 = stamps ? __builtin_amdgcn_s_memtime() : 0, c1 = 0, c2 = 0, c3 = 0;
+    uint32_t trips = 0;
     const uint64_t t0 = (uint64_t)blockIdx.x * kTileBytes;
     for (uint32_t k = threadIdx.x; k < kTileBytes / 16 + 2; k += 256) {
         const int64_t g = (int64_t)t0 - 16 + 16 * (int64_t)k;
@@ -333,6 +341,7 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
     uint32_t tot;
     block_scan_u32(__popc(bmask) | (__popc(zmask) << 16), lds, &tot);
     if (threadIdx.x == 0) tile_cnt[blockIdx.x] = make_uint2(tot & 0xFFFFu, tot >> 16);
+    if (stamps) c1 = __builtin_amdgcn_s_memtime();
 
     // ---- (2) Han rune entries of the tile, in text order ---------------------------
     uint32_t hs = ((hanb & ~covered & valid) >> 4) & 0xFFFFu;  // Han rune starts of the lane's bytes
@@ -359,6 +368,7 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
         s_e[i] = rune_code(im, ent_rune(e)) | (e & 0x3FFC0000u) | f;  // (position bits never change)
     }
     __syncthreads();
+    if (stamps) c2 = __builtin_amdgcn_s_memtime();
     // ---- walks: wave w takes the walk starts [lo, hi) of the tile ---------------------
     const uint32_t* ent = s_e;
     const uint32_t wv = threadIdx.x >> 6;
@@ -441,8 +451,10 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
                 finish();  // (:475-478)
             }
         }
+        trips++;
         if (!__any(act) && head >= hi) break;
     }
+    if (stamps) c3 = __builtin_amdgcn_s_memtime();
     __syncthreads();
     // ---- walks whose Han run goes past the tile: from global memory (rare) ------------
     const uint32_t ndef = s_ndef;
@@ -481,6 +493,15 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
             go = jb_cell_hc(ch) != 0u;
         }
         erec[p / 3u] = ovf ? 0ull : rc;
+    }
+    if (stamps && (threadIdx.x & 63u) == 0) {  // per-wave phase clocks, summed on the host
+        uint64_t* o = dbg + ((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * 8u;
+        o[0] = c1 - c0;
+        o[1] = c2 - c1;
+        o[2] = c3 - c2;
+        o[3] = __builtin_amdgcn_s_memtime() - c3;
+        o[4] = trips;
+        o[5] = 1;
     }
 }
 
@@ -1148,7 +1169,8 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         JB_TIMED(K_DOCBITS, hipLaunchKernelGGL(k_docbits, dim3((ndocs + 255) / 256), dim3(256), 0, stream,
                                                d_doc_off, ndocs, nbytes, w.docbits));
     JB_TIMED(K_MARK_WALK, hipLaunchKernelGGL(k_mark_walk, dim3(ntiles), dim3(256), 0, stream, d_text, nbytes,
-                                             w.docbits, im, w.lanemask, w.tile_cnt, w.erec, g_ablate));
+                                             w.docbits, im, w.lanemask, w.tile_cnt, w.erec, g_ablate,
+                                             w.dbg_walk));
     JB_TIMED(K_SCAN_BLOCKS, hipLaunchKernelGGL(k_scan2, dim3(1), dim3(1024), 0, stream, w.tile_cnt, ntiles,
                                                w.tile_off, w.counters + CNT_NBLK, nullptr, w.blk,
                                                (uint32_t)nbytes));
