@@ -29,7 +29,7 @@ enum {
 };
 
 constexpr int kTileBytes = 4096;       // k_blocks: 256 threads x 16 bytes
-constexpr int kTokTileWords = 1024;    // k_tok: 256 threads x 4 words (32 KiB of text)
+constexpr int kTokTileWords = 512;     // k_tok: 256 threads x 2 words (16 KiB of text)
 
 // Per-call device workspace, sized for `nbytes` of text.
 struct Work {

@@ -1057,24 +1057,27 @@ __global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits,
                                              uint64_t nwords, uint2* __restrict__ tile_cnt,
                                              const uint2* __restrict__ tile_off, uint32_t* __restrict__ tok_start,
                                              uint32_t* __restrict__ tok_end) {
+    constexpr uint32_t W = kTokTileWords / 256;  // bitmap words per lane
+    constexpr uint32_t kCap = 3072;              // tokens per tile staged in LDS
     __shared__ uint32_t lds[8];
-    const uint64_t w0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
-    uint32_t s[4], e[4];
-    if (w0 + 4 <= nwords) {
-        const uint4 a = *reinterpret_cast<const uint4*>(sbits + w0);
-        const uint4 b = *reinterpret_cast<const uint4*>(ebits + w0);
-        s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w;
-        e[0] = b.x; e[1] = b.y; e[2] = b.z; e[3] = b.w;
+    __shared__ uint32_t s_s[WRITE ? kCap : 1], s_e[WRITE ? kCap : 1];
+    const uint64_t w0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * W;
+    uint32_t s[W], e[W];
+    if (w0 + W <= nwords) {
+        const uint2 a = *reinterpret_cast<const uint2*>(sbits + w0);
+        const uint2 b = *reinterpret_cast<const uint2*>(ebits + w0);
+        s[0] = a.x; s[1] = a.y;
+        e[0] = b.x; e[1] = b.y;
     } else {
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (uint32_t k = 0; k < W; k++) {
             s[k] = w0 + k < nwords ? sbits[w0 + k] : 0u;
             e[k] = w0 + k < nwords ? ebits[w0 + k] : 0u;
         }
     }
     uint32_t cs = 0, ce = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (uint32_t k = 0; k < W; k++) {
         cs += __popc(s[k]);
         ce += __popc(e[k]);
     }
@@ -1086,22 +1089,30 @@ __global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits,
         return;
     }
     const uint2 to = tile_off[blockIdx.x];
-    uint32_t gs = to.x + xs, ge = to.y + xe;
+    // spans go to LDS in tile order, then out in one coalesced pass (a lane's own
+    // tokens are ~60 bytes apart in the output: direct stores touch a line each)
+    const bool staged = ts <= kCap && te <= kCap;
+    uint32_t* os = staged ? s_s : tok_start + to.x;
+    uint32_t* oe = staged ? s_e : tok_end + to.y;
+    uint32_t gs = xs, ge = xe;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (uint32_t k = 0; k < W; k++) {
         const uint32_t base = (uint32_t)((w0 + k) << 5);
         uint32_t m = s[k];
         while (m) {
-            const uint32_t b = __builtin_ctz(m);
-            tok_start[gs++] = base + b;
+            os[gs++] = base + (uint32_t)__builtin_ctz(m);
             m &= m - 1;
         }
         m = e[k];
         while (m) {
-            const uint32_t b = __builtin_ctz(m);
-            tok_end[ge++] = base + b + 1u;
+            oe[ge++] = base + (uint32_t)__builtin_ctz(m) + 1u;
             m &= m - 1;
         }
+    }
+    if (staged) {
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < ts; k += 256u) tok_start[to.x + k] = s_s[k];
+        for (uint32_t k = threadIdx.x; k < te; k += 256u) tok_end[to.y + k] = s_e[k];
     }
 }
 
