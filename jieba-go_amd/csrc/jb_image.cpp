@@ -413,6 +413,10 @@ int build_image(const Dictionary& d, const Emission& e, Image* img, std::string*
         img->code.assign(img->nrows, 0u);
         for (size_t i = 0; i < ord.size(); i++) img->code[jb_row(pm, ord[i].first)] = (uint32_t)i + 1u;
         img->ncodes = (uint32_t)ord.size() + 1u;
+        if (img->ncodes >= (1u << 17)) {  // k_mark_walk keeps 17-bit codes
+            *err = "more than 131071 distinct runes in the dictionary keys";
+            return JB_ELIMIT;
+        }
     }
     auto code_of = [&](uint32_t r) { return img->code[jb_row(pm, r)]; };
     std::vector<uint64_t>& cells = img->cells;

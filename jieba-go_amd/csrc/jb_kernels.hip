@@ -187,9 +187,10 @@ constexpr uint32_t kTileE = kTileBytes / 3 + 2;  // Han rune entries of a tile (
 // entry: rune (bits 0-17; Han runes are < 0x40000) | tile offset (bits 18-29)
 constexpr uint32_t kEntCont = 0x40000000u;  // the next entry continues the run
 constexpr uint32_t kEntEdge = 0x80000000u;  // the run may continue past the tile
-__device__ __forceinline__ uint32_t ent_rune(uint32_t e) { return e & 0x3FFFFu; }
+// entry: rune code [0,17) | 4-byte rune [17] | tile offset [18,30) | flags [30,32)
+__device__ __forceinline__ uint32_t ent_code(uint32_t e) { return e & 0x1FFFFu; }
 __device__ __forceinline__ uint32_t ent_pos(uint32_t e) { return (e >> 18) & 0xFFFu; }
-__device__ __forceinline__ uint32_t ent_w(uint32_t e) { return ent_rune(e) >= 0x10000u ? 4u : 3u; }
+__device__ __forceinline__ uint32_t ent_w(uint32_t e) { return 3u + ((e >> 17) & 1u); }
 
 // The Han rune encoded by x (Go-valid, within `lim` bytes), or 0.  A 3-byte
 // form with a Han value cannot be overlong (E0) or a surrogate (ED), and a
@@ -347,25 +348,47 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
     uint32_t hs = ((hanb & ~covered & valid) >> 4) & 0xFFFFu;  // Han rune starts of the lane's bytes
     uint32_t nent;
     uint32_t o = block_scan_u32(__popc(hs), lds, &nent);
-    while (hs) {
-        const uint32_t k = (uint32_t)__builtin_ctz(hs);
-        hs &= hs - 1u;
-        const uint32_t x = lds4(win, k + 4u);
-        const uint32_t r = (x & 0xF0u) == 0xE0u
-                               ? ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu)
-                               : ((x & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) | (((x >> 16) & 0x3Fu) << 6) |
-                                     ((x >> 24) & 0x3Fu);
-        s_c[o] = (ablate & 2u) ? 0ull : im.cells[rune_code(im, r)];
-        s_e[o++] = r | ((threadIdx.x * 16u + k) << 18);
+    {
+        // at most 6 Han runes start in a lane's 16 bytes: decode them and issue all
+        // code loads, then all level-1 cell loads (two round trips, not two per rune)
+        const uint32_t ne = __popc(hs);
+        uint32_t kk[6], rr[6], cd[6];
+        uint64_t cl[6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            kk[i] = 0u;
+            rr[i] = 0u;
+            cd[i] = 0u;
+            if ((uint32_t)i < ne) {
+                const uint32_t k = (uint32_t)__builtin_ctz(hs);
+                hs &= hs - 1u;
+                const uint32_t x = lds4(win, k + 4u);
+                const uint32_t r = (x & 0xF0u) == 0xE0u
+                                       ? ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu)
+                                       : ((x & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) |
+                                             (((x >> 16) & 0x3Fu) << 6) | ((x >> 24) & 0x3Fu);
+                kk[i] = k;
+                rr[i] = r;
+                cd[i] = rune_code(im, r);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 6; i++) cl[i] = ((uint32_t)i < ne && !(ablate & 2u)) ? im.cells[cd[i]] : 0ull;
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+            if ((uint32_t)i < ne) {
+                s_c[o + i] = cl[i];
+                s_e[o + i] = cd[i] | ((rr[i] >= 0x10000u ? 1u : 0u) << 17) | ((threadIdx.x * 16u + kk[i]) << 18);
+            }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nent; i += 256u) {  // run links; the rune field becomes its code
+    for (uint32_t i = threadIdx.x; i < nent; i += 256u) {  // run links
         const uint32_t e = s_e[i];
         const uint32_t nxt = ent_pos(e) + ent_w(e);
         uint32_t f = 0;
         if (nxt >= kTileBytes) f = kEntEdge;
         else if (i + 1u < nent && ent_pos(s_e[i + 1u]) == nxt && !((s_db[nxt >> 5] >> (nxt & 31u)) & 1u)) f = kEntCont;
-        s_e[i] = rune_code(im, ent_rune(e)) | (e & 0x3FFC0000u) | f;  // (position bits never change)
+        s_e[i] = e | f;
     }
     __syncthreads();
     if (stamps) c2 = __builtin_amdgcn_s_memtime();
@@ -414,7 +437,7 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
             ecur = ent[j0];
             cur = s_c[j0];
             q = ent_pos(ecur);
-            id = ent_rune(ecur);  // the rune's code: its level-1 cell
+            id = ent_code(ecur);  // its level-1 cell
             len = 1u;
             nedge = 0u;
             rc = 0ull;
@@ -437,7 +460,7 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
         uint32_t t = 0;
         if (act) {
             const uint32_t en = ent[min(j + 1u, elast)];
-            t = dat_slot_k(cur, ent_rune(en));
+            t = dat_slot_k(cur, ent_code(en));
             child = im.cells[t];
             if (dat_hit(child, id)) {
                 ++j;
