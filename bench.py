@@ -122,10 +122,7 @@ def main():
         step()
     torch.cuda.synchronize(dev)
 
-    prof = not args.no_profile
-    if prof:
-        tk.profile(True)
-        tk.profile_reset()
+    # timed region: the pipeline replays as one captured HIP graph per step
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -137,8 +134,23 @@ def main():
     elapsed = time.perf_counter() - t_start
     if dist:
         dist.barrier()
-    kprof = tk.profile_read() if prof else {}
-    tk.profile(False)
+
+    # per-kernel durations: the same K steps again, launched kernel by kernel
+    # with a HIP event pair around each launch on the launch stream
+    prof = not args.no_profile
+    kprof = {}
+    prof_ms = None
+    if prof:
+        tk.profile(True)
+        tk.profile_reset()
+        torch.cuda.synchronize(dev)
+        tp = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        prof_ms = (time.perf_counter() - tp) / args.steps * 1e3
+        kprof = tk.profile_read()
+        tk.profile(False)
 
     # whole-job aggregates: max time over ranks, sum of work
     if dist:
@@ -242,6 +254,7 @@ def main():
             "han_chars_per_s": round(tot_han / 3 * args.steps / elapsed, 1),
             "input_GBps": round(tot_bytes * args.steps / elapsed / 1e9, 3),
             "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
+            "ms_per_step_kernel_by_kernel": round(prof_ms, 4) if prof_ms else None,
             "gen_s": round(gen_s, 2),
             "loaded": J.loaded_runtime(),
         }

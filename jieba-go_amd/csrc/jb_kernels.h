@@ -36,6 +36,7 @@ struct Work {
     uint32_t* docbits;     // 1 bit per byte: a document starts here
     uint32_t* sbits;       // 1 bit per byte: a token starts here
     uint32_t* ebits;       // 1 bit per byte: a token ends here (last byte)
+    uint64_t bits_stride;  // words between docbits, sbits and ebits (one allocation)
     uint2* tile_cnt;       // per k_blocks tile (all, zh) counts, then exclusive offsets
     uint2* tile_off;
     uint2* ttile_cnt;      // per token tile (starts, ends)
