@@ -352,7 +352,7 @@ static int upload_image(Device* d, const Image& img) {
 static void free_work(Work* w) {
     dfree(w->docbits); dfree(w->tile_cnt); dfree(w->tile_off);
     dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->blk); dfree(w->lists); dfree(w->erec); dfree(w->lanemask);
-    dfree(w->gbl); dfree(w->gbest);
+    dfree(w->gbl); dfree(w->gbest); dfree(w->gstart);
     dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters); dfree(w->dbg); dfree(w->dbg_walk);
     *w = Work{};
 }
@@ -384,6 +384,7 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.erec, (nb / 3 + 8) * 8));
     HIPCHK(hipMalloc(&w.lanemask, ntiles * 256 * 4));
     HIPCHK(hipMalloc(&w.gbl, nb / 3 + 8));
+    HIPCHK(hipMalloc(&w.gstart, (nb / kZhGroupBytes + 4) * 4));
     HIPCHK(hipMalloc(&w.gbest, (nb / 3 + 8) * sizeof(double)));
 
     HIPCHK(hipMalloc(&w.tok_start, (nb + 4) * 4));
@@ -507,10 +508,10 @@ static int launch(jb_ctx* ctx, Device* d, const uint8_t* d_text, uint64_t nbytes
                 n++;
             }
         if (n == 0) n = 1;
-        fprintf(stderr, "[jb] k_zh clocks/wave: staging %.0f dp %.0f fwd+vit %.0f total %.0f; groups/wave %.1f; "
-                        "lane DP runes %.0f vs 64*max %.0f (DP lane use %.2f); lanes outside the window %.3f\n",
+        fprintf(stderr, "[jb] k_zh clocks/wave: setup %.0f dp %.0f fwd+vit %.0f total %.0f; chunks/wave %.1f; "
+                        "lane DP steps %.0f vs 64*max %.0f (DP lane use %.2f); blocks past the window per chunk %.3f\n",
                 a[0] / n, a[1] / n, a[2] / n, a[6] / n, a[3] / n, a[4] / n, 64.0 * a[5] / n,
-                a[4] / (64.0 * a[5] + 1e-9), a[7] / (64.0 * a[3] + 1e-9));
+                a[4] / (64.0 * a[5] + 1e-9), a[7] / (a[3] + 1e-9));
         HIPCHK(hipMemsetAsync(d->w.dbg, 0, (size_t)nwv * 64, s));
         const uint64_t nww = (nbytes + kTileBytes - 1) / kTileBytes * 4;
         std::vector<uint64_t> sw(nww * 8);

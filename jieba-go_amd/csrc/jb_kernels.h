@@ -24,12 +24,16 @@ enum {
     CNT_NTOK = 2,   // token starts
     CNT_NTOKE = 3,  // token ends (== CNT_NTOK when consistent)
     CNT_ERR = 4,    // bit 0: a zh block reached a tail index -1 (the reference panics)
-    CNT_WORK = 5,   // k_zh work counter: next chunk of 64 zh blocks
+    CNT_WORK = 5,   // k_zh work counter: next group (kZhGroupBytes of text)
     CNT_NWORDS = 8  // u32 slots reserved; u64 token count lives at byte offset 32
 };
 
 constexpr int kTileBytes = 4096;       // k_blocks: 256 threads x 16 bytes
 constexpr int kTokTileWords = 512;     // k_tok: 256 threads x 2 words (16 KiB of text)
+#ifndef JB_ZH_GROUP
+#define JB_ZH_GROUP 6144
+#endif
+constexpr uint32_t kZhGroupBytes = JB_ZH_GROUP;  // k_zh work unit: zh blocks starting in one such span (multiple of 32)
 
 // Per-call device workspace, sized for `nbytes` of text.
 struct Work {
@@ -45,6 +49,7 @@ struct Work {
     uint32_t* lists;       // zh block ids from the front, non-zh block ids from the back
     uint64_t* erec;        // per Han rune (slot = byte / 3): packed DAG edges (k_mark_walk -> k_zh)
     uint32_t* lanemask;    // per 16 bytes: block starts | Han block starts << 16
+    uint32_t* gstart;      // per k_zh group: first zh block index starting at or after g * kZhGroupBytes
     uint8_t* gbl;          // per Han rune: chosen piece length, then Viterbi back-pointers / labels
     double* gbest;         // per Han rune: best proba, kept only for blocks with an edge > 8 runes
     uint32_t* tok_start;

@@ -30,9 +30,6 @@
 #ifndef JB_STAMPS
 #define JB_STAMPS 0
 #endif
-#ifndef JB_ZH_CAP
-#define JB_ZH_CAP 3584  // k_zh window: text bytes staged per wave
-#endif
 
 namespace jb {
 
@@ -267,9 +264,9 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
     __shared__ __attribute__((aligned(16))) uint8_t s_t[kTileBytes + 32];  // bytes [t0-16, t0+4096+16)
     __shared__ uint32_t s_db[kTileBytes / 32 + 2];                        // document starts of the tile
     __shared__ uint32_t s_e[kTileE];
-    __shared__ uint64_t s_c[kTileE];  // the level-1 cell of each entry's rune
+    __shared__ uint64_t s_c[kTileE];  // the level-1 cell of each entry's rune, then the record of its walk
     __shared__ uint32_t lds[8];
-    __shared__ uint16_t s_def[256];  // walk starts whose run goes past the tile
+    __shared__ uint16_t s_def[256];  // entries whose walk's run goes past the tile
     __shared__ uint32_t s_ndef;
 #if JB_STAMPS
     const bool stamps = (ablate & 0x100u) != 0;  // diagnostic per-wave phase clocks (make STAMPS=1)
@@ -399,7 +396,7 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
     const uint32_t hi = (nent * (wv + 1u)) >> 2;
     const uint32_t elast = nent ? nent - 1u : 0u;
     bool act = false, ovf = false;
-    uint32_t q = 0, j = 0, ecur = 0, id = 0, len = 0, nedge = 0;
+    uint32_t q = 0, j = 0, js = 0, ecur = 0, id = 0, len = 0, nedge = 0;
     uint64_t cur = 0;  // the cell of the walk's current node
     uint64_t rc = 0;
     auto edge = [&](uint32_t L, uint32_t wi) {
@@ -410,12 +407,12 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
         rc |= (1ull << (L - 1u)) | ((uint64_t)wi << (8u + kEdgeIdxBits * nedge));
         nedge++;
     };
-    auto finish = [&]() {
-        erec[(t0 + q) / 3u] = ovf ? 0ull : rc;
+    auto finish = [&]() {  // the record waits in the start entry's LDS cell (read when the walk began)
+        s_c[js] = ovf ? 0ull : rc;
         act = false;
     };
     auto defer = [&]() {  // the run goes on past the tile: walked again from global memory below
-        s_def[atomicAdd(&s_ndef, 1u)] = (uint16_t)q;
+        s_def[atomicAdd(&s_ndef, 1u)] = (uint16_t)js;
         act = false;
     };
     // after a hit on node `id` (cell `cur`) whose rune is entry ecur: go on, defer or stop
@@ -434,6 +431,7 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
         head = min(hi, head + (uint32_t)__popcll(need));
         if (fresh) {  // level 1 from LDS; the walk goes on only with children and a next rune
             j = j0;
+            js = j0;
             ecur = ent[j0];
             cur = s_c[j0];
             q = ent_pos(ecur);
@@ -482,7 +480,8 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
     // ---- walks whose Han run goes past the tile: from global memory (rare) ------------
     const uint32_t ndef = s_ndef;
     for (uint32_t i = threadIdx.x; i < ndef; i += 256u) {
-        const uint64_t p = t0 + s_def[i];
+        const uint32_t ei = s_def[i];
+        const uint64_t p = t0 + ent_pos(s_e[ei]);
         uint32_t wr;
         const uint32_t r0 = han_rune(ld4(text, p), 4u, &wr);  // a Han rune of this tile (checked above)
         uint32_t nid = rune_code(im, r0);
@@ -515,8 +514,11 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
             pp += w2;
             go = jb_cell_hc(ch) != 0u;
         }
-        erec[p / 3u] = ovf ? 0ull : rc;
+        s_c[ei] = ovf ? 0ull : rc;
     }
+    __syncthreads();
+    // records out in entry (= text) order: consecutive lanes, mostly consecutive slots
+    for (uint32_t i = threadIdx.x; i < nent; i += 256u) erec[(t0 + ent_pos(s_e[i])) / 3u] = s_c[i];
     if (stamps && (threadIdx.x & 63u) == 0) {  // per-wave phase clocks, summed on the host
         uint64_t* o = dbg + ((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * 8u;
         o[0] = c1 - c0;
@@ -530,19 +532,23 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
 
 // k_blocks_write: the lane masks -> block list (start | zh<<31), zh block ids
 // (ascending) and non-zh block ids (from the end of `lists`, descending).
+// The thread whose 16 bytes begin a k_zh group (g * kZhGroupBytes) also writes
+// gstart[g]: the number of zh blocks that start before it.
 __global__ __launch_bounds__(256) void k_blocks_write(const uint32_t* __restrict__ lanemask,
                                                       const uint2* __restrict__ tile_off, uint32_t* __restrict__ blk,
-                                                      uint32_t* __restrict__ lists, uint32_t list_cap) {
+                                                      uint32_t* __restrict__ lists, uint32_t list_cap,
+                                                      uint32_t* __restrict__ gstart) {
     __shared__ uint32_t lds[8];
     uint32_t m = lanemask[blockIdx.x * 256u + threadIdx.x];
     const uint32_t bmask = m & 0xFFFFu, zmask = m >> 16;
     uint32_t tot;
     const uint32_t ex = block_scan_u32(__popc(bmask) | (__popc(zmask) << 16), lds, &tot);
-    if (!bmask) return;
+    const uint32_t p0 = (blockIdx.x * 256u + threadIdx.x) * 16u;
     const uint2 to = tile_off[blockIdx.x];
+    if (p0 % kZhGroupBytes == 0u) gstart[p0 / kZhGroupBytes] = to.y + (ex >> 16);
+    if (!bmask) return;
     uint32_t ga = to.x + (ex & 0xFFFFu);  // global block rank
     uint32_t gz = to.y + (ex >> 16);      // global zh rank
-    const uint32_t p0 = (blockIdx.x * 256u + threadIdx.x) * 16u;
     uint32_t b = bmask;
     while (b) {
         const uint32_t k = __builtin_ctz(b);
@@ -639,39 +645,47 @@ __global__ __launch_bounds__(1024) void k_scan2(const uint2* __restrict__ cnt, u
 }
 
 // ---------------------------------------------------------------------------
-// k_zh: one lane per Han block (cutZh, tokenizer.go:221-255).
+// k_zh: Han blocks (cutZh, tokenizer.go:221-255), balanced over a wave's lanes.
 //
-// Waves pull 64 consecutive blocks at a time (one per lane; fast waves take
-// more) and stage the text span that holds them in LDS, so rune stepping,
-// decoding and the per-rune scratch run out of LDS.  Per block, backward over
-// its runes (calcDagProba, :502-548): the rune's edges (i, i+L) from k_mark_walk,
-// ascending in L as the DAG lists them, fold into maxIndexProba's running
-// state (:565-578) with pieceProba = w + best(i+L) (:519-529); best(n) is the
-// {n, 0.0} sentinel (:522-525).  best(i+L) for L <= 8 comes from an 8-entry
-// LDS ring; a block with a longer edge (rare) is redone with every best value
-// also stored in gbest (index be/3 - c, inside the block's slot range).  The
-// chosen piece length goes to the rune's slot; the forward walk (findDagPath,
+// Work unit: a group = the zh blocks that start in one kZhGroupBytes span of
+// text (gstart[] from k_blocks_write), dequeued by whole waves.  The group's
+// blocks (in chunks of at most kZhChunk) are ranked by length and dealt to
+// the 64 lanes in a snake (lane i gets ranks i, 127-i, 128+i, ...), so every
+// lane carries about the same number of runes.  Per lane, one flattened
+// backward loop runs the DP over all of its blocks (calcDagProba, :502-548):
+// a rune's edges (i, i+L) from k_mark_walk, ascending in L as the DAG lists
+// them, fold into maxIndexProba's running state (:565-578) with
+// pieceProba = w + best(i+L) (:519-529); best(n) is the {n, 0.0} sentinel
+// (:522-525).  best(i+L) for L <= 8 comes from an 8-entry LDS ring; a block
+// with a longer edge (rare) is redone with every best value also stored in
+// gbest (index be/3 - c, inside the block's slot range).  The chosen piece
+// length goes to the rune's slot in LDS; the forward walk (findDagPath,
 // :552-562) then emits pieces or, with HMM, gathers runs of single-rune pieces
-// for the Viterbi (:228-253).  Blocks that do not fit the staged span run the
-// same code on global memory.
+// for the Viterbi (:228-253).  Token bits collect in LDS (over the ring, which
+// is dead by then) and leave with one atomicOr per word.  A block that ends
+// past the group window (kZhWin bytes) runs the same code on global memory.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kZhCap = JB_ZH_CAP;  // staged text bytes per wave
-constexpr uint32_t kZhRing = 8;    // LDS best ring per lane (runes)
+constexpr uint32_t kZhRing = 8;                            // LDS best ring per lane (runes)
+constexpr uint32_t kZhWin = kZhGroupBytes + 1024u;         // window: group span + slack for the last blocks
+constexpr uint32_t kZhChunk = 192;                         // blocks ranked together (3 per lane)
+constexpr uint32_t kZhWinWords = kZhWin / 32u + 1u;        // token bitmap words of a window
+static_assert(kZhGroupBytes % 32u == 0u && kZhGroupBytes >= kTileBytes, "k_zh group: whole words, one per tile");
+static_assert(2u * kZhWinWords <= 2u * kZhRing * 64u, "token bitmaps fit over the ring");
+static_assert(kZhWin < 65536u, "window offsets are packed in 16 bits");
 
 // A3: every rune of the block is 3 bytes (no 4-byte Han), so rune steps are
 // plain arithmetic instead of dependent byte reads.
 template <bool A3>
-struct LdsZvT {  // text and slots of the wave's staged span
+struct GrpZvT {  // text from HBM, slots of the group window in LDS
     static constexpr bool all3 = A3;
-    const uint8_t* tx;
+    const uint8_t* text;
     uint8_t* bls;
     uint32_t wb;
-    __device__ __forceinline__ uint32_t b(uint32_t q) const { return tx[q - wb]; }
-    __device__ __forceinline__ uint32_t x4(uint32_t q) const { return lds4(tx, q - wb); }
+    __device__ __forceinline__ uint32_t b(uint32_t q) const { return text[q]; }
+    __device__ __forceinline__ uint32_t x4(uint32_t q) const { return ld4(text, q); }
     __device__ __forceinline__ uint8_t& bl(uint32_t q) const { return bls[(q - wb) / 3u]; }
 };
-using LdsZv = LdsZvT<false>;
-struct GlbZv {  // the same, straight from HBM
+struct GlbZv {  // the same, slots in HBM (blocks past the window)
     static constexpr bool all3 = false;
     const uint8_t* text;
     uint8_t* gbl;
@@ -786,116 +800,270 @@ __device__ void viterbi_run(const V& v, const DevImage& im, uint32_t rs, uint32_
     }
 }
 
-// One Han block [bs, be).  Returns false where the reference panics (a rune
-// on the chosen path with no DAG edge: cutDAG slices with tail index -1).
-template <bool HMM, class V, class E>
-__device__ bool zh_block(const V& v, const DevImage& im, const uint64_t* __restrict__ erec,
-                         double* __restrict__ gbest, double* ring, uint32_t bs, uint32_t be, E& em,
-                         uint32_t ablate, uint64_t* st) {
-    const uint32_t key0 = be / 3u;
-    uint32_t c_done = 0;
-    // The best values of the last kZhRing runes live in the LDS ring.  A block
-    // with a longer edge is redone with every best value also kept in gbest.
-    for (bool longm = false;; longm = true) {
-        bool redo = false;
-        uint32_t q = z_prev(v, be, bs), c = 1;
-        uint64_t rc = erec[q / 3u];
-        for (;;) {
-            const bool more = q > bs;
-            double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT;
-            uint32_t bestL = 0, lastL = 0;
-            auto fold = [&](uint32_t L, double wt) {
-                double nb;
-                if (L == c) nb = 0.0;
-                else if (L <= kZhRing) nb = ring[((c - L) & (kZhRing - 1u)) * 64u];
-                else if (longm) nb = gbest[key0 - (c - L)];
-                else {
-                    redo = true;
-                    nb = 0.0;
-                }
-                const double pp = wt + nb;
-                if (pp >= prevP) {
-                    bestL = L;
-                    bestP = pp;
-                }
-                prevP = pp;
-                lastL = L;
-            };
-            uint32_t qn = 0;
-            uint64_t rn = 0;
-            if ((uint32_t)rc & 0xFFu) {
-                double w4[4];
-                uint32_t L4[4];
-                uint32_t m = (uint32_t)rc & 0xFFu;
-#pragma unroll
-                for (int k = 0; k < 4; k++) {  // weight loads of all edges first (independent)
-                    L4[k] = m ? (uint32_t)__builtin_ctz(m) + 1u : 0u;
-                    m &= m - 1u;
-                    const uint32_t idx = (uint32_t)(rc >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u);
-                    w4[k] = L4[k] ? im.wtab[idx] : 0.0;
-                }
-                if (more) {  // next rune's record, in flight while this rune folds
-                    qn = z_prev(v, q, bs);
-                    rn = (ablate & 64u) ? 1ull : erec[qn / 3u];
-                }
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    if (L4[k]) fold(L4[k], w4[k]);
-            } else {  // many or long edges: walk this rune here (the rules of k_mark_walk)
-                if (more) {
-                    qn = z_prev(v, q, bs);
-                    rn = erec[qn / 3u];
-                }
-                uint32_t w0;
-                const uint32_t r0 = z_dec(v, q, &w0);
-                uint32_t id = rune_code(im, r0);
-                uint64_t cc = im.cells[id];
-                if (jb_cell_check(cc) != JB_CHECK_ROOT) {
-                    fold(1u, im.wtab[JB_WIDX_ABSENT]);
-                } else if (jb_cell_fc(cc) == JB_FC_ZERO) {
-                    fold(1u, im.wtab[jb_cell_widx(cc)]);
-                } else {
-                    if (jb_cell_fc(cc) == JB_FC_POS) fold(1u, im.wtab[jb_cell_widx(cc)]);
-                    uint32_t qq = q + w0, len = 1;
-                    bool go = jb_cell_hc(cc) != 0u;
-                    while (go && qq < be) {
-                        uint32_t wr;
-                        const uint32_t r = z_dec(v, qq, &wr);
-                        const uint32_t tt = dat_slot(im, cc, r);
-                        const uint64_t ch = im.cells[tt];
-                        if (!dat_hit(ch, id)) break;
-                        ++len;
-                        qq += wr;
-                        if (jb_cell_fc(ch) == JB_FC_POS) fold(len, im.wtab[jb_cell_widx(ch)]);
-                        go = jb_cell_hc(ch) != 0u;
-                        id = tt;
-                        cc = ch;
-                    }
-                }
+// A lane's blocks of the current chunk: LDS table entries t[j * 64] for
+// j < nseg, (bs - wb) | (be - wb) << 16, ~0u = none.
+struct TblSrc {
+    const uint32_t* t;
+    uint32_t nseg, wb;
+    __device__ __forceinline__ bool next(uint32_t& j, uint32_t& bs, uint32_t& be) const {
+        while (j < nseg) {
+            const uint32_t x = t[j * 64u];
+            j++;
+            if (x != ~0u) {
+                bs = wb + (x & 0xFFFFu);
+                be = wb + (x >> 16);
+                return true;
             }
-            if (bestL == 0) {  // no item qualified: the last item (or {-1, minFloat})
-                bestL = lastL;
-                bestP = prevP;
+        }
+        return false;
+    }
+};
+struct OneSrc {  // a single block
+    uint32_t bs0, be0;
+    __device__ __forceinline__ bool next(uint32_t& j, uint32_t& bs, uint32_t& be) const {
+        if (j) return false;
+        j = 1;
+        bs = bs0;
+        be = be0;
+        return true;
+    }
+};
+
+// DP over all of a lane's blocks in one backward loop: when a block's first
+// rune is done the loop moves on to the lane's next block, so a lane's trip
+// count is its total rune count, not the per-block maximum over the wave.
+// Returns the number of DP steps (diagnostics).
+struct DpFold {  // maxIndexProba's running state over one rune's DAG items (:565-578)
+    double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT;
+    uint32_t bestL = 0, lastL = 0;
+    bool redo = false;
+    __device__ __forceinline__ void item(uint32_t L, double wt, uint32_t c, const double* ring, bool longm,
+                                         const double* __restrict__ gbest, uint32_t key0) {
+        double nb;
+        if (L == c) nb = 0.0;  // the {n, 0.0} sentinel
+        else if (L <= kZhRing) nb = ring[((c - L) & (kZhRing - 1u)) * 64u];
+        else if (longm) nb = gbest[key0 - (c - L)];
+        else {
+            redo = true;
+            nb = 0.0;
+        }
+        const double pp = wt + nb;
+        if (pp >= prevP) {
+            bestL = L;
+            bestP = pp;
+        }
+        prevP = pp;
+        lastL = L;
+    }
+    __device__ __forceinline__ void finish() {
+        if (bestL == 0) {  // no item qualified: the last item (or {-1, minFloat})
+            bestL = lastL;
+            bestP = prevP;
+        }
+    }
+};
+
+// A rune whose record overflowed (more than 4 edges, or an edge past 8 runes,
+// or a weight index past 14 bits): walk it here by the rules of k_mark_walk.
+template <class V>
+__device__ __forceinline__ void dp_walk_rune(const V& v, const DevImage& im, uint32_t q, uint32_t be, DpFold& f,
+                                             uint32_t c, const double* ring, bool longm,
+                                             const double* __restrict__ gbest, uint32_t key0) {
+    uint32_t w0;
+    const uint32_t r0 = z_dec(v, q, &w0);
+    uint32_t id = rune_code(im, r0);
+    uint64_t cc = im.cells[id];
+    if (jb_cell_check(cc) != JB_CHECK_ROOT) {
+        f.item(1u, im.wtab[JB_WIDX_ABSENT], c, ring, longm, gbest, key0);
+    } else if (jb_cell_fc(cc) == JB_FC_ZERO) {
+        f.item(1u, im.wtab[jb_cell_widx(cc)], c, ring, longm, gbest, key0);
+    } else {
+        if (jb_cell_fc(cc) == JB_FC_POS) f.item(1u, im.wtab[jb_cell_widx(cc)], c, ring, longm, gbest, key0);
+        uint32_t qq = q + w0, len = 1;
+        bool go = jb_cell_hc(cc) != 0u;
+        while (go && qq < be) {
+            uint32_t wr;
+            const uint32_t r = z_dec(v, qq, &wr);
+            const uint32_t tt = dat_slot(im, cc, r);
+            const uint64_t ch = im.cells[tt];
+            if (!dat_hit(ch, id)) break;
+            ++len;
+            qq += wr;
+            if (jb_cell_fc(ch) == JB_FC_POS) f.item(len, im.wtab[jb_cell_widx(ch)], c, ring, longm, gbest, key0);
+            go = jb_cell_hc(ch) != 0u;
+            id = tt;
+            cc = ch;
+        }
+    }
+}
+
+// The weights of a record's edges (ascending L): four loads issued now, with
+// no branch (an absent edge loads wtab[0] and is ignored), so the compiler's
+// vmcnt bookkeeping stays exact and later waits do not drain other loads.
+__device__ __forceinline__ void rec_weights(const DevImage& im, uint64_t rc, double w[4]) {
+    uint32_t m = (uint32_t)rc & 0xFFu;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const bool has = m != 0u;
+        m &= m - 1u;
+        const uint32_t idx = (uint32_t)(rc >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u);
+        w[k] = im.wtab[has ? idx : 0u];
+    }
+}
+// Fold a record's edges (L <= kZhRing, so best(i+L) is in the ring or is the
+// sentinel), branch-free: every LDS read is issued and the items are selected.
+__device__ __forceinline__ void rec_fold(uint32_t m, const double w[4], DpFold& f, uint32_t c, const double* ring) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const bool has = m != 0u;
+        const uint32_t L = has ? (uint32_t)__builtin_ctz(m) + 1u : 1u;
+        m &= m - 1u;
+        const double rv = ring[((c - L) & (kZhRing - 1u)) * 64u];
+        const double pp = w[k] + ((L == c) ? 0.0 : rv);
+        const bool take = has && pp >= f.prevP;
+        f.bestL = take ? L : f.bestL;
+        f.bestP = take ? pp : f.bestP;
+        f.prevP = has ? pp : f.prevP;
+        f.lastL = has ? L : f.lastL;
+    }
+}
+
+// General form (any rune widths): the next rune's record is loaded one step ahead.
+template <class V, class Src>
+__device__ uint32_t zh_dp(const V& v, const DevImage& im, const uint64_t* __restrict__ erec,
+                          double* __restrict__ gbest, double* ring, const Src& src, uint32_t ablate) {
+    uint32_t j = 0, bs = 0, be = 0;
+    if (!src.next(j, bs, be)) return 0;
+    uint32_t key0 = be / 3u, steps = 0;
+    bool longm = false;
+    uint32_t q = z_prev(v, be, bs), c = 1;
+    uint64_t rc = erec[q / 3u];
+    for (;;) {
+        const bool more = q > bs;
+        DpFold f;
+        uint32_t qn = 0;
+        uint64_t rn = 0;
+        if ((uint32_t)rc & 0xFFu) {
+            double w4[4];
+            rec_weights(im, rc, w4);
+            if (more) {  // next rune's record, in flight while this rune folds
+                qn = z_prev(v, q, bs);
+                rn = erec[qn / 3u];
             }
-            ring[(c & (kZhRing - 1u)) * 64u] = bestP;
-            if (longm) gbest[key0 - c] = bestP;
-            v.bl(q) = (uint8_t)bestL;
-            c_done = c;
-            if (redo || !more) break;
+            rec_fold((uint32_t)rc & 0xFFu, w4, f, c, ring);
+        } else {
+            if (more) {
+                qn = z_prev(v, q, bs);
+                rn = erec[qn / 3u];
+            }
+            dp_walk_rune(v, im, q, be, f, c, ring, longm, gbest, key0);
+        }
+        f.finish();
+        ring[(c & (kZhRing - 1u)) * 64u] = f.bestP;
+        if (longm) gbest[key0 - c] = f.bestP;
+        v.bl(q) = (uint8_t)f.bestL;
+        steps++;
+        if (f.redo) {  // an edge past the ring: this block again, every best value kept in gbest
+            longm = true;
+            q = z_prev(v, be, bs);
+            c = 1;
+            rc = erec[q / 3u];
+            continue;
+        }
+        if (more) {
             q = qn;
             rc = rn;
             ++c;
+            continue;
         }
-        if (!redo) break;
+        if (!src.next(j, bs, be)) break;
+        key0 = be / 3u;
+        longm = false;
+        q = z_prev(v, be, bs);
+        c = 1;
+        rc = erec[q / 3u];
     }
-    if (st) {  // diagnostic phase clocks (wave-uniform point: every lane has left the DP)
-        const uint64_t t = __builtin_amdgcn_s_memtime();
-        st[1] += t - st[7];
-        st[7] = t;
-        st[4] += c_done;
+    return steps;
+}
+
+// All-3-byte form, software-pipelined.  Rune k steps back has slot s - k, so
+// per step, in this issue order: the weights of the NEXT rune (its record
+// came two steps ago), then the record of the rune three back, then the fold
+// of this rune with the weights loaded one step ago.  vmcnt retires loads in
+// issue order, so this order is what lets each load have a whole step: the
+// fold's wait does not cover the record load issued after the weights.
+template <class Src>
+__device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const uint64_t* __restrict__ erec,
+                             double* __restrict__ gbest, double* ring, const Src& src) {
+    uint32_t j = 0, bs = 0, be = 0;
+    if (!src.next(j, bs, be)) return 0;
+    uint32_t key0 = 0, steps = 0, q = 0, c = 1, s0 = 0, s = 0, mc = 0;
+    bool longm = false;
+    // record k runes back (clamped to this rune past the block start; the
+    // consumer masks it then, so no instruction here waits for the load)
+    auto ld_rec = [&](uint32_t k) -> uint64_t { return erec[(s >= s0 + k) ? s - k : s]; };
+    // (re)start at the last rune of [bs, be): its edge mask and weights, the next record
+    auto prime = [&](uint64_t& r1, double (&w)[4]) {
+        key0 = be / 3u;
+        q = be - 3u;
+        c = 1;
+        s0 = bs / 3u;
+        s = q / 3u;
+        const uint64_t rc = erec[s];
+        mc = (uint32_t)rc & 0xFFu;
+        rec_weights(im, rc, w);
+        r1 = ld_rec(1);
+    };
+    // One rune.  r1: the next rune's record (landed); r2: gets the record two
+    // back; wc: this rune's weights (loaded a step ago); wn: gets the next
+    // rune's.  The loop below alternates two register sets, so nothing is
+    // copied out of a load's destination (a copy would wait for the load).
+    auto step = [&](uint64_t& r1, uint64_t& r2, double (&wc)[4], double (&wn)[4]) -> bool {
+        const bool more = q > bs;
+        r2 = ld_rec(2);  // first: the next step waits for it, and vmcnt retires in order
+        const uint64_t r1v = more ? r1 : 0ull;  // (the next rune exists)
+        const uint32_t mn = (uint32_t)r1v & 0xFFu;
+        rec_weights(im, r1v, wn);
+        DpFold f;
+        rec_fold(mc, wc, f, c, ring);
+        if (mc == 0u) dp_walk_rune(v, im, q, be, f, c, ring, longm, gbest, key0);  // overflowed record (rare)
+        f.finish();
+        ring[(c & (kZhRing - 1u)) * 64u] = f.bestP;
+        if (longm) gbest[key0 - c] = f.bestP;
+        v.bl(q) = (uint8_t)f.bestL;
+        steps++;
+        if (f.redo) {  // an edge past the ring: this block again, every best value kept in gbest
+            prime(r2, wn);
+            longm = true;
+            return false;
+        }
+        if (more) {
+            q -= 3u;
+            s -= 1u;
+            mc = mn;
+            ++c;
+            return false;
+        }
+        if (!src.next(j, bs, be)) return true;
+        longm = false;
+        prime(r2, wn);
+        return false;
+    };
+    uint64_t ra = 0, rb = 0;
+    double wa[4], wb[4];
+    prime(ra, wa);
+    for (;;) {
+        if (step(ra, rb, wa, wb)) break;
+        if (step(rb, ra, wb, wa)) break;
     }
-    if (ablate & 4u) return true;  // diagnostic only: DP without the forward walk
-    // ---- forward walk (findDagPath) + HMM runs ---------------------------------------
+    return steps;
+}
+
+// Forward walk of one block (findDagPath) + HMM runs.  Returns false where the
+// reference panics (a rune on the chosen path with no DAG edge: cutDAG slices
+// with tail index -1).
+template <bool HMM, class V, class E>
+__device__ bool zh_fwd(const V& v, const DevImage& im, uint32_t bs, uint32_t be, E& em, uint32_t ablate) {
     uint32_t p = bs, run_s = 0, run_n = 0;
     while (p < be) {
         const uint32_t L = v.bl(p);
@@ -926,27 +1094,87 @@ __device__ bool zh_block(const V& v, const DevImage& im, const uint64_t* __restr
     return true;
 }
 
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// any 4-byte UTF-8 lead byte (>= 0xF0) in the 16-byte words covering [bs, be)
+// (bytes of neighbours in the same words may give a false positive: that only
+// selects the general rune stepping)
+__device__ __forceinline__ bool text_has4(const uint8_t* __restrict__ text, uint32_t bs, uint32_t be) {
+    uint32_t acc = 0;
+    for (uint32_t a = bs & ~15u; a < be; a += 16u) {
+        const uint4 x = *reinterpret_cast<const uint4*>(text + a);
+        acc |= (x.x & (x.x << 1) & (x.x << 2) & (x.x << 3)) | (x.y & (x.y << 1) & (x.y << 2) & (x.y << 3)) |
+               (x.z & (x.z << 1) & (x.z << 2) & (x.z << 3)) | (x.w & (x.w << 1) & (x.w << 2) & (x.w << 3));
+    }
+    return (acc & 0x80808080u) != 0u;
+}
+
+template <bool HMM, bool A3>
+__device__ void zh_chunk_main(const uint8_t* __restrict__ text, const DevImage& im,
+                              const uint64_t* __restrict__ erec, double* __restrict__ gbest, uint8_t* bls,
+                              double* ring, uint32_t* rb32, const TblSrc& src, uint32_t wb, uint32_t lane,
+                              uint32_t* __restrict__ counters, uint32_t ablate, uint64_t* st) {
+    const GrpZvT<A3> v{text, bls, wb};
+    uint32_t steps;
+    if constexpr (A3) steps = zh_dp_a3(v, im, erec, gbest, ring, src);
+    else steps = zh_dp(v, im, erec, gbest, ring, src, ablate);
+    wave_sync();  // ring dead: its space takes the window's token bitmaps
+    if (st) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        st[1] += t - st[7];
+        st[7] = t;
+        st[4] += steps;
+        uint32_t mx = steps;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+        st[5] += mx;
+    }
+    uint32_t* sb = rb32;
+    uint32_t* eb = rb32 + kZhWinWords;
+    for (uint32_t k = lane; k < kZhWinWords; k += 64u) {
+        sb[k] = 0u;
+        eb[k] = 0u;
+    }
+    wave_sync();
+    if (!(ablate & 4u)) {
+        LdsEmitter le(sb, eb, wb >> 5);
+        bool ok = true;
+        uint32_t j = 0, bs, be;
+        while (src.next(j, bs, be)) ok &= zh_fwd<HMM>(v, im, bs, be, le, ablate);
+        le.flush();
+        if (!ok) atomicOr(counters + CNT_ERR, 1u);
+    }
+    wave_sync();
+}
+
 template <bool HMM>
 __global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, uint64_t nbytes,
                                             const uint32_t* __restrict__ blk, const uint32_t* __restrict__ lists,
+                                            const uint32_t* __restrict__ gstart,
                                             uint32_t* __restrict__ counters, DevImage im,
                                             const uint64_t* __restrict__ erec, uint8_t* __restrict__ gbl,
                                             double* __restrict__ gbest,
                                             uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
                                             uint32_t ablate, uint64_t* __restrict__ dbg) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_tx[4][kZhCap + 32];
-    __shared__ uint8_t s_bl[4][kZhCap / 3 + 4];
-    __shared__ double s_ring[4][kZhRing * 64];
-    __shared__ uint32_t s_sb[4][kZhCap / 32 + 4], s_eb[4][kZhCap / 32 + 4];  // token bits of the window
+    __shared__ uint8_t s_bl[4][kZhWin / 3u + 4u];
+    __shared__ double s_rb[4][kZhRing * 64];  // DP ring, then the window's token bitmaps
+    __shared__ uint32_t s_tbl[4][kZhChunk];
+    __shared__ uint32_t s_hist[4][64];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    uint8_t* tx = s_tx[wv];
-    double* ring = s_ring[wv] + lane;
+    double* ring = s_rb[wv] + lane;
+    uint32_t* rb32 = reinterpret_cast<uint32_t*>(s_rb[wv]);
+    uint32_t* tbl = s_tbl[wv];
+    uint32_t* hist = s_hist[wv];
     const uint32_t nzh = counters[CNT_NZH];
+    const uint32_t ngroups = (uint32_t)((nbytes + kZhGroupBytes - 1u) / kZhGroupBytes);
     Emitter em(sbits, ebits);
     em.off = (ablate & 128u) != 0;
-    // diagnostic per-wave clocks (JB_ABLATE bit 8): [0] staging [1] DP [2] forward+Viterbi [3] groups
-    // [4] sum of lane DP runes [5] sum of per-group max lane runes [6] total (out) / lanes outside the
-    // window (running) [7] scratch (running) / lanes outside the window (out)
+    // diagnostic per-wave clocks (JB_ABLATE bit 8): [0] setup [1] DP [2] forward+Viterbi+flush [3] chunks
+    // [4] sum of lane DP steps [5] sum of per-chunk max lane DP steps [6] blocks past the window [7] scratch
     uint64_t stv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #if JB_STAMPS
     uint64_t* st = (ablate & 0x100u) ? stv : nullptr;
@@ -955,91 +1183,124 @@ __global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, ui
 #endif
     const uint64_t tk0 = st ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
-        if (st) stv[7] = __builtin_amdgcn_s_memtime();
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(counters + CNT_WORK, 64u);
-        base = __shfl(base, 0, 64);
-        if (base >= nzh) break;
-        const uint32_t z = base + lane;
-        const bool valid = z < nzh;
-        uint32_t bs = 0, be = 0;
-        if (valid) {
-            const uint32_t g = lists[z];
-            bs = blk[g] & 0x7FFFFFFFu;
-            be = blk[g + 1] & 0x7FFFFFFFu;
-        }
-        const uint32_t lastl = min(63u, nzh - 1u - base);
-        const uint32_t first = __shfl(bs, 0, 64), last_be = __shfl(be, lastl, 64);
-        const uint32_t wb = first & ~15u;
-        const uint32_t wend = min(last_be, wb + kZhCap);
-        // stage [wb, wend + 16) (the text buffer is padded 64 bytes past its end)
-        const uint32_t n16 = (wend - wb + 16u + 15u) >> 4;
-        for (uint32_t k = lane; k < n16; k += 64u)
-            reinterpret_cast<uint4*>(tx)[k] = reinterpret_cast<const uint4*>(text + wb)[k];
-        // token bits of blocks inside the window collect in LDS words [wb >> 5, wend >> 5]
-        const uint32_t w0 = wb >> 5, nw = (wend >> 5) - w0 + 1u;
-        for (uint32_t k = lane; k < nw; k += 64u) {
-            s_sb[wv][k] = 0u;
-            s_eb[wv][k] = 0u;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (st) {
-            const uint64_t t = __builtin_amdgcn_s_memtime();
-            stv[0] += t - stv[7];
-            stv[7] = t;
-            stv[3]++;
-            stv[6] += __popcll(__ballot(valid && be > wend));  // lanes outside the window
-            // lane rune estimate for the max-lane statistic
-            uint32_t est = valid ? (be - bs) / 3u : 0u;
+        uint32_t g = 0;
+        if (lane == 0) g = atomicAdd(counters + CNT_WORK, 1u);
+        g = __builtin_amdgcn_readfirstlane(g);
+        if (g >= ngroups) break;
+        const uint32_t z0 = gstart[g];
+        const uint32_t z1 = (g + 1u < ngroups) ? gstart[g + 1u] : nzh;
+        if (z0 >= z1) continue;
+        const uint32_t wb = g * kZhGroupBytes, wend = wb + kZhWin;
+        const uint32_t n = z1 - z0;
+        const uint32_t nch = (n + kZhChunk - 1u) / kZhChunk;
+        const uint32_t cs = (n + nch - 1u) / nch;  // even chunks
+        for (uint32_t c0 = z0; c0 < z1; c0 += cs) {
+            if (st) stv[7] = __builtin_amdgcn_s_memtime();
+            const uint32_t m = min(cs, z1 - c0);
+            // this lane's items k = lane + 64 i of the chunk
+            uint32_t bsi[3], bei[3];
+            bool in[3], out[3];
+            bool has4 = false;
 #pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) est = max(est, (uint32_t)__shfl_xor((int)est, d, 64));
-            stv[5] += est;
-        }
-        if (valid) {
-            bool ok;
-            if (be <= wend) {
-                // any 4-byte rune (lead byte >= 0xF0) among the words that hold the block?
-                bool has4 = false;
-                for (uint32_t a = (bs & ~3u); a < be; a += 4u) {
-                    const uint32_t x = *reinterpret_cast<const uint32_t*>(tx + (a - wb));
-                    has4 |= (x & (x << 1) & (x << 2) & (x << 3) & 0x80808080u) != 0u;
+            for (int i = 0; i < 3; i++) {
+                const uint32_t k = lane + 64u * (uint32_t)i;
+                bsi[i] = bei[i] = 0;
+                in[i] = out[i] = false;
+                if (k < m) {
+                    const uint32_t gi = lists[c0 + k];
+                    bsi[i] = blk[gi] & 0x7FFFFFFFu;
+                    bei[i] = blk[gi + 1u] & 0x7FFFFFFFu;
+                    in[i] = bei[i] <= wend;
+                    out[i] = !in[i];
                 }
-                LdsEmitter le(s_sb[wv], s_eb[wv], w0);
-                if (!has4)
-                    ok = zh_block<HMM>(LdsZvT<true>{tx, s_bl[wv], wb}, im, erec, gbest, ring, bs, be, le, ablate, st);
-                else
-                    ok = zh_block<HMM>(LdsZv{tx, s_bl[wv], wb}, im, erec, gbest, ring, bs, be, le, ablate, st);
-                le.flush();
-            } else {
-                ok = zh_block<HMM>(GlbZv{text, gbl}, im, erec, gbest, ring, bs, be, em, ablate, st);
             }
-            if (!ok) atomicOr(counters + CNT_ERR, 1u);
-        }
-        if (st) {
-            const uint64_t t = __builtin_amdgcn_s_memtime();
-            stv[2] += t - stv[7];
-            stv[7] = t;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // the window's token words: consecutive words per lane, one OR each (edge
-        // words are shared with neighbouring waves and with k_nonzh)
-        if (!em.off)
-            for (uint32_t k = lane; k < nw; k += 64u) {
-                const uint32_t a = s_sb[wv][k], b = s_eb[wv][k];
-                if (a) atomicOr(sbits + w0 + k, a);
-                if (b) atomicOr(ebits + w0 + k, b);
+#pragma unroll
+            for (int i = 0; i < 3; i++)
+                if (in[i]) has4 |= text_has4(text, bsi[i], bei[i]);
+            const bool all3 = __ballot(has4) == 0ull;
+            // rank in-window blocks by length (descending; counting sort on len/4)
+            hist[lane] = 0u;
+            for (uint32_t k = lane; k < kZhChunk; k += 64u) tbl[k] = ~0u;
+            wave_sync();
+            uint32_t bkt[3], idx[3];
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                bkt[i] = min(63u, (bei[i] - bsi[i]) >> 2);
+                idx[i] = in[i] ? atomicAdd(hist + bkt[i], 1u) : 0u;
             }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            wave_sync();
+            {  // start of each bucket in descending order: sum of the counts of longer buckets
+                const uint32_t h = hist[lane];
+                uint32_t incl = h;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t t = __shfl_down(incl, d, 64);
+                    if (lane + (uint32_t)d < 64u) incl += t;
+                }
+                wave_sync();
+                hist[lane] = incl - h;
+            }
+            wave_sync();
+            uint32_t nin = 0;
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                nin += (uint32_t)__popcll(__ballot(in[i]));
+                if (in[i]) {
+                    const uint32_t r = hist[bkt[i]] + idx[i];
+                    const uint32_t sg = r >> 6, ps = r & 63u;
+                    const uint32_t ln = (sg & 1u) ? 63u - ps : ps;
+                    tbl[sg * 64u + ln] = (bsi[i] - wb) | ((bei[i] - wb) << 16);
+                }
+            }
+            wave_sync();
+            const TblSrc src{tbl + lane, (nin + 63u) >> 6, wb};
+            if (st) {
+                const uint64_t t = __builtin_amdgcn_s_memtime();
+                stv[0] += t - stv[7];
+                stv[7] = t;
+                stv[3]++;
+            }
+            if (all3)
+                zh_chunk_main<HMM, true>(text, im, erec, gbest, s_bl[wv], ring, rb32, src, wb, lane, counters, ablate,
+                                         st);
+            else
+                zh_chunk_main<HMM, false>(text, im, erec, gbest, s_bl[wv], ring, rb32, src, wb, lane, counters,
+                                          ablate, st);
+            // the window's token words: consecutive words per lane, one OR each (edge
+            // words are shared with neighbouring groups and with k_nonzh)
+            if (!em.off) {
+                const uint32_t w0 = wb >> 5;
+                const uint32_t* sb = rb32;
+                const uint32_t* eb = rb32 + kZhWinWords;
+                for (uint32_t k = lane; k < kZhWinWords; k += 64u) {
+                    const uint32_t a = sb[k], b = eb[k];
+                    if (a) atomicOr(sbits + w0 + k, a);
+                    if (b) atomicOr(ebits + w0 + k, b);
+                }
+            }
+            wave_sync();  // bitmaps read: the ring is free again
+            // blocks that end past the window (rare): each on its own, in HBM
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                if (st) stv[6] += __popcll(__ballot(out[i]));
+                if (out[i]) {
+                    const GlbZv gv{text, gbl};
+                    zh_dp(gv, im, erec, gbest, ring, OneSrc{bsi[i], bei[i]}, ablate);
+                    if (!(ablate & 4u) && !zh_fwd<HMM>(gv, im, bsi[i], bei[i], em, ablate))
+                        atomicOr(counters + CNT_ERR, 1u);
+                }
+            }
+            wave_sync();
+            if (st) {
+                const uint64_t t = __builtin_amdgcn_s_memtime();
+                stv[2] += t - stv[7];
+                stv[7] = t;
+            }
+        }
     }
     em.flush();
     if (st) {
-        // lane DP runes summed over the wave
+        // lane DP steps summed over the wave
         uint64_t sum = stv[4];
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) {
@@ -1247,14 +1508,14 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                                w.tile_off, w.counters + CNT_NBLK, nullptr, w.blk,
                                                (uint32_t)nbytes));
     JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL(k_blocks_write, dim3(ntiles), dim3(256), 0, stream, w.lanemask,
-                                                w.tile_off, w.blk, w.lists, list_cap));
+                                                w.tile_off, w.blk, w.lists, list_cap, w.gstart));
     if (hmm)
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
-                                          w.lists, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,
+                                          w.lists, w.gstart, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,
                                           g_ablate, w.dbg));
     else
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
-                                          w.lists, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,
+                                          w.lists, w.gstart, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,
                                           g_ablate, w.dbg));
     JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3(grid_nz), dim3(256), 0, stream, d_text, w.blk, w.lists,
                                          list_cap, w.counters, w.sbits, w.ebits));
