@@ -1059,11 +1059,30 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
     return steps;
 }
 
+// A lane's deferred Viterbi runs (all-3-byte chunks): LDS words t[r * 64],
+// (rs - wb) | (re - wb) << 16.  The forward walk only lists the runs; the
+// Viterbis then run with every lane on its r-th run at once, instead of one
+// divergent Viterbi whenever some lane's walk reaches the end of a run.
+constexpr uint32_t kZhRuns = 4;
+struct RunList {
+    uint32_t* t;
+    uint32_t wb;
+    uint32_t n;
+};
+
 // Forward walk of one block (findDagPath) + HMM runs.  Returns false where the
 // reference panics (a rune on the chosen path with no DAG edge: cutDAG slices
 // with tail index -1).
 template <bool HMM, class V, class E>
-__device__ bool zh_fwd(const V& v, const DevImage& im, uint32_t bs, uint32_t be, E& em, uint32_t ablate) {
+__device__ bool zh_fwd(const V& v, const DevImage& im, uint32_t bs, uint32_t be, E& em, uint32_t ablate,
+                       RunList* rl) {
+    auto run_end = [&](uint32_t rs, uint32_t re, uint32_t m) {
+        if ((ablate & 32u) || m == 1u) em.token(rs, re);  // a single rune is always "S" (:672-674)
+        else if (rl && rl->n < kZhRuns) {
+            rl->t[rl->n * 64u] = (rs - rl->wb) | ((re - rl->wb) << 16);
+            rl->n++;
+        } else viterbi_run(v, im, rs, re, m, em);
+    };
     uint32_t p = bs, run_s = 0, run_n = 0;
     while (p < be) {
         const uint32_t L = v.bl(p);
@@ -1079,18 +1098,14 @@ __device__ bool zh_fwd(const V& v, const DevImage& im, uint32_t bs, uint32_t be,
             run_n++;
         } else {
             if (run_n) {
-                if (ablate & 32u) em.token(run_s, p);
-                else viterbi_run(v, im, run_s, p, run_n, em);
+                run_end(run_s, p, run_n);
                 run_n = 0;
             }
             em.token(p, pe);
         }
         p = pe;
     }
-    if (HMM && run_n) {
-        if (ablate & 32u) em.token(run_s, be);
-        else viterbi_run(v, im, run_s, be, run_n, em);
-    }
+    if (HMM && run_n) run_end(run_s, be, run_n);
     return true;
 }
 
@@ -1116,7 +1131,8 @@ __device__ __forceinline__ bool text_has4(const uint8_t* __restrict__ text, uint
 template <bool HMM, bool A3>
 __device__ void zh_chunk_main(const uint8_t* __restrict__ text, const DevImage& im,
                               const uint64_t* __restrict__ erec, double* __restrict__ gbest, uint8_t* bls,
-                              double* ring, uint32_t* rb32, const TblSrc& src, uint32_t wb, uint32_t lane,
+                              double* ring, uint32_t* rb32, uint32_t* runs, const TblSrc& src, uint32_t wb,
+                              uint32_t lane,
                               uint32_t* __restrict__ counters, uint32_t ablate, uint64_t* st) {
     const GrpZvT<A3> v{text, bls, wb};
     uint32_t steps;
@@ -1144,7 +1160,16 @@ __device__ void zh_chunk_main(const uint8_t* __restrict__ text, const DevImage& 
         LdsEmitter le(sb, eb, wb >> 5);
         bool ok = true;
         uint32_t j = 0, bs, be;
-        while (src.next(j, bs, be)) ok &= zh_fwd<HMM>(v, im, bs, be, le, ablate);
+        RunList rl{runs, wb, 0u};
+        RunList* const rlp = (HMM && A3) ? &rl : nullptr;
+        while (src.next(j, bs, be)) ok &= zh_fwd<HMM>(v, im, bs, be, le, ablate, rlp);
+        if (HMM && A3)
+            for (uint32_t r = 0; r < kZhRuns; r++)
+                if (r < rl.n) {
+                    const uint32_t x = runs[r * 64u];
+                    const uint32_t rs = wb + (x & 0xFFFFu), re = wb + (x >> 16);
+                    viterbi_run(v, im, rs, re, (re - rs) / 3u, le);
+                }
         le.flush();
         if (!ok) atomicOr(counters + CNT_ERR, 1u);
     }
@@ -1164,6 +1189,7 @@ __global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, ui
     __shared__ double s_rb[4][kZhRing * 64];  // DP ring, then the window's token bitmaps
     __shared__ uint32_t s_tbl[4][kZhChunk];
     __shared__ uint32_t s_hist[4][64];
+    __shared__ uint32_t s_runs[4][kZhRuns * 64];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     double* ring = s_rb[wv] + lane;
     uint32_t* rb32 = reinterpret_cast<uint32_t*>(s_rb[wv]);
@@ -1261,11 +1287,12 @@ __global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, ui
                 stv[3]++;
             }
             if (all3)
-                zh_chunk_main<HMM, true>(text, im, erec, gbest, s_bl[wv], ring, rb32, src, wb, lane, counters, ablate,
+                zh_chunk_main<HMM, true>(text, im, erec, gbest, s_bl[wv], ring, rb32, s_runs[wv] + lane, src, wb, lane,
+                                         counters, ablate,
                                          st);
             else
-                zh_chunk_main<HMM, false>(text, im, erec, gbest, s_bl[wv], ring, rb32, src, wb, lane, counters,
-                                          ablate, st);
+                zh_chunk_main<HMM, false>(text, im, erec, gbest, s_bl[wv], ring, rb32, s_runs[wv] + lane, src, wb,
+                                          lane, counters, ablate, st);
             // the window's token words: consecutive words per lane, one OR each (edge
             // words are shared with neighbouring groups and with k_nonzh)
             if (!em.off) {
@@ -1286,7 +1313,7 @@ __global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, ui
                 if (out[i]) {
                     const GlbZv gv{text, gbl};
                     zh_dp(gv, im, erec, gbest, ring, OneSrc{bsi[i], bei[i]}, ablate);
-                    if (!(ablate & 4u) && !zh_fwd<HMM>(gv, im, bsi[i], bei[i], em, ablate))
+                    if (!(ablate & 4u) && !zh_fwd<HMM>(gv, im, bsi[i], bei[i], em, ablate, nullptr))
                         atomicOr(counters + CNT_ERR, 1u);
                 }
             }
