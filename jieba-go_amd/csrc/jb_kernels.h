@@ -49,7 +49,8 @@ struct Work {
     uint32_t* lists;       // zh block ids from the front, non-zh block ids from the back
     uint64_t* erec;        // per Han rune (slot = byte / 3): packed DAG edges (k_mark_walk -> k_zh)
     uint32_t* lanemask;    // per 16 bytes: block starts | Han block starts << 16
-    uint32_t* gstart;      // per k_zh group: first zh block index starting at or after g * kZhGroupBytes
+    uint2* gstart;         // per k_zh group g: (blocks, zh blocks) that start before g * kZhGroupBytes
+    uint32_t* tile4;       // per tile: a 4-byte Han rune starts in it
     uint8_t* gbl;          // per Han rune: chosen piece length, then Viterbi back-pointers / labels
     double* gbest;         // per Han rune: best proba, kept only for blocks with an edge > 8 runes
     uint32_t* tok_start;

@@ -259,8 +259,8 @@ __device__ __forceinline__ bool dat_hit(uint64_t child, uint32_t id) { return jb
 __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                    const uint32_t* __restrict__ docbits, DevImage im,
                                                    uint32_t* __restrict__ lanemask, uint2* __restrict__ tile_cnt,
-                                                   uint64_t* __restrict__ erec, uint32_t ablate,
-                                                   uint64_t* __restrict__ dbg) {
+                                                   uint64_t* __restrict__ erec, uint32_t* __restrict__ tile4,
+                                                   uint32_t ablate, uint64_t* __restrict__ dbg) {
     __shared__ __attribute__((aligned(16))) uint8_t s_t[kTileBytes + 32];  // bytes [t0-16, t0+4096+16)
     __shared__ uint32_t s_db[kTileBytes / 32 + 2];                        // document starts of the tile
     __shared__ uint32_t s_e[kTileE];
@@ -345,6 +345,7 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
     uint32_t hs = ((hanb & ~covered & valid) >> 4) & 0xFFFFu;  // Han rune starts of the lane's bytes
     uint32_t nent;
     uint32_t o = block_scan_u32(__popc(hs), lds, &nent);
+    bool has4 = false;  // a 4-byte Han rune starts in the lane's bytes
     {
         // at most 6 Han runes start in a lane's 16 bytes: decode them and issue all
         // code loads, then all level-1 cell loads (two round trips, not two per rune)
@@ -367,6 +368,7 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
                 kk[i] = k;
                 rr[i] = r;
                 cd[i] = rune_code(im, r);
+                has4 |= r >= 0x10000u;
             }
         }
 #pragma unroll
@@ -387,7 +389,8 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
         else if (i + 1u < nent && ent_pos(s_e[i + 1u]) == nxt && !((s_db[nxt >> 5] >> (nxt & 31u)) & 1u)) f = kEntCont;
         s_e[i] = e | f;
     }
-    __syncthreads();
+    const int any4 = __syncthreads_or(has4);  // (also the barrier after the run links)
+    if (threadIdx.x == 0) tile4[blockIdx.x] = any4 ? 1u : 0u;  // k_zh: general rune stepping near this tile
     if (stamps) c2 = __builtin_amdgcn_s_memtime();
     // ---- walks: wave w takes the walk starts [lo, hi) of the tile ---------------------
     const uint32_t* ent = s_e;
@@ -533,11 +536,11 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
 // k_blocks_write: the lane masks -> block list (start | zh<<31), zh block ids
 // (ascending) and non-zh block ids (from the end of `lists`, descending).
 // The thread whose 16 bytes begin a k_zh group (g * kZhGroupBytes) also writes
-// gstart[g]: the number of zh blocks that start before it.
+// gstart[g] = (blocks, zh blocks) that start before it.
 __global__ __launch_bounds__(256) void k_blocks_write(const uint32_t* __restrict__ lanemask,
                                                       const uint2* __restrict__ tile_off, uint32_t* __restrict__ blk,
                                                       uint32_t* __restrict__ lists, uint32_t list_cap,
-                                                      uint32_t* __restrict__ gstart) {
+                                                      uint2* __restrict__ gstart) {
     __shared__ uint32_t lds[8];
     uint32_t m = lanemask[blockIdx.x * 256u + threadIdx.x];
     const uint32_t bmask = m & 0xFFFFu, zmask = m >> 16;
@@ -545,7 +548,7 @@ __global__ __launch_bounds__(256) void k_blocks_write(const uint32_t* __restrict
     const uint32_t ex = block_scan_u32(__popc(bmask) | (__popc(zmask) << 16), lds, &tot);
     const uint32_t p0 = (blockIdx.x * 256u + threadIdx.x) * 16u;
     const uint2 to = tile_off[blockIdx.x];
-    if (p0 % kZhGroupBytes == 0u) gstart[p0 / kZhGroupBytes] = to.y + (ex >> 16);
+    if (p0 % kZhGroupBytes == 0u) gstart[p0 / kZhGroupBytes] = make_uint2(to.x + (ex & 0xFFFFu), to.y + (ex >> 16));
     if (!bmask) return;
     uint32_t ga = to.x + (ex & 0xFFFFu);  // global block rank
     uint32_t gz = to.y + (ex >> 16);      // global zh rank
@@ -1178,8 +1181,8 @@ __device__ void zh_chunk_main(const uint8_t* __restrict__ text, const DevImage& 
 
 template <bool HMM>
 __global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, uint64_t nbytes,
-                                            const uint32_t* __restrict__ blk, const uint32_t* __restrict__ lists,
-                                            const uint32_t* __restrict__ gstart,
+                                            const uint32_t* __restrict__ blk, const uint2* __restrict__ gstart,
+                                            const uint32_t* __restrict__ tile4,
                                             uint32_t* __restrict__ counters, DevImage im,
                                             const uint64_t* __restrict__ erec, uint8_t* __restrict__ gbl,
                                             double* __restrict__ gbest,
@@ -1187,7 +1190,7 @@ __global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, ui
                                             uint32_t ablate, uint64_t* __restrict__ dbg) {
     __shared__ uint8_t s_bl[4][kZhWin / 3u + 4u];
     __shared__ double s_rb[4][kZhRing * 64];  // DP ring, then the window's token bitmaps
-    __shared__ uint32_t s_tbl[4][kZhChunk];
+    __shared__ uint32_t s_tbl[4][kZhChunk];   // the chunk's blocks as found, then as dealt to the lanes
     __shared__ uint32_t s_hist[4][64];
     __shared__ uint32_t s_runs[4][kZhRuns * 64];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -1195,8 +1198,9 @@ __global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, ui
     uint32_t* rb32 = reinterpret_cast<uint32_t*>(s_rb[wv]);
     uint32_t* tbl = s_tbl[wv];
     uint32_t* hist = s_hist[wv];
-    const uint32_t nzh = counters[CNT_NZH];
+    const uint32_t nblk = counters[CNT_NBLK], nzh = counters[CNT_NZH];
     const uint32_t ngroups = (uint32_t)((nbytes + kZhGroupBytes - 1u) / kZhGroupBytes);
+    const uint32_t ntiles = (uint32_t)((nbytes + kTileBytes - 1u) / kTileBytes);
     Emitter em(sbits, ebits);
     em.off = (ablate & 128u) != 0;
     // diagnostic per-wave clocks (JB_ABLATE bit 8): [0] setup [1] DP [2] forward+Viterbi+flush [3] chunks
@@ -1213,41 +1217,74 @@ __global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, ui
         if (lane == 0) g = atomicAdd(counters + CNT_WORK, 1u);
         g = __builtin_amdgcn_readfirstlane(g);
         if (g >= ngroups) break;
-        const uint32_t z0 = gstart[g];
-        const uint32_t z1 = (g + 1u < ngroups) ? gstart[g + 1u] : nzh;
-        if (z0 >= z1) continue;
+        const uint2 g0 = gstart[g];
+        const uint2 g1 = (g + 1u < ngroups) ? gstart[g + 1u] : make_uint2(nblk, nzh);
+        if (g0.y >= g1.y) continue;  // no Han block starts here
         const uint32_t wb = g * kZhGroupBytes, wend = wb + kZhWin;
-        const uint32_t n = z1 - z0;
+        // all-3-byte window: no 4-byte Han rune starts in the tiles under it
+        bool any4 = false;
+        {
+            const uint32_t t0 = wb / kTileBytes, t1 = (uint32_t)((min((uint64_t)wend, nbytes) - 1u) / kTileBytes);
+            if (lane <= t1 - t0 && t0 + lane < ntiles) any4 = tile4[t0 + lane] != 0u;
+        }
+        const bool all3 = __ballot(any4) == 0ull;
+        const uint32_t n = g1.y - g0.y;
         const uint32_t nch = (n + kZhChunk - 1u) / kZhChunk;
         const uint32_t cs = (n + nch - 1u) / nch;  // even chunks
-        for (uint32_t c0 = z0; c0 < z1; c0 += cs) {
+        uint32_t cur = g0.x;                       // next block (all kinds) to look at
+        for (uint32_t c0 = 0; c0 < n; c0 += cs) {
             if (st) stv[7] = __builtin_amdgcn_s_memtime();
-            const uint32_t m = min(cs, z1 - c0);
+            const uint32_t m = min(cs, n - c0);
+            // the chunk's m zh blocks, in order, from the block list (coalesced): in-window
+            // ones as (bs - wb) | (be - wb) << 16, others as 0x80000000 | block index
+            for (uint32_t have = 0; have < m;) {
+                const uint32_t k = cur + lane;
+                uint32_t x = 0, y = 0;
+                if (k < g1.x) {
+                    x = blk[k];
+                    y = blk[k + 1u];
+                }
+                const bool z = (x >> 31) != 0u;
+                const uint64_t zm = __ballot(z);
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(zm >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)zm, 0u));
+                const uint32_t nz = (uint32_t)__popcll(zm);
+                const uint32_t take = min(nz, m - have);
+                if (z && rank < take) {
+                    const uint32_t bs = x & 0x7FFFFFFFu, be = y & 0x7FFFFFFFu;
+                    tbl[have + rank] = (be <= wend) ? (bs - wb) | ((be - wb) << 16) : (0x80000000u | k);
+                }
+                if (take < nz) cur += (uint32_t)__builtin_ctzll(__ballot(z && rank == take));  // first one left
+                else cur = min(cur + 64u, g1.x);
+                have += take;
+            }
+            wave_sync();
             // this lane's items k = lane + 64 i of the chunk
             uint32_t bsi[3], bei[3];
             bool in[3], out[3];
-            bool has4 = false;
 #pragma unroll
             for (int i = 0; i < 3; i++) {
                 const uint32_t k = lane + 64u * (uint32_t)i;
                 bsi[i] = bei[i] = 0;
                 in[i] = out[i] = false;
                 if (k < m) {
-                    const uint32_t gi = lists[c0 + k];
-                    bsi[i] = blk[gi] & 0x7FFFFFFFu;
-                    bei[i] = blk[gi + 1u] & 0x7FFFFFFFu;
-                    in[i] = bei[i] <= wend;
-                    out[i] = !in[i];
+                    const uint32_t x = tbl[k];
+                    if (x & 0x80000000u) {  // ends past the window (rare)
+                        const uint32_t gi = x & 0x7FFFFFFFu;
+                        bsi[i] = blk[gi] & 0x7FFFFFFFu;
+                        bei[i] = blk[gi + 1u] & 0x7FFFFFFFu;
+                        out[i] = true;
+                    } else {
+                        bsi[i] = wb + (x & 0xFFFFu);
+                        bei[i] = wb + (x >> 16);
+                        in[i] = true;
+                    }
                 }
             }
-#pragma unroll
-            for (int i = 0; i < 3; i++)
-                if (in[i]) has4 |= text_has4(text, bsi[i], bei[i]);
-            const bool all3 = __ballot(has4) == 0ull;
             // rank in-window blocks by length (descending; counting sort on len/4)
             hist[lane] = 0u;
-            for (uint32_t k = lane; k < kZhChunk; k += 64u) tbl[k] = ~0u;
             wave_sync();
+            for (uint32_t k = lane; k < kZhChunk; k += 64u) tbl[k] = ~0u;
             uint32_t bkt[3], idx[3];
 #pragma unroll
             for (int i = 0; i < 3; i++) {
@@ -1529,7 +1566,7 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         JB_TIMED(K_DOCBITS, hipLaunchKernelGGL(k_docbits, dim3((ndocs + 255) / 256), dim3(256), 0, stream,
                                                d_doc_off, ndocs, nbytes, w.docbits));
     JB_TIMED(K_MARK_WALK, hipLaunchKernelGGL(k_mark_walk, dim3(ntiles), dim3(256), 0, stream, d_text, nbytes,
-                                             w.docbits, im, w.lanemask, w.tile_cnt, w.erec, g_ablate,
+                                             w.docbits, im, w.lanemask, w.tile_cnt, w.erec, w.tile4, g_ablate,
                                              w.dbg_walk));
     JB_TIMED(K_SCAN_BLOCKS, hipLaunchKernelGGL(k_scan2, dim3(1), dim3(1024), 0, stream, w.tile_cnt, ntiles,
                                                w.tile_off, w.counters + CNT_NBLK, nullptr, w.blk,
@@ -1538,11 +1575,11 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                                 w.tile_off, w.blk, w.lists, list_cap, w.gstart));
     if (hmm)
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
-                                          w.lists, w.gstart, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,
+                                          w.gstart, w.tile4, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,
                                           g_ablate, w.dbg));
     else
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
-                                          w.lists, w.gstart, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,
+                                          w.gstart, w.tile4, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,
                                           g_ablate, w.dbg));
     JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3(grid_nz), dim3(256), 0, stream, d_text, w.blk, w.lists,
                                          list_cap, w.counters, w.sbits, w.ebits));

@@ -87,6 +87,11 @@ EDGE_TEXTS = [
     "a1+1=2 中文 x　y",
     "丁" * 2719, "丁" * 2720, "丁" * 2721, "一丁" * 1400, "𠀀" * 2041,   # around the k_zh window limit
     ("中文。" * 900) + "丁" * 3000 + ("，中文" * 900),                   # long block between short ones
+    # k_zh groups are 6144-byte spans with a 7168-byte window: blocks that start
+    # at or just before a group edge, and ones that end at / just past the window
+    "a" * 6141 + "丁" * 342, "a" * 6141 + "丁" * 343, "a" * 6144 + "丁" * 341 + "，" + "丁" * 5,
+    "a" * 6143 + "丁" * 400, "中，" * 3072 + "丁" * 700, "a" * 6140 + "𠀀" * 300 + "丁" * 30,
+    "，".join(["中文"] * 4000),                                           # many short blocks per group
 ]
 
 
