@@ -351,7 +351,7 @@ static int upload_image(Device* d, const Image& img) {
 
 static void free_work(Work* w) {
     dfree(w->docbits); dfree(w->tile_cnt); dfree(w->tile_off);
-    dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->blk); dfree(w->lists); dfree(w->erec); dfree(w->lanemask);
+    dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->blk); dfree(w->alnum16); dfree(w->erec); dfree(w->lanemask);
     dfree(w->gbl); dfree(w->gbest); dfree(w->gstart); dfree(w->tile4);
     dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters); dfree(w->dbg); dfree(w->dbg_walk);
     *w = Work{};
@@ -380,7 +380,7 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.ttile_cnt, nttiles * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.ttile_off, nttiles * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.blk, (nb + 4) * 4));
-    HIPCHK(hipMalloc(&w.lists, (nb + 4) * 4));
+    HIPCHK(hipMalloc(&w.alnum16, (nb / 1024 + 8) * 8));
     HIPCHK(hipMalloc(&w.erec, (nb / 3 + 8) * 8));
     HIPCHK(hipMalloc(&w.lanemask, ntiles * 256 * 4));
     HIPCHK(hipMalloc(&w.gbl, nb / 3 + 8));

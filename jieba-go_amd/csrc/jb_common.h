@@ -130,6 +130,16 @@ JB_HD bool jb_is_alnum(uint32_t b) {
     return (b - 'a' < 26u) || (b - 'A' < 26u) || (b - '0' < 10u);
 }
 
+// Bytes of x with m < b < n (b < 0x80; m <= 127, n <= 128), bit 7 of each byte.
+JB_HD uint32_t jb_bytes_between(uint32_t x, uint32_t m, uint32_t n) {
+    const uint32_t t = x & 0x7F7F7F7Fu;
+    return ((0x01010101u * (127u + n) - t) & ~x & (t + 0x01010101u * (127u - m))) & 0x80808080u;
+}
+// Some byte of x is [0-9A-Za-z] (jb_is_alnum), four at once.
+JB_HD bool jb_any_alnum4(uint32_t x) {
+    return (jb_bytes_between(x, 0x2Fu, 0x3Au) | jb_bytes_between(x | 0x20202020u, 0x60u, 0x7Bu)) != 0u;
+}
+
 // Go utf8.DecodeRune on the 4 bytes packed little-endian in x, with `lim`
 // (1..4) bytes available. Invalid, truncated, surrogate and overlong sequences
 // decode as U+FFFD with width 1. Returns width; writes the rune.

@@ -46,7 +46,7 @@ struct Work {
     uint2* ttile_cnt;      // per token tile (starts, ends)
     uint2* ttile_off;
     uint32_t* blk;         // block start | zh << 31, then sentinel nbytes
-    uint32_t* lists;       // zh block ids from the front, non-zh block ids from the back
+    uint64_t* alnum16;     // 1 bit per 16 bytes of text: some [0-9A-Za-z] byte there
     uint64_t* erec;        // per Han rune (slot = byte / 3): packed DAG edges (k_mark_walk -> k_zh)
     uint32_t* lanemask;    // per 16 bytes: block starts | Han block starts << 16
     uint2* gstart;         // per k_zh group g: (blocks, zh blocks) that start before g * kZhGroupBytes

@@ -260,7 +260,8 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
                                                    const uint32_t* __restrict__ docbits, DevImage im,
                                                    uint32_t* __restrict__ lanemask, uint2* __restrict__ tile_cnt,
                                                    uint64_t* __restrict__ erec, uint32_t* __restrict__ tile4,
-                                                   uint32_t ablate, uint64_t* __restrict__ dbg) {
+                                                   uint64_t* __restrict__ alnum16, uint32_t ablate,
+                                                   uint64_t* __restrict__ dbg) {
     __shared__ __attribute__((aligned(16))) uint8_t s_t[kTileBytes + 32];  // bytes [t0-16, t0+4096+16)
     __shared__ uint32_t s_db[kTileBytes / 32 + 2];                        // document starts of the tile
     __shared__ uint32_t s_e[kTileE];
@@ -310,6 +311,13 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
     }
     __syncthreads();
     const uint8_t* win = s_t + 12 + threadIdx.x * 16u;  // window index 0
+    {  // some [0-9A-Za-z] byte in the lane's 16 bytes (k_nonzh skips blocks without one; padding
+       // bytes past the batch can only add false positives)
+        const uint32_t* w4 = reinterpret_cast<const uint32_t*>(win) + 1;
+        const bool al = jb_any_alnum4(w4[0]) || jb_any_alnum4(w4[1]) || jb_any_alnum4(w4[2]) || jb_any_alnum4(w4[3]);
+        const uint64_t am = __ballot(al);
+        if ((threadIdx.x & 63u) == 0) alnum16[(t0 >> 10) + (threadIdx.x >> 6)] = am;
+    }
     // lead bytes (>= 0xC0) at window indices 0..19
     uint32_t lead = 0;
 #pragma unroll
@@ -533,13 +541,11 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
     }
 }
 
-// k_blocks_write: the lane masks -> block list (start | zh<<31), zh block ids
-// (ascending) and non-zh block ids (from the end of `lists`, descending).
+// k_blocks_write: the lane masks -> block list (start | zh<<31).
 // The thread whose 16 bytes begin a k_zh group (g * kZhGroupBytes) also writes
 // gstart[g] = (blocks, zh blocks) that start before it.
 __global__ __launch_bounds__(256) void k_blocks_write(const uint32_t* __restrict__ lanemask,
                                                       const uint2* __restrict__ tile_off, uint32_t* __restrict__ blk,
-                                                      uint32_t* __restrict__ lists, uint32_t list_cap,
                                                       uint2* __restrict__ gstart) {
     __shared__ uint32_t lds[8];
     uint32_t m = lanemask[blockIdx.x * 256u + threadIdx.x];
@@ -558,8 +564,6 @@ __global__ __launch_bounds__(256) void k_blocks_write(const uint32_t* __restrict
         b &= b - 1u;
         const bool h = (zmask >> k) & 1u;
         blk[ga] = (p0 + k) | (h ? 0x80000000u : 0u);
-        if (h) lists[gz++] = ga;
-        else lists[list_cap - 1u - (ga - gz)] = ga;
         ga++;
     }
 }
@@ -1389,44 +1393,83 @@ __global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, ui
 // ---------------------------------------------------------------------------
 // k_nonzh: one lane per non-Han block (cutNonZh, tokenizer.go:289-310)
 // ---------------------------------------------------------------------------
+// cutNonZh for one block [bs, be) (tokenizer.go:289-310)
+__device__ __forceinline__ void nonzh_block(const uint8_t* __restrict__ text, uint32_t bs, uint32_t be, Emitter& em) {
+    bool has = false;  // alnum.FindAllIndex found nothing -> no tokens (:290-293)
+    for (uint32_t p = bs; p < be && !has; p += 4) {
+        const uint32_t x = ld4(text, p);
+        const uint32_t nb = min(4u, be - p);
+        for (uint32_t k = 0; k < nb; k++) has |= jb_is_alnum((x >> (8 * k)) & 0xFFu);
+    }
+    if (!has) return;
+    uint32_t p = bs, run = 0;
+    bool in_run = false;
+    while (p < be) {
+        const uint32_t x = ld4(text, p);
+        if (jb_is_alnum(x & 0xFFu)) {  // alnum runs are kept whole
+            if (!in_run) {
+                in_run = true;
+                run = p;
+            }
+            p++;
+            continue;
+        }
+        if (in_run) {
+            em.token(run, p);
+            in_run = false;
+        }
+        uint32_t r;
+        const uint32_t w = jb_decode(x, min(4u, be - p), &r);
+        if (!jb_is_space(r)) em.token(p, p + w);  // one token per rune; spaces dropped
+        p += w;
+    }
+    if (in_run) em.token(run, be);
+}
+
+// One thread per 8 consecutive entries of the block list: the entries and the
+// lane bits under each non-Han block load in one round, and only blocks with a
+// [0-9A-Za-z] byte near them are read (the rest have no tokens, :290-293).
+constexpr uint32_t kNzPer = 8;
 __global__ __launch_bounds__(256) void k_nonzh(const uint8_t* __restrict__ text, const uint32_t* __restrict__ blk,
-                                               const uint32_t* __restrict__ lists, uint32_t list_cap,
+                                               const uint64_t* __restrict__ alnum16,
                                                const uint32_t* __restrict__ counters, uint32_t* __restrict__ sbits,
                                                uint32_t* __restrict__ ebits) {
-    const uint32_t nnz = counters[CNT_NBLK] - counters[CNT_NZH];
+    const uint32_t nblk = counters[CNT_NBLK];
     Emitter em(sbits, ebits);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nnz; i += gridDim.x * blockDim.x) {
-        const uint32_t g = lists[list_cap - 1u - i];
-        const uint32_t bs = blk[g] & 0x7FFFFFFFu, be = blk[g + 1] & 0x7FFFFFFFu;
-        bool has = false;  // alnum.FindAllIndex found nothing -> no tokens (:290-293)
-        for (uint32_t p = bs; p < be && !has; p += 4) {
-            const uint32_t x = ld4(text, p);
-            const uint32_t nb = min(4u, be - p);
-            for (uint32_t k = 0; k < nb; k++) has |= jb_is_alnum((x >> (8 * k)) & 0xFFu);
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c * kNzPer < nblk; c += gridDim.x * blockDim.x) {
+        const uint32_t i0 = c * kNzPer;
+        uint32_t e[kNzPer + 1];
+        if (i0 + kNzPer <= nblk) {  // blk[nblk] is the end sentinel
+            const uint4 u = *reinterpret_cast<const uint4*>(blk + i0);
+            const uint4 v = *reinterpret_cast<const uint4*>(blk + i0 + 4);
+            e[0] = u.x; e[1] = u.y; e[2] = u.z; e[3] = u.w;
+            e[4] = v.x; e[5] = v.y; e[6] = v.z; e[7] = v.w;
+            e[8] = blk[i0 + kNzPer];
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k <= kNzPer; k++) e[k] = (i0 + k <= nblk) ? blk[i0 + k] : 0x80000000u;
         }
-        if (!has) continue;
-        uint32_t p = bs, run = 0;
-        bool in_run = false;
-        while (p < be) {
-            const uint32_t x = ld4(text, p);
-            if (jb_is_alnum(x & 0xFFu)) {  // alnum runs are kept whole
-                if (!in_run) {
-                    in_run = true;
-                    run = p;
-                }
-                p++;
-                continue;
+        uint64_t aw[kNzPer];
+#pragma unroll
+        for (uint32_t k = 0; k < kNzPer; k++) aw[k] = alnum16[(e[k] & 0x7FFFFFFFu) >> 10];
+#pragma unroll
+        for (uint32_t k = 0; k < kNzPer; k++) {
+            if ((e[k] >> 31) || i0 + k >= nblk) continue;  // a zh block
+            const uint32_t bs = e[k], be = e[k + 1] & 0x7FFFFFFFu;
+            const uint32_t llast = (be - 1u) >> 4;
+            uint32_t l = bs >> 4;
+            bool maybe = false;
+            uint64_t w = aw[k];
+            for (;;) {
+                const uint32_t lo = l & 63u, hi = min(63u, lo + (llast - l));
+                const uint64_t m = (hi == 63u ? ~0ull : ((2ull << hi) - 1ull)) & (~0ull << lo);
+                maybe = (w & m) != 0ull;
+                l += hi - lo + 1u;
+                if (maybe || l > llast) break;
+                w = alnum16[l >> 6];  // a block over more than one 1 KiB word (rare)
             }
-            if (in_run) {
-                em.token(run, p);
-                in_run = false;
-            }
-            uint32_t r;
-            const uint32_t w = jb_decode(x, min(4u, be - p), &r);
-            if (!jb_is_space(r)) em.token(p, p + w);  // one token per rune; spaces dropped
-            p += w;
+            if (maybe) nonzh_block(text, bs, be, em);
         }
-        if (in_run) em.token(run, be);
     }
     em.flush();
 }
@@ -1547,7 +1590,6 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     const uint64_t nwords = (nbytes + 31) / 32;
     const uint32_t ntiles = (uint32_t)((nbytes + kTileBytes - 1) / kTileBytes);
     const uint32_t nttiles = (uint32_t)((nwords + kTokTileWords - 1) / kTokTileWords);
-    const uint32_t list_cap = (uint32_t)(nbytes + 2);
     hipError_t e;
     if ((e = hipMemsetAsync(w.counters, 0, CNT_NWORDS * sizeof(uint32_t) + sizeof(uint64_t), stream))) return e;
     if (w.bits_stride <= 2 * (nwords + 2)) {  // workspace sized for this batch: one clear for all three
@@ -1566,13 +1608,14 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         JB_TIMED(K_DOCBITS, hipLaunchKernelGGL(k_docbits, dim3((ndocs + 255) / 256), dim3(256), 0, stream,
                                                d_doc_off, ndocs, nbytes, w.docbits));
     JB_TIMED(K_MARK_WALK, hipLaunchKernelGGL(k_mark_walk, dim3(ntiles), dim3(256), 0, stream, d_text, nbytes,
-                                             w.docbits, im, w.lanemask, w.tile_cnt, w.erec, w.tile4, g_ablate,
+                                             w.docbits, im, w.lanemask, w.tile_cnt, w.erec, w.tile4, w.alnum16,
+                                             g_ablate,
                                              w.dbg_walk));
     JB_TIMED(K_SCAN_BLOCKS, hipLaunchKernelGGL(k_scan2, dim3(1), dim3(1024), 0, stream, w.tile_cnt, ntiles,
                                                w.tile_off, w.counters + CNT_NBLK, nullptr, w.blk,
                                                (uint32_t)nbytes));
     JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL(k_blocks_write, dim3(ntiles), dim3(256), 0, stream, w.lanemask,
-                                                w.tile_off, w.blk, w.lists, list_cap, w.gstart));
+                                                w.tile_off, w.blk, w.gstart));
     if (hmm)
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
                                           w.gstart, w.tile4, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,
@@ -1581,8 +1624,8 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
                                           w.gstart, w.tile4, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,
                                           g_ablate, w.dbg));
-    JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3(grid_nz), dim3(256), 0, stream, d_text, w.blk, w.lists,
-                                         list_cap, w.counters, w.sbits, w.ebits));
+    JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3(grid_nz), dim3(256), 0, stream, d_text, w.blk, w.alnum16,
+                                         w.counters, w.sbits, w.ebits));
     JB_TIMED(K_TOK_COUNT, hipLaunchKernelGGL((k_tok<false>), dim3(nttiles), dim3(256), 0, stream, w.sbits, w.ebits,
                                              nwords, w.ttile_cnt, nullptr, nullptr, nullptr));
     JB_TIMED(K_SCAN_TOK, hipLaunchKernelGGL(k_scan2, dim3(1), dim3(1024), 0, stream, w.ttile_cnt, nttiles,
