@@ -381,7 +381,7 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.ttile_off, nttiles * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.blk, (nb + 4) * 4));
     HIPCHK(hipMalloc(&w.alnum16, (nb / 1024 + 8) * 8));
-    HIPCHK(hipMalloc(&w.erec, (nb / 3 + 8) * 8));
+    HIPCHK(hipMalloc(&w.erec, (nb / 3 + 8 + kErecPad) * 8));
     HIPCHK(hipMalloc(&w.lanemask, ntiles * 256 * 4));
     HIPCHK(hipMalloc(&w.gbl, nb / 3 + 8));
     HIPCHK(hipMalloc(&w.gstart, (nb / kZhGroupBytes + 4) * sizeof(uint2)));

@@ -33,6 +33,7 @@ constexpr int kTokTileWords = 512;     // k_tok: 256 threads x 2 words (16 KiB o
 #ifndef JB_ZH_GROUP
 #define JB_ZH_GROUP 6144
 #endif
+constexpr uint32_t kErecPad = 8;  // erec slots before slot 0 (k_zh reads a few slots past a block's start)
 constexpr uint32_t kZhGroupBytes = JB_ZH_GROUP;  // k_zh work unit: zh blocks starting in one such span (multiple of 32)
 
 // Per-call device workspace, sized for `nbytes` of text.

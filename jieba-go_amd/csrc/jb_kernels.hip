@@ -1004,31 +1004,33 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
                              double* __restrict__ gbest, double* ring, const Src& src) {
     uint32_t j = 0, bs = 0, be = 0;
     if (!src.next(j, bs, be)) return 0;
-    uint32_t key0 = 0, steps = 0, q = 0, c = 1, s0 = 0, s = 0, mc = 0;
+    uint32_t key0 = 0, steps = 0, q = 0, c = 1, s = 0, mc = 0;
     bool longm = false;
-    // record k runes back (clamped to this rune past the block start; the
-    // consumer masks it then, so no instruction here waits for the load)
-    auto ld_rec = [&](uint32_t k) -> uint64_t { return erec[(s >= s0 + k) ? s - k : s]; };
-    // (re)start at the last rune of [bs, be): its edge mask and weights, the next record
-    auto prime = [&](uint64_t& r1, double (&w)[4]) {
+    // Records come two per load: slots (k, k+1) = runes two apart going back.
+    // A steps load the pair of the next-but-one and next-but-two runes; B steps
+    // load none.  Slots before a block (or before the text: erec has 8 slots of
+    // padding in front) are garbage that `more` masks at the use.
+    uint64_t lo = 0, hi = 0;  // the last pair: lo = the rune further back
+    auto pair = [&](uint32_t k) {  // slots k, k+1 in one 16-byte load
+        typedef uint64_t u64x2 __attribute__((ext_vector_type(2), aligned(8)));
+        const u64x2 x = *reinterpret_cast<const u64x2*>(erec + (int32_t)k);
+        lo = x.x;
+        hi = x.y;
+    };
+    auto setup = [&]() {
         key0 = be / 3u;
         q = be - 3u;
         c = 1;
-        s0 = bs / 3u;
         s = q / 3u;
-        const uint64_t rc = erec[s];
-        mc = (uint32_t)rc & 0xFFu;
-        rec_weights(im, rc, w);
-        r1 = ld_rec(1);
     };
-    // One rune.  r1: the next rune's record (landed); r2: gets the record two
-    // back; wc: this rune's weights (loaded a step ago); wn: gets the next
-    // rune's.  The loop below alternates two register sets, so nothing is
-    // copied out of a load's destination (a copy would wait for the load).
-    auto step = [&](uint64_t& r1, uint64_t& r2, double (&wc)[4], double (&wn)[4]) -> bool {
+    // One rune.  r1: the next rune's record (landed a step ago); wc: this rune's
+    // weights (loaded a step ago); wn: gets the next rune's.  Weight registers
+    // alternate between the two steps, so nothing is copied out of a load's
+    // destination (a copy would wait for the load).
+    auto step = [&](const bool A, double (&wc)[4], double (&wn)[4]) -> bool {
         const bool more = q > bs;
-        r2 = ld_rec(2);  // first: the next step waits for it, and vmcnt retires in order
-        const uint64_t r1v = more ? r1 : 0ull;  // (the next rune exists)
+        const uint64_t r1v = more ? (A ? lo : hi) : 0ull;  // (the next rune exists)
+        if (A) pair(s - 3u);  // runes t+3, t+2 (first: vmcnt retires in order)
         const uint32_t mn = (uint32_t)r1v & 0xFFu;
         rec_weights(im, r1v, wn);
         DpFold f;
@@ -1039,29 +1041,41 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
         if (longm) gbest[key0 - c] = f.bestP;
         v.bl(q) = (uint8_t)f.bestL;
         steps++;
-        if (f.redo) {  // an edge past the ring: this block again, every best value kept in gbest
-            prime(r2, wn);
-            longm = true;
-            return false;
-        }
-        if (more) {
+        const bool restart = f.redo || !more;
+        if (!restart) {
             q -= 3u;
             s -= 1u;
             mc = mn;
             ++c;
             return false;
         }
-        if (!src.next(j, bs, be)) return true;
-        longm = false;
-        prime(r2, wn);
+        if (f.redo) longm = true;  // an edge past the ring: this block again, every best value kept in gbest
+        else {
+            if (!src.next(j, bs, be)) return true;
+            longm = false;
+        }
+        // (re)start at the last rune of [bs, be); the next step is the other kind
+        setup();
+        if (A) {  // next: B, which wants hi = E(s-1); the A after it wants lo = E(s-2)
+            pair(s - 2u);
+            const uint64_t rc = erec[s];
+            mc = (uint32_t)rc & 0xFFu;
+            rec_weights(im, rc, wn);
+        } else {  // next: A, which wants lo = E(s-1)
+            pair(s - 1u);
+            mc = (uint32_t)hi & 0xFFu;
+            rec_weights(im, hi, wn);
+        }
         return false;
     };
-    uint64_t ra = 0, rb = 0;
     double wa[4], wb[4];
-    prime(ra, wa);
+    setup();  // first block: the next step is an A
+    pair(s - 1u);
+    mc = (uint32_t)hi & 0xFFu;
+    rec_weights(im, hi, wa);
     for (;;) {
-        if (step(ra, rb, wa, wb)) break;
-        if (step(rb, ra, wb, wa)) break;
+        if (step(true, wa, wb)) break;
+        if (step(false, wb, wa)) break;
     }
     return steps;
 }
@@ -1608,7 +1622,8 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         JB_TIMED(K_DOCBITS, hipLaunchKernelGGL(k_docbits, dim3((ndocs + 255) / 256), dim3(256), 0, stream,
                                                d_doc_off, ndocs, nbytes, w.docbits));
     JB_TIMED(K_MARK_WALK, hipLaunchKernelGGL(k_mark_walk, dim3(ntiles), dim3(256), 0, stream, d_text, nbytes,
-                                             w.docbits, im, w.lanemask, w.tile_cnt, w.erec, w.tile4, w.alnum16,
+                                             w.docbits, im, w.lanemask, w.tile_cnt, w.erec + kErecPad, w.tile4,
+                                             w.alnum16,
                                              g_ablate,
                                              w.dbg_walk));
     JB_TIMED(K_SCAN_BLOCKS, hipLaunchKernelGGL(k_scan2, dim3(1), dim3(1024), 0, stream, w.tile_cnt, ntiles,
@@ -1618,11 +1633,11 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                                 w.tile_off, w.blk, w.gstart));
     if (hmm)
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
-                                          w.gstart, w.tile4, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,
+                                          w.gstart, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
                                           g_ablate, w.dbg));
     else
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
-                                          w.gstart, w.tile4, w.counters, im, w.erec, w.gbl, w.gbest, w.sbits, w.ebits,
+                                          w.gstart, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
                                           g_ablate, w.dbg));
     JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3(grid_nz), dim3(256), 0, stream, d_text, w.blk, w.alnum16,
                                          w.counters, w.sbits, w.ebits));
