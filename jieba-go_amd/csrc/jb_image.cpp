@@ -368,8 +368,10 @@ int build_image(const Dictionary& d, const Emission& e, Image* img, std::string*
     const uint16_t* pm = img->pagemap.data();
 
     // distinct weights: pieceFreq := math.Log(tf) - total (tokenizer.go:519).  Indices go to
-    // the weights in order of how many keys use them (ties by value bits), so the
-    // common ones get small indices (k_mark_walk packs 14-bit indices).
+    // the weights in order of the summed frequency of the keys that use them (a key's
+    // frequency is how often the reference's corpus saw it, so this is the order in
+    // which text looks them up, so the hot weights share a few cache lines; ties by key
+    // count, then value bits).  k_mark_walk packs 14-bit indices.
     img->wtab.assign(1, img->w_absent);
     std::unordered_map<uint64_t, uint32_t> widx_of;
     auto wbits = [&](int64_t f) -> uint64_t {
@@ -379,17 +381,29 @@ int build_image(const Dictionary& d, const Emission& e, Image* img, std::string*
         return bits;
     };
     {
-        std::unordered_map<uint64_t, uint64_t> uses;
-        for (const Key& k : keys) uses[wbits(k.f)]++;
-        std::vector<std::pair<uint64_t, uint64_t>> order(uses.begin(), uses.end());
-        std::sort(order.begin(), order.end(), [](const std::pair<uint64_t, uint64_t>& a,
-                                                 const std::pair<uint64_t, uint64_t>& b) {
-            return a.second != b.second ? a.second > b.second : a.first < b.first;
+        struct Use { uint64_t bits; double mass; uint64_t keys; };
+        std::unordered_map<uint64_t, size_t> at;
+        std::vector<Use> uses;
+        for (const Key& k : keys) {
+            const uint64_t b = wbits(k.f);
+            auto it = at.find(b);
+            if (it == at.end()) {
+                at.emplace(b, uses.size());
+                uses.push_back(Use{b, 0.0, 0});
+                it = at.find(b);
+            }
+            Use& u = uses[it->second];
+            u.mass += k.f > 0 ? (double)k.f : 0.0;
+            u.keys++;
+        }
+        std::sort(uses.begin(), uses.end(), [](const Use& a, const Use& b) {
+            if (a.mass != b.mass) return a.mass > b.mass;
+            return a.keys != b.keys ? a.keys > b.keys : a.bits < b.bits;
         });
-        for (const auto& o : order) {
+        for (const Use& u : uses) {
             double w;
-            memcpy(&w, &o.first, 8);
-            widx_of.emplace(o.first, (uint32_t)img->wtab.size());
+            memcpy(&w, &u.bits, 8);
+            widx_of.emplace(u.bits, (uint32_t)img->wtab.size());
             img->wtab.push_back(w);
         }
     }
