@@ -52,11 +52,12 @@ const char* const kKernelNames[K_NUM] = {"k_docbits", "k_mark_walk", "k_scan_blo
 // ---------------------------------------------------------------------------
 // small device helpers
 // ---------------------------------------------------------------------------
-// 4 bytes at any offset: two aligned dword loads + v_alignbyte.  The text
-// buffer is 4-byte aligned and readable 8 bytes past every offset used.
+// 4 bytes at any offset: one 8-byte load at the dword below + v_alignbyte.  The
+// text buffer is 4-byte aligned and readable 8 bytes past every offset used.
 __device__ __forceinline__ uint32_t ld4(const uint8_t* __restrict__ t, uint64_t q) {
-    const uint32_t* a = reinterpret_cast<const uint32_t*>(t + (q & ~3ull));
-    return __builtin_amdgcn_alignbyte(a[1], a[0], (uint32_t)(q & 3));
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2), aligned(4)));
+    const u32x2 a = *reinterpret_cast<const u32x2*>(t + (q & ~3ull));
+    return __builtin_amdgcn_alignbyte(a.y, a.x, (uint32_t)(q & 3));
 }
 
 // 4 bytes at window offset k of staged text (k + 8 readable).
@@ -745,6 +746,43 @@ __device__ __forceinline__ void route2(double a, double b, uint32_t* code, doubl
 // Back-pointers (2 bits per state) go to each rune's slot; the traceback
 // stops at the first "" route: the reference's path then restarts at that
 // step (fullPath[""] is nil, :715) and cutHMM labels runes from the run start.
+// The traceback + cutHMM half of viterbi (tokenizer.go:715-729, 273-285):
+// back-pointers are in the runes' slots, st is the final state.
+template <class V, class E>
+__device__ void viterbi_back(const V& v, uint32_t rs, uint32_t re, uint32_t m, uint32_t st, E& em) {
+    uint32_t t = m - 1, reset = 0;
+    uint32_t qt = z_prev(v, re, rs);
+    for (;;) {
+        if (t == 0) {
+            v.bl(qt) = (uint8_t)st;
+            break;
+        }
+        const uint32_t code = (v.bl(qt) >> (2u * st)) & 3u;
+        v.bl(qt) = (uint8_t)st;
+        if (code == 2u) {
+            reset = t;
+            break;
+        }
+        st = (st == JB_B || st == JB_S) ? 2u + code : code;  // B,S <- {E,S}; M,E <- {B,M}
+        --t;
+        qt = z_prev(v, qt, rs);
+    }
+    uint32_t qa = rs, qb = qt, ts = rs;
+    for (uint32_t k = 0; k < m - reset; k++) {
+        const uint32_t lab = v.bl(qb);
+        qa += z_w(v, qa);
+        qb += z_w(v, qb);
+        if (lab >= (uint32_t)JB_E) {
+            em.token(ts, qa);
+            ts = qa;
+        }
+    }
+}
+
+// viterbi (tokenizer.go:668-730) over the m runes [rs, re) + cutHMM (:273-285).
+// Back-pointers (2 bits per state) go to each rune's slot; the traceback
+// stops at the first "" route: the reference's path then restarts at that
+// step (fullPath[""] is nil, :715) and cutHMM labels runes from the run start.
 template <class V, class E>
 __device__ void viterbi_run(const V& v, const DevImage& im, uint32_t rs, uint32_t re, uint32_t m, E& em) {
     if (m == 1) {  // always "S" for a single rune (:672-674)
@@ -777,34 +815,7 @@ __device__ void viterbi_run(const V& v, const DevImage& im, uint32_t rs, uint32_
         w = wn;
         e[0] = en[0]; e[1] = en[1]; e[2] = en[2]; e[3] = en[3];
     }
-    uint32_t st = vE > vS ? (uint32_t)JB_E : (uint32_t)JB_S;  // (:723-729)
-    uint32_t t = m - 1, reset = 0;
-    uint32_t qt = z_prev(v, re, rs);
-    for (;;) {
-        if (t == 0) {
-            v.bl(qt) = (uint8_t)st;
-            break;
-        }
-        const uint32_t code = (v.bl(qt) >> (2u * st)) & 3u;
-        v.bl(qt) = (uint8_t)st;
-        if (code == 2u) {
-            reset = t;
-            break;
-        }
-        st = (st == JB_B || st == JB_S) ? 2u + code : code;  // B,S <- {E,S}; M,E <- {B,M}
-        --t;
-        qt = z_prev(v, qt, rs);
-    }
-    uint32_t qa = rs, qb = qt, ts = rs;
-    for (uint32_t k = 0; k < m - reset; k++) {
-        const uint32_t lab = v.bl(qb);
-        qa += z_w(v, qa);
-        qb += z_w(v, qb);
-        if (lab >= (uint32_t)JB_E) {
-            em.token(ts, qa);
-            ts = qa;
-        }
-    }
+    viterbi_back(v, rs, re, m, vE > vS ? (uint32_t)JB_E : (uint32_t)JB_S, em);  // (:723-729)
 }
 
 // A lane's blocks of the current chunk: LDS table entries t[j * 64] for
@@ -1091,6 +1102,81 @@ struct RunList {
     uint32_t n;
 };
 
+// The forward half of viterbi for all of a lane's deferred runs (all-3-byte
+// chunk) in one loop: one rune per step, runs back to back, so a lane's trip
+// count is its total run length.  The text of the rune two steps ahead and
+// the emissions of the next rune are in flight during each step, in two
+// register sets that alternate between steps (nothing copied out of a load's
+// destination).  Returns the final states, bit r set for E (:723-729).
+template <class E>
+__device__ uint32_t viterbi_fwd_runs(const GrpZvT<true>& v, const DevImage& im, const uint32_t* runs, uint32_t n) {
+    // rune cursor: position q and run r of the current, next and next-but-one rune
+    uint32_t q0 = 0, r0 = 0, q1 = 0, r1 = 0, q2 = 0, r2 = 0, t = 0;
+    auto rs_of = [&](uint32_t r) { return v.wb + (runs[r * 64u] & 0xFFFFu); };
+    auto re_of = [&](uint32_t r) { return v.wb + (runs[r * 64u] >> 16); };
+    auto adv = [&](uint32_t& q, uint32_t& r) {  // the rune after (q, r); r == n past the last
+        if (r >= n) return;
+        if (q + 3u < re_of(r)) {
+            q += 3u;
+        } else {
+            ++r;
+            if (r < n) q = rs_of(r);
+        }
+    };
+    uint32_t stbits = 0;
+    if (n == 0) return 0;
+    q0 = rs_of(0);
+    q1 = q0;
+    r1 = 0;
+    adv(q1, r1);
+    q2 = q1;
+    r2 = r1;
+    adv(q2, r2);
+    double vB = 0, vM = 0, vE = 0, vS = 0;
+    uint32_t xa = 0, xb = 0;  // text dwords (rune two ahead), alternating
+    double ea[4], eb[4];      // emissions (rune one ahead), alternating
+    uint32_t w0;
+    load_emit(im, z_dec(v, q0, &w0), ea);
+    xa = v.x4(q1);
+    bool act = true;
+    auto step = [&](uint32_t& xn, uint32_t& xnn, double (&ec)[4], double (&en)[4]) {
+        // xn: text of rune 1 ahead (landed); xnn: gets rune 2 ahead; ec: this rune's emissions
+        if (r2 < n) xnn = v.x4(q2);
+        if (r1 < n) {
+            const uint32_t x = xn;
+            const uint32_t rn = ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
+            load_emit(im, rn, en);
+        }
+        uint32_t cB, cM, cE, cS;
+        double pB, pM, pE, pS;
+        route2(vE + T_EB, vS + T_SB, &cB, &pB);  // B <- E, S
+        route2(vB + T_BM, vM + T_MM, &cM, &pM);  // M <- B, M
+        route2(vB + T_BE, vM + T_ME, &cE, &pE);  // E <- B, M
+        route2(vE + T_ES, vS + T_SS, &cS, &pS);  // S <- E, S
+        const bool first = t == 0;
+        vB = (first ? START_B : pB) + ec[0];
+        vM = (first ? JB_MIN_FLOAT : pM) + ec[1];
+        vE = (first ? JB_MIN_FLOAT : pE) + ec[2];
+        vS = (first ? START_S : pS) + ec[3];
+        v.bl(q0) = (uint8_t)(cB | (cM << 2) | (cE << 4) | (cS << 6));  // (unread for the first rune)
+        const bool last = r1 != r0;
+        if (last) stbits |= (vE > vS ? 1u : 0u) << r0;
+        t = last ? 0u : t + 1u;
+        q0 = q1;
+        r0 = r1;
+        q1 = q2;
+        r1 = r2;
+        adv(q2, r2);
+        act = r0 < n;
+    };
+    while (act) {
+        step(xa, xb, ea, eb);
+        if (!act) break;
+        step(xb, xa, eb, ea);
+    }
+    return stbits;
+}
+
 // Forward walk of one block (findDagPath) + HMM runs.  Returns false where the
 // reference panics (a rune on the chosen path with no DAG edge: cutDAG slices
 // with tail index -1).
@@ -1184,13 +1270,16 @@ __device__ void zh_chunk_main(const uint8_t* __restrict__ text, const DevImage& 
         RunList rl{runs, wb, 0u};
         RunList* const rlp = (HMM && A3) ? &rl : nullptr;
         while (src.next(j, bs, be)) ok &= zh_fwd<HMM>(v, im, bs, be, le, ablate, rlp);
-        if (HMM && A3)
+        if constexpr (HMM && A3) {
+            const uint32_t stb = viterbi_fwd_runs<LdsEmitter>(v, im, runs, rl.n);
             for (uint32_t r = 0; r < kZhRuns; r++)
                 if (r < rl.n) {
                     const uint32_t x = runs[r * 64u];
                     const uint32_t rs = wb + (x & 0xFFFFu), re = wb + (x >> 16);
-                    viterbi_run(v, im, rs, re, (re - rs) / 3u, le);
+                    viterbi_back(v, rs, re, (re - rs) / 3u, ((stb >> r) & 1u) ? (uint32_t)JB_E : (uint32_t)JB_S,
+                                 le);
                 }
+        }
         le.flush();
         if (!ok) atomicOr(counters + CNT_ERR, 1u);
     }
