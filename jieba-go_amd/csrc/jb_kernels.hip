@@ -408,7 +408,7 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
     const uint32_t hi = (nent * (wv + 1u)) >> 2;
     const uint32_t elast = nent ? nent - 1u : 0u;
     bool act = false, ovf = false;
-    uint32_t q = 0, j = 0, js = 0, ecur = 0, id = 0, len = 0, nedge = 0;
+    uint32_t j = 0, js = 0, ecur = 0, id = 0, len = 0, nedge = 0;
     uint64_t cur = 0;  // the cell of the walk's current node
     uint64_t rc = 0;
     auto edge = [&](uint32_t L, uint32_t wi) {
@@ -446,7 +446,6 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
             js = j0;
             ecur = ent[j0];
             cur = s_c[j0];
-            q = ent_pos(ecur);
             id = ent_code(ecur);  // its level-1 cell
             len = 1u;
             nedge = 0u;
@@ -558,7 +557,6 @@ __global__ __launch_bounds__(256) void k_blocks_write(const uint32_t* __restrict
     if (p0 % kZhGroupBytes == 0u) gstart[p0 / kZhGroupBytes] = make_uint2(to.x + (ex & 0xFFFFu), to.y + (ex >> 16));
     if (!bmask) return;
     uint32_t ga = to.x + (ex & 0xFFFFu);  // global block rank
-    uint32_t gz = to.y + (ex >> 16);      // global zh rank
     uint32_t b = bmask;
     while (b) {
         const uint32_t k = __builtin_ctz(b);
@@ -1216,6 +1214,57 @@ __device__ bool zh_fwd(const V& v, const DevImage& im, uint32_t bs, uint32_t be,
     return true;
 }
 
+// The forward walk over all of a lane's blocks in one loop (a lane's trip
+// count is its total piece count, not the per-block maximum over the wave).
+template <bool HMM, class V, class E, class Src>
+__device__ bool zh_fwd_lane(const V& v, const DevImage& im, const Src& src, E& em, uint32_t ablate, RunList* rl) {
+    auto run_end = [&](uint32_t rs, uint32_t re, uint32_t m) {
+        if ((ablate & 32u) || m == 1u) em.token(rs, re);  // a single rune is always "S" (:672-674)
+        else if (rl && rl->n < kZhRuns) {
+            rl->t[rl->n * 64u] = (rs - rl->wb) | ((re - rl->wb) << 16);
+            rl->n++;
+        } else viterbi_run(v, im, rs, re, m, em);
+    };
+    uint32_t j = 0, bs = 0, be = 0;
+    bool ok = true;
+    if (!src.next(j, bs, be)) return ok;
+    uint32_t p = bs, run_s = 0, run_n = 0;
+    for (;;) {
+        if (p >= be) {  // the block is done: its last run, then the lane's next block
+            if (HMM && run_n) run_end(run_s, be, run_n);
+            run_n = 0;
+            if (!src.next(j, bs, be)) break;
+            p = bs;
+            continue;
+        }
+        const uint32_t L = v.bl(p);
+        if (L == 0) {  // tail index -1: cutDAG's slice panics in the reference
+            ok = false;
+            p = be;
+            run_n = 0;
+            continue;
+        }
+        uint32_t pe = p;
+        if (V::all3) pe += 3u * L;
+        else
+            for (uint32_t k = 0; k < L; k++) pe += z_w(v, pe);
+        if (!HMM) {
+            em.token(p, pe);
+        } else if (L == 1) {
+            if (run_n == 0) run_s = p;
+            run_n++;
+        } else {
+            if (run_n) {
+                run_end(run_s, p, run_n);
+                run_n = 0;
+            }
+            em.token(p, pe);
+        }
+        p = pe;
+    }
+    return ok;
+}
+
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1265,11 +1314,10 @@ __device__ void zh_chunk_main(const uint8_t* __restrict__ text, const DevImage& 
     wave_sync();
     if (!(ablate & 4u)) {
         LdsEmitter le(sb, eb, wb >> 5);
-        bool ok = true;
-        uint32_t j = 0, bs, be;
+        bool ok;
         RunList rl{runs, wb, 0u};
         RunList* const rlp = (HMM && A3) ? &rl : nullptr;
-        while (src.next(j, bs, be)) ok &= zh_fwd<HMM>(v, im, bs, be, le, ablate, rlp);
+        ok = zh_fwd_lane<HMM>(v, im, src, le, ablate, rlp);
         if constexpr (HMM && A3) {
             const uint32_t stb = viterbi_fwd_runs<LdsEmitter>(v, im, runs, rl.n);
             for (uint32_t r = 0; r < kZhRuns; r++)
