@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
     __shared__ uint64_t s_c[kTileE];  // the level-1 cell of each entry's rune, then the record of its walk
     __shared__ uint32_t lds[8];
     __shared__ uint16_t s_def[256];  // entries whose walk's run goes past the tile
-    __shared__ uint32_t s_ndef;
+    __shared__ uint32_t s_ndef, s_nwl;
 #if JB_STAMPS
     const bool stamps = (ablate & 0x100u) != 0;  // diagnostic per-wave phase clocks (make STAMPS=1)
 #else
@@ -289,7 +289,10 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
         const uint64_t wi = (t0 >> 5) + threadIdx.x;
         s_db[threadIdx.x] = wi < lastw ? docbits[wi] : 0u;
     }
-    if (threadIdx.x == 0) s_ndef = 0;
+    if (threadIdx.x == 0) {
+        s_ndef = 0;
+        s_nwl = 0;
+    }
     const uint64_t p0 = t0 + threadIdx.x * 16u;
     // doc-start / past-the-end mask, bit k <-> byte p0 - 4 + k (k < 24)
     uint64_t M;
@@ -390,23 +393,46 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
             }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nent; i += 256u) {  // run links
+    // Run links, then level 1 of every entry: a rune that is absent, has count 0,
+    // has no children or ends its Han run gets its record now (in its LDS cell,
+    // which only its own walk would read); the others go on the walk list (over
+    // the staged text, no longer needed) or, when the next rune is past the
+    // tile, straight to the deferred list.
+    uint16_t* s_wl = reinterpret_cast<uint16_t*>(s_t);
+    for (uint32_t i = threadIdx.x; i < nent; i += 256u) {
         const uint32_t e = s_e[i];
         const uint32_t nxt = ent_pos(e) + ent_w(e);
         uint32_t f = 0;
         if (nxt >= kTileBytes) f = kEntEdge;
         else if (i + 1u < nent && ent_pos(s_e[i + 1u]) == nxt && !((s_db[nxt >> 5] >> (nxt & 31u)) & 1u)) f = kEntCont;
         s_e[i] = e | f;
+        const uint64_t c1 = s_c[i];
+        const uint32_t fc = jb_cell_fc(c1), wi = jb_cell_widx(c1);
+        uint64_t r1 = 0;
+        bool go = false;
+        if (jb_cell_check(c1) != JB_CHECK_ROOT) {
+            r1 = 1ull | ((uint64_t)JB_WIDX_ABSENT << 8);  // absent: the single edge only, Log(1) (:468-471)
+        } else if (wi >= (1u << kEdgeIdxBits) && fc != JB_FC_NEG) {
+            r1 = 0ull;  // the weight index does not fit a record: k_zh walks this rune
+        } else if (fc == JB_FC_ZERO) {
+            r1 = 1ull | ((uint64_t)wi << 8);  // count 0: the single edge only, Log(0) = -Inf
+        } else {
+            if (fc == JB_FC_POS) r1 = 1ull | ((uint64_t)wi << 8);  // (a negative count has no edge)
+            go = jb_cell_hc(c1) != 0u && f != 0u;
+        }
+        if (!go) s_c[i] = r1;
+        else if (f == kEntCont) s_wl[atomicAdd(&s_nwl, 1u)] = (uint16_t)i;
+        else s_def[atomicAdd(&s_ndef, 1u)] = (uint16_t)i;
     }
     const int any4 = __syncthreads_or(has4);  // (also the barrier after the run links)
     if (threadIdx.x == 0) tile4[blockIdx.x] = any4 ? 1u : 0u;  // k_zh: general rune stepping near this tile
     if (stamps) c2 = __builtin_amdgcn_s_memtime();
-    // ---- walks: wave w takes the walk starts [lo, hi) of the tile ---------------------
+    // ---- walks: wave w takes a quarter of the walk list ------------------------------
     const uint32_t* ent = s_e;
     const uint32_t wv = threadIdx.x >> 6;
-    uint32_t head = (nent * wv) >> 2;
-    const uint32_t hi = (nent * (wv + 1u)) >> 2;
-    const uint32_t elast = nent ? nent - 1u : 0u;
+    const uint32_t nwl = s_nwl;
+    uint32_t head = (nwl * wv) >> 2;
+    const uint32_t hi = (nwl * (wv + 1u)) >> 2;
     bool act = false, ovf = false;
     uint32_t j = 0, js = 0, ecur = 0, id = 0, len = 0, nedge = 0;
     uint64_t cur = 0;  // the cell of the walk's current node
@@ -441,36 +467,24 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
         const uint32_t j0 = head + rank;
         const bool fresh = !act && j0 < hi;
         head = min(hi, head + (uint32_t)__popcll(need));
-        if (fresh) {  // level 1 from LDS; the walk goes on only with children and a next rune
-            j = j0;
-            js = j0;
-            ecur = ent[j0];
-            cur = s_c[j0];
+        if (fresh) {  // a walk from the list: its rune has children and the run goes on in the tile
+            j = s_wl[j0];
+            js = j;
+            ecur = ent[j];
+            cur = s_c[j];
             id = ent_code(ecur);  // its level-1 cell
             len = 1u;
             nedge = 0u;
-            rc = 0ull;
             ovf = false;
-            const uint32_t fc = jb_cell_fc(cur);
-            if (jb_cell_check(cur) != JB_CHECK_ROOT) {
-                edge(1u, JB_WIDX_ABSENT);  // absent: the single edge only, Log(1) (:468-471)
-                finish();
-            } else if (fc == JB_FC_ZERO) {
-                edge(1u, jb_cell_widx(cur));  // count 0: the single edge only, Log(0) = -Inf
-                finish();
-            } else {
-                if (fc == JB_FC_POS) edge(1u, jb_cell_widx(cur));  // (a negative count has no edge)
-                if (ablate & 1u) finish();
-                else next_or_stop();
-            }
+            rc = jb_cell_fc(cur) == JB_FC_POS ? 1ull | ((uint64_t)jb_cell_widx(cur) << 8) : 0ull;
+            nedge = jb_cell_fc(cur) == JB_FC_POS ? 1u : 0u;
+            act = true;
         }
         // one round trip: the next rune's cell for every walk under way
-        uint64_t child = 0;
-        uint32_t t = 0;
         if (act) {
-            const uint32_t en = ent[min(j + 1u, elast)];
-            t = dat_slot_k(cur, ent_code(en));
-            child = im.cells[t];
+            const uint32_t en = ent[j + 1u];
+            const uint32_t t = dat_slot_k(cur, ent_code(en));
+            const uint64_t child = im.cells[t];
             if (dat_hit(child, id)) {
                 ++j;
                 ecur = en;
