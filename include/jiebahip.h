@@ -46,11 +46,18 @@ typedef struct jb_image jb_image;
 /* Dictionary semantics. */
 #define JB_DICT_TXT 0    /* NewTokenizer(dictionaryFile): newPrefixDictionaryFromFile, tokenizer.go:61,389-437
                             (first occurrence wins, size = sum of first occurrences, no prefix entries) */
-#define JB_DICT_PREFIX 1 /* NewJiebaTokenizer(): prefix_dictionary.gob = buildPrefixDictionary output,
-                            tokenizer.go:69,340-366,439-458 (last value wins, freq-0 prefix entries) */
+#define JB_DICT_PREFIX 1 /* dict.txt-format lines read as buildPrefixDictionary does, tokenizer.go:340-366
+                            (last value wins, freq-0 prefix entries): the map prefix_dictionary.gob holds */
+#define JB_DICT_GOB 2    /* NewJiebaTokenizer(): prefix_dictionary.gob itself, an encoding/gob map[string]int
+                            (newJiebaPrefixDictionary, tokenizer.go:69,439-458); size = 60,101,967
+                            (tokenizer.go:454) unless size_override > 0 */
+#define JB_DICT_IMAGE 3  /* a serialized image written by jb_save / jb_image_save (dictionary, emission
+                            table and device arrays; emit_path is ignored): skips parsing and the trie
+                            build.  size_override > 0 and different from the saved size rebuilds the weights */
+#define JB_JIEBA_SIZE 60101967 /* newJiebaPrefixDictionary's pd.size (tokenizer.go:454) */
 
 typedef struct {
-    const char *dict_path;   /* dict.txt-format file ("word freq [tag]" lines); NULL: use dict_buf */
+    const char *dict_path;   /* dictionary file in the dict_kind format; NULL: use dict_buf */
     const char *dict_buf;
     size_t dict_len;
     int dict_kind;           /* JB_DICT_TXT or JB_DICT_PREFIX */
@@ -122,9 +129,18 @@ int jb_profile_enable(jb_ctx *ctx, int on);
 int jb_profile_read(jb_ctx *ctx, const char **names, double *ms, uint64_t *launches, int cap);
 int jb_profile_reset(jb_ctx *ctx);
 
+/* Write ctx's current image (including words added by jb_add_word) to `path`,
+ * to be opened later with dict_kind JB_DICT_IMAGE: the fast-start counterpart of
+ * the reference shipping prefix_dictionary.gob instead of rebuilding the map
+ * from dict.txt (tokenizer.go:439-458 vs :389-437). */
+int jb_save(jb_ctx *ctx, const char *path);
+
 /* ---- host-only image access (no GPU needed; used by CPU tests) ---------- */
 int jb_image_build(const jb_config *cfg, jb_image **out);
 void jb_image_free(jb_image *img);
+int jb_image_save(const jb_image *img, const char *path);
+/* prefixDictionary view of an image: number of termFreq entries and pd.size. */
+int jb_image_dict_info(const jb_image *img, uint64_t *nentries, int64_t *size);
 /* Look up a key as the device walk sees it: returns 1 if reachable, with freq and w. */
 int jb_image_lookup(const jb_image *img, const char *word, size_t len, int64_t *freq, double *w);
 /* nodes stored, hash capacity, pages, max key length in runes, size, -Log(size) */

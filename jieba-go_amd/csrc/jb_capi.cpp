@@ -246,8 +246,9 @@ static int read_file(const char* path, std::string* out) {
 
 extern "C" int jb_image_build(const jb_config* cfg, jb_image** out) {
     if (!cfg || !out) return fail(JB_EINVAL, "jb_image_build: null argument");
-    if (cfg->dict_kind != JB_DICT_TXT && cfg->dict_kind != JB_DICT_PREFIX)
-        return fail(JB_EINVAL, "unknown dict_kind %d", cfg->dict_kind);
+    const int kind = cfg->dict_kind;
+    if (kind != JB_DICT_TXT && kind != JB_DICT_PREFIX && kind != JB_DICT_GOB && kind != JB_DICT_IMAGE)
+        return fail(JB_EINVAL, "unknown dict_kind %d", kind);
     std::string dbuf, ebuf;
     const char* d = cfg->dict_buf;
     size_t dl = cfg->dict_len;
@@ -259,22 +260,68 @@ extern "C" int jb_image_build(const jb_config* cfg, jb_image** out) {
         d = dbuf.data();
         dl = dbuf.size();
     }
+    if (!d && dl) return fail(JB_EINVAL, "no dictionary given");
+    auto im = std::make_unique<jb_image>();
+    im->dict_kind = kind;
+    std::string err;
+    if (kind == JB_DICT_IMAGE) {
+        if ((rc = load_image(d ? d : "", dl, &im->dict, &im->emit, &im->img, &err))) return fail(rc, "%s", err.c_str());
+        if (cfg->size_override > 0 && cfg->size_override != im->dict.size) {
+            im->dict.size = cfg->size_override;
+            if ((rc = build_image(im->dict, im->emit, &im->img, &err))) return fail(rc, "%s", err.c_str());
+        }
+        *out = im.release();
+        return JB_OK;
+    }
     if (cfg->emit_path) {
         if ((rc = read_file(cfg->emit_path, &ebuf))) return rc;
         e = ebuf.data();
         el = ebuf.size();
     }
-    if (!d && dl) return fail(JB_EINVAL, "no dictionary given");
     if (!e) return fail(JB_EINVAL, "no emission table given (prob_emit.json)");
-    auto im = std::make_unique<jb_image>();
-    im->dict_kind = cfg->dict_kind;
-    std::string err;
-    if ((rc = parse_dictionary(d ? d : "", dl, cfg->dict_kind, &im->dict, &err))) return fail(rc, "%s", err.c_str());
+    if (kind == JB_DICT_GOB) {
+        // newJiebaPrefixDictionary (tokenizer.go:439-458): the gob map as stored, size hard-coded
+        if ((rc = parse_gob_dictionary(d ? d : "", dl, &im->dict, &err))) return fail(rc, "%s", err.c_str());
+        im->dict.size = JB_JIEBA_SIZE;
+    } else if ((rc = parse_dictionary(d ? d : "", dl, kind, &im->dict, &err))) {
+        return fail(rc, "%s", err.c_str());
+    }
     if (cfg->size_override > 0) im->dict.size = cfg->size_override;
     if ((rc = parse_emission(e, el, &im->emit, &err))) return fail(rc, "%s", err.c_str());
     if ((rc = build_image(im->dict, im->emit, &im->img, &err))) return fail(rc, "%s", err.c_str());
     if (im->img.maxlen > 255) return fail(JB_ELIMIT, "dictionary word of %u runes (max 255)", im->img.maxlen);
     *out = im.release();
+    return JB_OK;
+}
+
+static int write_file(const char* path, const std::string& data) {
+    // write to a temporary name and rename, so a reader never sees half an image
+    const std::string tmp = std::string(path) + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (!f) return fail(JB_EIO, "create %s: %s", tmp.c_str(), strerror(errno));
+    const bool ok = fwrite(data.data(), 1, data.size(), f) == data.size();
+    if (fclose(f) != 0 || !ok) {
+        remove(tmp.c_str());
+        return fail(JB_EIO, "write %s failed", tmp.c_str());
+    }
+    if (rename(tmp.c_str(), path) != 0) {
+        remove(tmp.c_str());
+        return fail(JB_EIO, "rename to %s: %s", path, strerror(errno));
+    }
+    return JB_OK;
+}
+
+extern "C" int jb_image_save(const jb_image* img, const char* path) {
+    if (!img || !path) return fail(JB_EINVAL, "jb_image_save: null argument");
+    std::string data;
+    save_image(img->dict, img->emit, img->img, &data);
+    return write_file(path, data);
+}
+
+extern "C" int jb_image_dict_info(const jb_image* img, uint64_t* nentries, int64_t* size) {
+    if (!img) return fail(JB_EINVAL, "jb_image_dict_info: null argument");
+    if (nentries) *nentries = img->dict.term_freq.size();
+    if (size) *size = img->dict.size;
     return JB_OK;
 }
 
@@ -889,6 +936,16 @@ extern "C" int jb_add_word(jb_ctx* ctx, const char* word, size_t len, int64_t fr
         if ((rc = upload_image(d.get(), ctx->im->img))) return rc;
     }
     return JB_OK;
+}
+
+extern "C" int jb_save(jb_ctx* ctx, const char* path) {
+    if (!ctx || !path) return fail(JB_EINVAL, "jb_save: null argument");
+    std::string data;
+    {
+        std::shared_lock<std::shared_mutex> rl(ctx->lock);
+        save_image(ctx->im->dict, ctx->im->emit, ctx->im->img, &data);
+    }
+    return write_file(path, data);
 }
 
 // ---------------------------------------------------------------------------

@@ -177,6 +177,126 @@ int parse_dictionary(const char* buf, size_t len, int kind, Dictionary* out, std
 }
 
 // ---------------------------------------------------------------------------
+// prefix_dictionary.gob: encoding/gob stream of one map[string]int
+// (newJiebaPrefixDictionary, tokenizer.go:439-458: decoder.Decode(&pd.termFreq)).
+// Restated from the encoding/gob wire format of Go 1.18 (go.mod:3):
+//   message  = uint(byte count) int(type id) payload
+//   id < 0   : definition of type -id, payload = wireType struct
+//   id > 0   : a value of type id; a non-struct value is preceded by the
+//              singleton field delta, which is 0
+//   uint     : < 0x80 one byte; else byte (256 - n) then n big-endian bytes
+//   int      : uint u; u & 1 ? ^(u >> 1) : u >> 1
+//   struct   : (uint field delta, field)* then delta 0
+//   wireType : field 3 (MapT) = mapType{CommonType{Name, Id}, Key, Elem}
+//   map      : uint count, then count x (key, elem)
+//   string   : uint byte length, bytes (not checked as UTF-8)
+// Predefined type ids: int = 2, string = 6.
+// ---------------------------------------------------------------------------
+namespace {
+struct GobReader {
+    const uint8_t* p;
+    size_t n, i = 0;
+    bool uint_(uint64_t* v) {
+        if (i >= n) return false;
+        const uint8_t b = p[i++];
+        if (b < 0x80) { *v = b; return true; }
+        const unsigned k = 256u - b;  // byte count
+        if (k > 8 || n - i < k) return false;
+        uint64_t x = 0;
+        for (unsigned j = 0; j < k; j++) x = (x << 8) | p[i++];
+        *v = x;
+        return true;
+    }
+    bool int_(int64_t* v) {
+        uint64_t u;
+        if (!uint_(&u)) return false;
+        *v = (u & 1) ? (int64_t)~(u >> 1) : (int64_t)(u >> 1);
+        return true;
+    }
+};
+
+constexpr int64_t kGobInt = 2, kGobString = 6;
+
+// Skip a CommonType struct {Name string; Id typeId}; returns the Id.
+bool gob_common_type(GobReader& r, int64_t* id) {
+    int field = -1;
+    for (;;) {
+        uint64_t d;
+        if (!r.uint_(&d)) return false;
+        if (d == 0) return true;
+        field += (int)d;
+        if (field == 0) {  // Name
+            uint64_t l;
+            if (!r.uint_(&l) || r.n - r.i < l) return false;
+            r.i += (size_t)l;
+        } else if (field == 1) {  // Id
+            if (!r.int_(id)) return false;
+        } else {
+            return false;
+        }
+    }
+}
+}  // namespace
+
+int parse_gob_dictionary(const char* buf, size_t len, Dictionary* out, std::string* err) {
+    out->term_freq.clear();
+    out->size = 0;
+    GobReader r{(const uint8_t*)buf, len};
+    std::unordered_map<int64_t, std::pair<int64_t, int64_t>> maps;  // id -> (key, elem)
+    for (;;) {
+        uint64_t mlen;
+        if (!r.uint_(&mlen) || mlen == 0 || r.n - r.i < mlen) {
+            *err = r.i >= r.n ? "gob: no map value in stream (EOF)" : "gob: truncated message";
+            return JB_EPARSE;
+        }
+        GobReader m{r.p + r.i, (size_t)mlen};
+        r.i += (size_t)mlen;
+        int64_t id;
+        if (!m.int_(&id)) { *err = "gob: bad type id"; return JB_EPARSE; }
+        if (id < 0) {
+            // wireType: only MapT (field 3) can describe map[string]int
+            uint64_t d;
+            if (!m.uint_(&d) || d != 4) { *err = "gob: type definition is not a map (expected map[string]int)"; return JB_EPARSE; }
+            int field = -1;
+            int64_t tid = 0, key = 0, elem = 0;
+            for (;;) {
+                if (!m.uint_(&d)) { *err = "gob: truncated mapType"; return JB_EPARSE; }
+                if (d == 0) break;
+                field += (int)d;
+                bool ok = false;
+                if (field == 0) ok = gob_common_type(m, &tid);
+                else if (field == 1) ok = m.int_(&key);
+                else if (field == 2) ok = m.int_(&elem);
+                if (!ok) { *err = "gob: bad mapType"; return JB_EPARSE; }
+            }
+            if (!m.uint_(&d) || d != 0) { *err = "gob: bad wireType end"; return JB_EPARSE; }
+            if (tid != -id) { *err = "gob: type id mismatch in definition"; return JB_EPARSE; }
+            maps[tid] = {key, elem};
+            continue;
+        }
+        auto it = maps.find(id);
+        if (it == maps.end() || it->second.first != kGobString || it->second.second != kGobInt) {
+            *err = "gob: value is not a map[string]int (type " + std::to_string(id) + ")";
+            return JB_EPARSE;
+        }
+        uint64_t d, cnt;
+        if (!m.uint_(&d) || d != 0) { *err = "gob: corrupted data: non-zero delta for singleton"; return JB_EPARSE; }
+        if (!m.uint_(&cnt) || cnt > m.n) { *err = "gob: bad map length"; return JB_EPARSE; }
+        out->term_freq.reserve((size_t)cnt);
+        for (uint64_t k = 0; k < cnt; k++) {
+            uint64_t l;
+            int64_t v;
+            if (!m.uint_(&l) || m.n - m.i < l) { *err = "gob: truncated map key"; return JB_EPARSE; }
+            std::string key((const char*)m.p + m.i, (size_t)l);
+            m.i += (size_t)l;
+            if (!m.int_(&v)) { *err = "gob: truncated map value"; return JB_EPARSE; }
+            out->term_freq[std::move(key)] = v;  // reflect.Value.SetMapIndex: a repeated key overwrites
+        }
+        return JB_OK;  // Decode reads exactly one value; later messages are not read
+    }
+}
+
+// ---------------------------------------------------------------------------
 // prob_emit.json: encoding/json into map[string]map[string]float64
 // ---------------------------------------------------------------------------
 namespace {
@@ -568,6 +688,151 @@ Lookup image_lookup(const Image& img, const uint32_t* runes, size_t n) {
     out.widx = jb_cell_widx(c);
     out.id = id;
     return out;
+}
+
+}  // namespace jb
+
+namespace jb {
+
+// ---------------------------------------------------------------------------
+// Serialized image (a fast-start cache, the role prefix_dictionary.gob plays
+// for the reference's map, tokenizer.go:439-458): the host dictionary and
+// emission maps that AddWord and suggestFreq need, plus the built device
+// arrays, so that opening skips parsing and build_image.  Little-endian,
+// versioned, checksummed; written and read only by this library.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr char kImgMagic[8] = {'J', 'B', 'I', 'M', 'A', 'G', 'E', '\0'};
+constexpr uint32_t kImgVersion = 1;
+
+uint64_t img_hash(const uint8_t* p, size_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        memcpy(&w, p + i, 8);
+        h = (h ^ w) * 0xff51afd7ed558ccdull;
+        h ^= h >> 32;
+    }
+    for (; i < n; i++) h = (h ^ p[i]) * 0x100000001b3ull;
+    return h ^ (h >> 29);
+}
+
+struct Out {
+    std::string* s;
+    template <class T> void pod(const T& v) { s->append((const char*)&v, sizeof v); }
+    template <class T> void vec(const std::vector<T>& v) {
+        pod((uint64_t)v.size());
+        s->append((const char*)v.data(), v.size() * sizeof(T));
+    }
+};
+
+struct In {
+    const uint8_t* p;
+    size_t n, i = 0;
+    template <class T> bool pod(T* v) {
+        if (n - i < sizeof(T)) return false;
+        memcpy(v, p + i, sizeof(T));
+        i += sizeof(T);
+        return true;
+    }
+    template <class T> bool vec(std::vector<T>* v, uint64_t max) {
+        uint64_t c;
+        if (!pod(&c) || c > max || (n - i) / sizeof(T) < c) return false;
+        v->resize((size_t)c);
+        memcpy(v->data(), p + i, (size_t)c * sizeof(T));
+        i += (size_t)c * sizeof(T);
+        return true;
+    }
+};
+}  // namespace
+
+void save_image(const Dictionary& d, const Emission& e, const Image& img, std::string* out) {
+    std::string body;
+    Out o{&body};
+    o.pod(d.size);
+    o.pod((uint64_t)d.term_freq.size());
+    for (const auto& kv : d.term_freq) {
+        o.pod((uint32_t)kv.first.size());
+        body.append(kv.first);
+        o.pod(kv.second);
+    }
+    for (int s = 0; s < 4; s++) {
+        o.pod((uint64_t)e.by_rune[s].size());
+        for (const auto& kv : e.by_rune[s]) {
+            o.pod(kv.first);
+            o.pod(kv.second);
+        }
+    }
+    o.vec(img.pagemap);
+    o.vec(img.emit);
+    o.vec(img.code);
+    o.vec(img.cells);
+    o.vec(img.wtab);
+    o.pod(img.npages); o.pod(img.nrows); o.pod(img.ncells); o.pod(img.ncodes); o.pod(img.maxlen);
+    o.pod(img.nnodes); o.pod(img.total); o.pod(img.w_absent); o.pod(img.size);
+    out->clear();
+    out->append(kImgMagic, 8);
+    Out h{out};
+    h.pod(kImgVersion);
+    h.pod((uint32_t)0);
+    h.pod((uint64_t)body.size());
+    h.pod(img_hash((const uint8_t*)body.data(), body.size()));
+    out->append(body);
+}
+
+int load_image(const char* buf, size_t len, Dictionary* d, Emission* e, Image* img, std::string* err) {
+    In h{(const uint8_t*)buf, len};
+    uint32_t ver = 0, pad = 0;
+    uint64_t blen = 0, hash = 0;
+    if (len < 8 || memcmp(buf, kImgMagic, 8) != 0) { *err = "not a jiebahip image (bad magic)"; return JB_EPARSE; }
+    h.i = 8;
+    if (!h.pod(&ver) || !h.pod(&pad) || !h.pod(&blen) || !h.pod(&hash)) { *err = "image: truncated header"; return JB_EPARSE; }
+    if (ver != kImgVersion) { *err = "image: version " + std::to_string(ver) + " (this library reads " +
+                              std::to_string(kImgVersion) + "); rebuild it"; return JB_EPARSE; }
+    if (len - h.i != blen) { *err = "image: truncated body"; return JB_EPARSE; }
+    const uint8_t* body = h.p + h.i;
+    if (img_hash(body, (size_t)blen) != hash) { *err = "image: checksum mismatch"; return JB_EPARSE; }
+    In b{body, (size_t)blen};
+    const char* bad = "image: corrupt body";
+    uint64_t n;
+    if (!b.pod(&d->size) || !b.pod(&n) || n > blen) { *err = bad; return JB_EPARSE; }
+    d->term_freq.clear();
+    d->term_freq.reserve((size_t)n);
+    for (uint64_t k = 0; k < n; k++) {
+        uint32_t l;
+        int64_t f;
+        if (!b.pod(&l) || b.n - b.i < l) { *err = bad; return JB_EPARSE; }
+        std::string key((const char*)b.p + b.i, l);
+        b.i += l;
+        if (!b.pod(&f)) { *err = bad; return JB_EPARSE; }
+        d->term_freq.emplace(std::move(key), f);
+    }
+    for (int s = 0; s < 4; s++) {
+        e->by_rune[s].clear();
+        if (!b.pod(&n) || n > blen) { *err = bad; return JB_EPARSE; }
+        for (uint64_t k = 0; k < n; k++) {
+            uint32_t r;
+            double v;
+            if (!b.pod(&r) || !b.pod(&v)) { *err = bad; return JB_EPARSE; }
+            e->by_rune[s][r] = v;
+        }
+    }
+    if (!b.vec(&img->pagemap, JB_NPAGES_MAX) || !b.vec(&img->emit, blen) || !b.vec(&img->code, blen) ||
+        !b.vec(&img->cells, blen) || !b.vec(&img->wtab, blen) || !b.pod(&img->npages) || !b.pod(&img->nrows) ||
+        !b.pod(&img->ncells) || !b.pod(&img->ncodes) || !b.pod(&img->maxlen) || !b.pod(&img->nnodes) ||
+        !b.pod(&img->total) || !b.pod(&img->w_absent) || !b.pod(&img->size) || b.i != b.n) {
+        *err = bad;
+        return JB_EPARSE;
+    }
+    // the arrays must be the sizes the kernels index
+    if (img->pagemap.size() != JB_NPAGES_MAX || img->code.size() != (size_t)img->npages * 256 ||
+        img->emit.size() != (size_t)img->npages * 256 * 4 || img->cells.size() != img->ncells ||
+        img->nrows != img->npages * 256 || img->wtab.empty() || img->wtab.size() > JB_MAX_WIDX) {
+        *err = "image: inconsistent array sizes";
+        return JB_EPARSE;
+    }
+    return JB_OK;
 }
 
 }  // namespace jb

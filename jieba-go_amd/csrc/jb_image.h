@@ -56,9 +56,16 @@ double go_log(double x);
 // (kind 0: newPrefixDictionaryFromFile, kind 1: buildPrefixDictionary).
 // Returns 0 or a negative JB_E* code; err receives a message.
 int parse_dictionary(const char* buf, size_t len, int kind, Dictionary* out, std::string* err);
+// prefix_dictionary.gob (tokenizer.go:439-458): a gob-encoded map[string]int;
+// size is left 0 (the caller applies the reference's hard-coded 60,101,967).
+int parse_gob_dictionary(const char* buf, size_t len, Dictionary* out, std::string* err);
 int parse_emission(const char* buf, size_t len, Emission* out, std::string* err);
 // Returns 0 or JB_ELIMIT (too many trie nodes / distinct weights for the packed layout).
 int build_image(const Dictionary& d, const Emission& e, Image* img, std::string* err);
+
+// Serialized image: dictionary + emission maps + device arrays (fast start).
+void save_image(const Dictionary& d, const Emission& e, const Image& img, std::string* out);
+int load_image(const char* buf, size_t len, Dictionary* d, Emission* e, Image* img, std::string* err);
 
 // Walk the image like the kernels do.
 Lookup image_lookup(const Image& img, const uint32_t* runes, size_t n);

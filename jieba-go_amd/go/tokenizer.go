@@ -15,6 +15,7 @@ package jiebahip
 import "C"
 
 import (
+	"errors"
 	"log"
 	"runtime"
 	"sync"
@@ -60,11 +61,27 @@ func NewTokenizer(dictionaryFile string) *Tokenizer {
 	return open(dictionaryFile, "prob_emit.json", C.JB_DICT_TXT, 0)
 }
 
-// NewJiebaTokenizer is the reference's default tokenizer (tokenizer.go:69).
-// The reference decodes prefix_dictionary.gob; this reads dict.txt with the
-// same semantics (prefix entries, last value wins, size 60,101,967).
+// NewJiebaTokenizer is the reference's default tokenizer (tokenizer.go:69):
+// it decodes prefix_dictionary.gob (tokenizer.go:439-458) with size 60,101,967.
 func NewJiebaTokenizer() *Tokenizer {
-	return open("dict.txt", "prob_emit.json", C.JB_DICT_PREFIX, JiebaSize)
+	return open("prefix_dictionary.gob", "prob_emit.json", C.JB_DICT_GOB, 0)
+}
+
+// NewTokenizerFromImage opens an image written by Save: no parsing, no trie build.
+func NewTokenizerFromImage(path string) *Tokenizer {
+	return open(path, "", C.JB_DICT_IMAGE, 0)
+}
+
+// Save writes the current dictionary (AddWord changes included) as an image.
+func (t *Tokenizer) Save(path string) error {
+	t.mu.RLock()
+	defer t.mu.RUnlock()
+	cp := C.CString(path)
+	defer C.free(unsafe.Pointer(cp))
+	if rc := C.jb_save(t.ctx, cp); rc != C.JB_OK {
+		return errors.New("jiebahip: " + lastError())
+	}
+	return nil
 }
 
 // Close releases the device context.

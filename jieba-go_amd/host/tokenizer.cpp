@@ -29,10 +29,19 @@ std::unique_ptr<Tokenizer> Tokenizer::NewTokenizer(const std::string& dictionary
 std::unique_ptr<Tokenizer> Tokenizer::NewJiebaTokenizer(int device) {
     jb_config cfg;
     std::memset(&cfg, 0, sizeof cfg);
-    cfg.dict_path = "dict.txt";
-    cfg.dict_kind = JB_DICT_PREFIX;
-    cfg.size_override = 60101967;
+    cfg.dict_path = "prefix_dictionary.gob";
+    cfg.dict_kind = JB_DICT_GOB;  // size 60,101,967 (tokenizer.go:454)
     cfg.emit_path = "prob_emit.json";
+    cfg.device = device;
+    cfg.ndevices = 1;
+    return Open(cfg);
+}
+
+std::unique_ptr<Tokenizer> Tokenizer::FromImage(const std::string& path, int device) {
+    jb_config cfg;
+    std::memset(&cfg, 0, sizeof cfg);
+    cfg.dict_path = path.c_str();
+    cfg.dict_kind = JB_DICT_IMAGE;
     cfg.device = device;
     cfg.ndevices = 1;
     return Open(cfg);
@@ -80,5 +89,7 @@ std::vector<std::vector<std::string>> Tokenizer::CutBatch(const std::vector<std:
 void Tokenizer::AddWord(const std::string& word, int freq) {
     check(jb_add_word(ctx_, word.data(), word.size(), freq));
 }
+
+void Tokenizer::Save(const std::string& path) { check(jb_save(ctx_, path.c_str())); }
 
 }  // namespace jiebago

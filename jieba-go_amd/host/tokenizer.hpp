@@ -28,11 +28,12 @@ public:
     // NewTokenizer(dictionaryFile) (tokenizer.go:61): dict.txt semantics, HMM from
     // "prob_emit.json" in the working directory (tokenizer.go:654).
     static std::unique_ptr<Tokenizer> NewTokenizer(const std::string& dictionaryFile, int device = 0);
-    // NewJiebaTokenizer() (tokenizer.go:69): prefix-dictionary semantics with
-    // size 60_101_967 (tokenizer.go:454).  The prefix map is rebuilt from
-    // "dict.txt" in the working directory (buildPrefixDictionary, tokenizer.go:340),
-    // which is what prefix_dictionary.gob caches.
+    // NewJiebaTokenizer() (tokenizer.go:69): decodes "prefix_dictionary.gob" from
+    // the working directory (newJiebaPrefixDictionary, tokenizer.go:439-458), size
+    // 60_101_967 (tokenizer.go:454).
     static std::unique_ptr<Tokenizer> NewJiebaTokenizer(int device = 0);
+    // A serialized image written by Save (no parsing or trie build at start).
+    static std::unique_ptr<Tokenizer> FromImage(const std::string& path, int device = 0);
     // Full control (paths, semantics, size override, devices).
     static std::unique_ptr<Tokenizer> Open(const jb_config& cfg);
 
@@ -50,6 +51,8 @@ public:
     std::vector<std::vector<std::string>> CutBatch(const std::vector<std::string>& docs, bool hmm);
     // AddWord (tokenizer.go:372) without the reference's self-deadlock.
     void AddWord(const std::string& word, int freq);
+    // Write the current image (AddWord changes included) for FromImage.
+    void Save(const std::string& path);
 
     jb_ctx* handle() { return ctx_; }
 

@@ -19,15 +19,16 @@ PKG_DIR = os.path.dirname(_HERE)
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libjiebahip.so")
 
 JB_OK, JB_EINVAL, JB_EIO, JB_EPARSE, JB_EDEVICE, JB_ENOMEM, JB_EPANIC, JB_ELIMIT = 0, -1, -2, -3, -4, -5, -6, -7
-JB_DICT_TXT, JB_DICT_PREFIX = 0, 1
+JB_DICT_TXT, JB_DICT_PREFIX, JB_DICT_GOB, JB_DICT_IMAGE = 0, 1, 2, 3
 JIEBA_SIZE = 60_101_967  # tokenizer.go:454
 
 # Every symbol include/jiebahip.h declares.
 EXPORTS = [
     "jb_open", "jb_close", "jb_last_error", "jb_cut", "jb_cut_batch", "jb_cut_batch_into", "jb_spans_free",
     "jb_cut_device",
-    "jb_add_word", "jb_dict_get", "jb_dict_size", "jb_profile_enable", "jb_profile_read", "jb_profile_reset",
-    "jb_image_build", "jb_image_free", "jb_image_lookup", "jb_image_stats", "jb_image_emit", "jb_go_log",
+    "jb_add_word", "jb_dict_get", "jb_dict_size", "jb_save", "jb_profile_enable", "jb_profile_read",
+    "jb_profile_reset", "jb_image_build", "jb_image_free", "jb_image_save", "jb_image_dict_info", "jb_image_lookup",
+    "jb_image_stats", "jb_image_emit", "jb_go_log",
 ]
 
 
@@ -89,6 +90,9 @@ def lib():
         L.jb_dict_get.argtypes = [vp, cp, C.c_size_t, C.POINTER(C.c_int64)]
         L.jb_dict_size.argtypes = [vp]
         L.jb_dict_size.restype = C.c_int64
+        L.jb_save.argtypes = [vp, cp]
+        L.jb_image_save.argtypes = [vp, cp]
+        L.jb_image_dict_info.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_int64)]
         L.jb_profile_enable.argtypes = [vp, C.c_int]
         L.jb_profile_reset.argtypes = [vp]
         L.jb_profile_read.argtypes = [vp, C.POINTER(cp), C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.c_int]
@@ -189,6 +193,14 @@ class Image:
     def emit(self, state, ch):
         return lib().jb_image_emit(self.h, "BMES".index(state), ord(ch))
 
+    def save(self, path):
+        _check(lib().jb_image_save(self.h, os.fsencode(path)))
+
+    def dict_info(self):
+        n, sz = C.c_uint64(), C.c_int64()
+        _check(lib().jb_image_dict_info(self.h, C.byref(n), C.byref(sz)))
+        return n.value, sz.value
+
 
 class Tokenizer:
     """jieba-go Tokenizer over the MI355X path."""
@@ -204,10 +216,22 @@ class Tokenizer:
         return cls(make_config(dict_path=dictionaryFile, emit_path=emit_path, kind=JB_DICT_TXT, device=device))
 
     @classmethod
-    def NewJiebaTokenizer(cls, dict_path="dict.txt", emit_path="prob_emit.json", device=0):
-        """tokenizer.go:69 — prefix-dictionary semantics, size 60,101,967."""
-        return cls(make_config(dict_path=dict_path, emit_path=emit_path, kind=JB_DICT_PREFIX,
-                               size_override=JIEBA_SIZE, device=device))
+    def NewJiebaTokenizer(cls, dict_path="prefix_dictionary.gob", emit_path="prob_emit.json", device=0):
+        """tokenizer.go:69 — decodes prefix_dictionary.gob (tokenizer.go:439-458), size 60,101,967.
+        A path ending in .txt is read with buildPrefixDictionary semantics instead (the map the gob holds)."""
+        if str(dict_path).endswith(".txt"):
+            return cls(make_config(dict_path=dict_path, emit_path=emit_path, kind=JB_DICT_PREFIX,
+                                   size_override=JIEBA_SIZE, device=device))
+        return cls(make_config(dict_path=dict_path, emit_path=emit_path, kind=JB_DICT_GOB, device=device))
+
+    @classmethod
+    def FromImage(cls, image_path, device=0, ndevices=1):
+        """Open a serialized image written by save() (no parsing, no trie build)."""
+        return cls(make_config(dict_path=image_path, kind=JB_DICT_IMAGE, device=device, ndevices=ndevices))
+
+    def save(self, path):
+        """Write the current image (including AddWord changes) for FromImage."""
+        _check(lib().jb_save(self.h, os.fsencode(path)))
 
     def close(self):
         if self.h:

@@ -171,6 +171,47 @@ def test_prefix_semantics_and_size_override(syn_small):
     tk.close()
 
 
+def test_gob_dictionary_and_saved_image(syn_small, tmp_path):
+    """NewJiebaTokenizer's gob loader (tokenizer.go:439-458) on a gob-encoded
+    prefix map, then the same tokenizer saved and reopened from its image, and
+    after AddWord: every form cuts as the oracle does on the same map."""
+    import gobenc
+    dp, ep, s = syn_small
+    m = {}
+    with open(dp, "rb") as f:
+        for line in f.read().splitlines():
+            w, c = line.split(b" ")[:2]
+            m[w] = int(c)
+            t = w.decode("utf-8")
+            for i in range(1, len(t)):
+                m.setdefault(t[:i].encode("utf-8"), 0)
+    gp = str(tmp_path / "prefix_dictionary.gob")
+    with open(gp, "wb") as f:
+        f.write(gobenc.encode_map(m.items()))
+    tk = J.Tokenizer.NewJiebaTokenizer(gp, ep)
+    o = O.Oracle(gobenc.map_to_dict_lines(m).decode(), open(ep, encoding="utf-8").read(), 0,
+                 size_override=J.JIEBA_SIZE)
+    buf, off, nr = s.corpus(synth.KIND_DOCS, 6, target_bytes=1 << 20)
+    for hmm in (0, 1):
+        _cmp_batch(tk, o, buf, off, hmm, "gob dict")
+    ip = str(tmp_path / "syn.jbimg")
+    tk.save(ip)
+    tk2 = J.Tokenizer.FromImage(ip)
+    for hmm in (0, 1):
+        _cmp_batch(tk2, o, buf, off, hmm, "image")
+    word = "天氣很好"
+    tk2.AddWord(word, 777)
+    o.add_term(word, 777)
+    tk2.save(ip)
+    tk3 = J.Tokenizer.FromImage(ip)
+    assert tk3.dict_get(word) == 777 and tk3.size == o.size
+    text = "今天天氣很好，" + bytes(np.asarray(buf)[:4000]).decode("utf-8", "ignore")
+    for hmm in (False, True):
+        assert tk3.Cut(text, hmm) == o.cut(text, hmm)
+    for t in (tk, tk2, tk3):
+        t.close()
+
+
 def test_add_word(mini_paths):
     tk = J.Tokenizer(J.make_config(dict_path=mini_paths[0], emit_path=mini_paths[1]))
     o = O.Oracle.from_files(*mini_paths, kind=0)

@@ -181,6 +181,20 @@ def test_real_data_kats(kats):
         assert o.viterbi(c["text"]) == c["want"]
     for s, v in kats["load_hmm_real_data"]["want"].items():
         assert o.emit(s, kats["load_hmm_real_data"]["char"]) == v
+    # NewJiebaTokenizer proper: the genuine prefix_dictionary.gob (sha256-checked),
+    # decoded by the test-side gob restatement and loaded with txt semantics
+    import hashlib
+
+    import gobenc
+    gp = os.path.join(d, "prefix_dictionary.gob")
+    if os.path.exists(gp):
+        data = open(gp, "rb").read()
+        assert hashlib.sha256(data).hexdigest() == kats["real_data_sha256"]["prefix_dictionary.gob"]
+        m = gobenc.decode_map(data)
+        og = O.Oracle(gobenc.map_to_dict_lines(m),
+                      open(os.path.join(d, "prob_emit.json"), encoding="utf-8").read(), 0, size_override=60_101_967)
+        for c in kats["cut_real_data"]["cases"]:
+            assert og.cut(c["text"], c["hmm"]) == c["want"], c["name"]
 
 
 def test_batch_equals_per_doc(syn_small):
