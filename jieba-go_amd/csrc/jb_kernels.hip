@@ -182,6 +182,20 @@ __device__ __forceinline__ bool han_cp(uint32_t r) {
 constexpr uint32_t kEdgeMaxL = 8;     // edge lengths a record holds
 constexpr uint32_t kEdgeIdxBits = 14;
 constexpr uint32_t kTileE = kTileBytes / 3 + 2;  // Han rune entries of a tile (>= 3 bytes each)
+constexpr uint32_t kLA = 8;                      // lookahead entries: runes of the last run past the tile end
+constexpr uint32_t kLABytes = 40;                // ... starting in the first 40 bytes after it
+constexpr uint32_t kTileEX = kTileE + kLA;
+constexpr uint32_t kMwStage = kTileBytes + 64u;  // staged text: bytes [t0-16, t0+4096+48)
+// k_mark_walk's LDS carve-up (bytes)
+constexpr uint32_t kMwOffE = kTileEX * 8u;                                // after s_c (u64 per entry)
+constexpr uint32_t kMwOffDb = kMwOffE + kTileEX * 4u;                     // u32 per 32 bytes of the tile, +2
+constexpr uint32_t kMwOffWl = kMwOffDb + (kTileBytes / 32u + 3u) * 4u;    // u16 per entry
+constexpr uint32_t kMwOffScan = (kMwOffWl + kTileE * 2u + 3u) & ~3u;      // u32 x 8
+constexpr uint32_t kMwLds = kMwOffScan + 8u * 4u;
+static_assert(kMwOffE >= kMwStage, "staged text must fit under the entry cells");
+static_assert(kTileBytes + kLABytes + 4u <= kMwStage - 16u && kTileBytes + kLABytes + 4u <= kTileBytes + 64u,
+              "lookahead bytes are staged and have document bits");
+static_assert(kMwLds + 16u <= 163840u / 8u, "k_mark_walk: 8 workgroups per CU");
 // entry: rune (bits 0-17; Han runes are < 0x40000) | tile offset (bits 18-29)
 constexpr uint32_t kEntCont = 0x40000000u;  // the next entry continues the run
 constexpr uint32_t kEntEdge = 0x80000000u;  // the run may continue past the tile
@@ -257,19 +271,28 @@ __device__ __forceinline__ bool dat_hit(uint64_t child, uint32_t id) { return jb
 // then walks that rune itself.  A rune that is absent or has count 0 gets the
 // single edge L = 1 (:468-471) with weight index 0 (Log(1) - Log(size)) or
 // that of Log(0) - Log(size) = -Inf.
-__global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ text, uint64_t nbytes,
+// At most 80 SGPRs (the rest spill to VGPR lanes) and 20.2 KB of LDS: 8
+// workgroups per CU instead of 6 (k_mark_walk is latency-bound: 0.695 -> 0.618 ms).
+#ifndef JB_MW_SGPR
+#define JB_MW_SGPR 80
+#endif
+#define JB_MW_ATTR __attribute__((amdgpu_num_sgpr(JB_MW_SGPR)))
+__global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                    const uint32_t* __restrict__ docbits, DevImage im,
                                                    uint32_t* __restrict__ lanemask, uint2* __restrict__ tile_cnt,
                                                    uint64_t* __restrict__ erec, uint32_t* __restrict__ tile4,
                                                    uint64_t* __restrict__ alnum16, uint32_t ablate,
                                                    uint64_t* __restrict__ dbg) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_t[kTileBytes + 32];  // bytes [t0-16, t0+4096+16)
-    __shared__ uint32_t s_db[kTileBytes / 32 + 2];                        // document starts of the tile
-    __shared__ uint32_t s_e[kTileE];
-    __shared__ uint64_t s_c[kTileE];  // the level-1 cell of each entry's rune, then the record of its walk
-    __shared__ uint32_t lds[8];
-    __shared__ uint16_t s_def[256];  // entries whose walk's run goes past the tile
-    __shared__ uint32_t s_ndef, s_nwl;
+    // LDS: 20.2 KB, so that 8 workgroups fit a CU (160 KB).  The staged text is
+    // dead once the entries are decoded; the entry cells/records reuse its bytes.
+    __shared__ __attribute__((aligned(16))) uint8_t s_raw[kMwLds];
+    uint64_t* const s_c = reinterpret_cast<uint64_t*>(s_raw);  // level-1 cell of each entry's rune, then its record
+    uint8_t* const s_t = s_raw;                                 // bytes [t0-16, t0+4096+48) (phase 1 and decode)
+    uint32_t* const s_e = reinterpret_cast<uint32_t*>(s_raw + kMwOffE);
+    uint32_t* const s_db = reinterpret_cast<uint32_t*>(s_raw + kMwOffDb);  // document starts of the tile
+    uint16_t* const s_wl = reinterpret_cast<uint16_t*>(s_raw + kMwOffWl);  // walk list
+    uint32_t* const lds = reinterpret_cast<uint32_t*>(s_raw + kMwOffScan);
+    __shared__ uint32_t s_nla, s_nwl;
 #if JB_STAMPS
     const bool stamps = (ablate & 0x100u) != 0;  // diagnostic per-wave phase clocks (make STAMPS=1)
 #else
@@ -278,19 +301,19 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
     uint64_t c0 = stamps ? __builtin_amdgcn_s_memtime() : 0, c1 = 0, c2 = 0, c3 = 0;
     uint32_t trips = 0;
     const uint64_t t0 = (uint64_t)blockIdx.x * kTileBytes;
-    for (uint32_t k = threadIdx.x; k < kTileBytes / 16 + 2; k += 256) {
+    for (uint32_t k = threadIdx.x; k < kMwStage / 16; k += 256) {
         const int64_t g = (int64_t)t0 - 16 + 16 * (int64_t)k;
         uint4 v = make_uint4(0, 0, 0, 0);
         if (g >= 0 && (uint64_t)g + 16 <= nbytes + 64) v = *reinterpret_cast<const uint4*>(text + g);
         reinterpret_cast<uint4*>(s_t)[k] = v;
     }
     const uint64_t lastw = (nbytes + 31) >> 5;
-    if (threadIdx.x < kTileBytes / 32 + 2) {
+    if (threadIdx.x < kTileBytes / 32 + 3) {
         const uint64_t wi = (t0 >> 5) + threadIdx.x;
         s_db[threadIdx.x] = wi < lastw ? docbits[wi] : 0u;
     }
     if (threadIdx.x == 0) {
-        s_ndef = 0;
+        s_nla = 0;
         s_nwl = 0;
     }
     const uint64_t p0 = t0 + threadIdx.x * 16u;
@@ -364,6 +387,7 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
         const uint32_t ne = __popc(hs);
         uint32_t kk[6], rr[6], cd[6];
         uint64_t cl[6];
+        uint32_t lastend = 0;  // window index past the lane's last Han rune
 #pragma unroll
         for (int i = 0; i < 6; i++) {
             kk[i] = 0u;
@@ -381,29 +405,69 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
                 rr[i] = r;
                 cd[i] = rune_code(im, r);
                 has4 |= r >= 0x10000u;
+                lastend = k + 4u + (r >= 0x10000u ? 4u : 3u);
             }
         }
 #pragma unroll
         for (int i = 0; i < 6; i++) cl[i] = ((uint32_t)i < ne && !(ablate & 2u)) ? im.cells[cd[i]] : 0ull;
 #pragma unroll
-        for (int i = 0; i < 6; i++)
-            if ((uint32_t)i < ne) {
-                s_c[o + i] = cl[i];
+        for (int i = 0; i < 6; i++)  // (s_e is not under the staged text)
+            if ((uint32_t)i < ne)
                 s_e[o + i] = cd[i] | ((rr[i] >= 0x10000u ? 1u : 0u) << 17) | ((threadIdx.x * 16u + kk[i]) << 18);
+        // Lookahead (the last lane, while the cell loads fly): when the tile's last
+        // Han rune ends at or past the tile end, the runes that continue its run
+        // (same document, Go-valid, Han) in the next kLABytes bytes become entries
+        // nent.. so that walks go on through them like any other (their records
+        // belong to the next tile and are not written here).  A walk that reaches
+        // past the last of them gets record 0: k_zh walks that rune itself.
+        uint32_t la_cd[kLA], nla = 0, la_w4 = 0;  // (only the last lane has any)
+        bool la_go = threadIdx.x == 255u && lastend >= 20u;
+        uint32_t q = kTileBytes + lastend - 20u;  // tile offset of the rune after it
+#pragma unroll
+        for (int i = 0; i < (int)kLA; i++) {
+            la_cd[i] = 0u;
+            if (la_go && q < kTileBytes + kLABytes) {
+                const uint64_t db = ((((uint64_t)s_db[(q >> 5) + 1u]) << 32) | s_db[q >> 5]) >> (q & 31u);
+                uint32_t lim = 1u + (uint32_t)__builtin_ctzll(((db >> 1) & 7ull) | 8ull);
+                const uint64_t gq = t0 + q;
+                if (gq + lim > nbytes) lim = gq < nbytes ? (uint32_t)(nbytes - gq) : 0u;
+                uint32_t w = 0;
+                const uint32_t r = (db & 1ull) ? 0u : han_rune(lds4(s_t, q + 16u), lim, &w);
+                if (r) {
+                    la_cd[i] = rune_code(im, r);
+                    la_w4 |= (w == 4u ? 1u : 0u) << i;
+                    nla = (uint32_t)i + 1u;
+                    q += w;
+                } else {
+                    la_go = false;
+                }
+            } else {
+                la_go = false;
             }
+        }
+        if (nla) {
+#pragma unroll
+            for (int i = 0; i < (int)kLA; i++)
+                if ((uint32_t)i < nla)  // the last one: the run may go on (all kLA decoded) or ends
+                    s_e[nent + i] = la_cd[i] | (((la_w4 >> i) & 1u) << 17) |
+                                    ((uint32_t)i + 1u < nla ? kEntCont : (la_go ? kEntEdge : 0u));
+            s_nla = nla;
+        }
+        __syncthreads();  // every lane has decoded from s_t: its bytes now take the cells
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+            if ((uint32_t)i < ne) s_c[o + i] = cl[i];
     }
     __syncthreads();
     // Run links, then level 1 of every entry: a rune that is absent, has count 0,
     // has no children or ends its Han run gets its record now (in its LDS cell,
-    // which only its own walk would read); the others go on the walk list (over
-    // the staged text, no longer needed) or, when the next rune is past the
-    // tile, straight to the deferred list.
-    uint16_t* s_wl = reinterpret_cast<uint16_t*>(s_t);
+    // which only its own walk would read); the others go on the walk list.
+    const uint32_t nla = s_nla;
     for (uint32_t i = threadIdx.x; i < nent; i += 256u) {
         const uint32_t e = s_e[i];
         const uint32_t nxt = ent_pos(e) + ent_w(e);
         uint32_t f = 0;
-        if (nxt >= kTileBytes) f = kEntEdge;
+        if (nxt >= kTileBytes) f = nla ? kEntCont : 0u;  // (the tile's last rune: the lookahead goes on)
         else if (i + 1u < nent && ent_pos(s_e[i + 1u]) == nxt && !((s_db[nxt >> 5] >> (nxt & 31u)) & 1u)) f = kEntCont;
         s_e[i] = e | f;
         const uint64_t c1 = s_c[i];
@@ -421,8 +485,7 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
             go = jb_cell_hc(c1) != 0u && f != 0u;
         }
         if (!go) s_c[i] = r1;
-        else if (f == kEntCont) s_wl[atomicAdd(&s_nwl, 1u)] = (uint16_t)i;
-        else s_def[atomicAdd(&s_ndef, 1u)] = (uint16_t)i;
+        else s_wl[atomicAdd(&s_nwl, 1u)] = (uint16_t)i;
     }
     const int any4 = __syncthreads_or(has4);  // (also the barrier after the run links)
     if (threadIdx.x == 0) tile4[blockIdx.x] = any4 ? 1u : 0u;  // k_zh: general rune stepping near this tile
@@ -449,8 +512,8 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
         s_c[js] = ovf ? 0ull : rc;
         act = false;
     };
-    auto defer = [&]() {  // the run goes on past the tile: walked again from global memory below
-        s_def[atomicAdd(&s_ndef, 1u)] = (uint16_t)js;
+    auto defer = [&]() {  // the run goes on past the lookahead: k_zh walks this rune itself
+        s_c[js] = 0ull;
         act = false;
     };
     // after a hit on node `id` (cell `cur`) whose rune is entry ecur: go on, defer or stop
@@ -501,46 +564,6 @@ __global__ __launch_bounds__(256) void k_mark_walk(const uint8_t* __restrict__ t
         if (!__any(act) && head >= hi) break;
     }
     if (stamps) c3 = __builtin_amdgcn_s_memtime();
-    __syncthreads();
-    // ---- walks whose Han run goes past the tile: from global memory (rare) ------------
-    const uint32_t ndef = s_ndef;
-    for (uint32_t i = threadIdx.x; i < ndef; i += 256u) {
-        const uint32_t ei = s_def[i];
-        const uint64_t p = t0 + ent_pos(s_e[ei]);
-        uint32_t wr;
-        const uint32_t r0 = han_rune(ld4(text, p), 4u, &wr);  // a Han rune of this tile (checked above)
-        uint32_t nid = rune_code(im, r0);
-        uint64_t c = im.cells[nid];
-        rc = 0ull;
-        nedge = 0u;
-        ovf = false;
-        if (jb_cell_fc(c) == JB_FC_POS) edge(1u, jb_cell_widx(c));
-        uint32_t n = 1u;
-        uint64_t pp = p + wr;
-        bool go = jb_cell_hc(c) != 0u;  // (present with children: the walk went on)
-        while (go) {
-            const uint64_t wi = pp >> 5;
-            const uint32_t sh = (uint32_t)pp & 31u;
-            const uint64_t v = ((((uint64_t)docbits[wi + 1]) << 32) | docbits[wi]) >> sh;
-            if (v & 1ull) break;  // next document
-            uint32_t lim = 1u + (uint32_t)__builtin_ctzll(((v >> 1) & 7ull) | 8ull);
-            if (pp + lim > nbytes) lim = pp < nbytes ? (uint32_t)(nbytes - pp) : 0u;
-            uint32_t w2;
-            const uint32_t r2 = han_rune(ld4(text, pp), lim, &w2);
-            if (!r2) break;  // end of the Han run
-            const uint32_t tt = dat_slot(im, c, r2);
-            const uint64_t ch = im.cells[tt];
-            if (!dat_hit(ch, nid)) break;  // (:475-478)
-            n++;
-            if (jb_cell_fc(ch) == JB_FC_POS) edge(n, jb_cell_widx(ch));
-            if (ovf) break;
-            nid = tt;
-            c = ch;
-            pp += w2;
-            go = jb_cell_hc(ch) != 0u;
-        }
-        s_c[ei] = ovf ? 0ull : rc;
-    }
     __syncthreads();
     // records out in entry (= text) order: consecutive lanes, mostly consecutive slots
     for (uint32_t i = threadIdx.x; i < nent; i += 256u) erec[(t0 + ent_pos(s_e[i])) / 3u] = s_c[i];
@@ -937,7 +960,11 @@ __device__ __forceinline__ void rec_weights(const DevImage& im, uint64_t rc, dou
         const bool has = m != 0u;
         m &= m - 1u;
         const uint32_t idx = (uint32_t)(rc >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u);
+#if JB_X_NOW  // diagnostic: no weight gathers (wrong results)
+        w[k] = (double)(has ? idx : 0u) * -0.001;
+#else
         w[k] = im.wtab[has ? idx : 0u];
+#endif
     }
 }
 // Fold a record's edges (L <= kZhRing, so best(i+L) is in the ring or is the
@@ -1036,9 +1063,14 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
     uint64_t lo = 0, hi = 0;  // the last pair: lo = the rune further back
     auto pair = [&](uint32_t k) {  // slots k, k+1 in one 16-byte load
         typedef uint64_t u64x2 __attribute__((ext_vector_type(2), aligned(8)));
+#if JB_X_NOREC  // diagnostic: no record loads (wrong results)
+        lo = 0x0000000000000103ull + k;
+        hi = 0x0000000000000101ull;
+#else
         const u64x2 x = *reinterpret_cast<const u64x2*>(erec + (int32_t)k);
         lo = x.x;
         hi = x.y;
+#endif
     };
     auto setup = [&]() {
         key0 = be / 3u;
@@ -1348,8 +1380,13 @@ __device__ void zh_chunk_main(const uint8_t* __restrict__ text, const DevImage& 
     wave_sync();
 }
 
+#ifdef JB_ZH_WAVES
+#define JB_ZH_ATTR __attribute__((amdgpu_waves_per_eu(JB_ZH_WAVES)))
+#else
+#define JB_ZH_ATTR
+#endif
 template <bool HMM>
-__global__ __launch_bounds__(256) void k_zh(const uint8_t* __restrict__ text, uint64_t nbytes,
+__global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict__ text, uint64_t nbytes,
                                             const uint32_t* __restrict__ blk, const uint2* __restrict__ gstart,
                                             const uint32_t* __restrict__ tile4,
                                             uint32_t* __restrict__ counters, DevImage im,

@@ -16,7 +16,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libjiebahip.so")
+# JB_LIB: another in-tree build of the same library (diagnostic variants, e.g. make STAMPS=1 OUT=var/stamps)
+LIB_PATH = os.environ.get("JB_LIB") or os.path.join(PKG_DIR, "lib", "libjiebahip.so")
 
 JB_OK, JB_EINVAL, JB_EIO, JB_EPARSE, JB_EDEVICE, JB_ENOMEM, JB_EPANIC, JB_ELIMIT = 0, -1, -2, -3, -4, -5, -6, -7
 JB_DICT_TXT, JB_DICT_PREFIX, JB_DICT_GOB, JB_DICT_IMAGE = 0, 1, 2, 3
