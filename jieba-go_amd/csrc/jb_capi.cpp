@@ -398,7 +398,7 @@ static int upload_image(Device* d, const Image& img) {
 
 static void free_work(Work* w) {
     dfree(w->docbits); dfree(w->tile_cnt); dfree(w->tile_off);
-    dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->blk); dfree(w->alnum16); dfree(w->erec); dfree(w->lanemask);
+    dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->supb); dfree(w->supt); dfree(w->blk); dfree(w->alnum16); dfree(w->erec); dfree(w->lanemask);
     dfree(w->gbl); dfree(w->gbest); dfree(w->gstart); dfree(w->tile4);
     dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters); dfree(w->dbg); dfree(w->dbg_walk);
     *w = Work{};
@@ -439,6 +439,8 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.tok_end, (nb + 4) * 4));
     HIPCHK(hipMalloc(&w.doc_tok, ((uint64_t)ndc + 2) * 8));
     HIPCHK(hipMalloc(&w.counters, 64 * 4));
+    HIPCHK(hipMalloc(&w.supb, (ntiles / 256 + 2) * sizeof(uint2)));
+    HIPCHK(hipMalloc(&w.supt, (nttiles / 256 + 2) * sizeof(uint2)));
     if (getenv("JB_ABLATE") && (atoi(getenv("JB_ABLATE")) & 0x100)) {
         HIPCHK(hipMalloc(&w.dbg, 65536 * 8 * 8));
         HIPCHK(hipMalloc(&w.dbg_walk, ntiles * 4 * 8 * 8));

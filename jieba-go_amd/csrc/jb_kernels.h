@@ -42,6 +42,8 @@ struct Work {
     uint32_t* sbits;       // 1 bit per byte: a token starts here
     uint32_t* ebits;       // 1 bit per byte: a token ends here (last byte)
     uint64_t bits_stride;  // words between docbits, sbits and ebits (one allocation)
+    uint2* supb;           // per 256 k_mark_walk tiles: (blocks, zh blocks) (k_sup)
+    uint2* supt;           // per 256 token tiles: (starts, ends) (k_sup)
     uint2* tile_cnt;       // per k_blocks tile (all, zh) counts, then exclusive offsets
     uint2* tile_off;
     uint2* ttile_cnt;      // per token tile (starts, ends)

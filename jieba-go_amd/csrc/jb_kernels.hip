@@ -7,8 +7,8 @@
 //                 tokenizer.go:21,154-155,165-210); then the trie walk (DAG
 //                 edges) of every Han rune of the tile, one walk per lane at a
 //                 time from an LDS entry list (buildDag, :462-497)
-//   k_scan2       tile counts -> offsets
-//   k_blocks_write  block list (start | zh<<31), zh ids, non-zh ids
+//   k_blocks_write  block list (start | zh<<31); its offsets from per-tile counts
+//                 and 256-tile sums that k_mark_walk adds up with atomics
 //   k_zh          one lane per Han block: backward max-prob DP over those edges +
 //                 forward path + BMES Viterbi on singleton runs
 //                                               (cutZh/cutDAG/buildDag/calcDagProba/
@@ -16,7 +16,7 @@
 //                                                tokenizer.go:221-285,462-578,668-756)
 //   k_nonzh       one lane per non-Han block: alnum runs, single runes, spaces
 //                 dropped, no-alnum blocks dropped (cutNonZh, tokenizer.go:289-310)
-//   k_tok<0>/scan/k_tok<1>  token start/end bitmaps -> (start, end) spans
+//   k_tok<0>/k_tok<1>  token start/end bitmaps -> counts (+ 256-tile sums) -> (start, end) spans
 //   k_doc_tok     per document first token (Cut per document)
 //
 // Output format on the device: two bitmaps, 1 bit per input byte each (token
@@ -163,6 +163,62 @@ __device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t* lds, ui
     __syncthreads();
     *total = tot;
     return base + x - v;
+}
+
+// Exclusive prefix of tile t's (x, y) counts, by a 256-thread workgroup: the
+// 256-tile sums (k_sup) before t's group of 256, plus the counts of the tiles
+// before t in its own group.  The loads are issued first (pf_load) and summed
+// later (pf_sum), so their latency hides under the caller's own loads.
+// Replaces a single-workgroup scan launch.
+struct PrefixLoads {
+    uint32_t x, y;
+};
+__device__ __forceinline__ PrefixLoads pf_load(const uint2* __restrict__ cnt, const uint2* __restrict__ sup,
+                                               uint32_t t) {
+    PrefixLoads p{0u, 0u};
+    const uint32_t sn = t >> 8, r = t & 255u;
+    for (uint32_t i = threadIdx.x; i < sn; i += 256u) {
+        const uint2 v = sup[i];
+        p.x += v.x;
+        p.y += v.y;
+    }
+    if (threadIdx.x < r) {
+        const uint2 c = cnt[(t & ~255u) + threadIdx.x];
+        p.x += c.x;
+        p.y += c.y;
+    }
+    return p;
+}
+__device__ uint2 pf_sum(PrefixLoads p, uint32_t* lds) {
+    uint32_t x = p.x, y = p.y;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        x += (uint32_t)__shfl_xor((int)x, d, 64);
+        y += (uint32_t)__shfl_xor((int)y, d, 64);
+    }
+    const uint32_t wid = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 0) {
+        lds[wid] = x;
+        lds[4u + wid] = y;
+    }
+    __syncthreads();
+    const uint2 out = make_uint2(lds[0] + lds[1] + lds[2] + lds[3], lds[4] + lds[5] + lds[6] + lds[7]);
+    __syncthreads();
+    return out;
+}
+
+// k_sup: the (x, y) sums of each group of 256 consecutive tile counts.
+__global__ __launch_bounds__(256) void k_sup(const uint2* __restrict__ cnt, uint32_t n, uint2* __restrict__ sup) {
+    __shared__ uint32_t lds[8];
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    PrefixLoads p{0u, 0u};
+    if (i < n) {
+        const uint2 c = cnt[i];
+        p.x = c.x;
+        p.y = c.y;
+    }
+    const uint2 s = pf_sum(p, lds);
+    if (threadIdx.x == 0) sup[blockIdx.x] = s;
 }
 
 // \p{Han} (unicode.Han, Unicode 13) with the common ranges first: the two
@@ -582,15 +638,24 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
 // The thread whose 16 bytes begin a k_zh group (g * kZhGroupBytes) also writes
 // gstart[g] = (blocks, zh blocks) that start before it.
 __global__ __launch_bounds__(256) void k_blocks_write(const uint32_t* __restrict__ lanemask,
-                                                      const uint2* __restrict__ tile_off, uint32_t* __restrict__ blk,
-                                                      uint2* __restrict__ gstart) {
+                                                      const uint2* __restrict__ tile_cnt,
+                                                      const uint2* __restrict__ supb, uint32_t* __restrict__ blk,
+                                                      uint2* __restrict__ gstart, uint32_t* __restrict__ counters,
+                                                      uint32_t nbytes) {
     __shared__ uint32_t lds[8];
+    const PrefixLoads pl = pf_load(tile_cnt, supb, blockIdx.x);
     uint32_t m = lanemask[blockIdx.x * 256u + threadIdx.x];
     const uint32_t bmask = m & 0xFFFFu, zmask = m >> 16;
     uint32_t tot;
     const uint32_t ex = block_scan_u32(__popc(bmask) | (__popc(zmask) << 16), lds, &tot);
     const uint32_t p0 = (blockIdx.x * 256u + threadIdx.x) * 16u;
-    const uint2 to = tile_off[blockIdx.x];
+    const uint2 to = pf_sum(pl, lds);
+    if (blockIdx.x == gridDim.x - 1u && threadIdx.x == 0) {  // totals and the end sentinel
+        const uint32_t na = to.x + (tot & 0xFFFFu), nz = to.y + (tot >> 16);
+        counters[CNT_NBLK] = na;
+        counters[CNT_NZH] = nz;
+        blk[na] = nbytes;
+    }
     if (p0 % kZhGroupBytes == 0u) gstart[p0 / kZhGroupBytes] = make_uint2(to.x + (ex & 0xFFFFu), to.y + (ex >> 16));
     if (!bmask) return;
     uint32_t ga = to.x + (ex & 0xFFFFu);  // global block rank
@@ -1595,35 +1660,58 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
 // ---------------------------------------------------------------------------
 // k_nonzh: one lane per non-Han block (cutNonZh, tokenizer.go:289-310)
 // ---------------------------------------------------------------------------
-// cutNonZh for one block [bs, be) (tokenizer.go:289-310)
-__device__ __forceinline__ void nonzh_block(const uint8_t* __restrict__ text, uint32_t bs, uint32_t be, Emitter& em) {
+// cutNonZh for one block [bs, be) (tokenizer.go:289-310).  The block's bytes
+// come in 16-byte loads issued together (a byte-by-byte walk over global
+// memory made every byte a dependent round trip); the tokenizing pass reads
+// them from the lane's 80-byte LDS window.
+__device__ __forceinline__ uint32_t nz_keep(uint32_t base, uint32_t bs, uint32_t be) {  // bytes in [bs, be)
+    const uint32_t lo = bs > base ? min(bs - base, 4u) : 0u, hi = be > base ? min(be - base, 4u) : 0u;
+    if (hi <= lo) return 0u;
+    return (uint32_t)(((1ull << (8u * hi)) - 1ull) & ~((1ull << (8u * lo)) - 1ull));
+}
+__device__ void nonzh_block(const uint8_t* __restrict__ text, uint32_t bs, uint32_t be, Emitter& em, uint8_t* buf) {
     bool has = false;  // alnum.FindAllIndex found nothing -> no tokens (:290-293)
-    for (uint32_t p = bs; p < be && !has; p += 4) {
-        const uint32_t x = ld4(text, p);
-        const uint32_t nb = min(4u, be - p);
-        for (uint32_t k = 0; k < nb; k++) has |= jb_is_alnum((x >> (8 * k)) & 0xFFu);
+    for (uint32_t a = bs & ~15u; a < be && !has; a += 64u) {
+        uint4 c[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            c[k] = (a + 16u * k < be) ? *reinterpret_cast<const uint4*>(text + a + 16u * k) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t b = a + 16u * k;
+            has |= jb_any_alnum4(c[k].x & nz_keep(b, bs, be)) || jb_any_alnum4(c[k].y & nz_keep(b + 4u, bs, be)) ||
+                   jb_any_alnum4(c[k].z & nz_keep(b + 8u, bs, be)) || jb_any_alnum4(c[k].w & nz_keep(b + 12u, bs, be));
+        }
     }
     if (!has) return;
     uint32_t p = bs, run = 0;
     bool in_run = false;
     while (p < be) {
-        const uint32_t x = ld4(text, p);
-        if (jb_is_alnum(x & 0xFFu)) {  // alnum runs are kept whole
-            if (!in_run) {
-                in_run = true;
-                run = p;
+        const uint32_t a = p & ~15u;
+#pragma unroll
+        for (int k = 0; k < 5; k++)  // bytes up to be + 3 (decode reads 4; padding follows the text)
+            if (a + 16u * k < be + 4u)
+                reinterpret_cast<uint4*>(buf)[k] = *reinterpret_cast<const uint4*>(text + a + 16u * k);
+        const uint32_t pe = min(be, a + 64u);
+        while (p < pe) {
+            const uint32_t x = lds4(buf, p - a);
+            if (jb_is_alnum(x & 0xFFu)) {  // alnum runs are kept whole
+                if (!in_run) {
+                    in_run = true;
+                    run = p;
+                }
+                p++;
+                continue;
             }
-            p++;
-            continue;
+            if (in_run) {
+                em.token(run, p);
+                in_run = false;
+            }
+            uint32_t r;
+            const uint32_t w = jb_decode(x, min(4u, be - p), &r);
+            if (!jb_is_space(r)) em.token(p, p + w);  // one token per rune; spaces dropped
+            p += w;
         }
-        if (in_run) {
-            em.token(run, p);
-            in_run = false;
-        }
-        uint32_t r;
-        const uint32_t w = jb_decode(x, min(4u, be - p), &r);
-        if (!jb_is_space(r)) em.token(p, p + w);  // one token per rune; spaces dropped
-        p += w;
     }
     if (in_run) em.token(run, be);
 }
@@ -1636,6 +1724,7 @@ __global__ __launch_bounds__(256) void k_nonzh(const uint8_t* __restrict__ text,
                                                const uint64_t* __restrict__ alnum16,
                                                const uint32_t* __restrict__ counters, uint32_t* __restrict__ sbits,
                                                uint32_t* __restrict__ ebits) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[256][80];
     const uint32_t nblk = counters[CNT_NBLK];
     Emitter em(sbits, ebits);
     for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c * kNzPer < nblk; c += gridDim.x * blockDim.x) {
@@ -1670,7 +1759,7 @@ __global__ __launch_bounds__(256) void k_nonzh(const uint8_t* __restrict__ text,
                 if (maybe || l > llast) break;
                 w = alnum16[l >> 6];  // a block over more than one 1 KiB word (rare)
             }
-            if (maybe) nonzh_block(text, bs, be, em);
+            if (maybe) nonzh_block(text, bs, be, em, s_win[threadIdx.x]);
         }
     }
     em.flush();
@@ -1682,13 +1771,15 @@ __global__ __launch_bounds__(256) void k_nonzh(const uint8_t* __restrict__ text,
 template <bool WRITE>
 __global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits, const uint32_t* __restrict__ ebits,
                                              uint64_t nwords, uint2* __restrict__ tile_cnt,
-                                             const uint2* __restrict__ tile_off, uint32_t* __restrict__ tok_start,
-                                             uint32_t* __restrict__ tok_end) {
+                                             const uint2* __restrict__ supt, uint32_t* __restrict__ counters,
+                                             uint32_t* __restrict__ tok_start, uint32_t* __restrict__ tok_end) {
     constexpr uint32_t W = kTokTileWords / 256;  // bitmap words per lane
     constexpr uint32_t kCap = 3072;              // tokens per tile staged in LDS
     __shared__ uint32_t lds[8];
     __shared__ uint32_t s_s[WRITE ? kCap : 1], s_e[WRITE ? kCap : 1];
     const uint64_t w0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * W;
+    PrefixLoads pl{0u, 0u};
+    if (WRITE) pl = pf_load(tile_cnt, supt, blockIdx.x);
     uint32_t s[W], e[W];
     if (w0 + W <= nwords) {
         const uint2 a = *reinterpret_cast<const uint2*>(sbits + w0);
@@ -1715,7 +1806,12 @@ __global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits,
         if (threadIdx.x == 0) tile_cnt[blockIdx.x] = make_uint2(ts, te);
         return;
     }
-    const uint2 to = tile_off[blockIdx.x];
+    const uint2 to = pf_sum(pl, lds);
+    if (blockIdx.x == gridDim.x - 1u && threadIdx.x == 0) {  // token totals
+        counters[CNT_NTOK] = to.x + ts;
+        counters[CNT_NTOKE] = to.y + te;
+        *reinterpret_cast<uint64_t*>(counters + CNT_NWORDS) = to.x + ts;
+    }
     // spans go to LDS in tile order, then out in one coalesced pass (a lane's own
     // tokens are ~60 bytes apart in the output: direct stores touch a line each)
     const bool staged = ts <= kCap && te <= kCap;
@@ -1801,7 +1897,6 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         if ((e = hipMemsetAsync(w.sbits, 0, (nwords + 2) * 4, stream))) return e;
         if ((e = hipMemsetAsync(w.ebits, 0, (nwords + 2) * 4, stream))) return e;
     }
-    uint64_t* ntok64 = reinterpret_cast<uint64_t*>(w.counters + CNT_NWORDS);
     if (nbytes == 0) {
         if ((e = hipMemsetAsync(w.doc_tok, 0, (ndocs + 1) * sizeof(uint64_t), stream))) return e;
         return hipSuccess;
@@ -1810,15 +1905,12 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         JB_TIMED(K_DOCBITS, hipLaunchKernelGGL(k_docbits, dim3((ndocs + 255) / 256), dim3(256), 0, stream,
                                                d_doc_off, ndocs, nbytes, w.docbits));
     JB_TIMED(K_MARK_WALK, hipLaunchKernelGGL(k_mark_walk, dim3(ntiles), dim3(256), 0, stream, d_text, nbytes,
-                                             w.docbits, im, w.lanemask, w.tile_cnt, w.erec + kErecPad, w.tile4,
-                                             w.alnum16,
-                                             g_ablate,
-                                             w.dbg_walk));
-    JB_TIMED(K_SCAN_BLOCKS, hipLaunchKernelGGL(k_scan2, dim3(1), dim3(1024), 0, stream, w.tile_cnt, ntiles,
-                                               w.tile_off, w.counters + CNT_NBLK, nullptr, w.blk,
-                                               (uint32_t)nbytes));
+                                             w.docbits, im, w.lanemask, w.tile_cnt, w.erec + kErecPad,
+                                             w.tile4, w.alnum16, g_ablate, w.dbg_walk));
+    JB_TIMED(K_SCAN_BLOCKS, hipLaunchKernelGGL(k_sup, dim3((ntiles + 255) / 256), dim3(256), 0, stream, w.tile_cnt,
+                                               ntiles, w.supb));
     JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL(k_blocks_write, dim3(ntiles), dim3(256), 0, stream, w.lanemask,
-                                                w.tile_off, w.blk, w.gstart));
+                                                w.tile_cnt, w.supb, w.blk, w.gstart, w.counters, (uint32_t)nbytes));
     if (hmm)
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
                                           w.gstart, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
@@ -1830,11 +1922,11 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3(grid_nz), dim3(256), 0, stream, d_text, w.blk, w.alnum16,
                                          w.counters, w.sbits, w.ebits));
     JB_TIMED(K_TOK_COUNT, hipLaunchKernelGGL((k_tok<false>), dim3(nttiles), dim3(256), 0, stream, w.sbits, w.ebits,
-                                             nwords, w.ttile_cnt, nullptr, nullptr, nullptr));
-    JB_TIMED(K_SCAN_TOK, hipLaunchKernelGGL(k_scan2, dim3(1), dim3(1024), 0, stream, w.ttile_cnt, nttiles,
-                                            w.ttile_off, w.counters + CNT_NTOK, ntok64, nullptr, 0u));
+                                             nwords, w.ttile_cnt, w.supt, w.counters, nullptr, nullptr));
+    JB_TIMED(K_SCAN_TOK, hipLaunchKernelGGL(k_sup, dim3((nttiles + 255) / 256), dim3(256), 0, stream, w.ttile_cnt,
+                                            nttiles, w.supt));
     JB_TIMED(K_TOK_WRITE, hipLaunchKernelGGL((k_tok<true>), dim3(nttiles), dim3(256), 0, stream, w.sbits, w.ebits,
-                                             nwords, nullptr, w.ttile_off, w.tok_start, w.tok_end));
+                                             nwords, w.ttile_cnt, w.supt, w.counters, w.tok_start, w.tok_end));
     JB_TIMED(K_DOC_TOK, hipLaunchKernelGGL(k_doc_tok, dim3((ndocs + 1 + 255) / 256), dim3(256), 0, stream,
                                            d_doc_off, ndocs, w.tok_start, w.counters, w.doc_tok));
     return hipGetLastError();
