@@ -496,10 +496,13 @@ static int ensure_span_staging(Device* d, uint64_t ntok) {
 
 static uint32_t grid_zh_override = 0;
 
+#ifndef JB_NZ_PER_CU
+#define JB_NZ_PER_CU 8  // k_nonzh workgroups per CU (persistent grid; 4: 0.075 ms, 8: 0.058)
+#endif
 static int launch(jb_ctx* ctx, Device* d, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off,
                   uint32_t ndocs, bool hmm, hipStream_t s) {
     const uint32_t grid_zh = d->ncu * std::max(1u, zh_blocks_per_cu(hmm));
-    const uint32_t grid_nz = d->ncu * std::max(1u, std::min(4u, nonzh_blocks_per_cu()));
+    const uint32_t grid_nz = d->ncu * std::max(1u, std::min((uint32_t)JB_NZ_PER_CU, nonzh_blocks_per_cu()));
     static const bool dbg = getenv("JB_DEBUG") != nullptr;
     if (const char* a = getenv("JB_ABLATE")) g_ablate = (uint32_t)atoi(a);
     if (const char* gz = getenv("JB_GRID_ZH")) grid_zh_override = (uint32_t)atoi(gz);

@@ -637,35 +637,45 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
 // k_blocks_write: the lane masks -> block list (start | zh<<31).
 // The thread whose 16 bytes begin a k_zh group (g * kZhGroupBytes) also writes
 // gstart[g] = (blocks, zh blocks) that start before it.
+constexpr uint32_t kBwTiles = 4;  // k_blocks_write: tiles per workgroup
 __global__ __launch_bounds__(256) void k_blocks_write(const uint32_t* __restrict__ lanemask,
                                                       const uint2* __restrict__ tile_cnt,
                                                       const uint2* __restrict__ supb, uint32_t* __restrict__ blk,
                                                       uint2* __restrict__ gstart, uint32_t* __restrict__ counters,
-                                                      uint32_t nbytes) {
+                                                      uint32_t nbytes, uint32_t ntiles) {
     __shared__ uint32_t lds[8];
-    const PrefixLoads pl = pf_load(tile_cnt, supb, blockIdx.x);
-    uint32_t m = lanemask[blockIdx.x * 256u + threadIdx.x];
-    const uint32_t bmask = m & 0xFFFFu, zmask = m >> 16;
-    uint32_t tot;
-    const uint32_t ex = block_scan_u32(__popc(bmask) | (__popc(zmask) << 16), lds, &tot);
-    const uint32_t p0 = (blockIdx.x * 256u + threadIdx.x) * 16u;
-    const uint2 to = pf_sum(pl, lds);
-    if (blockIdx.x == gridDim.x - 1u && threadIdx.x == 0) {  // totals and the end sentinel
-        const uint32_t na = to.x + (tot & 0xFFFFu), nz = to.y + (tot >> 16);
-        counters[CNT_NBLK] = na;
-        counters[CNT_NZH] = nz;
-        blk[na] = nbytes;
+    const uint32_t tb = blockIdx.x * kBwTiles;
+    const PrefixLoads pl = pf_load(tile_cnt, supb, tb);
+    uint32_t mm[kBwTiles];
+#pragma unroll
+    for (uint32_t k = 0; k < kBwTiles; k++) mm[k] = tb + k < ntiles ? lanemask[(tb + k) * 256u + threadIdx.x] : 0u;
+    uint2 to = pf_sum(pl, lds);  // blocks (all, zh) before tile tb
+#pragma unroll
+    for (uint32_t k = 0; k < kBwTiles; k++) {
+        const uint32_t t = tb + k;
+        if (t >= ntiles) break;
+        const uint32_t bmask = mm[k] & 0xFFFFu, zmask = mm[k] >> 16;
+        uint32_t tot;
+        const uint32_t ex = block_scan_u32(__popc(bmask) | (__popc(zmask) << 16), lds, &tot);
+        const uint32_t p0 = (t * 256u + threadIdx.x) * 16u;
+        if (p0 % kZhGroupBytes == 0u)
+            gstart[p0 / kZhGroupBytes] = make_uint2(to.x + (ex & 0xFFFFu), to.y + (ex >> 16));
+        uint32_t ga = to.x + (ex & 0xFFFFu);  // global block rank
+        uint32_t b = bmask;
+        while (b) {
+            const uint32_t kk = __builtin_ctz(b);
+            b &= b - 1u;
+            const bool h = (zmask >> kk) & 1u;
+            blk[ga] = (p0 + kk) | (h ? 0x80000000u : 0u);
+            ga++;
+        }
+        to.x += tot & 0xFFFFu;
+        to.y += tot >> 16;
     }
-    if (p0 % kZhGroupBytes == 0u) gstart[p0 / kZhGroupBytes] = make_uint2(to.x + (ex & 0xFFFFu), to.y + (ex >> 16));
-    if (!bmask) return;
-    uint32_t ga = to.x + (ex & 0xFFFFu);  // global block rank
-    uint32_t b = bmask;
-    while (b) {
-        const uint32_t k = __builtin_ctz(b);
-        b &= b - 1u;
-        const bool h = (zmask >> k) & 1u;
-        blk[ga] = (p0 + k) | (h ? 0x80000000u : 0u);
-        ga++;
+    if (blockIdx.x == gridDim.x - 1u && threadIdx.x == 0) {  // totals and the end sentinel
+        counters[CNT_NBLK] = to.x;
+        counters[CNT_NZH] = to.y;
+        blk[to.x] = nbytes;
     }
 }
 
@@ -1719,7 +1729,10 @@ __device__ void nonzh_block(const uint8_t* __restrict__ text, uint32_t bs, uint3
 // One thread per 8 consecutive entries of the block list: the entries and the
 // lane bits under each non-Han block load in one round, and only blocks with a
 // [0-9A-Za-z] byte near them are read (the rest have no tokens, :290-293).
-constexpr uint32_t kNzPer = 8;
+#ifndef JB_NZ_PER
+#define JB_NZ_PER 8
+#endif
+constexpr uint32_t kNzPer = JB_NZ_PER;
 __global__ __launch_bounds__(256) void k_nonzh(const uint8_t* __restrict__ text, const uint32_t* __restrict__ blk,
                                                const uint64_t* __restrict__ alnum16,
                                                const uint32_t* __restrict__ counters, uint32_t* __restrict__ sbits,
@@ -1909,8 +1922,9 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                              w.tile4, w.alnum16, g_ablate, w.dbg_walk));
     JB_TIMED(K_SCAN_BLOCKS, hipLaunchKernelGGL(k_sup, dim3((ntiles + 255) / 256), dim3(256), 0, stream, w.tile_cnt,
                                                ntiles, w.supb));
-    JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL(k_blocks_write, dim3(ntiles), dim3(256), 0, stream, w.lanemask,
-                                                w.tile_cnt, w.supb, w.blk, w.gstart, w.counters, (uint32_t)nbytes));
+    JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL(k_blocks_write, dim3((ntiles + kBwTiles - 1) / kBwTiles), dim3(256), 0,
+                                                stream, w.lanemask, w.tile_cnt, w.supb, w.blk, w.gstart, w.counters,
+                                                (uint32_t)nbytes, ntiles));
     if (hmm)
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
                                           w.gstart, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
