@@ -570,15 +570,16 @@ static int launch(jb_ctx* ctx, Device* d, const uint8_t* d_text, uint64_t nbytes
         std::vector<uint64_t> sw(nww * 8);
         HIPCHK(hipMemcpyAsync(sw.data(), d->w.dbg_walk, sw.size() * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        double b[5] = {0, 0, 0, 0, 0}, m = 0;
+        double b[8] = {0, 0, 0, 0, 0, 0, 0, 0}, m = 0;
         for (uint64_t i = 0; i < nww; i++)
             if (sw[i * 8 + 5] == 1) {
-                for (int k = 0; k < 5; k++) b[k] += (double)sw[i * 8 + k];
+                for (int k = 0; k < 8; k++) b[k] += (double)sw[i * 8 + k];
                 m++;
             }
         if (m == 0) m = 1;
-        fprintf(stderr, "[jb] k_mark_walk clocks/wave: mark %.0f entries %.0f walk %.0f deferred %.0f; trips/wave %.2f\n",
-                b[0] / m, b[1] / m, b[2] / m, b[3] / m, b[4] / m);
+        fprintf(stderr, "[jb] k_mark_walk clocks/wave: mark %.0f (staging %.0f) entries %.0f (loads %.0f) walk %.0f "
+                        "tail %.0f; trips/wave %.2f\n",
+                b[0] / m, b[6] / m, b[1] / m, b[7] / m, b[2] / m, b[3] / m, b[4] / m);
     }
     return JB_OK;
 }

@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
 #else
     const bool stamps = false;
 #endif
-    uint64_t c0 = stamps ? __builtin_amdgcn_s_memtime() : 0, c1 = 0, c2 = 0, c3 = 0;
+    uint64_t c0 = stamps ? __builtin_amdgcn_s_memtime() : 0, c1 = 0, c2 = 0, c3 = 0, c0b = 0, c1b = 0;
     uint32_t trips = 0;
     const uint64_t t0 = (uint64_t)blockIdx.x * kTileBytes;
     for (uint32_t k = threadIdx.x; k < kMwStage / 16; k += 256) {
@@ -393,6 +393,7 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         }
     }
     __syncthreads();
+    if (stamps) c0b = __builtin_amdgcn_s_memtime();  // (text staged)
     const uint8_t* win = s_t + 12 + threadIdx.x * 16u;  // window index 0
     {  // some [0-9A-Za-z] byte in the lane's 16 bytes (k_nonzh skips blocks without one; padding
        // bytes past the batch can only add false positives)
@@ -510,6 +511,7 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
             s_nla = nla;
         }
         __syncthreads();  // every lane has decoded from s_t: its bytes now take the cells
+        if (stamps) c1b = __builtin_amdgcn_s_memtime();  // (codes, cells and lookahead in)
 #pragma unroll
         for (int i = 0; i < 6; i++)
             if ((uint32_t)i < ne) s_c[o + i] = cl[i];
@@ -631,6 +633,8 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         o[3] = __builtin_amdgcn_s_memtime() - c3;
         o[4] = trips;
         o[5] = 1;
+        o[6] = c0b - c0;
+        o[7] = c1b - c1;
     }
 }
 
