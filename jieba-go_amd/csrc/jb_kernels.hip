@@ -252,6 +252,26 @@ static_assert(kMwOffE >= kMwStage, "staged text must fit under the entry cells")
 static_assert(kTileBytes + kLABytes + 4u <= kMwStage - 16u && kTileBytes + kLABytes + 4u <= kTileBytes + 64u,
               "lookahead bytes are staged and have document bits");
 static_assert(kMwLds + 16u <= 163840u / 8u, "k_mark_walk: 8 workgroups per CU");
+// utf8.DecodeRune (Go rules, as jb_decode) at a lead byte (>= 0xC0), without
+// branches: the phase-1 lead loop runs every lane's leads in step, so a
+// branchy decode diverged on every byte class (k_mark_walk 0.601 -> 0.598 ms).
+__device__ __forceinline__ uint32_t dec_lead(uint32_t x, uint32_t lim, uint32_t* rune) {
+    const uint32_t b0 = x & 0xFFu, b1 = (x >> 8) & 0xFFu, b2 = (x >> 16) & 0xFFu, b3 = x >> 24;
+    const uint32_t n = b0 >= 0xF0u ? 4u : (b0 >= 0xE0u ? 3u : 2u);
+    uint32_t lo = b0 == 0xE0u ? 0xA0u : 0x80u;
+    lo = b0 == 0xF0u ? 0x90u : lo;
+    uint32_t hi = b0 == 0xEDu ? 0x9Fu : 0xBFu;
+    hi = b0 == 0xF4u ? 0x8Fu : hi;
+    const bool ok = (b0 - 0xC2u <= 0xF4u - 0xC2u) & (b1 >= lo) & (b1 <= hi) &
+                    ((n < 3u) | ((b2 & 0xC0u) == 0x80u)) & ((n < 4u) | ((b3 & 0xC0u) == 0x80u)) & (n <= lim);
+    const uint32_t m0 = n == 2u ? 0x1Fu : (n == 3u ? 0x0Fu : 0x07u);
+    uint32_t cp = ((b0 & m0) << 6) | (b1 & 0x3Fu);
+    cp = n >= 3u ? ((cp << 6) | (b2 & 0x3Fu)) : cp;
+    cp = n == 4u ? ((cp << 6) | (b3 & 0x3Fu)) : cp;
+    *rune = ok ? cp : 0xFFFDu;
+    return ok ? n : 1u;
+}
+
 // entry: rune (bits 0-17; Han runes are < 0x40000) | tile offset (bits 18-29)
 constexpr uint32_t kEntCont = 0x40000000u;  // the next entry continues the run
 constexpr uint32_t kEntEdge = 0x80000000u;  // the run may continue past the tile
@@ -416,11 +436,9 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         lead &= lead - 1u;
         const uint32_t lim = 1u + (uint32_t)__builtin_ctzll(((M >> (k + 1)) & 7ull) | 8ull);
         uint32_t r;
-        const uint32_t w = jb_decode(lds4(win, k), lim, &r);
-        if (w > 1u) {
-            covered |= ((1u << (w - 1u)) - 1u) << (k + 1u);
-            if (w >= 3u && han_cp(r)) hanb |= ((1u << w) - 1u) << k;
-        }
+        const uint32_t w = dec_lead(lds4(win, k), lim, &r);
+        covered |= ((1u << (w - 1u)) - 1u) << (k + 1u);  // (nothing for w == 1)
+        if (w >= 3u && han_cp(r)) hanb |= ((1u << w) - 1u) << k;
     }
     if (p0 == 0) hanb &= ~0xFu;
     uint32_t valid = 0xFFFF0u;  // window indices 4..19 that are inside the batch
