@@ -69,6 +69,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mib", type=float, default=128.0, help="corpus MiB per GPU")
+    ap.add_argument("--workload", choices=["docs", "s10k", "long-punct", "long-oov"], default="docs",
+                    help="docs: C_syn document shard (config 4, the headline); s10k: 10,000 sentences (configs 2/3 "
+                         "with --hmm 0/1); long-punct / long-oov: one 1,000,000-rune document (configs 5a / 5b)")
     ap.add_argument("--hmm", type=int, default=1)
     ap.add_argument("--nwords", type=int, default=350_000)
     ap.add_argument("--dict-kind", choices=["prefix", "txt"], default="prefix",
@@ -102,7 +105,14 @@ def main():
     s = synth.Synth(nwords=args.nwords)
     tmp = tempfile.mkdtemp(prefix=f"jb_bench_r{rank}_")
     dpath, epath = s.write_files(tmp)
-    buf, off, nrunes = s.corpus(synth.KIND_DOCS, rank * DOC_STRIDE, target_bytes=int(args.mib * (1 << 20)))
+    if args.workload == "docs":
+        buf, off, nrunes = s.corpus(synth.KIND_DOCS, rank * DOC_STRIDE, target_bytes=int(args.mib * (1 << 20)))
+    elif args.workload == "s10k":
+        buf, off, nrunes = s.corpus(synth.KIND_SENTENCES, rank * DOC_STRIDE, max_docs=10_000,
+                                    target_bytes=64 << 20)
+    else:
+        buf, off, nrunes = s.corpus(synth.KIND_LONG_PUNCT if args.workload == "long-punct" else synth.KIND_LONG_OOV,
+                                    rank, target_runes=1_000_000)
     nbytes = int(off[-1])
     ndocs = len(off) - 1
     hbytes = han_bytes(buf, nbytes)
@@ -207,13 +217,16 @@ def main():
         sbytes = int(off[dend])
         s_runes = int(np.count_nonzero((buf[:sbytes] & 0xC0) != 0x80))
         o = O.Oracle.from_files(dpath, epath, kind, size_override)
+        backptr = args.workload.startswith("long")  # the literal path copy is O(m^2) on a 1M-rune run
+        O.set_viterbi_backptr(backptr)
         threads = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
         tc = time.perf_counter()
         os_, oe, od = o.cut_batch(buf[: sbytes + 16], off[: dend + 1], bool(args.hmm), nthreads=threads)
         cpu_s = time.perf_counter() - tc
         cpu = {"value": round(s_runes / cpu_s, 1), "unit": "chars/s", "cores": threads, "kind": "port",
                "sample": f"first {dend} documents ({sbytes / 2**20:.1f} MiB, {s_runes} chars) of rank 0's shard, "
-                         f"oracle/jieba_oracle.c (C restatement of tokenizer.go, literal path-copy Viterbi), "
+                         f"oracle/jieba_oracle.c (C restatement of tokenizer.go, "
+                         f"{'O(n) back-pointer' if backptr else 'literal path-copy'} Viterbi), "
                          f"{threads} threads over documents, {cpu_s:.2f} s",
                "cpu_model": _cpu_model()}
         ps, pe, pd, pn = ptrs
@@ -254,8 +267,12 @@ def main():
             "value": round(value, 1), "unit": "chars/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic (seeded D_syn 350k-word dict, E_syn emissions, C_syn Zipf corpus)",
-            "config": {"workload": f"C_syn corpus shard {args.mib:g} MiB/GPU (1 GiB over 8 GPUs = config 4), "
-                                   f"Cut hmm={'on' if args.hmm else 'off'}, "
+            "config": {"workload": (f"C_syn corpus shard {args.mib:g} MiB/GPU (1 GiB over 8 GPUs = config 4), "
+                                    if args.workload == "docs" else
+                                    "S10k: 10,000 synthetic sentences (configs 2/3), " if args.workload == "s10k" else
+                                    f"L1M: one 1,000,000-rune document, "
+                                    f"{'punctuated (5a)' if args.workload == 'long-punct' else 'unpunctuated, 30% OOV (5b)'}, ")
+                                   + f"Cut hmm={'on' if args.hmm else 'off'}, "
                                    f"{'NewJiebaTokenizer (prefix dict, size 60,101,967)' if args.dict_kind == 'prefix' else 'NewTokenizer(dict.txt)'}",
                        "bytes_per_gpu": nbytes, "chars_per_gpu": nrunes, "han_bytes_per_gpu": hbytes,
                        "docs_per_gpu": ndocs, "dict_words": s.nwords, "parallelism": f"doc-shard x{world}, no collectives"},
