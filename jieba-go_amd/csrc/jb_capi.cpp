@@ -399,7 +399,7 @@ static int upload_image(Device* d, const Image& img) {
 static void free_work(Work* w) {
     dfree(w->docbits); dfree(w->tile_cnt); dfree(w->tile_off);
     dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->supb); dfree(w->supt); dfree(w->blk); dfree(w->alnum16); dfree(w->erec); dfree(w->lanemask);
-    dfree(w->gbl); dfree(w->gbest); dfree(w->gstart); dfree(w->tile4);
+    dfree(w->gbl); dfree(w->gbest); dfree(w->gstart); dfree(w->tile4); dfree(w->longblk);
     dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters); dfree(w->dbg); dfree(w->dbg_walk);
     *w = Work{};
 }
@@ -433,6 +433,7 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.gbl, nb / 3 + 8));
     HIPCHK(hipMalloc(&w.gstart, (nb / kZhGroupBytes + 4) * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.tile4, ntiles * 4));
+    HIPCHK(hipMalloc(&w.longblk, (nb / kZhLongMin + 2) * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.gbest, (nb / 3 + 8) * sizeof(double)));
 
     HIPCHK(hipMalloc(&w.tok_start, (nb + 4) * 4));

@@ -25,6 +25,7 @@ enum {
     CNT_NTOKE = 3,  // token ends (== CNT_NTOK when consistent)
     CNT_ERR = 4,    // bit 0: a zh block reached a tail index -1 (the reference panics)
     CNT_WORK = 5,   // k_zh work counter: next group (kZhGroupBytes of text)
+    CNT_NLONG = 6,  // long zh blocks k_zh left to k_zh_long
     CNT_NWORDS = 8  // u32 slots reserved; u64 token count lives at byte offset 32
 };
 
@@ -34,7 +35,8 @@ constexpr int kTokTileWords = 512;     // k_tok: 256 threads x 2 words (16 KiB o
 #define JB_ZH_GROUP 6144
 #endif
 constexpr uint32_t kErecPad = 8;  // erec slots before slot 0 (k_zh reads a few slots past a block's start)
-constexpr uint32_t kZhGroupBytes = JB_ZH_GROUP;  // k_zh work unit: zh blocks starting in one such span (multiple of 32)
+constexpr uint32_t kZhGroupBytes = JB_ZH_GROUP;
+constexpr uint32_t kZhLongMin = 8192;  // zh blocks of at least this many bytes go to k_zh_long  // k_zh work unit: zh blocks starting in one such span (multiple of 32)
 
 // Per-call device workspace, sized for `nbytes` of text.
 struct Work {
@@ -53,6 +55,7 @@ struct Work {
     uint64_t* erec;        // per Han rune (slot = byte / 3): packed DAG edges (k_mark_walk -> k_zh)
     uint32_t* lanemask;    // per 16 bytes: block starts | Han block starts << 16
     uint2* gstart;         // per k_zh group g: (blocks, zh blocks) that start before g * kZhGroupBytes
+    uint2* longblk;        // (start, end) of each long zh block (k_zh -> k_zh_long)
     uint32_t* tile4;       // per tile: a 4-byte Han rune starts in it
     uint8_t* gbl;          // per Han rune: chosen piece length, then Viterbi back-pointers / labels
     double* gbest;         // per Han rune: best proba, kept only for blocks with an edge > 8 runes
@@ -69,7 +72,7 @@ struct Work {
 // Kernel ids for per-launch timing.
 enum KernelId {
     K_DOCBITS = 0, K_MARK_WALK, K_SCAN_BLOCKS, K_BLOCKS_WRITE, K_ZH, K_NONZH,
-    K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_NUM
+    K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_ZH_LONG, K_NUM
 };
 extern const char* const kKernelNames[K_NUM];
 

@@ -35,7 +35,7 @@ namespace jb {
 
 const char* const kKernelNames[K_NUM] = {"k_docbits", "k_mark_walk", "k_scan_blocks", "k_blocks_write",
                                          "k_zh", "k_nonzh", "k_tok_count", "k_scan_tok",
-                                         "k_tok_write", "k_doc_tok"};
+                                         "k_tok_write", "k_doc_tok", "k_zh_long"};
 
 // newJiebaHMM literals (tokenizer.go:629-652)
 #define START_B (-0.26268660809250016)
@@ -1490,6 +1490,7 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
                                             const uint64_t* __restrict__ erec, uint8_t* __restrict__ gbl,
                                             double* __restrict__ gbest,
                                             uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
+                                            uint2* __restrict__ longblk,
                                             uint32_t ablate, uint64_t* __restrict__ dbg) {
     __shared__ uint8_t s_bl[4][kZhWin / 3u + 4u];
     __shared__ double s_rb[4][kZhRing * 64];  // DP ring, then the window's token bitmaps
@@ -1650,7 +1651,10 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
 #pragma unroll
             for (int i = 0; i < 3; i++) {
                 if (st) stv[6] += __popcll(__ballot(out[i]));
-                if (out[i]) {
+                if (out[i] && bei[i] - bsi[i] >= kZhLongMin) {  // k_zh_long cuts it with a whole wave
+                    const uint32_t li = atomicAdd(counters + CNT_NLONG, 1u);
+                    longblk[li] = make_uint2(bsi[i], bei[i]);
+                } else if (out[i]) {
                     const GlbZv gv{text, gbl};
                     zh_dp(gv, im, erec, gbest, ring, OneSrc{bsi[i], bei[i]}, ablate);
                     if (!(ablate & 4u) && !zh_fwd<HMM>(gv, im, bsi[i], bei[i], em, ablate, nullptr))
@@ -1687,6 +1691,271 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
             o[7] = stv[6];
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// k_zh_long: the long zh blocks (>= kZhLongMin bytes; e.g. an unpunctuated
+// document), one wave each.  Their DP, path and Viterbi are serial chains
+// (bit-exact float64 order forbids reassociating them), so the wave runs each
+// chain as one uniform program on all lanes at once, from LDS: windows of
+// kLW runes are staged cooperatively (records and their weights for the DP,
+// piece lengths and emissions for the path and the Viterbi), then every lane
+// steps through the window with the same values (broadcast LDS reads, no
+// divergence), so the next refill is again a parallel, coalesced load.  One
+// lane's walk over global memory took a memory round trip per rune.
+// All-3-byte blocks only; a block with a 4-byte Han rune takes the one-lane
+// path of k_zh.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kLW = 1024;  // runes per staged window
+constexpr uint32_t kZhLongGrid = 256;  // k_zh_long waves (persistent over the long-block list)
+struct LongLds {
+    uint64_t rec[kLW];      // DP: records
+    double wt[kLW][4];      // DP: weights; path: emissions B, M, E, S
+    double best[kLW + 64];  // DP: best values of the window, then 64 carried from the window after it
+    uint8_t b[kLW];         // DP: piece lengths; path: lengths, then back-pointers / labels
+};
+
+template <bool HMM>
+__global__ __launch_bounds__(64) void k_zh_long(const uint8_t* __restrict__ text, DevImage im,
+                                                const uint64_t* __restrict__ erec, uint8_t* __restrict__ gbl,
+                                                double* __restrict__ gbest, const uint2* __restrict__ longblk,
+                                                uint32_t* __restrict__ counters, uint32_t* __restrict__ sbits,
+                                                uint32_t* __restrict__ ebits, double* __restrict__ ring_g) {
+    __shared__ LongLds L;
+    __shared__ double s_ring[kZhRing * 64];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t nlong = counters[CNT_NLONG];
+    Emitter em(sbits, ebits);
+    em.off = lane != 0u;  // every lane runs the chains; lane 0 writes the tokens
+    for (uint32_t bi = blockIdx.x; bi < nlong; bi += gridDim.x) {
+        const uint2 bb = longblk[bi];
+        const uint32_t bs = bb.x, be = bb.y;
+        bool any4 = false;  // a 4-byte Han rune (lead >= 0xF0) anywhere in the block
+        for (uint32_t a = (bs & ~15u) + 16u * lane; a < be; a += 1024u) {
+            const uint4 x = *reinterpret_cast<const uint4*>(text + a);
+            any4 |= ((x.x & (x.x << 1) & (x.x << 2) & (x.x << 3)) | (x.y & (x.y << 1) & (x.y << 2) & (x.y << 3)) |
+                     (x.z & (x.z << 1) & (x.z << 2) & (x.z << 3)) | (x.w & (x.w << 1) & (x.w << 2) & (x.w << 3))) &
+                    0x80808080u;
+        }
+        if (__any(any4)) {  // the general one-lane path (k_zh's)
+            if (lane == 0) {
+                const GlbZv gv{text, gbl};
+                zh_dp(gv, im, erec, gbest, s_ring + lane, OneSrc{bs, be}, 0u);
+                if (!zh_fwd<HMM>(gv, im, bs, be, em, 0u, nullptr)) atomicOr(counters + CNT_ERR, 1u);
+                em.flush();
+            }
+            __syncthreads();
+            continue;
+        }
+        const uint32_t n = (be - bs) / 3u, s0 = bs / 3u;  // rune i: bytes bs + 3i, slot s0 + i
+        // ---- DP (calcDagProba + maxIndexProba, tokenizer.go:502-578), backwards by window ----
+        bool bad = false;
+        for (uint32_t hi = n; hi > 0u;) {
+            const uint32_t lo = hi > kLW ? hi - kLW : 0u, m = hi - lo;
+            for (uint32_t k = lane; k < m; k += 64u) L.rec[k] = erec[s0 + lo + k];
+            __syncthreads();
+            for (uint32_t k = lane; k < m; k += 64u) rec_weights(im, L.rec[k], L.wt[k]);
+            __syncthreads();
+            auto best_at = [&](uint32_t j) -> double {  // best(j), j > i (j < n)
+                if (j - lo < m + 64u) return L.best[j - lo];
+                return gbest[s0 + j];
+            };
+            // The window's best values sit at best[k], the carried ones right after them at
+            // best[m ..], so best(i + L) is best[k + L] for any L <= 64 (one LDS read, no
+            // branch); best(i + 1), the value the chain just made, stays in a register.
+            {
+                double cv = 0.0;
+                if (lane < 64u && hi + lane < n) cv = L.best[kLW + lane];
+                __syncthreads();
+                if (lane < 64u) L.best[m + lane] = cv;
+                __syncthreads();
+            }
+            double b1 = (hi < n) ? L.best[m] : 0.0;
+            for (uint32_t i = hi; i-- > lo;) {
+                const uint32_t k = i - lo, c = n - i;
+                const uint64_t rc = L.rec[k];
+                uint32_t mm = (uint32_t)rc & 0xFFu;
+                DpFold f;
+                if (mm) {
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        if (mm == 0u) break;
+                        const uint32_t Ln = (uint32_t)__builtin_ctz(mm) + 1u;
+                        mm &= mm - 1u;
+                        const double bl = L.best[k + Ln];
+                        const double nb = (Ln == c) ? 0.0 : (Ln == 1u ? b1 : bl);
+                        const double pp = L.wt[k][e] + nb;
+                        if (pp >= f.prevP) {
+                            f.bestL = Ln;
+                            f.bestP = pp;
+                        }
+                        f.prevP = pp;
+                        f.lastL = Ln;
+                    }
+                } else {  // overflowed record (rare): walk the rune here, every item folded
+                    auto item = [&](uint32_t Ln, double wt) {
+                        const double pp = wt + ((Ln == c) ? 0.0 : best_at(i + Ln));
+                        if (pp >= f.prevP) {
+                            f.bestL = Ln;
+                            f.bestP = pp;
+                        }
+                        f.prevP = pp;
+                        f.lastL = Ln;
+                    };
+                    auto dec3 = [&](uint32_t q) {
+                        const uint32_t x = ld4(text, q);
+                        return ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
+                    };
+                    const uint32_t q = bs + 3u * i;
+                    uint32_t id = rune_code(im, dec3(q));
+                    uint64_t cc = im.cells[id];
+                    if (jb_cell_check(cc) != JB_CHECK_ROOT) {
+                        item(1u, im.wtab[JB_WIDX_ABSENT]);
+                    } else if (jb_cell_fc(cc) == JB_FC_ZERO) {
+                        item(1u, im.wtab[jb_cell_widx(cc)]);
+                    } else {
+                        if (jb_cell_fc(cc) == JB_FC_POS) item(1u, im.wtab[jb_cell_widx(cc)]);
+                        uint32_t qq = q + 3u, len = 1;
+                        bool go = jb_cell_hc(cc) != 0u;
+                        while (go && qq < be) {
+                            const uint32_t tt = dat_slot(im, cc, dec3(qq));
+                            const uint64_t ch = im.cells[tt];
+                            if (!dat_hit(ch, id)) break;  // (:475-478)
+                            ++len;
+                            qq += 3u;
+                            if (jb_cell_fc(ch) == JB_FC_POS) item(len, im.wtab[jb_cell_widx(ch)]);
+                            go = jb_cell_hc(ch) != 0u;
+                            id = tt;
+                            cc = ch;
+                        }
+                    }
+                }
+                f.finish();
+                L.best[k] = f.bestP;
+                L.b[k] = (uint8_t)f.bestL;
+                b1 = f.bestP;
+            }
+            __syncthreads();
+            for (uint32_t k = lane; k < m; k += 64u) {
+                gbl[s0 + lo + k] = L.b[k];
+                gbest[s0 + lo + k] = L.best[k];
+            }
+            const double carry = lane < m ? L.best[lane] : 0.0;
+            __syncthreads();
+            if (lane < m) L.best[kLW + lane] = carry;
+            __syncthreads();
+            hi = lo;
+        }
+        // ---- path (findDagPath, :552-562) + HMM runs (viterbi + cutHMM, :668-756, 273-285) ----
+        // Window [flo, flo + fm) holds piece lengths (then back-pointers) and emissions.
+        uint32_t flo = 0, fm = 0;
+        auto stage = [&](uint32_t from) {  // (uniform)
+            __syncthreads();
+            flo = from;
+            fm = min(kLW, n - from);
+            for (uint32_t k = lane; k < fm; k += 64u) {
+                L.b[k] = gbl[s0 + flo + k];
+                if (HMM) {
+                    const uint32_t x = ld4(text, bs + 3u * (flo + k));
+                    const uint32_t r = ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
+                    load_emit(im, r, L.wt[k]);
+                }
+            }
+            __syncthreads();
+        };
+        // slot bytes (piece length / back-pointer / label): LDS inside the window, else HBM
+        auto getb = [&](uint32_t j) -> uint32_t { return (j - flo < fm) ? L.b[j - flo] : gbl[s0 + j]; };
+        auto setb = [&](uint32_t j, uint32_t v) {
+            if (j - flo < fm) L.b[j - flo] = (uint8_t)v;
+            gbl[s0 + j] = (uint8_t)v;  // (every lane: its own later reads see its own store)
+        };
+        auto token = [&](uint32_t a, uint32_t e) { em.token(bs + 3u * a, bs + 3u * e); };  // runes [a, e)
+        uint32_t p = 0, run_s = 0, run_n = 0;
+        double vB = 0, vM = 0, vE = 0, vS = 0;
+        auto run_end = [&](uint32_t re) {  // the run of single-rune pieces [run_s, re)
+            const uint32_t m = re - run_s;
+            if (m == 1u) {  // always "S" (:672-674)
+                token(run_s, re);
+                return;
+            }
+            uint32_t st = vE > vS ? (uint32_t)JB_E : (uint32_t)JB_S;  // (:723-729)
+            uint32_t t = m - 1u, reset = 0, jt = re - 1u;
+            for (;;) {
+                if (t == 0u) {
+                    setb(jt, st);
+                    break;
+                }
+                const uint32_t code = (getb(jt) >> (2u * st)) & 3u;
+                setb(jt, st);
+                if (code == 2u) {
+                    reset = t;
+                    break;
+                }
+                st = (st == JB_B || st == JB_S) ? 2u + code : code;
+                --t;
+                --jt;
+            }
+            uint32_t ja = run_s, jb = jt, ts = run_s;
+            for (uint32_t k = 0; k < m - reset; k++) {
+                const uint32_t lab = getb(jb);
+                ++ja;
+                ++jb;
+                if (lab >= (uint32_t)JB_E) {
+                    token(ts, ja);
+                    ts = ja;
+                }
+            }
+        };
+        stage(0u);
+#if JB_X_NOPATH  // diagnostic: DP only (wrong results)
+        p = n;
+#endif
+        while (p < n) {
+            if (p - flo >= fm) stage(p);
+            const uint32_t Ln = L.b[p - flo];
+            if (Ln == 0u) {  // tail index -1: cutDAG's slice panics in the reference
+                bad = true;
+                break;
+            }
+            if (!HMM) {
+                token(p, p + Ln);
+            } else if (Ln == 1u) {
+                const double* e = L.wt[p - flo];
+                if (run_n == 0u) {
+                    run_s = p;
+                    vB = START_B + e[0];
+                    vM = JB_MIN_FLOAT + e[1];
+                    vE = JB_MIN_FLOAT + e[2];
+                    vS = START_S + e[3];
+                } else {
+                    uint32_t cB, cM, cE, cS;
+                    double pB, pM, pE, pS;
+                    route2(vE + T_EB, vS + T_SB, &cB, &pB);  // B <- E, S
+                    route2(vB + T_BM, vM + T_MM, &cM, &pM);  // M <- B, M
+                    route2(vB + T_BE, vM + T_ME, &cE, &pE);  // E <- B, M
+                    route2(vE + T_ES, vS + T_SS, &cS, &pS);  // S <- E, S
+                    vB = pB + e[0];
+                    vM = pM + e[1];
+                    vE = pE + e[2];
+                    vS = pS + e[3];
+                    setb(p, cB | (cM << 2) | (cE << 4) | (cS << 6));
+                }
+                run_n++;
+            } else {
+                if (run_n) {
+                    run_end(p);
+                    run_n = 0;
+                }
+                token(p, p + Ln);
+            }
+            p += Ln;
+        }
+        if (HMM && run_n && !bad) run_end(n);
+        em.flush();
+        if (bad && lane == 0u) atomicOr(counters + CNT_ERR, 1u);
+        __syncthreads();
+    }
+    (void)ring_g;
 }
 
 // ---------------------------------------------------------------------------
@@ -1950,11 +2219,19 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     if (hmm)
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
                                           w.gstart, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
-                                          g_ablate, w.dbg));
+                                          w.longblk, g_ablate, w.dbg));
     else
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
                                           w.gstart, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
-                                          g_ablate, w.dbg));
+                                          w.longblk, g_ablate, w.dbg));
+    if (hmm)
+        JB_TIMED(K_ZH_LONG, hipLaunchKernelGGL((k_zh_long<true>), dim3(kZhLongGrid), dim3(64), 0, stream, d_text, im,
+                                               w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters, w.sbits,
+                                               w.ebits, nullptr));
+    else
+        JB_TIMED(K_ZH_LONG, hipLaunchKernelGGL((k_zh_long<false>), dim3(kZhLongGrid), dim3(64), 0, stream, d_text, im,
+                                               w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters, w.sbits,
+                                               w.ebits, nullptr));
     JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3(grid_nz), dim3(256), 0, stream, d_text, w.blk, w.alnum16,
                                          w.counters, w.sbits, w.ebits));
     JB_TIMED(K_TOK_COUNT, hipLaunchKernelGGL((k_tok<false>), dim3(nttiles), dim3(256), 0, stream, w.sbits, w.ebits,

@@ -92,6 +92,10 @@ EDGE_TEXTS = [
     "a" * 6141 + "丁" * 342, "a" * 6141 + "丁" * 343, "a" * 6144 + "丁" * 341 + "，" + "丁" * 5,
     "a" * 6143 + "丁" * 400, "中，" * 3072 + "丁" * 700, "a" * 6140 + "𠀀" * 300 + "丁" * 30,
     "，".join(["中文"] * 4000),                                           # many short blocks per group
+    # k_zh_long (blocks of >= 8 KiB): all-3-byte ones by the whole-wave path, across its
+    # 1024-rune windows; one with a 4-byte Han rune by the one-lane path
+    "丁" * 2731, "一丁㐀中文" * 700, "中文" * 1500 + "𠀀" + "中文" * 1500,
+    "a" * 6000 + "一丁㐀中文" * 900 + "。" + "中" * 10,
 ]
 
 
