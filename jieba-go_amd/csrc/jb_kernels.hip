@@ -1723,6 +1723,12 @@ __global__ __launch_bounds__(64) void k_zh_long(const uint8_t* __restrict__ text
                                                 uint32_t* __restrict__ ebits, double* __restrict__ ring_g) {
     __shared__ LongLds L;
     __shared__ double s_ring[kZhRing * 64];
+    // LDS pointers typed as such: the lambdas below would otherwise see generic
+    // pointers and the compiler would emit flat loads
+    typedef uint8_t __attribute__((address_space(3))) LU8;
+    typedef double __attribute__((address_space(3))) LF64;
+    LU8* const Lb = (LU8*)L.b;
+    LF64* const Lbest = (LF64*)L.best;
     const uint32_t lane = threadIdx.x;
     const uint32_t nlong = counters[CNT_NLONG];
     Emitter em(sbits, ebits);
@@ -1757,8 +1763,8 @@ __global__ __launch_bounds__(64) void k_zh_long(const uint8_t* __restrict__ text
             for (uint32_t k = lane; k < m; k += 64u) rec_weights(im, L.rec[k], L.wt[k]);
             __syncthreads();
             auto best_at = [&](uint32_t j) -> double {  // best(j), j > i (j < n)
-                if (j - lo < m + 64u) return L.best[j - lo];
-                return gbest[s0 + j];
+                if (j - lo < m + 64u) return Lbest[j - lo];
+                return *reinterpret_cast<const volatile double*>(gbest + s0 + j);
             };
             // The window's best values sit at best[k], the carried ones right after them at
             // best[m ..], so best(i + L) is best[k + L] for any L <= 64 (one LDS read, no
@@ -1854,7 +1860,7 @@ __global__ __launch_bounds__(64) void k_zh_long(const uint8_t* __restrict__ text
             flo = from;
             fm = min(kLW, n - from);
             for (uint32_t k = lane; k < fm; k += 64u) {
-                L.b[k] = gbl[s0 + flo + k];
+                Lb[k] = gbl[s0 + flo + k];
                 if (HMM) {
                     const uint32_t x = ld4(text, bs + 3u * (flo + k));
                     const uint32_t r = ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
@@ -1864,9 +1870,12 @@ __global__ __launch_bounds__(64) void k_zh_long(const uint8_t* __restrict__ text
             __syncthreads();
         };
         // slot bytes (piece length / back-pointer / label): LDS inside the window, else HBM
-        auto getb = [&](uint32_t j) -> uint32_t { return (j - flo < fm) ? L.b[j - flo] : gbl[s0 + j]; };
+        auto getb = [&](uint32_t j) -> uint32_t {  // (volatile: two loads, not one flat load of either)
+            if (j - flo < fm) return Lb[j - flo];
+            return *reinterpret_cast<const volatile uint8_t*>(gbl + s0 + j);
+        };
         auto setb = [&](uint32_t j, uint32_t v) {
-            if (j - flo < fm) L.b[j - flo] = (uint8_t)v;
+            if (j - flo < fm) Lb[j - flo] = (uint8_t)v;
             gbl[s0 + j] = (uint8_t)v;  // (every lane: its own later reads see its own store)
         };
         auto token = [&](uint32_t a, uint32_t e) { em.token(bs + 3u * a, bs + 3u * e); };  // runes [a, e)
