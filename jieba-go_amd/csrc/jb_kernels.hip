@@ -1707,7 +1707,7 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
 // path of k_zh.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kLW = 1024;  // runes per staged window
-constexpr uint32_t kZhLongGrid = 256;  // k_zh_long waves (persistent over the long-block list)
+constexpr uint32_t kZhLongGrid = 64;   // k_zh_long waves (persistent over the long-block list)
 struct LongLds {
     uint64_t rec[kLW];      // DP: records
     double wt[kLW][4];      // DP: weights; path: emissions B, M, E, S
