@@ -357,7 +357,8 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
                                                    const uint32_t* __restrict__ docbits, DevImage im,
                                                    uint32_t* __restrict__ lanemask, uint2* __restrict__ tile_cnt,
                                                    uint64_t* __restrict__ erec, uint32_t* __restrict__ tile4,
-                                                   uint64_t* __restrict__ alnum16, uint32_t ablate,
+                                                   uint64_t* __restrict__ alnum16, uint32_t* __restrict__ sbits,
+                                                   uint32_t* __restrict__ ebits, uint32_t ablate,
                                                    uint64_t* __restrict__ dbg) {
     // LDS: 20.2 KB, so that 8 workgroups fit a CU (160 KB).  The staged text is
     // dead once the entries are decoded; the entry cells/records reuse its bytes.
@@ -384,6 +385,10 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         reinterpret_cast<uint4*>(s_t)[k] = v;
     }
     const uint64_t lastw = (nbytes + 31) >> 5;
+    {  // clear the tile's words of the token bitmaps (k_zh and k_nonzh OR into them): no memset pass
+        const uint64_t wz = (t0 >> 5) + (threadIdx.x & 127u);
+        if (wz < lastw + 2u) (threadIdx.x < 128u ? sbits : ebits)[wz] = 0u;
+    }
     if (threadIdx.x < kTileBytes / 32 + 3) {
         const uint64_t wi = (t0 >> 5) + threadIdx.x;
         s_db[threadIdx.x] = wi < lastw ? docbits[wi] : 0u;
@@ -2203,13 +2208,8 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     const uint32_t nttiles = (uint32_t)((nwords + kTokTileWords - 1) / kTokTileWords);
     hipError_t e;
     if ((e = hipMemsetAsync(w.counters, 0, CNT_NWORDS * sizeof(uint32_t) + sizeof(uint64_t), stream))) return e;
-    if (w.bits_stride <= 2 * (nwords + 2)) {  // workspace sized for this batch: one clear for all three
-        if ((e = hipMemsetAsync(w.docbits, 0, (2 * w.bits_stride + nwords + 2) * 4, stream))) return e;
-    } else {
-        if ((e = hipMemsetAsync(w.docbits, 0, (nwords + 2) * 4, stream))) return e;
-        if ((e = hipMemsetAsync(w.sbits, 0, (nwords + 2) * 4, stream))) return e;
-        if ((e = hipMemsetAsync(w.ebits, 0, (nwords + 2) * 4, stream))) return e;
-    }
+    // (k_mark_walk clears the token bitmaps tile by tile)
+    if ((e = hipMemsetAsync(w.docbits, 0, (nwords + 2) * 4, stream))) return e;
     if (nbytes == 0) {
         if ((e = hipMemsetAsync(w.doc_tok, 0, (ndocs + 1) * sizeof(uint64_t), stream))) return e;
         return hipSuccess;
@@ -2219,7 +2219,7 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                                d_doc_off, ndocs, nbytes, w.docbits));
     JB_TIMED(K_MARK_WALK, hipLaunchKernelGGL(k_mark_walk, dim3(ntiles), dim3(256), 0, stream, d_text, nbytes,
                                              w.docbits, im, w.lanemask, w.tile_cnt, w.erec + kErecPad,
-                                             w.tile4, w.alnum16, g_ablate, w.dbg_walk));
+                                             w.tile4, w.alnum16, w.sbits, w.ebits, g_ablate, w.dbg_walk));
     JB_TIMED(K_SCAN_BLOCKS, hipLaunchKernelGGL(k_sup, dim3((ntiles + 255) / 256), dim3(256), 0, stream, w.tile_cnt,
                                                ntiles, w.supb));
     JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL(k_blocks_write, dim3((ntiles + kBwTiles - 1) / kBwTiles), dim3(256), 0,
