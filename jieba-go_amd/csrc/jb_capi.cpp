@@ -11,12 +11,14 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
 #include <string>
 #include <thread>
+#include <chrono>
 #include <vector>
 
 #include "../../include/jiebahip.h"
@@ -126,6 +128,7 @@ struct Device {
     uint64_t* h_misc = nullptr;  // doc offsets in / doc_tok out (u64)
     uint64_t h_misc_cap = 0;
     uint32_t* h_cnt = nullptr;   // counters (64 u32)
+    std::vector<hipEvent_t> ev;  // span pieces landed (host batches)
     uint32_t ncu = 0;
     EventTimer timer;
     bool profile = false;
@@ -166,6 +169,16 @@ void par_copy(void* dst, const void* src, size_t n) {
         if (a < b) th.emplace_back([=] { memcpy((char*)dst + a, (const char*)src + a, b - a); });
     }
     for (auto& t : th) t.join();
+}
+
+// fn(0..n-1) on n threads (the caller's thread runs fn(0))
+constexpr unsigned kCopyThreads = 8;
+template <class F>
+void run_threads(unsigned n, F& fn) {
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < n; t++) th.emplace_back([&fn, t] { fn(t); });
+    fn(0);
+    for (auto& x : th) x.join();
 }
 
 // out[k] = base + in[k] (u32 device spans -> u64 batch offsets), a few threads when large
@@ -625,6 +638,7 @@ extern "C" void jb_close(jb_ctx* ctx) {
         dfree(d->text); dfree(d->doc_off); dfree(d->pagemap); dfree(d->emit); dfree(d->cells); dfree(d->code);
         dfree(d->wtab);
         hfree(d->h_text); hfree(d->h_span); hfree(d->h_misc); hfree(d->h_cnt);
+        for (hipEvent_t e : d->ev) (void)hipEventDestroy(e);
         (void)hipStreamDestroy(d->stream);
     }
     delete ctx;
@@ -657,37 +671,97 @@ static int cut_range(jb_ctx* ctx, Device* d, const uint8_t* text, const uint64_t
         int rc;
         if ((rc = ensure_staging(d, nbytes, nd))) return rc;
         if ((rc = ensure_work(d, nbytes, nd))) return rc;
-        par_copy(d->h_text, text + base, nbytes);
+        static const bool tdbg = getenv("JB_DEBUG") != nullptr;
+        auto now = [] { return std::chrono::steady_clock::now(); };
+        auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+            return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        const auto c0 = now();
+        // text into pinned staging in 32 MiB pieces, each sent while the next is copied
         memset(d->h_text + nbytes, 0, 64);
         for (uint32_t k = 0; k <= nd; k++) d->h_misc[k] = doc_off[a + k] - base;
-        HIPCHK(hipMemcpyAsync(d->text, d->h_text, nbytes + 64, hipMemcpyHostToDevice, d->stream));
         HIPCHK(hipMemcpyAsync(d->doc_off, d->h_misc, (nd + 1) * 8, hipMemcpyHostToDevice, d->stream));
+        {
+            // kCopyThreads threads each copy their share of the text in 4 MiB pieces and queue
+            // each piece's H2D as soon as it is staged, so the DMA runs behind the copies
+            const uint64_t total = nbytes + 64, kPiece = 4ull << 20;
+            const unsigned nth = total >= (16ull << 20) ? kCopyThreads : 1u;
+            const uint64_t share = ((total + nth - 1) / nth + 4095) & ~4095ull;
+            std::atomic<int> err{0};
+            auto work = [&](unsigned t) {
+                if (hipSetDevice(d->ordinal) != hipSuccess) err = 1;
+                const uint64_t lo = std::min(total, t * share), hi = std::min(total, lo + share);
+                for (uint64_t o = lo; o < hi; o += kPiece) {
+                    const uint64_t l = std::min(kPiece, hi - o);
+                    if (o < nbytes) memcpy(d->h_text + o, text + base + o, std::min(l, nbytes - o));
+                    if (hipMemcpyAsync(d->text + o, d->h_text + o, l, hipMemcpyHostToDevice, d->stream) != hipSuccess)
+                        err = 1;
+                }
+            };
+            run_threads(nth, work);
+            if (err) return fail(JB_EDEVICE, "H2D copy failed");
+        }
+        const auto c1 = now();
         if ((rc = launch(ctx, d, d->text, nbytes, d->doc_off, nd, hmm, d->stream))) return rc;
         HIPCHK(hipMemcpyAsync(d->h_cnt, d->w.counters, 8 * 4, hipMemcpyDeviceToHost, d->stream));
         HIPCHK(hipStreamSynchronize(d->stream));
+        const auto c2 = now();
         if (d->h_cnt[CNT_ERR]) return fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)");
         if (d->h_cnt[CNT_NTOK] != d->h_cnt[CNT_NTOKE])
             return fail(JB_EDEVICE, "internal: %u token starts vs %u ends", d->h_cnt[CNT_NTOK], d->h_cnt[CNT_NTOKE]);
         const uint32_t nt = d->h_cnt[CNT_NTOK];
         if ((rc = ensure_span_staging(d, nt))) return rc;
-        if (nt) {
-            HIPCHK(hipMemcpyAsync(d->h_span, d->w.tok_start, (uint64_t)nt * 4, hipMemcpyDeviceToHost, d->stream));
-            HIPCHK(hipMemcpyAsync(d->h_span + nt, d->w.tok_end, (uint64_t)nt * 4, hipMemcpyDeviceToHost, d->stream));
+        const bool write = out->reserve(out->n + nt);
+        if (!write && !out->external) return fail(JB_ENOMEM, "out of host memory for %u tokens", nt);
+        // spans back in pieces of 2M tokens; each piece is widened while the next ones are in flight
+        const uint32_t kTokPiece = 1u << 21;
+        const uint32_t np = (nt + kTokPiece - 1) / kTokPiece;
+        while (d->ev.size() < 2 * (size_t)np) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            d->ev.push_back(e);
+        }
+        for (uint32_t q = 0; q < np; q++) {
+            const uint64_t t0 = (uint64_t)q * kTokPiece, l = std::min<uint64_t>(kTokPiece, nt - t0);
+            HIPCHK(hipMemcpyAsync(d->h_span + t0, d->w.tok_start + t0, l * 4, hipMemcpyDeviceToHost, d->stream));
+            HIPCHK(hipEventRecord(d->ev[2 * q], d->stream));
+            HIPCHK(hipMemcpyAsync(d->h_span + nt + t0, d->w.tok_end + t0, l * 4, hipMemcpyDeviceToHost, d->stream));
+            HIPCHK(hipEventRecord(d->ev[2 * q + 1], d->stream));
         }
         HIPCHK(hipMemcpyAsync(d->h_misc, d->w.doc_tok, (uint64_t)(nd + 1) * 8, hipMemcpyDeviceToHost, d->stream));
-        HIPCHK(hipStreamSynchronize(d->stream));
-        if (!out->reserve(out->n + nt)) {
-            if (out->external) {  // count the rest, write nothing more
-                out->needed = out->n + nt;
-                out->n += nt;
-                out->cap = 0;
-                a = b;
-                continue;
-            }
-            return fail(JB_ENOMEM, "out of host memory for %u tokens", nt);
+        const auto c3 = now();
+        {
+            // kCopyThreads threads widen their share of each piece as soon as it has landed
+            const unsigned nth = nt >= (1u << 20) ? kCopyThreads : 1u;
+            uint64_t* const os = out->s + out->n;
+            uint64_t* const oe = out->e + out->n;
+            const uint32_t* const hs = d->h_span;
+            auto work = [&](unsigned t) {
+                for (uint32_t q = 0; q < np; q++) {
+                    const uint64_t t0 = (uint64_t)q * kTokPiece, l = std::min<uint64_t>(kTokPiece, nt - t0);
+                    const uint64_t a0 = t0 + l * t / nth, a1 = t0 + l * (t + 1) / nth;
+                    (void)hipEventSynchronize(d->ev[2 * q]);
+                    if (write)
+                        for (uint64_t k = a0; k < a1; k++) os[k] = base + hs[k];
+                    (void)hipEventSynchronize(d->ev[2 * q + 1]);
+                    if (write)
+                        for (uint64_t k = a0; k < a1; k++) oe[k] = base + hs[nt + k];
+                }
+            };
+            run_threads(nth, work);
         }
-        par_widen(out->s + out->n, d->h_span, nt, base);
-        par_widen(out->e + out->n, d->h_span + nt, nt, base);
+        HIPCHK(hipStreamSynchronize(d->stream));
+        if (!write) {  // caller arrays too small: count the rest, write nothing more
+            out->needed = out->n + nt;
+            out->n += nt;
+            out->cap = 0;
+            for (uint32_t k = 0; k < nd; k++) out->per_doc.push_back(d->h_misc[k + 1] - d->h_misc[k]);
+            a = b;
+            continue;
+        }
+        if (tdbg)
+            fprintf(stderr, "[jb] host batch %.1f MiB: copy in %.2f ms, H2D+kernels %.2f, D2H spans %.2f, widen %.2f\n",
+                    nbytes / 1048576.0, ms(c0, c1), ms(c1, c2), ms(c2, c3), ms(c3, now()));  // (D2H: the enqueue)
         out->n += nt;
         for (uint32_t k = 0; k < nd; k++) out->per_doc.push_back(d->h_misc[k + 1] - d->h_misc[k]);
         a = b;
