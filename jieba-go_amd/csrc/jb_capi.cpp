@@ -113,6 +113,7 @@ struct Device {
     uint64_t* cells = nullptr;
     uint32_t* code = nullptr;
     double* wtab = nullptr;
+    uint64_t* l1row = nullptr;
     DevImage dim{};
     // workspace
     Work w{};
@@ -400,6 +401,15 @@ static int upload_image(Device* d, const Image& img) {
     if ((rc = upload(&d->pagemap, img.pagemap)) || (rc = upload(&d->emit, img.emit)) ||
         (rc = upload(&d->cells, img.cells)) || (rc = upload(&d->code, img.code)) || (rc = upload(&d->wtab, img.wtab)))
         return rc;
+    {  // row-indexed level-1 table: code and level-1 cell of a rune in one 8-byte load
+        std::vector<uint64_t> l1(img.code.size());
+        for (size_t r = 0; r < l1.size(); r++) {
+            const uint32_t cd = img.code[r];
+            l1[r] = jb_l1row_make(cd, cd < img.cells.size() ? img.cells[cd] : 0ull);
+        }
+        if ((rc = upload(&d->l1row, l1))) return rc;
+    }
+    d->dim.l1row = d->l1row;
     d->dim.pagemap = d->pagemap;
     d->dim.emit = d->emit;
     d->dim.cells = d->cells;
@@ -636,7 +646,7 @@ extern "C" void jb_close(jb_ctx* ctx) {
         d->gexec = nullptr;
         free_work(&d->w);
         dfree(d->text); dfree(d->doc_off); dfree(d->pagemap); dfree(d->emit); dfree(d->cells); dfree(d->code);
-        dfree(d->wtab);
+        dfree(d->wtab); dfree(d->l1row);
         hfree(d->h_text); hfree(d->h_span); hfree(d->h_misc); hfree(d->h_cnt);
         for (hipEvent_t e : d->ev) (void)hipEventDestroy(e);
         (void)hipStreamDestroy(d->stream);

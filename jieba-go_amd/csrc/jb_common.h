@@ -63,6 +63,20 @@ JB_HD uint32_t jb_cell_fc(uint64_t c) { return (uint32_t)(c >> 44) & 3u; }
 JB_HD uint32_t jb_cell_hc(uint64_t c) { return (uint32_t)(c >> 46) & 1u; }
 JB_HD uint32_t jb_cell_widx(uint64_t c) { return (uint32_t)(c >> 47); }
 
+// Row-indexed level-1 table (device only, derived at upload): the cell
+// cells[code] of a row with its check field holding the code instead (codes
+// are < 2^17) and bit 21 set when that check was JB_CHECK_ROOT, i.e. when the
+// single rune is a key.  jb_l1row_cell gives back a cell whose check is the
+// root exactly when the original's was (0 otherwise: "absent").
+#define JB_L1_ROOTBIT (1u << 21)
+JB_HD uint64_t jb_l1row_make(uint32_t code, uint64_t cell) {
+    return (cell & ~0x3FFFFFull) | code | (jb_cell_check(cell) == JB_CHECK_ROOT ? JB_L1_ROOTBIT : 0u);
+}
+JB_HD uint32_t jb_l1row_code(uint64_t v) { return (uint32_t)v & 0x1FFFFu; }
+JB_HD uint64_t jb_l1row_cell(uint64_t v) {
+    return (v & ~0x3FFFFFull) | (((uint32_t)v & JB_L1_ROOTBIT) ? (uint64_t)JB_CHECK_ROOT : 0ull);
+}
+
 // Pages U+3400..U+9FFF (CJK Ext-A + URO) sit at fixed page ids 1..108.
 #define JB_DIRECT_LO 0x3400u
 #define JB_DIRECT_N 0x6C00u

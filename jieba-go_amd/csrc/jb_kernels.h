@@ -14,6 +14,10 @@ struct DevImage {
     const uint32_t* code;   // dense rune code per row (0: in no key)
     const uint64_t* cells;  // double-array trie over codes; level-1 nodes at their codes
     const double* wtab;
+    // per row: the rune's level-1 cell cells[code] with its check field
+    // replaced by the code (bits 0-16) and bit 21 = "that check was the root",
+    // so k_mark_walk gets code and level-1 cell in one load (jb_l1row_make)
+    const uint64_t* l1row;
     uint32_t nrows;
 };
 

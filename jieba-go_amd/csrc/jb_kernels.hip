@@ -472,7 +472,7 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         for (int i = 0; i < 6; i++) {
             kk[i] = 0u;
             rr[i] = 0u;
-            cd[i] = 0u;
+            cl[i] = 0ull;
             if ((uint32_t)i < ne) {
                 const uint32_t k = (uint32_t)__builtin_ctz(hs);
                 hs &= hs - 1u;
@@ -483,13 +483,16 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
                                              (((x >> 16) & 0x3Fu) << 6) | ((x >> 24) & 0x3Fu);
                 kk[i] = k;
                 rr[i] = r;
-                cd[i] = rune_code(im, r);
+                cl[i] = im.l1row[jb_row(im.pagemap, r)];  // code and level-1 cell: one load per rune
                 has4 |= r >= 0x10000u;
                 lastend = k + 4u + (r >= 0x10000u ? 4u : 3u);
             }
         }
 #pragma unroll
-        for (int i = 0; i < 6; i++) cl[i] = ((uint32_t)i < ne && !(ablate & 2u)) ? im.cells[cd[i]] : 0ull;
+        for (int i = 0; i < 6; i++) {
+            cd[i] = jb_l1row_code(cl[i]);
+            cl[i] = ((uint32_t)i < ne && !(ablate & 2u)) ? jb_l1row_cell(cl[i]) : 0ull;
+        }
 #pragma unroll
         for (int i = 0; i < 6; i++)  // (s_e is not under the staged text)
             if ((uint32_t)i < ne)
