@@ -436,6 +436,31 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         lead |= ((f * 0x204081u) >> 21 & 0xFu) << (4 * j);
     }
     uint32_t covered = 0, hanb = 0;
+    {  // Plain 3-byte leads (E1..EC, EE, EF: no overlong or surrogate bound on the
+       // second byte) with a common Han value or none, the leads of nearly all
+       // Chinese text, in a short loop; every other lead (2- and 4-byte forms, E0,
+       // ED, the rare Han ranges) goes to the general decode below.
+        constexpr uint64_t k3000 = (1ull << 5) | (1ull << 7) | (0x1FFull << 0x21) | (0xFull << 0x38);
+        uint32_t l = lead, slow = 0;
+        while (l) {
+            const uint32_t k = __builtin_ctz(l);
+            l &= l - 1u;
+            const uint32_t x = lds4(win, k);
+            const uint32_t b0 = x & 0xFFu;
+            const uint32_t r = ((b0 & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
+            const bool plain = (b0 - 0xE1u < 12u) | (b0 - 0xEEu < 2u);
+            const bool rare = (r - 0x2E80u < 0x180u) | (r - 0xF900u < 0x200u);
+            const bool ok = ((x & 0x00C0C000u) == 0x00808000u) & (((uint32_t)(M >> (k + 1u)) & 3u) == 0u);
+            const uint32_t o = r - 0x3000u;
+            const bool h = (r - 0x4E00u <= 0x9FFCu - 0x4E00u) | (r - 0x3400u <= 0x4DBFu - 0x3400u) |
+                           ((o < 64u) & (((k3000 >> (o & 63u)) & 1ull) != 0ull));
+            const bool fast = plain & !(ok & rare);
+            slow |= (fast ? 0u : 1u) << k;
+            covered |= ((fast & ok) ? 3u : 0u) << (k + 1u);
+            hanb |= ((fast & ok & h) ? 7u : 0u) << k;
+        }
+        lead = slow;
+    }
     while (lead) {
         const uint32_t k = __builtin_ctz(lead);
         lead &= lead - 1u;
