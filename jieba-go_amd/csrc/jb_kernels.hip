@@ -605,33 +605,15 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     const uint32_t nwl = s_nwl;
     uint32_t head = (nwl * wv) >> 2;
     const uint32_t hi = (nwl * (wv + 1u)) >> 2;
+    // Walk state per lane: entry j of the current node's rune, start entry js,
+    // the current node's cell index id and base.  The record builds as an edge
+    // mask m and a shift register rw of weight indices (each new one enters at
+    // bit 50, so after k edges the first is at bit 50 - 14(k-1); shifting right
+    // by 14(4-k) puts it at bit 8, the record's layout).  One trip = one probe,
+    // with selects instead of branches (k_mark_walk is issue-bound).
     bool act = false, ovf = false;
-    uint32_t j = 0, js = 0, ecur = 0, id = 0, len = 0, nedge = 0;
-    uint64_t cur = 0;  // the cell of the walk's current node
-    uint64_t rc = 0;
-    auto edge = [&](uint32_t L, uint32_t wi) {
-        if (L > kEdgeMaxL || nedge >= 4u || wi >= (1u << kEdgeIdxBits)) {
-            ovf = true;
-            return;
-        }
-        rc |= (1ull << (L - 1u)) | ((uint64_t)wi << (8u + kEdgeIdxBits * nedge));
-        nedge++;
-    };
-    auto finish = [&]() {  // the record waits in the start entry's LDS cell (read when the walk began)
-        s_c[js] = ovf ? 0ull : rc;
-        act = false;
-    };
-    auto defer = [&]() {  // the run goes on past the lookahead: k_zh walks this rune itself
-        s_c[js] = 0ull;
-        act = false;
-    };
-    // after a hit on node `id` (cell `cur`) whose rune is entry ecur: go on, defer or stop
-    auto next_or_stop = [&]() {
-        if (!jb_cell_hc(cur) || ovf) finish();
-        else if (ecur & kEntCont) act = true;
-        else if (ecur & kEntEdge) defer();
-        else finish();  // the Han run ends
-    };
+    uint32_t j = 0, js = 0, id = 0, base = 0, len = 0, nedge = 0, m = 0;
+    uint64_t rw = 0;
     for (;;) {
         const uint64_t need = __ballot(!act);
         const uint32_t rank =
@@ -640,33 +622,42 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         const bool fresh = !act && j0 < hi;
         head = min(hi, head + (uint32_t)__popcll(need));
         if (fresh) {  // a walk from the list: its rune has children and the run goes on in the tile
-            j = s_wl[j0];
-            js = j;
-            ecur = ent[j];
-            cur = s_c[j];
-            id = ent_code(ecur);  // its level-1 cell
+            js = s_wl[j0];
+            j = js;
+            const uint64_t c = s_c[j];
+            id = ent_code(ent[j]);  // its level-1 cell
+            base = jb_cell_base(c);
+            const bool pos = jb_cell_fc(c) == JB_FC_POS;  // (weight index < 2^14: checked by the run links)
+            m = pos ? 1u : 0u;
+            nedge = m;
+            rw = pos ? (uint64_t)jb_cell_widx(c) << 50 : 0ull;
             len = 1u;
-            nedge = 0u;
             ovf = false;
-            rc = jb_cell_fc(cur) == JB_FC_POS ? 1ull | ((uint64_t)jb_cell_widx(cur) << 8) : 0ull;
-            nedge = jb_cell_fc(cur) == JB_FC_POS ? 1u : 0u;
             act = true;
         }
-        // one round trip: the next rune's cell for every walk under way
-        if (act) {
+        if (act) {  // one round trip: the next rune's cell
             const uint32_t en = ent[j + 1u];
-            const uint32_t t = dat_slot_k(cur, ent_code(en));
+            const uint32_t t = base + ent_code(en);
             const uint64_t child = im.cells[t];
-            if (dat_hit(child, id)) {
-                ++j;
-                ecur = en;
-                id = t;
-                cur = child;
-                len++;
-                if (jb_cell_fc(child) == JB_FC_POS) edge(len, jb_cell_widx(child));
-                next_or_stop();
-            } else {
-                finish();  // (:475-478)
+            const bool hit = dat_hit(child, id);
+            ++len;
+            const uint32_t wi = jb_cell_widx(child);
+            const bool pos = hit && jb_cell_fc(child) == JB_FC_POS;
+            const bool bad = pos && (len > kEdgeMaxL || nedge >= 4u || wi >= (1u << kEdgeIdxBits));
+            const bool add = pos && !bad;
+            ovf |= bad;
+            m |= add ? 1u << ((len - 1u) & 7u) : 0u;
+            rw = add ? (rw >> kEdgeIdxBits) | ((uint64_t)wi << 50) : rw;
+            nedge += add ? 1u : 0u;
+            const bool more = hit && jb_cell_hc(child) && !ovf;
+            const bool go = more && (en & kEntCont);
+            const bool dfr = more && !(en & kEntCont) && (en & kEntEdge);  // past the lookahead: k_zh walks it
+            ++j;
+            id = t;
+            base = jb_cell_base(child);
+            if (!go) {  // the record goes to the start entry's LDS cell (read when the walk began)
+                s_c[js] = (ovf || dfr) ? 0ull : ((uint64_t)m | (rw >> (kEdgeIdxBits * (4u - nedge))));
+                act = false;
             }
         }
         trips++;
