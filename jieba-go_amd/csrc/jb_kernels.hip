@@ -1106,6 +1106,25 @@ __device__ __forceinline__ void rec_fold(uint32_t m, const double w[4], DpFold& 
     }
 }
 
+// The same with the {n, 0.0} sentinel kept in the ring: the caller writes 0.0
+// to slot 0 when a block (re)starts at c = 1, so the edge with L == c reads
+// best(n) = 0.0 from slot (c - L) & 7 = 0, which step 8 is the first to
+// overwrite (after its reads).  No per-edge select for the sentinel.
+__device__ __forceinline__ void rec_fold_s(uint32_t m, const double w[4], DpFold& f, uint32_t c, const double* ring) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const bool has = m != 0u;
+        const uint32_t L = has ? (uint32_t)__builtin_ctz(m) + 1u : 1u;
+        m &= m - 1u;
+        const double pp = w[k] + ring[((c - L) & (kZhRing - 1u)) * 64u];
+        const bool take = has && pp >= f.prevP;
+        f.bestL = take ? L : f.bestL;
+        f.bestP = take ? pp : f.bestP;
+        f.prevP = has ? pp : f.prevP;
+        f.lastL = has ? L : f.lastL;
+    }
+}
+
 // General form (any rune widths): the next rune's record is loaded one step ahead.
 template <class V, class Src>
 __device__ uint32_t zh_dp(const V& v, const DevImage& im, const uint64_t* __restrict__ erec,
@@ -1198,6 +1217,7 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
         q = be - 3u;
         c = 1;
         s = q / 3u;
+        ring[0] = 0.0;  // best(n), the {n, 0.0} sentinel (rec_fold_s)
     };
     // One rune.  r1: the next rune's record (landed a step ago); wc: this rune's
     // weights (loaded a step ago); wn: gets the next rune's.  Weight registers
@@ -1210,7 +1230,7 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
         const uint32_t mn = (uint32_t)r1v & 0xFFu;
         rec_weights(im, r1v, wn);
         DpFold f;
-        rec_fold(mc, wc, f, c, ring);
+        rec_fold_s(mc, wc, f, c, ring);
         if (mc == 0u) dp_walk_rune(v, im, q, be, f, c, ring, longm, gbest, key0);  // overflowed record (rare)
         f.finish();
         ring[(c & (kZhRing - 1u)) * 64u] = f.bestP;
