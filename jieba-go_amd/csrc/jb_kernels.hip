@@ -436,29 +436,45 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         lead |= ((f * 0x204081u) >> 21 & 0xFu) << (4 * j);
     }
     uint32_t covered = 0, hanb = 0;
+    uint64_t cl[7];        // level-1 rows of the lane's Han starts, by slot (see below)
+    uint32_t hsm = 0, kp = 0;  // slots holding one; their byte offsets in the lane, 4 bits per slot
+    uint32_t rowp[4] = {0u, 0u, 0u, 0u};  // their level-1 rows, 16 bits per slot
     {  // Plain 3-byte leads (E1..EC, EE, EF: no overlong or surrogate bound on the
        // second byte) with a common Han value or none, the leads of nearly all
        // Chinese text, in a short loop; every other lead (2- and 4-byte forms, E0,
        // ED, the rare Han ranges) goes to the general decode below.
         constexpr uint64_t k3000 = (1ull << 5) | (1ull << 7) | (0x1FFull << 0x21) | (0xFull << 0x38);
+        // Unrolled over the first 7 leads (a 20-byte window of 3-byte runes has at most
+        // 7), so that each lead has fixed registers: a Han rune of the common ranges
+        // starting in the lane's own bytes issues its level-1 load here (slot i),
+        // in flight during the block scan.  Leads past the 7th go to the general decode.
         uint32_t l = lead, slow = 0;
-        while (l) {
-            const uint32_t k = __builtin_ctz(l);
-            l &= l - 1u;
-            const uint32_t x = lds4(win, k);
-            const uint32_t b0 = x & 0xFFu;
-            const uint32_t r = ((b0 & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
-            const bool plain = (b0 - 0xE1u < 12u) | (b0 - 0xEEu < 2u);
-            const bool rare = (r - 0x2E80u < 0x180u) | (r - 0xF900u < 0x200u);
-            const bool ok = ((x & 0x00C0C000u) == 0x00808000u) & (((uint32_t)(M >> (k + 1u)) & 3u) == 0u);
-            const uint32_t o = r - 0x3000u;
-            const bool h = (r - 0x4E00u <= 0x9FFCu - 0x4E00u) | (r - 0x3400u <= 0x4DBFu - 0x3400u) |
-                           ((o < 64u) & (((k3000 >> (o & 63u)) & 1ull) != 0ull));
-            const bool fast = plain & !(ok & rare);
-            slow |= (fast ? 0u : 1u) << k;
-            covered |= ((fast & ok) ? 3u : 0u) << (k + 1u);
-            hanb |= ((fast & ok & h) ? 7u : 0u) << k;
+#pragma unroll
+        for (int i = 0; i < 7; i++) {
+            if (l) {
+                const uint32_t k = __builtin_ctz(l);
+                l &= l - 1u;
+                const uint32_t x = lds4(win, k);
+                const uint32_t b0 = x & 0xFFu;
+                const uint32_t r = ((b0 & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
+                const bool plain = (b0 - 0xE1u < 12u) | (b0 - 0xEEu < 2u);
+                const bool rare = (r - 0x2E80u < 0x180u) | (r - 0xF900u < 0x200u);
+                const bool ok = ((x & 0x00C0C000u) == 0x00808000u) & (((uint32_t)(M >> (k + 1u)) & 3u) == 0u);
+                const uint32_t o = r - 0x3000u;
+                const bool h = (r - 0x4E00u <= 0x9FFCu - 0x4E00u) | (r - 0x3400u <= 0x4DBFu - 0x3400u) |
+                               ((o < 64u) & (((k3000 >> (o & 63u)) & 1ull) != 0ull));
+                const bool fast = plain & !(ok & rare);
+                slow |= (fast ? 0u : 1u) << k;
+                covered |= ((fast & ok) ? 3u : 0u) << (k + 1u);
+                hanb |= ((fast & ok & h) ? 7u : 0u) << k;
+                if (fast & ok & h & (k >= 4u) & (r >= JB_DIRECT_LO)) {  // (rows of U+3400..U+9FFF are direct)
+                    rowp[i >> 1] |= (r - 0x3300u) << (16 * (i & 1));
+                    hsm |= 1u << i;
+                    kp |= (k - 4u) << (4 * i);
+                }
+            }
         }
+        slow |= l;
         lead = slow;
     }
     while (lead) {
@@ -483,45 +499,53 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
 
     // ---- (2) Han rune entries of the tile, in text order ---------------------------
     uint32_t hs = ((hanb & ~covered & valid) >> 4) & 0xFFFFu;  // Han rune starts of the lane's bytes
+#pragma unroll
+    for (int i = 0; i < 7; i++)  // the level-1 loads, in flight during the entry scan
+        cl[i] = ((hsm >> i) & 1u) ? im.l1row[(rowp[i >> 1] >> (16 * (i & 1))) & 0xFFFFu] : 0ull;
     uint32_t nent;
     uint32_t o = block_scan_u32(__popc(hs), lds, &nent);
     bool has4 = false;  // a 4-byte Han rune starts in the lane's bytes
     {
-        // at most 6 Han runes start in a lane's 16 bytes: decode them and issue all
-        // code loads, then all level-1 cell loads (two round trips, not two per rune)
-        const uint32_t ne = __popc(hs);
-        uint32_t kk[6], rr[6], cd[6];
-        uint64_t cl[6];
-        uint32_t lastend = 0;  // window index past the lane's last Han rune
+        // Slot i of the lane holds its Han rune number popc(hsm & ((1 << i) - 1)).
+        // A lane with a Han start the fast loop did not take (a 4-byte rune, the
+        // U+3000 page, past 7 leads) decodes all of its starts again here, slots =
+        // rune numbers (at most 6 Han runes start in 16 bytes).
+        uint32_t w4m = 0;
+        if (__popc(hs) != __popc(hsm)) {
+            const uint32_t ne = __popc(hs);
+            uint32_t h2 = hs;
+            hsm = 0;
+            kp = 0;
 #pragma unroll
-        for (int i = 0; i < 6; i++) {
-            kk[i] = 0u;
-            rr[i] = 0u;
-            cl[i] = 0ull;
-            if ((uint32_t)i < ne) {
-                const uint32_t k = (uint32_t)__builtin_ctz(hs);
-                hs &= hs - 1u;
-                const uint32_t x = lds4(win, k + 4u);
-                const uint32_t r = (x & 0xF0u) == 0xE0u
-                                       ? ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu)
-                                       : ((x & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) |
-                                             (((x >> 16) & 0x3Fu) << 6) | ((x >> 24) & 0x3Fu);
-                kk[i] = k;
-                rr[i] = r;
-                cl[i] = im.l1row[jb_row(im.pagemap, r)];  // code and level-1 cell: one load per rune
-                has4 |= r >= 0x10000u;
-                lastend = k + 4u + (r >= 0x10000u ? 4u : 3u);
+            for (int i = 0; i < 6; i++) {
+                cl[i] = 0ull;
+                if ((uint32_t)i < ne) {
+                    const uint32_t k = (uint32_t)__builtin_ctz(h2);
+                    h2 &= h2 - 1u;
+                    const uint32_t x = lds4(win, k + 4u);
+                    const uint32_t r = (x & 0xF0u) == 0xE0u
+                                           ? ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu)
+                                           : ((x & 0x07u) << 18) | (((x >> 8) & 0x3Fu) << 12) |
+                                                 (((x >> 16) & 0x3Fu) << 6) | ((x >> 24) & 0x3Fu);
+                    cl[i] = im.l1row[jb_row(im.pagemap, r)];  // code and level-1 cell: one load per rune
+                    hsm |= 1u << i;
+                    kp |= k << (4 * i);
+                    w4m |= (r >= 0x10000u ? 1u : 0u) << i;
+                }
             }
+            cl[6] = 0ull;
         }
+        has4 = w4m != 0u;
+        const uint32_t top = hsm ? 31u - (uint32_t)__builtin_clz(hsm) : 0u;
+        const uint32_t lastend =  // window index past the lane's last Han rune
+            hsm ? ((kp >> (4u * top)) & 15u) + 4u + 3u + ((w4m >> top) & 1u) : 0u;
 #pragma unroll
-        for (int i = 0; i < 6; i++) {
-            cd[i] = jb_l1row_code(cl[i]);
-            cl[i] = ((uint32_t)i < ne && !(ablate & 2u)) ? jb_l1row_cell(cl[i]) : 0ull;
+        for (int i = 0; i < 7; i++) {  // (s_e is not under the staged text)
+            if ((hsm >> i) & 1u)
+                s_e[o + __popc(hsm & ((1u << i) - 1u))] = jb_l1row_code(cl[i]) | (((w4m >> i) & 1u) << 17) |
+                                                          ((threadIdx.x * 16u + ((kp >> (4 * i)) & 15u)) << 18);
+            cl[i] = (((hsm >> i) & 1u) && !(ablate & 2u)) ? jb_l1row_cell(cl[i]) : 0ull;
         }
-#pragma unroll
-        for (int i = 0; i < 6; i++)  // (s_e is not under the staged text)
-            if ((uint32_t)i < ne)
-                s_e[o + i] = cd[i] | ((rr[i] >= 0x10000u ? 1u : 0u) << 17) | ((threadIdx.x * 16u + kk[i]) << 18);
         // Lookahead (the last lane, while the cell loads fly): when the tile's last
         // Han rune ends at or past the tile end, the runes that continue its run
         // (same document, Go-valid, Han) in the next kLABytes bytes become entries
@@ -564,8 +588,8 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         __syncthreads();  // every lane has decoded from s_t: its bytes now take the cells
         if (stamps) c1b = __builtin_amdgcn_s_memtime();  // (codes, cells and lookahead in)
 #pragma unroll
-        for (int i = 0; i < 6; i++)
-            if ((uint32_t)i < ne) s_c[o + i] = cl[i];
+        for (int i = 0; i < 7; i++)
+            if ((hsm >> i) & 1u) s_c[o + __popc(hsm & ((1u << i) - 1u))] = cl[i];
     }
     __syncthreads();
     // Run links, then level 1 of every entry: a rune that is absent, has count 0,
