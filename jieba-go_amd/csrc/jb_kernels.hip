@@ -552,38 +552,43 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         // nent.. so that walks go on through them like any other (their records
         // belong to the next tile and are not written here).  A walk that reaches
         // past the last of them gets record 0: k_zh walks that rune itself.
-        uint32_t la_cd[kLA], nla = 0, la_w4 = 0;  // (only the last lane has any)
-        bool la_go = threadIdx.x == 255u && lastend >= 20u;
-        uint32_t q = kTileBytes + lastend - 20u;  // tile offset of the rune after it
-#pragma unroll
-        for (int i = 0; i < (int)kLA; i++) {
-            la_cd[i] = 0u;
-            if (la_go && q < kTileBytes + kLABytes) {
+        // The last wave does it, one candidate position per lane: lane j decodes at
+        // tile offset kTileBytes + j (j < kLABytes) and loads that rune's code;
+        // the chain from the rune after lane 255's last one is then walked on the
+        // ballot masks (scalar), and each lane on it writes its entry.  (One lane
+        // stepping rune by rune took a long serial chain and a large code body.)
+        const uint32_t le255 = __builtin_amdgcn_readlane(lastend, 63);  // (meaningful in the last wave)
+        if (threadIdx.x >= 192u && le255 >= 20u) {
+            const uint32_t j = threadIdx.x & 63u, q = kTileBytes + j;
+            uint32_t w = 0, r = 0;
+            if (j < kLABytes) {
                 const uint64_t db = ((((uint64_t)s_db[(q >> 5) + 1u]) << 32) | s_db[q >> 5]) >> (q & 31u);
                 uint32_t lim = 1u + (uint32_t)__builtin_ctzll(((db >> 1) & 7ull) | 8ull);
                 const uint64_t gq = t0 + q;
                 if (gq + lim > nbytes) lim = gq < nbytes ? (uint32_t)(nbytes - gq) : 0u;
-                uint32_t w = 0;
-                const uint32_t r = (db & 1ull) ? 0u : han_rune(lds4(s_t, q + 16u), lim, &w);
-                if (r) {
-                    la_cd[i] = rune_code(im, r);
-                    la_w4 |= (w == 4u ? 1u : 0u) << i;
-                    nla = (uint32_t)i + 1u;
-                    q += w;
-                } else {
-                    la_go = false;
-                }
-            } else {
-                la_go = false;
+                r = (db & 1ull) ? 0u : han_rune(lds4(s_t, q + 16u), lim, &w);
             }
-        }
-        if (nla) {
+            const uint32_t cdj = r ? rune_code(im, r) : 0u;
+            const uint64_t hm = __ballot(r != 0u), w4b = __ballot(w == 4u);
+            // the chain (wave-uniform): runes at jj, jj + w, ... while Han, at most kLA
+            uint64_t chain = 0;
+            uint32_t jj = le255 - 20u, n = 0;
+            bool go = true;
 #pragma unroll
-            for (int i = 0; i < (int)kLA; i++)
-                if ((uint32_t)i < nla)  // the last one: the run may go on (all kLA decoded) or ends
-                    s_e[nent + i] = la_cd[i] | (((la_w4 >> i) & 1u) << 17) |
-                                    ((uint32_t)i + 1u < nla ? kEntCont : (la_go ? kEntEdge : 0u));
-            s_nla = nla;
+            for (int i = 0; i < (int)kLA; i++) {
+                if (go && jj < kLABytes && ((hm >> jj) & 1ull)) {
+                    chain |= 1ull << jj;
+                    n++;
+                    jj += ((w4b >> jj) & 1ull) ? 4u : 3u;
+                } else {
+                    go = false;
+                }
+            }
+            if ((chain >> j) & 1ull) {  // the last one: the run may go on (all kLA decoded) or ends
+                const uint32_t ix = (uint32_t)__popcll(chain & ((1ull << j) - 1ull));
+                s_e[nent + ix] = cdj | ((w == 4u ? 1u : 0u) << 17) | (ix + 1u < n ? kEntCont : (go ? kEntEdge : 0u));
+            }
+            if (j == 0u) s_nla = n;
         }
         __syncthreads();  // every lane has decoded from s_t: its bytes now take the cells
         if (stamps) c1b = __builtin_amdgcn_s_memtime();  // (codes, cells and lookahead in)
