@@ -1309,7 +1309,10 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
 // (rs - wb) | (re - wb) << 16.  The forward walk only lists the runs; the
 // Viterbis then run with every lane on its r-th run at once, instead of one
 // divergent Viterbi whenever some lane's walk reaches the end of a run.
-constexpr uint32_t kZhRuns = 4;
+#ifndef JB_ZH_RUNS
+#define JB_ZH_RUNS 4
+#endif
+constexpr uint32_t kZhRuns = JB_ZH_RUNS;
 struct RunList {
     uint32_t* t;
     uint32_t wb;
