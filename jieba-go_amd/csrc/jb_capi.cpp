@@ -454,7 +454,7 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.erec, (nb / 3 + 8 + kErecPad) * 8));
     HIPCHK(hipMalloc(&w.lanemask, ntiles * 256 * 4));
     HIPCHK(hipMalloc(&w.gbl, nb / 3 + 8));
-    HIPCHK(hipMalloc(&w.gstart, (nb / kZhGroupBytes + 4) * sizeof(uint2)));
+    HIPCHK(hipMalloc(&w.gstart, (nb / kZhGroupSmall + 4) * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.tile4, ntiles * 4));
     HIPCHK(hipMalloc(&w.longblk, (nb / kZhLongMin + 2) * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.gbest, (nb / 3 + 8) * sizeof(double)));

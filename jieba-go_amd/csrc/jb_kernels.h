@@ -40,6 +40,8 @@ constexpr int kTokTileWords = 512;     // k_tok: 256 threads x 2 words (16 KiB o
 #endif
 constexpr uint32_t kErecPad = 8;  // erec slots before slot 0 (k_zh reads a few slots past a block's start)
 constexpr uint32_t kZhGroupBytes = JB_ZH_GROUP;
+constexpr uint32_t kZhGroupSmall = 1024;         // the k_zh group of batches under kZhSmallBatch bytes
+constexpr uint64_t kZhSmallBatch = 16ull << 20;
 constexpr uint32_t kZhLongMin = 8192;  // zh blocks of at least this many bytes go to k_zh_long  // k_zh work unit: zh blocks starting in one such span (multiple of 32)
 
 // Per-call device workspace, sized for `nbytes` of text.

@@ -710,14 +710,14 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
 }
 
 // k_blocks_write: the lane masks -> block list (start | zh<<31).
-// The thread whose 16 bytes begin a k_zh group (g * kZhGroupBytes) also writes
+// The thread whose 16 bytes begin a k_zh group (g * grp) also writes
 // gstart[g] = (blocks, zh blocks) that start before it.
 constexpr uint32_t kBwTiles = 4;  // k_blocks_write: tiles per workgroup
 __global__ __launch_bounds__(256) void k_blocks_write(const uint32_t* __restrict__ lanemask,
                                                       const uint2* __restrict__ tile_cnt,
                                                       const uint2* __restrict__ supb, uint32_t* __restrict__ blk,
                                                       uint2* __restrict__ gstart, uint32_t* __restrict__ counters,
-                                                      uint32_t nbytes, uint32_t ntiles) {
+                                                      uint32_t nbytes, uint32_t ntiles, uint32_t grp) {
     __shared__ uint32_t lds[8];
     const uint32_t tb = blockIdx.x * kBwTiles;
     const PrefixLoads pl = pf_load(tile_cnt, supb, tb);
@@ -733,8 +733,7 @@ __global__ __launch_bounds__(256) void k_blocks_write(const uint32_t* __restrict
         uint32_t tot;
         const uint32_t ex = block_scan_u32(__popc(bmask) | (__popc(zmask) << 16), lds, &tot);
         const uint32_t p0 = (t * 256u + threadIdx.x) * 16u;
-        if (p0 % kZhGroupBytes == 0u)
-            gstart[p0 / kZhGroupBytes] = make_uint2(to.x + (ex & 0xFFFFu), to.y + (ex >> 16));
+        if (p0 % grp == 0u) gstart[p0 / grp] = make_uint2(to.x + (ex & 0xFFFFu), to.y + (ex >> 16));
         uint32_t ga = to.x + (ex & 0xFFFFu);  // global block rank
         uint32_t b = bmask;
         while (b) {
@@ -1566,7 +1565,7 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
                                             const uint64_t* __restrict__ erec, uint8_t* __restrict__ gbl,
                                             double* __restrict__ gbest,
                                             uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
-                                            uint2* __restrict__ longblk,
+                                            uint2* __restrict__ longblk, uint32_t grp,
                                             uint32_t ablate, uint64_t* __restrict__ dbg) {
     __shared__ uint8_t s_bl[4][kZhWin / 3u + 4u];
     __shared__ double s_rb[4][kZhRing * 64];  // DP ring, then the window's token bitmaps
@@ -1579,7 +1578,7 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
     uint32_t* tbl = s_tbl[wv];
     uint32_t* hist = s_hist[wv];
     const uint32_t nblk = counters[CNT_NBLK], nzh = counters[CNT_NZH];
-    const uint32_t ngroups = (uint32_t)((nbytes + kZhGroupBytes - 1u) / kZhGroupBytes);
+    const uint32_t ngroups = (uint32_t)((nbytes + grp - 1u) / grp);  // (grp <= kZhGroupBytes)
     const uint32_t ntiles = (uint32_t)((nbytes + kTileBytes - 1u) / kTileBytes);
     Emitter em(sbits, ebits);
     em.off = (ablate & 128u) != 0;
@@ -1600,7 +1599,7 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
         const uint2 g0 = gstart[g];
         const uint2 g1 = (g + 1u < ngroups) ? gstart[g + 1u] : make_uint2(nblk, nzh);
         if (g0.y >= g1.y) continue;  // no Han block starts here
-        const uint32_t wb = g * kZhGroupBytes, wend = wb + kZhWin;
+        const uint32_t wb = g * grp, wend = wb + grp + (kZhWin - kZhGroupBytes);
         // all-3-byte window: no 4-byte Han rune starts in the tiles under it
         bool any4 = false;
         {
@@ -2276,6 +2275,8 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                         hipStream_t stream, KernelTimer* timer) {
     const uint64_t nwords = (nbytes + 31) / 32;
     const uint32_t ntiles = (uint32_t)((nbytes + kTileBytes - 1) / kTileBytes);
+    // k_zh work unit: a small batch gets small groups, so that enough waves share it
+    const uint32_t grp = nbytes < kZhSmallBatch ? kZhGroupSmall : kZhGroupBytes;
     const uint32_t nttiles = (uint32_t)((nwords + kTokTileWords - 1) / kTokTileWords);
     hipError_t e;
     if ((e = hipMemsetAsync(w.counters, 0, CNT_NWORDS * sizeof(uint32_t) + sizeof(uint64_t), stream))) return e;
@@ -2295,15 +2296,15 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                                ntiles, w.supb));
     JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL(k_blocks_write, dim3((ntiles + kBwTiles - 1) / kBwTiles), dim3(256), 0,
                                                 stream, w.lanemask, w.tile_cnt, w.supb, w.blk, w.gstart, w.counters,
-                                                (uint32_t)nbytes, ntiles));
+                                                (uint32_t)nbytes, ntiles, grp));
     if (hmm)
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
                                           w.gstart, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
-                                          w.longblk, g_ablate, w.dbg));
+                                          w.longblk, grp, g_ablate, w.dbg));
     else
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
                                           w.gstart, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
-                                          w.longblk, g_ablate, w.dbg));
+                                          w.longblk, grp, g_ablate, w.dbg));
     if (hmm)
         JB_TIMED(K_ZH_LONG, hipLaunchKernelGGL((k_zh_long<true>), dim3(kZhLongGrid), dim3(64), 0, stream, d_text, im,
                                                w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters, w.sbits,
