@@ -1,21 +1,31 @@
 #!/usr/bin/env python3
 """bench.py — jieba-go Cut on MI355X: UTF-8 Chinese chars/s segmented.
 
-Workload (BASELINE.json config 4, "1 GB synthetic Zipf corpus, doc-sharded
-across 8 GPUs"): every rank segments its own shard of the synthetic C_syn
-corpus — 1 GiB / 8 = 128 MiB of documents per GPU, HMM on (the reference's
-big-text benchmark setting, tokenizer_test.go:510,521) — with the 350k-word
-D_syn dictionary and E_syn emissions.  Per-GPU work is fixed,
-so N GPUs process N x 128 MiB (weak scaling; N = 8 is config 4).  A step is
-one full Cut pass (all kernels, spans out) over the shard, inputs resident in
-HBM.  Documents shard with no data-path collective; ranks only meet at the
-timing barriers.
+Headline workload (BASELINE.json configs[3], the config the metric is quoted
+on): ONE fixed 1 GiB corpus of synthetic C_syn documents (seeded Zipf text,
+SURVEY.md §8d), cut with HMM on (the reference's big-text benchmark setting,
+tokenizer_test.go:608-609) against the 350k-word D_syn dictionary and E_syn
+emissions.  `--gpus N` strong-scales that same corpus: rank r cuts the
+byte-balanced document range shard.shard_bounds(...)[r] (jb_shard_bounds, the
+rule jb_cut_batch uses across the devices of one context), so N = 1 cuts the
+whole GiB on one GPU.  Documents are independent (tokenizer.go:158-160): no
+data-path collective, ranks only meet at the timing barriers and for the
+job-level sums.
 
-Prints one JSON line (rank 0).  `roofline` is for the dominant kernel (by
-average launch time; `roofline_kernels` has both big kernels),
-`cpu_baseline` is the oracle (C restatement of tokenizer.go) on this host's
-cores over a bounded sample of the same shard, checked token for token
-against the GPU output of the same documents.
+A step is one full Cut pass (every kernel, token spans out) over the rank's
+shard, inputs already resident in HBM.  `value` = all ranks' runes x K / the
+slowest rank's time for the K timed steps.
+
+After timing, every rank downloads its spans and checks ALL of its shard
+token for token against the oracle (oracle/jieba_oracle.c, the C restatement
+of tokenizer.go) on the host's CPUs; at N = 1 that full-corpus oracle run is
+also `cpu_baseline` (threads = the CPUs this process may use).  `roofline` is
+the dominant kernel's, from HIP event pairs around each launch on the launch
+stream (a second pass of the K steps, kernel by kernel).
+
+Other BASELINE configs: --workload sentence (config 1: jb_cut latency on the
+19-rune sentence of tokenizer_test.go:531), s10k (configs 2/3 with --hmm 0/1),
+long-punct / long-oov (configs 5a / 5b).
 """
 import argparse
 import json
@@ -28,39 +38,389 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 for _sub in ("oracle", "gen", os.path.join("jieba-go_amd", "python")):
-    sys.path.insert(0, os.path.join(ROOT, _sub))
+    _p = os.path.join(ROOT, _sub)
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 HBM_MEASURED_GBS = 6290.0   # float4 copy, same guide
-DOC_STRIDE = 10_000_000     # rank r generates documents r*DOC_STRIDE, r*DOC_STRIDE+1, ...
+METRIC = "UTF-8 Chinese chars/sec segmented (whole node) + achieved HBM GB/s vs peak"
+SENTENCE = "我昨天去上海交通大學與老師討論量子力學"  # tokenizer_test.go:531
+REF_SENTENCE_NS = 30726                         # tokenizer_test.go:610 (i5-9400)
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
 
 
-def han_bytes(buf, n):
-    """Bytes of `buf[:n]` that belong to \\p{Han} runes (3-byte BMP Han + 4-byte Han)."""
-    b = buf[:n]
-    lead3 = np.nonzero((b[:-2] >= 0xE0) & (b[:-2] < 0xF0))[0]
-    cp = ((b[lead3].astype(np.uint32) & 0x0F) << 12) | ((b[lead3 + 1].astype(np.uint32) & 0x3F) << 6) | \
-        (b[lead3 + 2].astype(np.uint32) & 0x3F)
-    h3 = ((cp >= 0x3400) & (cp <= 0x4DBF)) | ((cp >= 0x4E00) & (cp <= 0x9FFC)) | \
-        ((cp >= 0x2E80) & (cp <= 0x2FD5)) | ((cp >= 0xF900) & (cp <= 0xFAD9)) | (cp == 0x3005) | (cp == 0x3007) | \
-        ((cp >= 0x3021) & (cp <= 0x3029)) | ((cp >= 0x3038) & (cp <= 0x303B))
-    lead4 = int(np.count_nonzero((b >= 0xF0) & (b <= 0xF4)))  # synthetic corpora hold no 4-byte runes
-    return int(h3.sum()) * 3 + lead4 * 4
-
-
-def load_pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (separate
-    rocprofv3 --pmc passes, FETCH_SIZE x2 gfx950 correction), or None."""
-    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+# ---------------------------------------------------------------------------
+# host helpers
+# ---------------------------------------------------------------------------
+def effective_cpus():
+    """CPUs this process may use: its affinity set, capped by a cgroup CPU quota
+    (cpu.max) when one is set.  On the GPU box `nproc` shows the whole machine
+    while the job's share is enforced by the quota."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
     try:
-        with open(p) as f:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), n, quota
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def han_bytes(buf, n, chunk=64 << 20):
+    """Bytes of buf[:n] that belong to \\p{Han} runes (3-byte BMP Han + 4-byte forms)."""
+    total = 0
+    for a in range(0, n, chunk):
+        b = np.asarray(buf[a:min(n, a + chunk) + 2])
+        m = len(b) - 2 if a + chunk < n else min(len(b), n - a)
+        lead3 = np.nonzero((b[:m] >= 0xE0) & (b[:m] < 0xF0))[0]
+        lead3 = lead3[lead3 + 2 < len(b)]
+        cp = ((b[lead3].astype(np.uint32) & 0x0F) << 12) | ((b[lead3 + 1].astype(np.uint32) & 0x3F) << 6) | \
+            (b[lead3 + 2].astype(np.uint32) & 0x3F)
+        h3 = ((cp >= 0x3400) & (cp <= 0x4DBF)) | ((cp >= 0x4E00) & (cp <= 0x9FFC)) | \
+            ((cp >= 0x2E80) & (cp <= 0x2FD5)) | ((cp >= 0xF900) & (cp <= 0xFAD9)) | (cp == 0x3005) | \
+            (cp == 0x3007) | ((cp >= 0x3021) & (cp <= 0x3029)) | ((cp >= 0x3038) & (cp <= 0x303B))
+        total += int(h3.sum()) * 3 + int(np.count_nonzero((b[:m] >= 0xF0) & (b[:m] <= 0xF4))) * 4
+    return total
+
+
+def count_runes(buf, n, chunk=256 << 20):
+    return sum(int(np.count_nonzero((np.asarray(buf[a:min(n, a + chunk)]) & 0xC0) != 0x80))
+               for a in range(0, n, chunk))
+
+
+def load_pmc_traffic(kernel, workload_key):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (separate
+    rocprofv3 --pmc passes, corrected as MI355X_MICROARCH.md prescribes), when
+    that summary was collected on this same workload; else None."""
+    try:
+        with open(PMC_FILE) as f:
             d = json.load(f)
+        if d.get("workload_key") != workload_key:
+            return None
         for name, e in d["kernels"].items():  # e.g. "k_zh<true>" for kernel "k_zh"
             if name == kernel or name.startswith(kernel + "<"):
                 return e["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+# ---------------------------------------------------------------------------
+# workload
+# ---------------------------------------------------------------------------
+def make_workload(args, s, rank):
+    """(buf, doc_off, description) of the WHOLE job's input (every rank builds the
+    same one and takes its shard) — or of this rank's own input for the
+    single-document / per-GPU workloads."""
+    import synth
+    if args.workload == "docs":
+        mib = args.corpus_mib
+        buf, off, _ = s.corpus_parallel(synth.KIND_DOCS, 0, target_bytes=int(mib * (1 << 20)),
+                                        threads=max(1, min(16, effective_cpus()[0])))
+        return buf, off, f"C_syn corpus, {mib:g} MiB fixed ({'1 GiB = config 4' if mib == 1024 else 'reduced'})"
+    if args.workload == "s10k":
+        buf, off, _ = s.corpus(synth.KIND_SENTENCES, 0, max_docs=10_000, target_bytes=64 << 20)
+        return buf, off, "S10k: 10,000 synthetic sentences (configs 2/3)"
+    if args.workload in ("long-punct", "long-oov"):
+        kind = synth.KIND_LONG_PUNCT if args.workload == "long-punct" else synth.KIND_LONG_OOV
+        buf, off, _ = s.corpus(kind, rank, target_runes=1_000_000)
+        return buf, off, ("L1M: one 1,000,000-rune document, " +
+                          ("punctuated (5a)" if args.workload == "long-punct" else "unpunctuated, 30% OOV (5b)"))
+    raise ValueError(args.workload)
+
+
+def shard_for(buf, off, world, rank, sharded):
+    """(shard buffer with 64 padding bytes, rebased offsets, first doc, base byte)."""
+    import shard
+    if not sharded or world == 1:
+        return buf, np.asarray(off, np.uint64), 0, 0
+    cut = shard.shard_bounds(off, world)
+    d0, d1 = cut[rank], cut[rank + 1]
+    base, end = int(off[d0]), int(off[d1])
+    sub = np.zeros(end - base + 64, np.uint8)
+    sub[: end - base] = buf[base:end]
+    return sub, np.asarray(off[d0:d1 + 1], np.uint64) - np.uint64(base), d0, base
+
+
+# ---------------------------------------------------------------------------
+# the measured path
+# ---------------------------------------------------------------------------
+class GpuCutter:
+    """jb_cut_device on HBM-resident input: one rank's shard, one GPU."""
+
+    def __init__(self, tk, buf, off, hmm, local):
+        import torch
+        import jiebahip as J
+        self.torch, self.J, self.tk = torch, J, tk
+        self.dev = torch.device("cuda", local)
+        self.nbytes = int(off[-1])
+        self.ndocs = len(off) - 1
+        self.hmm = bool(hmm)
+        self.d_text = torch.from_numpy(np.asarray(buf[: self.nbytes + 64])).to(self.dev)
+        self.d_off = torch.from_numpy(np.asarray(off, np.int64)).to(self.dev)
+        self.stream = torch.cuda.current_stream(self.dev).cuda_stream
+        self.ptrs = None
+
+    def step(self):
+        self.ptrs = self.tk.cut_device(self.d_text.data_ptr(), self.nbytes, self.d_off.data_ptr(), self.ndocs,
+                                       self.hmm, self.stream)
+
+    def sync(self):
+        self.torch.cuda.synchronize(self.dev)
+
+    def profile(self, steps):
+        """Per-kernel (total ms, launches) over `steps` more steps, launched kernel
+        by kernel with HIP events on the launch stream; and their ms per step."""
+        self.tk.profile(True)
+        self.tk.profile_reset()
+        self.sync()
+        t = time.perf_counter()
+        for _ in range(steps):
+            self.step()
+        self.sync()
+        ms = (time.perf_counter() - t) / steps * 1e3
+        k = self.tk.profile_read()
+        self.tk.profile(False)
+        return k, ms
+
+    def results(self):
+        """(starts u32, ends u32, doc_tok u64[ndocs+1]) of the last step."""
+        J = self.J
+        ps, pe, pd, pn = self.ptrs
+        self.sync()
+        ntok = int(J.dev_to_host(pn, 8, np.uint64)[0])
+        return (J.dev_to_host(ps, 4 * ntok, np.uint32), J.dev_to_host(pe, 4 * ntok, np.uint32),
+                J.dev_to_host(pd, 8 * (self.ndocs + 1), np.uint64))
+
+    def ties(self):
+        return self.tk.last_ties()
+
+
+def check_shard(results, o, buf, off, hmm, threads):
+    """The rank's GPU spans against the oracle over its WHOLE shard (timed: at
+    N = 1 this run is cpu_baseline).  Returns a dict."""
+    gs, ge, gd = results
+    t = time.perf_counter()
+    os_, oe, od = o.cut_batch(buf, off, bool(hmm), nthreads=threads)
+    cpu_s = time.perf_counter() - t
+    ok = bool(np.array_equal(gs, os_) and np.array_equal(ge, oe) and np.array_equal(gd, od))
+    mism = 0
+    if not ok:
+        n = min(len(gs), len(os_))
+        mism = int(np.count_nonzero((gs[:n] != os_[:n]) | (ge[:n] != oe[:n]))) + abs(len(gs) - len(os_))
+        mism = max(mism, 1)
+    return {"ok": ok, "mismatches": mism, "tokens": int(len(os_)), "gpu_tokens": int(len(gs)), "cpu_s": cpu_s,
+            "oracle_ties": int(o.ties)}
+
+
+def job_sums(dist, agg_dev, vals, op="sum"):
+    """Element-wise sum (or max) of a list of floats over ranks."""
+    if dist is None:
+        return [float(v) for v in vals]
+    import torch
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=agg_dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+    return [float(x) for x in t.tolist()]
+
+
+def roofline_of(kernels, units, traffic_of):
+    """Algorithmic bytes: 1 B read per byte of a kernel's units +
+    2 output bits per byte = 1.25 B per unit byte.  Units: every input byte for
+    k_mark_walk (it classifies and walks the whole batch), the Han bytes for
+    k_zh / k_zh_long (DP + Viterbi over zh blocks)."""
+    out = {}
+    for kname, u in units.items():
+        kk = kernels.get(kname)
+        if not kk or not u:
+            continue
+        alg = 1.25 * u
+        achieved = alg / (kk["avg_ms"] * 1e-3) / 1e9
+        out[kname] = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic_of(kname),
+                      "kernel": kname, "alg_bytes_per_launch": alg, "avg_launch_ms": kk["avg_ms"],
+                      "frac_of_measured_copy": round(achieved / HBM_MEASURED_GBS, 5)}
+    return out
+
+
+def run(args, world, rank, dist, agg_dev, make_cutter, open_oracle, log=print):
+    """Everything but process setup: workload, shard, timing, per-rank parity,
+    job-level aggregation.  make_cutter(buf, off, hmm) gives the rank's measured
+    path (GpuCutter on a GPU); open_oracle() the checker.  Returns rank 0's bench
+    line (a dict), None on other ranks."""
+    import synth
+    t0 = time.time()
+    s = synth.Synth(nwords=args.nwords)
+    sharded = args.workload == "docs"
+    buf, off, wdesc = make_workload(args, s, rank)
+    sbuf, soff, d0, base = shard_for(buf, off, world, rank, sharded)
+    if sharded and world > 1:
+        del buf
+    nbytes = int(soff[-1])
+    nrunes = count_runes(sbuf, nbytes)
+    hbytes = han_bytes(sbuf, nbytes)
+    gen_s = time.time() - t0
+
+    cutter = make_cutter(sbuf, soff, args.hmm)
+    for _ in range(args.warmup):
+        cutter.step()
+    cutter.sync()
+    if dist:
+        dist.barrier()
+    cutter.sync()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        cutter.step()
+    cutter.sync()
+    elapsed = time.perf_counter() - t
+    if dist:
+        dist.barrier()
+    results = cutter.results()
+    ties = cutter.ties()
+
+    kprof, prof_ms = ({}, None) if args.no_profile else cutter.profile(args.steps)
+    kernels = {k: {"avg_ms": ms / n, "launches": int(n)} for k, (ms, n) in kprof.items() if n}
+
+    # ---- parity: this rank's whole shard against the oracle ----------------
+    ncpu, nproc, quota = effective_cpus()
+    par = None
+    o = None
+    if not args.no_parity:
+        o = open_oracle()
+        import oracle as O
+        O.set_viterbi_backptr(args.workload.startswith("long"))  # path copy is O(m^2) on a 1M-rune run
+        par = check_shard(results, o, sbuf, soff, args.hmm, max(1, ncpu // world))
+
+    # ---- job-level aggregates ----------------------------------------------
+    (elapsed_max,) = job_sums(dist, agg_dev, [elapsed], "max")
+    sums = job_sums(dist, agg_dev, [nrunes, nbytes, hbytes, len(soff) - 1, ties,
+                                    par["mismatches"] if par else 0, par["tokens"] if par else 0,
+                                    0 if par is None else (0 if par["ok"] else 1),
+                                    par["oracle_ties"] if par else 0])
+    tot_runes, tot_bytes, tot_han, tot_docs, tot_ties, tot_mism, tot_tok, bad_ranks, tot_oties = sums
+
+    cpu = None
+    if rank == 0 and world == 1 and par is not None:
+        cpu = {"value": round(nrunes / par["cpu_s"], 1), "unit": "chars/s", "cores": max(1, ncpu // world),
+               "kind": "port",
+               "sample": (f"the whole workload ({nbytes / 2**20:.1f} MiB, {nrunes} chars, {len(soff) - 1} docs): "
+                          f"oracle/jieba_oracle.c (C restatement of tokenizer.go, "
+                          f"{'O(n) back-pointer' if args.workload.startswith('long') else 'literal path-copy'} "
+                          f"Viterbi), threads over documents, {par['cpu_s']:.2f} s; the same run is the parity check"),
+               "cpu_model": cpu_model(), "nproc": nproc, "cgroup_quota_cpus": quota}
+        if args.cpu1_sample_mib > 0 and args.workload == "docs":
+            lim = int(args.cpu1_sample_mib * (1 << 20))
+            d1 = max(1, min(len(soff) - 1, int(np.searchsorted(soff, min(lim, nbytes), side="right")) - 1))
+            b1 = int(soff[d1])
+            r1 = count_runes(sbuf, b1)
+            tc = time.perf_counter()
+            o.cut_batch(sbuf[: b1 + 16], soff[: d1 + 1], bool(args.hmm), nthreads=1)
+            c1 = time.perf_counter() - tc
+            cpu["value_1thread"] = round(r1 / c1, 1)
+            cpu["sample_1thread"] = f"first {d1} documents ({b1 / 2**20:.1f} MiB, {r1} chars), 1 thread, {c1:.2f} s"
+
+    if rank != 0:
         return None
-    except Exception:
-        return None
+    units = {"k_mark_walk": float(nbytes), "k_zh": float(hbytes)}
+    if args.workload == "long-oov":  # one unpunctuated block: its Han bytes all go through k_zh_long
+        units["k_zh_long"] = float(hbytes)
+    wkey = f"{args.workload}:{nbytes}:{'hmm' if args.hmm else 'nohmm'}:{args.dict_kind}"
+    rooflines = roofline_of(kernels, units, lambda k: load_pmc_traffic(k, wkey))
+    roof = None
+    if kernels:
+        dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
+        if dom in rooflines:
+            roof = dict(rooflines[dom], dominant_kernel=dom)
+        elif rooflines:
+            roof = dict(max(rooflines.values(), key=lambda r: r["avg_launch_ms"]), dominant_kernel=dom)
+    ms_per_step = elapsed_max / args.steps * 1e3
+    value = tot_runes * args.steps / elapsed_max
+    parity = None
+    if par is not None:
+        parity = {"scope": "every token of every rank's shard" if sharded else "every token of the workload",
+                  "bytes": int(tot_bytes), "docs": int(tot_docs), "tokens": int(tot_tok),
+                  "bit_exact": bad_ranks == 0 and tot_mism == 0, "mismatches": int(tot_mism),
+                  "ranks_checked": world, "oracle_threads_per_rank": max(1, ncpu // world)}
+    line = {
+        "metric": METRIC, "value": round(value, 1), "unit": "chars/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "scaling": "strong" if sharded else "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded D_syn 350k-word dict, E_syn emissions, C_syn Zipf corpus)",
+        "config": {"workload": f"{wdesc}, Cut hmm={'on' if args.hmm else 'off'}, "
+                               f"{'NewJiebaTokenizer (prefix dict, size 60,101,967)' if args.dict_kind == 'prefix' else 'NewTokenizer(dict.txt)'}",
+                   "corpus_bytes": int(tot_bytes), "corpus_chars": int(tot_runes), "corpus_han_bytes": int(tot_han),
+                   "corpus_docs": int(tot_docs), "rank0_shard_bytes": nbytes, "dict_words": s.nwords,
+                   "parallelism": f"doc-shard x{world} (byte-balanced contiguous ranges), no collectives"},
+        "roofline": roof,
+        "roofline_kernels": rooflines,
+        "cpu_baseline": cpu,
+        "parity": parity,
+        "viterbi_ties": {"gpu": int(tot_ties), "oracle": int(tot_oties) if par else None,
+                         "what": "exact stateTransitionRoute ties a == b > minFloat (Q12, tokenizer.go:748-753), "
+                                 "resolved in stateChange order; the reference resolves them in Go map order"},
+        "han_chars_per_s": round(tot_han / 3 * args.steps / elapsed_max, 1),
+        "input_GBps": round(tot_bytes * args.steps / elapsed_max / 1e9, 3),
+        "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
+        "ms_per_step_kernel_by_kernel": round(prof_ms, 4) if prof_ms else None,
+        "gen_s": round(gen_s, 2),
+    }
+    return line, (sbuf, soff, cutter)
+
+
+def end_to_end(tk, buf, off, hmm, nrunes, reps=3):
+    """jb_cut_batch_into from host memory: pinned staging, H2D, all kernels, D2H
+    spans, u64 batch offsets into caller arrays (never `value`)."""
+    res = tk.cut_batch_into(buf, off, bool(hmm))  # warm the pinned staging and the output arrays
+    t = time.perf_counter()
+    for _ in range(reps):
+        res = tk.cut_batch_into(buf, off, bool(hmm), res[3])
+    s = (time.perf_counter() - t) / reps
+    return {"value": round(nrunes / s, 1), "unit": "chars/s", "ms": round(s * 1e3, 2),
+            "what": "jb_cut_batch_into from host memory: pinned staging, H2D text + offsets, all kernels, "
+                    "D2H spans, u64 batch offsets into caller arrays"}
+
+
+def sentence_latency(tk, o, n):
+    """Config 1: Cut(sentence, hmm=true) through jb_cut (host string in, spans out,
+    the same call a Go caller makes); the oracle on one core beside it."""
+    import ctypes as C
+    import jiebahip as J
+    import oracle as O
+    t = SENTENCE.encode("utf-8")
+    sp = J.jb_spans()
+    L = J.lib()
+    assert tk.Cut(SENTENCE, True) == o.cut(SENTENCE, True)
+    for _ in range(50):
+        J._check(L.jb_cut(tk.h, t, len(t), 1, C.byref(sp)))
+        L.jb_spans_free(C.byref(sp))
+    lat = np.empty(n)
+    for i in range(n):
+        a = time.perf_counter_ns()
+        J._check(L.jb_cut(tk.h, t, len(t), 1, C.byref(sp)))
+        lat[i] = time.perf_counter_ns() - a
+        L.jb_spans_free(C.byref(sp))
+    ol = O.lib()
+    s = np.zeros(64, np.uint32)
+    e = np.zeros(64, np.uint32)
+    olat = np.empty(n)
+    for i in range(n):
+        a = time.perf_counter_ns()
+        ol.or_cut(o.h, t, len(t), 1, s.ctypes.data, e.ctypes.data, 64)
+        olat[i] = time.perf_counter_ns() - a
+    return lat, olat
 
 
 def main():
@@ -68,21 +428,20 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mib", type=float, default=128.0, help="corpus MiB per GPU")
-    ap.add_argument("--workload", choices=["docs", "s10k", "long-punct", "long-oov"], default="docs",
-                    help="docs: C_syn document shard (config 4, the headline); s10k: 10,000 sentences (configs 2/3 "
-                         "with --hmm 0/1); long-punct / long-oov: one 1,000,000-rune document (configs 5a / 5b)")
+    ap.add_argument("--workload", choices=["docs", "sentence", "s10k", "long-punct", "long-oov"], default="docs")
+    ap.add_argument("--corpus-mib", type=float, default=1024.0,
+                    help="docs: the fixed corpus (MiB), strong-scaled over the ranks; 1024 = config 4")
     ap.add_argument("--hmm", type=int, default=1)
     ap.add_argument("--nwords", type=int, default=350_000)
     ap.add_argument("--dict-kind", choices=["prefix", "txt"], default="prefix",
                     help="prefix: NewJiebaTokenizer semantics (prefix_dictionary.gob, size 60,101,967) as in the "
                          "reference's own benchmarks; txt: NewTokenizer(dict.txt)")
-    ap.add_argument("--cpu-sample-mib", type=float, default=128.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu1-sample-mib", type=float, default=8.0)
-    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu1-sample-mib", type=float, default=96.0,
+                    help="one-thread oracle sample (docs, N = 1); 0: skip")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle check (and cpu_baseline)")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--sentence-iters", type=int, default=5000)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -98,215 +457,53 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", init_method="env://")
-    dev = torch.device("cuda", local)
+    agg_dev = torch.device("cuda", local)
 
-    # ---- data (synthetic, seeded) ---------------------------
-    t0 = time.time()
-    s = synth.Synth(nwords=args.nwords)
     tmp = tempfile.mkdtemp(prefix=f"jb_bench_r{rank}_")
-    dpath, epath = s.write_files(tmp)
-    if args.workload == "docs":
-        buf, off, nrunes = s.corpus(synth.KIND_DOCS, rank * DOC_STRIDE, target_bytes=int(args.mib * (1 << 20)))
-    elif args.workload == "s10k":
-        buf, off, nrunes = s.corpus(synth.KIND_SENTENCES, rank * DOC_STRIDE, max_docs=10_000,
-                                    target_bytes=64 << 20)
-    else:
-        buf, off, nrunes = s.corpus(synth.KIND_LONG_PUNCT if args.workload == "long-punct" else synth.KIND_LONG_OOV,
-                                    rank, target_runes=1_000_000)
-    nbytes = int(off[-1])
-    ndocs = len(off) - 1
-    hbytes = han_bytes(buf, nbytes)
-    gen_s = time.time() - t0
-
+    dpath, epath = synth.Synth(nwords=args.nwords).write_files(tmp)
     kind = J.JB_DICT_PREFIX if args.dict_kind == "prefix" else J.JB_DICT_TXT
     size_override = J.JIEBA_SIZE if args.dict_kind == "prefix" else 0
     tk = J.Tokenizer(J.make_config(dict_path=dpath, emit_path=epath, kind=kind, size_override=size_override,
                                    device=local))
-    d_text = torch.from_numpy(buf).to(dev)                      # nbytes + 64 zero padding bytes
-    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
 
-    def step():
-        return tk.cut_device(d_text.data_ptr(), nbytes, d_off.data_ptr(), ndocs, bool(args.hmm), stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-
-    # timed region: the pipeline replays as one captured HIP graph per step
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t_start = time.perf_counter()
-    ptrs = None
-    for _ in range(args.steps):
-        ptrs = step()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t_start
-    if dist:
-        dist.barrier()
-
-    # per-kernel durations: the same K steps again, launched kernel by kernel
-    # with a HIP event pair around each launch on the launch stream
-    prof = not args.no_profile
-    kprof = {}
-    prof_ms = None
-    if prof:
-        tk.profile(True)
-        tk.profile_reset()
-        torch.cuda.synchronize(dev)
-        tp = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize(dev)
-        prof_ms = (time.perf_counter() - tp) / args.steps * 1e3
-        kprof = tk.profile_read()
-        tk.profile(False)
-
-    # whole-job aggregates: max time over ranks, sum of work
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        w = torch.tensor([nrunes, nbytes, hbytes], dtype=torch.float64, device=dev)
-        dist.all_reduce(w, op=dist.ReduceOp.SUM)
-        tot_runes, tot_bytes, tot_han = (float(x) for x in w.tolist())
-    else:
-        tot_runes, tot_bytes, tot_han = float(nrunes), float(nbytes), float(hbytes)
-
-    ms_per_step = elapsed / args.steps * 1e3
-    value = tot_runes * args.steps / elapsed
-
-    # ---- roofline of the dominant kernel --------------------------------------
-    # Algorithmic bytes: 1 B read per input byte + 2 output bits
-    # per byte = 1.25 B per byte of the units a kernel processes: every input
-    # byte for k_mark_walk (it classifies and walks the whole batch), the Han
-    # bytes for k_zh (DP + Viterbi over zh blocks).
-    roof = None
-    rooflines = {}
-    kernels = {}
-    if kprof:
-        for name, (ms, n) in kprof.items():
-            if n:
-                kernels[name] = {"avg_ms": ms / n, "launches": int(n)}
-        dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
-        units = {"k_mark_walk": float(nbytes), "k_zh": float(hbytes)}
-        if args.workload == "long-oov":  # one unpunctuated block: its Han bytes all go through k_zh_long
-            units["k_zh_long"] = float(hbytes)
-        for kname, u in units.items():
-            kk = kernels.get(kname)
-            if not kk:
-                continue
-            alg = 1.25 * u
-            achieved = alg / (kk["avg_ms"] * 1e-3) / 1e9
-            rooflines[kname] = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": round(achieved / HBM_PEAK_GBS, 5),
-                                # the committed PMC summary is of the headline workload only
-                                "traffic": load_pmc_traffic(kname) if args.workload == "docs" else None,
-                                "kernel": kname, "alg_bytes_per_launch": alg, "avg_launch_ms": kk["avg_ms"],
-                                "frac_of_measured_copy": round(achieved / HBM_MEASURED_GBS, 5)}
-        if dom in rooflines:
-            roof = dict(rooflines[dom], dominant_kernel=dom)
-        elif rooflines:
-            roof = dict(next(iter(rooflines.values())), dominant_kernel=dom)
-
-    # ---- CPU baseline + parity sample (rank 0, N = 1) -----------------------
-    cpu = None
-    parity = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    def open_oracle():
         import oracle as O
-        lim = int(args.cpu_sample_mib * (1 << 20))
-        dend = int(np.searchsorted(off, min(lim, nbytes), side="right")) - 1
-        dend = max(1, min(dend, ndocs))
-        sbytes = int(off[dend])
-        s_runes = int(np.count_nonzero((buf[:sbytes] & 0xC0) != 0x80))
-        o = O.Oracle.from_files(dpath, epath, kind, size_override)
-        backptr = args.workload.startswith("long")  # the literal path copy is O(m^2) on a 1M-rune run
-        O.set_viterbi_backptr(backptr)
-        threads = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
-        tc = time.perf_counter()
-        os_, oe, od = o.cut_batch(buf[: sbytes + 16], off[: dend + 1], bool(args.hmm), nthreads=threads)
-        cpu_s = time.perf_counter() - tc
-        cpu = {"value": round(s_runes / cpu_s, 1), "unit": "chars/s", "cores": threads, "kind": "port",
-               "sample": f"first {dend} documents ({sbytes / 2**20:.1f} MiB, {s_runes} chars) of rank 0's shard, "
-                         f"oracle/jieba_oracle.c (C restatement of tokenizer.go, "
-                         f"{'O(n) back-pointer' if backptr else 'literal path-copy'} Viterbi), "
-                         f"{threads} threads over documents, {cpu_s:.2f} s",
-               "cpu_model": _cpu_model()}
-        ps, pe, pd, pn = ptrs
-        ntok = int(J.dev_to_host(pn, 8, np.uint64)[0])
-        gd = J.dev_to_host(pd, 8 * (ndocs + 1), np.uint64)
-        k1 = int(gd[dend])
-        gs = J.dev_to_host(ps, 4 * k1, np.uint32)
-        ge = J.dev_to_host(pe, 4 * k1, np.uint32)
-        ok = bool(np.array_equal(gs, os_) and np.array_equal(ge, oe) and np.array_equal(gd[: dend + 1], od))
-        parity = {"docs": dend, "tokens": int(len(os_)), "bit_exact": ok, "gpu_tokens_total": ntok}
-        # one-thread oracle on a smaller sample (SURVEY.md §8d asks for 1 and n threads)
-        d1 = max(1, min(ndocs, int(np.searchsorted(off, min(int(args.cpu1_sample_mib * (1 << 20)), nbytes),
-                                                   side="right")) - 1))
-        b1 = int(off[d1])
-        r1 = int(np.count_nonzero((buf[:b1] & 0xC0) != 0x80))
-        tc = time.perf_counter()
-        o.cut_batch(buf[: b1 + 16], off[: d1 + 1], bool(args.hmm), nthreads=1)
-        c1 = time.perf_counter() - tc
-        cpu["value_1thread"] = round(r1 / c1, 1)
-        cpu["sample_1thread"] = f"first {d1} documents ({b1 / 2**20:.1f} MiB, {r1} chars), 1 thread, {c1:.2f} s"
-        del o
+        return O.Oracle.from_files(dpath, epath, kind, size_override)
 
-    # ---- end to end from host memory (PCIe in and out; rank 0, N = 1) -------
-    e2e = None
-    if rank == 0 and world == 1 and not args.no_e2e:
-        res = tk.cut_batch_into(buf, off, bool(args.hmm))  # warm the pinned staging and the output arrays
-        te = time.perf_counter()
-        for _ in range(3):
-            res = tk.cut_batch_into(buf, off, bool(args.hmm), res[3])
-        e2e_s = (time.perf_counter() - te) / 3
-        e2e = {"value": round(nrunes / e2e_s, 1), "unit": "chars/s", "ms": round(e2e_s * 1e3, 2),
-               "what": "jb_cut_batch_into from host memory: pinned staging, H2D text + offsets, all kernels, "
-                       "D2H spans, u64 batch offsets into caller arrays"}
+    if args.workload == "sentence":
+        o = open_oracle()
+        lat, olat = sentence_latency(tk, o, args.sentence_iters)
+        med = float(np.median(lat))
+        line = {"metric": METRIC, "value": round(19 / (med * 1e-9), 1), "unit": "chars/s", "n_gpus": 1,
+                "steps": args.sentence_iters, "warmup": 50, "ms_per_step": round(med * 1e-6, 5),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+                "data": "the reference's benchmark sentence", "config": {
+                    "workload": f"config 1: Cut({SENTENCE!r}, hmm=true) through jb_cut, one call at a time "
+                                "(host string in, H2D, kernels, D2H spans), 19 runes / 57 bytes",
+                    "parallelism": "one call"},
+                "latency_ns": {"median": med, "p10": float(np.percentile(lat, 10)),
+                               "p99": float(np.percentile(lat, 99)), "mean": float(lat.mean())},
+                "reference_ns_per_op": {"value": REF_SENTENCE_NS, "hardware": "i5-9400 (tokenizer_test.go:610)"},
+                "cpu_baseline": {"value": round(19 / (float(np.median(olat)) * 1e-9), 1), "unit": "chars/s",
+                                 "cores": 1, "kind": "port", "latency_ns_median": float(np.median(olat)),
+                                 "sample": f"{args.sentence_iters} calls of or_cut (oracle/jieba_oracle.c) on the "
+                                           "same sentence, ctypes call overhead included", "cpu_model": cpu_model()},
+                "roofline": None}
+        print(json.dumps(line), flush=True)
+        tk.close()
+        return
 
+    out = run(args, world, rank, dist, agg_dev,
+              lambda b, o_, h: GpuCutter(tk, b, o_, h, local), open_oracle)
     if rank == 0:
-        line = {
-            "metric": "UTF-8 Chinese chars/sec segmented (whole node) + achieved HBM GB/s vs peak",
-            "value": round(value, 1), "unit": "chars/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f64", "data": "synthetic (seeded D_syn 350k-word dict, E_syn emissions, C_syn Zipf corpus)",
-            "config": {"workload": (f"C_syn corpus shard {args.mib:g} MiB/GPU (1 GiB over 8 GPUs = config 4), "
-                                    if args.workload == "docs" else
-                                    "S10k: 10,000 synthetic sentences (configs 2/3), " if args.workload == "s10k" else
-                                    f"L1M: one 1,000,000-rune document, "
-                                    f"{'punctuated (5a)' if args.workload == 'long-punct' else 'unpunctuated, 30% OOV (5b)'}, ")
-                                   + f"Cut hmm={'on' if args.hmm else 'off'}, "
-                                   f"{'NewJiebaTokenizer (prefix dict, size 60,101,967)' if args.dict_kind == 'prefix' else 'NewTokenizer(dict.txt)'}",
-                       "bytes_per_gpu": nbytes, "chars_per_gpu": nrunes, "han_bytes_per_gpu": hbytes,
-                       "docs_per_gpu": ndocs, "dict_words": s.nwords, "parallelism": f"doc-shard x{world}, no collectives"},
-            "roofline": roof,
-            "roofline_kernels": rooflines,
-            "cpu_baseline": cpu,
-            "parity_sample": parity,
-            "end_to_end_host": e2e,
-            "han_chars_per_s": round(tot_han / 3 * args.steps / elapsed, 1),
-            "input_GBps": round(tot_bytes * args.steps / elapsed / 1e9, 3),
-            "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
-            "ms_per_step_kernel_by_kernel": round(prof_ms, 4) if prof_ms else None,
-            "gen_s": round(gen_s, 2),
-            "loaded": J.loaded_runtime(),
-        }
+        line, (sbuf, soff, _) = out
+        if world == 1 and not args.no_e2e:
+            line["end_to_end_host"] = end_to_end(tk, sbuf, soff, args.hmm, line["config"]["corpus_chars"])
+        line["loaded"] = J.loaded_runtime()
         print(json.dumps(line), flush=True)
     tk.close()
     if dist:
         dist.destroy_process_group()
-
-
-def _cpu_model():
-    try:
-        with open("/proc/cpuinfo") as f:
-            for l in f:
-                if l.startswith("model name"):
-                    return l.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return "unknown"
 
 
 if __name__ == "__main__":

@@ -92,3 +92,59 @@ class Synth:
         out = np.zeros(n + pad, np.uint8)
         out[:n] = buf[:n]
         return out, off[: nd.value + 1].copy(), int(nr.value)
+
+    def _docs_range(self, kind, doc0, count, cap_per_doc=48 << 10):
+        """Documents doc0 .. doc0+count-1 (each from its own seed 3 + index,
+        gen/synth.c), concatenated: (bytes, doc lengths, runes)."""
+        parts, lens, runes = [], [], 0
+        done = 0
+        while done < count:
+            want = count - done
+            cap = want * cap_per_doc + (1 << 20)
+            buf = np.empty(cap, np.uint8)
+            off = np.zeros(want + 1, np.uint64)
+            nd, nr = C.c_uint64(), C.c_uint64()
+            n = lib().syn_corpus(self.h, kind, doc0 + done, want, 1 << 62, 0, buf.ctypes.data, cap,
+                                 off.ctypes.data, C.byref(nd), C.byref(nr))
+            if nd.value == 0:
+                raise RuntimeError("document larger than the generator buffer")
+            parts.append(buf[:n].copy())
+            lens.append(np.diff(off[: nd.value + 1]))
+            runes += int(nr.value)
+            done += int(nd.value)
+        return np.concatenate(parts), np.concatenate(lens), runes
+
+    def corpus_parallel(self, kind=KIND_DOCS, doc0=0, target_bytes=1 << 30, threads=8, chunk_docs=2048, pad=64):
+        """The same corpus as corpus(kind, doc0, target_bytes=...) (documents
+        doc0, doc0+1, ... up to the first one that reaches target_bytes),
+        generated chunk by chunk on `threads` threads (the C generator releases
+        the GIL).  Returns (buf with `pad` zero bytes, doc_off, nrunes)."""
+        from concurrent.futures import ThreadPoolExecutor
+        assert kind in (KIND_DOCS, KIND_SENTENCES)
+        chunks, total, k = [], 0, 0
+        with ThreadPoolExecutor(threads) as ex:
+            while total < target_bytes:
+                futs = [ex.submit(self._docs_range, kind, doc0 + (k + i) * chunk_docs, chunk_docs)
+                        for i in range(threads)]
+                for f in futs:
+                    b, l, r = f.result()
+                    chunks.append((b, l, r))
+                    total += len(b)
+                k += threads
+        lens = np.concatenate([c[1] for c in chunks])
+        off = np.zeros(len(lens) + 1, np.uint64)
+        np.cumsum(lens, out=off[1:])
+        nd = int(np.searchsorted(off, target_bytes, side="left"))  # first doc count reaching the target
+        nd = max(1, min(nd, len(lens)))
+        n = int(off[nd])
+        out = np.zeros(n + pad, np.uint8)
+        pos = 0
+        for b, _, _ in chunks:
+            if pos >= n:
+                break
+            m = min(len(b), n - pos)
+            out[pos : pos + m] = b[:m]
+            pos += m
+        nrunes = int(np.count_nonzero((out[:n] & 0xC0) != 0x80))
+        return out, off[: nd + 1].copy(), nrunes
+

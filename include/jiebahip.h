@@ -115,6 +115,13 @@ int jb_cut_device(jb_ctx *ctx, const uint8_t *d_text, uint64_t nbytes, const uin
                   uint32_t ndocs, int hmm, void *stream, uint32_t **d_start, uint32_t **d_end,
                   uint64_t **d_doc_tok, uint64_t **d_ntok);
 
+/* Contiguous byte-balanced document ranges, the multi-device partition of
+ * jb_cut_batch (the reference's CutParallel deals blocks to
+ * goroutines instead, tokenizer.go:81-148): part k owns documents
+ * [cut[k], cut[k+1]), cut has nparts + 1 entries, cut[0] = 0 and
+ * cut[nparts] = ndocs.  Host only. */
+int jb_shard_bounds(const uint64_t *doc_off, uint32_t ndocs, uint32_t nparts, uint32_t *cut);
+
 /* Replaces Tokenizer.AddWord (tokenizer.go:372; the reference deadlocks there,
  * :376 + :581).  freq < 1 takes suggestFreq's value (tokenizer.go:589-614). */
 int jb_add_word(jb_ctx *ctx, const char *word, size_t len, int64_t freq);
@@ -122,6 +129,20 @@ int jb_add_word(jb_ctx *ctx, const char *word, size_t len, int64_t freq);
 /* Dictionary introspection (prefixDictionary.termFreq / size, tokenizer.go:382-383). */
 int jb_dict_get(jb_ctx *ctx, const char *word, size_t len, int64_t *freq); /* 1 found, 0 absent */
 int64_t jb_dict_size(jb_ctx *ctx);
+
+/* Counters of the last pipeline run on each device of ctx, summed over the
+ * devices (for a host batch larger than 1 GiB: of its last piece).
+ * Synchronises the devices' streams. */
+typedef struct {
+    uint64_t tokens;       /* tokens written */
+    uint64_t blocks;       /* splitText blocks, zh and non-zh (tokenizer.go:165-210) */
+    uint64_t zh_blocks;    /* of which Han runs (cutZh, tokenizer.go:221) */
+    uint64_t long_blocks;  /* zh blocks of >= 8 KiB, cut by the long-block kernel */
+    uint64_t viterbi_ties; /* exact stateTransitionRoute ties a == b > minFloat, which the reference
+                              resolves in Go's random map order (tokenizer.go:748-753); here the first
+                              candidate of stateChange wins */
+} jb_stats;
+int jb_last_stats(jb_ctx *ctx, jb_stats *out);
 
 /* Per-kernel timing with HIP events on the launch stream (bench / profiling). */
 int jb_profile_enable(jb_ctx *ctx, int on);

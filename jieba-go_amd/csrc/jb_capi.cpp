@@ -131,16 +131,17 @@ struct Device {
     uint32_t* h_cnt = nullptr;   // counters (64 u32)
     std::vector<hipEvent_t> ev;  // span pieces landed (host batches)
     uint32_t ncu = 0;
+    LaunchCfg lc{};  // launch shape, fixed at jb_open
     EventTimer timer;
     bool profile = false;
     // replay cache: the whole pipeline captured as one HIP graph for the last
     // (buffers, sizes, grids) it ran with; any change re-captures
     struct GraphKey {
         const void* text; uint64_t nbytes; const void* doc_off; uint32_t ndocs; bool hmm;
-        uint32_t gzh, gnz; uint64_t work_gen; hipStream_t stream;
+        uint64_t work_gen; hipStream_t stream;
         bool operator==(const GraphKey& o) const {
             return text == o.text && nbytes == o.nbytes && doc_off == o.doc_off && ndocs == o.ndocs &&
-                   hmm == o.hmm && gzh == o.gzh && gnz == o.gnz && work_gen == o.work_gen && stream == o.stream;
+                   hmm == o.hmm && work_gen == o.work_gen && stream == o.stream;
         }
     } gkey{};
     hipGraphExec_t gexec = nullptr;  // captured for gkey (null until the key repeats)
@@ -416,6 +417,10 @@ static int upload_image(Device* d, const Image& img) {
     d->dim.code = d->code;
     d->dim.wtab = d->wtab;
     d->dim.nrows = img.nrows;
+    // a captured pipeline holds the old image pointers in its kernel arguments
+    if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
+    d->gexec = nullptr;
+    d->gkey_gen = 0;
     return JB_OK;
 }
 
@@ -465,7 +470,7 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.counters, 64 * 4));
     HIPCHK(hipMalloc(&w.supb, (ntiles / 256 + 2) * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.supt, (nttiles / 256 + 2) * sizeof(uint2)));
-    if (getenv("JB_ABLATE") && (atoi(getenv("JB_ABLATE")) & 0x100)) {
+    if (d->lc.diag & 0x100u) {
         HIPCHK(hipMalloc(&w.dbg, 65536 * 8 * 8));
         HIPCHK(hipMalloc(&w.dbg_walk, ntiles * 4 * 8 * 8));
         HIPCHK(hipMemset(w.dbg_walk, 0, ntiles * 4 * 8 * 8));
@@ -518,33 +523,56 @@ static int ensure_span_staging(Device* d, uint64_t ntok) {
     return JB_OK;
 }
 
-static uint32_t grid_zh_override = 0;
-
 #ifndef JB_NZ_PER_CU
 #define JB_NZ_PER_CU 8  // k_nonzh workgroups per CU (persistent grid; 4: 0.075 ms, 8: 0.058)
 #endif
-static int launch(jb_ctx* ctx, Device* d, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off,
-                  uint32_t ndocs, bool hmm, hipStream_t s) {
-    const uint32_t grid_zh = d->ncu * std::max(1u, zh_blocks_per_cu(hmm));
-    const uint32_t grid_nz = d->ncu * std::max(1u, std::min((uint32_t)JB_NZ_PER_CU, nonzh_blocks_per_cu()));
+static int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+
+// The launch shape of a device, fixed at jb_open.  Tuning knobs come from the
+// environment once, here (results do not depend on them):
+//   JB_GRID_ZH   k_zh workgroups (default: resident workgroups per CU x CUs)
+//   JB_ZH_GROUP  k_zh group bytes, a multiple of 32 in [kZhGroupSmall, kZhGroupBytes]
+//                (default: by batch size, zh_group_for)
+//   JB_STAMPS    (STAMPS=1 builds only) per-wave phase clocks to stderr
+static int init_launch_cfg(Device* d) {
+    LaunchCfg& lc = d->lc;
+    lc.grid_zh = d->ncu * std::max(zh_blocks_per_cu(true), zh_blocks_per_cu(false));
+    lc.grid_nz = d->ncu * std::max(1u, std::min((uint32_t)JB_NZ_PER_CU, nonzh_blocks_per_cu()));
+    const int gz = env_int("JB_GRID_ZH", 0);
+    if (gz > 0) lc.grid_zh = (uint32_t)gz;
+    const int grp = env_int("JB_ZH_GROUP", 0);
+    if (grp != 0) {
+        if (grp < (int)kZhGroupSmall || grp > (int)kZhGroupBytes || grp % 32 != 0)
+            return fail(JB_EINVAL, "JB_ZH_GROUP=%d: want a multiple of 32 in [%u, %u]", grp, kZhGroupSmall,
+                        kZhGroupBytes);
+        lc.zh_group = (uint32_t)grp;
+    }
+#if JB_STAMPS
+    lc.diag = (uint32_t)env_int("JB_STAMPS", 0) ? 0x100u : 0u;
+#endif
+    return JB_OK;
+}
+
+static int launch(Device* d, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off, uint32_t ndocs,
+                  bool hmm, hipStream_t s) {
     static const bool dbg = getenv("JB_DEBUG") != nullptr;
-    if (const char* a = getenv("JB_ABLATE")) g_ablate = (uint32_t)atoi(a);
-    if (const char* gz = getenv("JB_GRID_ZH")) grid_zh_override = (uint32_t)atoi(gz);
-    const uint32_t gzh = grid_zh_override ? grid_zh_override : grid_zh;
+    const LaunchCfg& lc = d->lc;
     if (dbg)
-        fprintf(stderr, "[jb] nbytes=%llu ndocs=%u grid_zh=%u (occ %u/CU) grid_nz=%u ablate=%u\n",
-                (unsigned long long)nbytes, ndocs, gzh, zh_blocks_per_cu(hmm), grid_nz, g_ablate);
-    static const bool use_graph = !(getenv("JB_GRAPH") && atoi(getenv("JB_GRAPH")) == 0);
-    if (use_graph && !d->profile && g_ablate == 0 && s != nullptr) {
-        const Device::GraphKey key{d_text, nbytes, d_doc_off, ndocs, hmm, gzh, grid_nz, d->work_gen, s};
+        fprintf(stderr, "[jb] nbytes=%llu ndocs=%u grid_zh=%u grid_nz=%u zh_group=%u\n", (unsigned long long)nbytes,
+                ndocs, lc.grid_zh, lc.grid_nz, lc.zh_group ? lc.zh_group : zh_group_for(nbytes));
+    static const bool use_graph = env_int("JB_GRAPH", 1) != 0;
+    if (use_graph && !d->profile && lc.diag == 0 && s != nullptr) {
+        const Device::GraphKey key{d_text, nbytes, d_doc_off, ndocs, hmm, d->work_gen, s};
         const bool repeat = d->gkey_gen != 0 && key == d->gkey;
         if (!repeat) {  // first call with this key: run directly, capture if it comes again
             if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
             d->gexec = nullptr;
             d->gkey = key;
             d->gkey_gen = 1;
-            const hipError_t e = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, gzh, grid_nz, s,
-                                              nullptr);
+            const hipError_t e = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, lc, s, nullptr);
             if (e != hipSuccess) return fail(JB_EDEVICE, "pipeline launch: %s", hipGetErrorString(e));
             return JB_OK;
         }
@@ -553,8 +581,7 @@ static int launch(jb_ctx* ctx, Device* d, const uint8_t* d_text, uint64_t nbytes
             d->gexec = nullptr;
             hipGraph_t g = nullptr;
             HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-            const hipError_t ec = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, gzh, grid_nz, s,
-                                               nullptr);
+            const hipError_t ec = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, lc, s, nullptr);
             const hipError_t ee = hipStreamEndCapture(s, &g);
             if (ec != hipSuccess) return fail(JB_EDEVICE, "pipeline capture: %s", hipGetErrorString(ec));
             if (ee != hipSuccess) return fail(JB_EDEVICE, "pipeline capture end: %s", hipGetErrorString(ee));
@@ -569,11 +596,11 @@ static int launch(jb_ctx* ctx, Device* d, const uint8_t* d_text, uint64_t nbytes
         if (el != hipSuccess) return fail(JB_EDEVICE, "pipeline graph launch: %s", hipGetErrorString(el));
         return JB_OK;
     }
-    const hipError_t e = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, gzh, grid_nz, s,
+    const hipError_t e = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, lc, s,
                                       d->profile ? &d->timer : nullptr);
     if (e != hipSuccess) return fail(JB_EDEVICE, "pipeline launch: %s", hipGetErrorString(e));
-    if ((g_ablate & 0x100u) && d->w.dbg) {  // diagnostic: per-wave clocks of k_zh (JB_ABLATE bit 8)
-        const uint32_t nwv = std::min<uint32_t>(gzh * 4u, 65536u);
+    if ((lc.diag & 0x100u) && d->w.dbg) {  // diagnostic: per-wave clocks of k_zh (STAMPS builds)
+        const uint32_t nwv = std::min<uint32_t>(lc.grid_zh * 4u, 65536u);
         std::vector<uint64_t> st((size_t)nwv * 8);
         HIPCHK(hipMemcpyAsync(st.data(), d->w.dbg, st.size() * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
@@ -630,6 +657,7 @@ extern "C" int jb_open(const jb_config* cfg, jb_ctx** out) {
         d->ncu = (uint32_t)prop.multiProcessorCount;
         HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
         if ((rc = upload_image(d.get(), img->img))) return rc;
+        if ((rc = init_launch_cfg(d.get()))) return rc;
         ctx->devs.push_back(std::move(d));
     }
     *out = ctx.release();
@@ -712,7 +740,7 @@ static int cut_range(jb_ctx* ctx, Device* d, const uint8_t* text, const uint64_t
             if (err) return fail(JB_EDEVICE, "H2D copy failed");
         }
         const auto c1 = now();
-        if ((rc = launch(ctx, d, d->text, nbytes, d->doc_off, nd, hmm, d->stream))) return rc;
+        if ((rc = launch(d, d->text, nbytes, d->doc_off, nd, hmm, d->stream))) return rc;
         HIPCHK(hipMemcpyAsync(d->h_cnt, d->w.counters, 8 * 4, hipMemcpyDeviceToHost, d->stream));
         HIPCHK(hipStreamSynchronize(d->stream));
         const auto c2 = now();
@@ -779,25 +807,39 @@ static int cut_range(jb_ctx* ctx, Device* d, const uint8_t* text, const uint64_t
     return JB_OK;
 }
 
-// Shard [0, ndocs) over the devices (contiguous byte-balanced ranges) and cut.
-// sb[k] receives device k's spans; ext (optional) makes device 0 write into
-// caller-owned arrays when there is a single device.
-static int cut_sharded(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off, uint32_t ndocs, int hmm,
-                       std::vector<SpanBuf>* sbp) {
+// Contiguous byte-balanced document ranges: part k owns
+// documents [cut[k], cut[k+1]); cut[0] = 0, cut[nparts] = ndocs.  The cut
+// before part k is the first document that does not end at or before byte
+// total * k / nparts (jieba-go_amd/python/shard.py restates the rule for
+// bench.py's one-process-per-GPU runs).
+extern "C" int jb_shard_bounds(const uint64_t* doc_off, uint32_t ndocs, uint32_t nparts, uint32_t* cut) {
+    if (!cut || nparts == 0 || (!doc_off && ndocs)) return fail(JB_EINVAL, "jb_shard_bounds: bad argument");
     for (uint32_t k = 0; k < ndocs; k++)
         if (doc_off[k + 1] < doc_off[k]) return fail(JB_EINVAL, "doc_off not monotonic at %u", k);
-    if (ndocs && !text && doc_off[ndocs] > doc_off[0]) return fail(JB_EINVAL, "null text");
-    std::vector<SpanBuf>& sb = *sbp;
-    const size_t nd = ctx->devs.size();
-    std::vector<uint32_t> cut(nd + 1, ndocs);
+    for (uint32_t k = 0; k <= nparts; k++) cut[k] = ndocs;
     cut[0] = 0;
     const uint64_t total = ndocs ? doc_off[ndocs] - doc_off[0] : 0;
-    for (size_t k = 1; k < nd; k++) {
-        const uint64_t target = (ndocs ? doc_off[0] : 0) + total * k / nd;
+    for (uint32_t k = 1; k < nparts; k++) {
+        // (total * k fits u64: total < 2^56 for any batch a host holds)
+        const uint64_t target = (ndocs ? doc_off[0] : 0) + total * k / nparts;
         uint32_t lo = cut[k - 1];
         while (lo < ndocs && doc_off[lo + 1] <= target) lo++;
         cut[k] = lo;
     }
+    return JB_OK;
+}
+
+// Shard [0, ndocs) over the devices (jb_shard_bounds) and cut, one host
+// thread per device.  sb[k] receives device k's spans.  The caller holds
+// ctx->lock (shared for cuts, exclusive inside jb_add_word).
+static int cut_sharded(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off, uint32_t ndocs, int hmm,
+                       std::vector<SpanBuf>* sbp) {
+    if (ndocs && !text && doc_off[ndocs] > doc_off[0]) return fail(JB_EINVAL, "null text");
+    std::vector<SpanBuf>& sb = *sbp;
+    const size_t nd = ctx->devs.size();
+    std::vector<uint32_t> cut(nd + 1, ndocs);
+    int rc0 = jb_shard_bounds(doc_off, ndocs, (uint32_t)nd, cut.data());
+    if (rc0) return rc0;
     std::vector<int> rcs(nd, JB_OK);
     std::vector<std::string> errs(nd);
     auto work = [&](size_t k) {
@@ -832,11 +874,9 @@ static void fill_doc_tok(const std::vector<SpanBuf>& sb, uint32_t ndocs, uint64_
     while (di < ndocs) doc_tok[++di] = w;
 }
 
-extern "C" int jb_cut_batch(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off, uint32_t ndocs, int hmm,
+// jb_cut_batch with ctx->lock already held by the caller.
+static int cut_batch_locked(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off, uint32_t ndocs, int hmm,
                             jb_spans* out) {
-    if (!ctx || !out || (!doc_off && ndocs)) return fail(JB_EINVAL, "jb_cut_batch: null argument");
-    memset(out, 0, sizeof *out);
-    std::shared_lock<std::shared_mutex> rl(ctx->lock);
     const size_t nd = ctx->devs.size();
     std::vector<SpanBuf> sb(nd);
     auto release_all = [&] {
@@ -878,6 +918,14 @@ extern "C" int jb_cut_batch(jb_ctx* ctx, const uint8_t* text, const uint64_t* do
     fill_doc_tok(sb, ndocs, out->doc_tok);
     release_all();
     return JB_OK;
+}
+
+extern "C" int jb_cut_batch(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off, uint32_t ndocs, int hmm,
+                            jb_spans* out) {
+    if (!ctx || !out || (!doc_off && ndocs)) return fail(JB_EINVAL, "jb_cut_batch: null argument");
+    memset(out, 0, sizeof *out);
+    std::shared_lock<std::shared_mutex> rl(ctx->lock);
+    return cut_batch_locked(ctx, text, doc_off, ndocs, hmm, out);
 }
 
 extern "C" int jb_cut_batch_into(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off, uint32_t ndocs,
@@ -953,7 +1001,7 @@ extern "C" int jb_cut_device(jb_ctx* ctx, const uint8_t* d_text, uint64_t nbytes
     HIPCHK(hipSetDevice(d->ordinal));
     int rc;
     if ((rc = ensure_work(d, nbytes, ndocs))) return rc;
-    if ((rc = launch(ctx, d, d_text, nbytes, d_doc_off, ndocs, hmm != 0, (hipStream_t)stream))) return rc;
+    if ((rc = launch(d, d_text, nbytes, d_doc_off, ndocs, hmm != 0, (hipStream_t)stream))) return rc;
     if (d_start) *d_start = d->w.tok_start;
     if (d_end) *d_end = d->w.tok_end;
     if (d_doc_tok) *d_doc_tok = d->w.doc_tok;
@@ -979,14 +1027,17 @@ extern "C" int64_t jb_dict_size(jb_ctx* ctx) {
     return ctx->im->dict.size;
 }
 
-// suggestFreq (tokenizer.go:589-614)
+// suggestFreq (tokenizer.go:589-614); the caller holds ctx->lock
 static int suggest_freq(jb_ctx* ctx, const char* word, size_t len, int64_t* out) {
     const Dictionary& dict = ctx->im->dict;
     double dsize = (double)dict.size;
     if (dsize < 1.0) dsize = 1.0;
     double freq = 1.0;
     jb_spans sp;
-    int rc = jb_cut(ctx, (const uint8_t*)word, len, 0, &sp);
+    memset(&sp, 0, sizeof sp);
+    static const uint8_t empty[1] = {0};
+    const uint64_t off[2] = {0, (uint64_t)len};
+    int rc = cut_batch_locked(ctx, word ? (const uint8_t*)word : empty, off, 1, 0, &sp);
     if (rc) return rc;
     for (uint64_t k = 0; k < sp.ntokens; k++) {
         std::string piece;
@@ -1008,11 +1059,8 @@ static int suggest_freq(jb_ctx* ctx, const char* word, size_t len, int64_t* out)
 extern "C" int jb_add_word(jb_ctx* ctx, const char* word, size_t len, int64_t freq) {
     if (!ctx || (!word && len)) return fail(JB_EINVAL, "jb_add_word: null argument");
     int rc;
-    if (freq < 1) {
-        std::shared_lock<std::shared_mutex> rl(ctx->lock);
-        if ((rc = suggest_freq(ctx, word, len, &freq))) return rc;
-    }
-    std::unique_lock<std::shared_mutex> wl(ctx->lock);
+    std::unique_lock<std::shared_mutex> wl(ctx->lock);  // (the reference deadlocks here: :376 + :581)
+    if (freq < 1 && (rc = suggest_freq(ctx, word, len, &freq))) return rc;
     // addTerm (tokenizer.go:580-585): no prefix entries are added
     Dictionary& dict = ctx->im->dict;
     dict.term_freq[std::string(word, len)] = freq;
@@ -1037,6 +1085,28 @@ extern "C" int jb_save(jb_ctx* ctx, const char* path) {
         save_image(ctx->im->dict, ctx->im->emit, ctx->im->img, &data);
     }
     return write_file(path, data);
+}
+
+extern "C" int jb_last_stats(jb_ctx* ctx, jb_stats* out) {
+    if (!ctx || !out) return fail(JB_EINVAL, "jb_last_stats: null argument");
+    memset(out, 0, sizeof *out);
+    std::shared_lock<std::shared_mutex> rl(ctx->lock);
+    for (auto& d : ctx->devs) {
+        std::lock_guard<std::mutex> g(d->mu);
+        if (!d->w.counters) continue;
+        HIPCHK(hipSetDevice(d->ordinal));
+        HIPCHK(hipDeviceSynchronize());  // (jb_cut_device may have queued on a caller's stream)
+        uint32_t c[CNT_NWORDS + 2];
+        HIPCHK(hipMemcpy(c, d->w.counters, sizeof c, hipMemcpyDeviceToHost));
+        uint64_t ntok;
+        memcpy(&ntok, c + CNT_NWORDS, 8);
+        out->tokens += ntok;
+        out->blocks += c[CNT_NBLK];
+        out->zh_blocks += c[CNT_NZH];
+        out->long_blocks += c[CNT_NLONG];
+        out->viterbi_ties += c[CNT_TIES];
+    }
+    return JB_OK;
 }
 
 // ---------------------------------------------------------------------------

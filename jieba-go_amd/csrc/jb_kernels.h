@@ -30,6 +30,7 @@ enum {
     CNT_ERR = 4,    // bit 0: a zh block reached a tail index -1 (the reference panics)
     CNT_WORK = 5,   // k_zh work counter: next group (kZhGroupBytes of text)
     CNT_NLONG = 6,  // long zh blocks k_zh left to k_zh_long
+    CNT_TIES = 7,   // exact Viterbi route ties (Q12)
     CNT_NWORDS = 8  // u32 slots reserved; u64 token count lives at byte offset 32
 };
 
@@ -39,10 +40,14 @@ constexpr int kTokTileWords = 512;     // k_tok: 256 threads x 2 words (16 KiB o
 #define JB_ZH_GROUP 6144
 #endif
 constexpr uint32_t kErecPad = 8;  // erec slots before slot 0 (k_zh reads a few slots past a block's start)
+// k_zh work unit: the zh blocks that start in one group of text bytes (a
+// multiple of 32): kZhGroupBytes, or kZhGroupSmall for batches under
+// kZhSmallBatch bytes so that a small batch still spreads over enough waves
 constexpr uint32_t kZhGroupBytes = JB_ZH_GROUP;
-constexpr uint32_t kZhGroupSmall = 1024;         // the k_zh group of batches under kZhSmallBatch bytes
+constexpr uint32_t kZhGroupSmall = 1024;
 constexpr uint64_t kZhSmallBatch = 16ull << 20;
-constexpr uint32_t kZhLongMin = 8192;  // zh blocks of at least this many bytes go to k_zh_long  // k_zh work unit: zh blocks starting in one such span (multiple of 32)
+constexpr uint32_t kZhLongMin = 8192;  // zh blocks of at least this many bytes go to k_zh_long
+inline uint32_t zh_group_for(uint64_t nbytes) { return nbytes < kZhSmallBatch ? kZhGroupSmall : kZhGroupBytes; }
 
 // Per-call device workspace, sized for `nbytes` of text.
 struct Work {
@@ -60,7 +65,7 @@ struct Work {
     uint64_t* alnum16;     // 1 bit per 16 bytes of text: some [0-9A-Za-z] byte there
     uint64_t* erec;        // per Han rune (slot = byte / 3): packed DAG edges (k_mark_walk -> k_zh)
     uint32_t* lanemask;    // per 16 bytes: block starts | Han block starts << 16
-    uint2* gstart;         // per k_zh group g: (blocks, zh blocks) that start before g * kZhGroupBytes
+    uint2* gstart;         // per k_zh group g: (blocks, zh blocks) that start before g * group bytes
     uint2* longblk;        // (start, end) of each long zh block (k_zh -> k_zh_long)
     uint32_t* tile4;       // per tile: a 4-byte Han rune starts in it
     uint8_t* gbl;          // per Han rune: chosen piece length, then Viterbi back-pointers / labels
@@ -89,16 +94,22 @@ struct KernelTimer {
     virtual ~KernelTimer() {}
 };
 
+// Launch shape of one pipeline run (fixed per device at jb_open).
+struct LaunchCfg {
+    uint32_t grid_zh;   // persistent grid of k_zh
+    uint32_t grid_nz;   // persistent grid of k_nonzh
+    uint32_t zh_group;  // k_zh group bytes (0: zh_group_for(nbytes))
+    uint32_t diag;      // diagnostic clocks (STAMPS builds only; 0 otherwise)
+};
+
 // Enqueue the whole Cut pipeline on `stream`.  Returns hipSuccess or the first
-// launch error.  grid_zh / grid_nz: persistent grids of k_zh / k_nonzh.
-// d_text must be readable 64 bytes past nbytes.
+// launch error.  d_text must be readable 64 bytes past nbytes.
 hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text, uint64_t nbytes,
-                        const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, uint32_t grid_zh, uint32_t grid_nz,
+                        const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, const LaunchCfg& lc,
                         hipStream_t stream, KernelTimer* timer);
 
 // Resident k_zh workgroups per CU (occupancy API).
 uint32_t zh_blocks_per_cu(bool hmm);
-extern uint32_t g_ablate;  // diagnostic ablations from JB_ABLATE (results are wrong when non-zero)
 uint32_t nonzh_blocks_per_cu();
 
 }  // namespace jb

@@ -72,7 +72,8 @@ struct Emitter {
     uint32_t* sb;
     uint32_t* eb;
     uint32_t word, s, e;
-    bool off = false;  // diagnostic (JB_ABLATE bit 7): drop the bits instead of flushing them
+    uint32_t ties = 0;  // exact Viterbi route ties seen by this lane (Q12)
+    bool off = false;   // drop the bits instead of flushing them (k_zh_long: only lane 0 writes)
     __device__ Emitter(uint32_t* s_, uint32_t* e_) : sb(s_), eb(e_), word(0xFFFFFFFFu), s(0), e(0) {}
     __device__ __forceinline__ void flush() {
         if (!off) {
@@ -103,6 +104,7 @@ struct LdsEmitter {
     uint32_t* eb;
     uint32_t w0;
     uint32_t word, s, e;
+    uint32_t ties = 0;  // exact Viterbi route ties seen by this lane (Q12)
     __device__ LdsEmitter(uint32_t* s_, uint32_t* e_, uint32_t w0_)
         : sb(s_), eb(e_), w0(w0_), word(0xFFFFFFFFu), s(0), e(0) {}
     __device__ __forceinline__ void flush() {
@@ -358,7 +360,7 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
                                                    uint32_t* __restrict__ lanemask, uint2* __restrict__ tile_cnt,
                                                    uint64_t* __restrict__ erec, uint32_t* __restrict__ tile4,
                                                    uint64_t* __restrict__ alnum16, uint32_t* __restrict__ sbits,
-                                                   uint32_t* __restrict__ ebits, uint32_t ablate,
+                                                   uint32_t* __restrict__ ebits, uint32_t diag,
                                                    uint64_t* __restrict__ dbg) {
     // LDS: 20.2 KB, so that 8 workgroups fit a CU (160 KB).  The staged text is
     // dead once the entries are decoded; the entry cells/records reuse its bytes.
@@ -371,7 +373,7 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     uint32_t* const lds = reinterpret_cast<uint32_t*>(s_raw + kMwOffScan);
     __shared__ uint32_t s_nla, s_nwl;
 #if JB_STAMPS
-    const bool stamps = (ablate & 0x100u) != 0;  // diagnostic per-wave phase clocks (make STAMPS=1)
+    const bool stamps = (diag & 0x100u) != 0;  // diagnostic per-wave phase clocks (make STAMPS=1)
 #else
     const bool stamps = false;
 #endif
@@ -544,7 +546,7 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
             if ((hsm >> i) & 1u)
                 s_e[o + __popc(hsm & ((1u << i) - 1u))] = jb_l1row_code(cl[i]) | (((w4m >> i) & 1u) << 17) |
                                                           ((threadIdx.x * 16u + ((kp >> (4 * i)) & 15u)) << 18);
-            cl[i] = (((hsm >> i) & 1u) && !(ablate & 2u)) ? jb_l1row_cell(cl[i]) : 0ull;
+            cl[i] = ((hsm >> i) & 1u) ? jb_l1row_cell(cl[i]) : 0ull;
         }
         // Lookahead (the last lane, while the cell loads fly): when the tile's last
         // Han rune ends at or past the tile end, the runes that continue its run
@@ -861,7 +863,8 @@ constexpr uint32_t kZhRing = 8;                            // LDS best ring per 
 constexpr uint32_t kZhWin = kZhGroupBytes + 1024u;         // window: group span + slack for the last blocks
 constexpr uint32_t kZhChunk = 192;                         // blocks ranked together (3 per lane)
 constexpr uint32_t kZhWinWords = kZhWin / 32u + 1u;        // token bitmap words of a window
-static_assert(kZhGroupBytes % 32u == 0u && kZhGroupBytes >= kTileBytes, "k_zh group: whole words, one per tile");
+static_assert(kZhGroupBytes % 32u == 0u && kZhGroupSmall % 32u == 0u && kZhGroupSmall <= kZhGroupBytes,
+              "k_zh groups are whole token-bitmap words");
 static_assert(2u * kZhWinWords <= 2u * kZhRing * 64u, "token bitmaps fit over the ring");
 static_assert(kZhWin < 65536u, "window offsets are packed in 16 bits");
 
@@ -917,11 +920,14 @@ __device__ __forceinline__ void load_emit(const DevImage& im, uint32_t r, double
 
 // stateTransitionRoute (tokenizer.go:736-756): candidates in stateChange
 // order, strict '>' against minFloat; code 0/1 = candidate, 2 = no route ("").
-__device__ __forceinline__ void route2(double a, double b, uint32_t* code, double* p) {
+// An exact tie a == b > minFloat is counted in nt: the reference picks either
+// one, in Go's randomized map order (:748-753, Q12); here the first wins.
+__device__ __forceinline__ void route2(double a, double b, uint32_t* code, double* p, uint32_t& nt) {
     uint32_t c = 2u;
     double best = JB_MIN_FLOAT;
     if (a > best) { c = 0u; best = a; }
     if (b > best) { c = 1u; best = b; }
+    nt += (a == b && a > JB_MIN_FLOAT) ? 1u : 0u;
     *code = c;
     *p = best;
 }
@@ -986,10 +992,10 @@ __device__ void viterbi_run(const V& v, const DevImage& im, uint32_t rs, uint32_
         if (qn < re) load_emit(im, z_dec(v, qn, &wn), en);  // next rune's emissions, in flight
         uint32_t cB, cM, cE, cS;
         double pB, pM, pE, pS;
-        route2(vE + T_EB, vS + T_SB, &cB, &pB);  // B <- E, S
-        route2(vB + T_BM, vM + T_MM, &cM, &pM);  // M <- B, M
-        route2(vB + T_BE, vM + T_ME, &cE, &pE);  // E <- B, M
-        route2(vE + T_ES, vS + T_SS, &cS, &pS);  // S <- E, S
+        route2(vE + T_EB, vS + T_SB, &cB, &pB, em.ties);  // B <- E, S
+        route2(vB + T_BM, vM + T_MM, &cM, &pM, em.ties);  // M <- B, M
+        route2(vB + T_BE, vM + T_ME, &cE, &pE, em.ties);  // E <- B, M
+        route2(vE + T_ES, vS + T_SS, &cS, &pS, em.ties);  // S <- E, S
         vB = pB + e[0];
         vM = pM + e[1];
         vE = pE + e[2];
@@ -1109,11 +1115,7 @@ __device__ __forceinline__ void rec_weights(const DevImage& im, uint64_t rc, dou
         const bool has = m != 0u;
         m &= m - 1u;
         const uint32_t idx = (uint32_t)(rc >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u);
-#if JB_X_NOW  // diagnostic: no weight gathers (wrong results)
-        w[k] = (double)(has ? idx : 0u) * -0.001;
-#else
         w[k] = im.wtab[has ? idx : 0u];
-#endif
     }
 }
 // Fold a record's edges (L <= kZhRing, so best(i+L) is in the ring or is the
@@ -1156,7 +1158,7 @@ __device__ __forceinline__ void rec_fold_s(uint32_t m, const double w[4], DpFold
 // General form (any rune widths): the next rune's record is loaded one step ahead.
 template <class V, class Src>
 __device__ uint32_t zh_dp(const V& v, const DevImage& im, const uint64_t* __restrict__ erec,
-                          double* __restrict__ gbest, double* ring, const Src& src, uint32_t ablate) {
+                          double* __restrict__ gbest, double* ring, const Src& src) {
     uint32_t j = 0, bs = 0, be = 0;
     if (!src.next(j, bs, be)) return 0;
     uint32_t key0 = be / 3u, steps = 0;
@@ -1231,14 +1233,9 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
     uint64_t lo = 0, hi = 0;  // the last pair: lo = the rune further back
     auto pair = [&](uint32_t k) {  // slots k, k+1 in one 16-byte load
         typedef uint64_t u64x2 __attribute__((ext_vector_type(2), aligned(8)));
-#if JB_X_NOREC  // diagnostic: no record loads (wrong results)
-        lo = 0x0000000000000103ull + k;
-        hi = 0x0000000000000101ull;
-#else
         const u64x2 x = *reinterpret_cast<const u64x2*>(erec + (int32_t)k);
         lo = x.x;
         hi = x.y;
-#endif
     };
     auto setup = [&]() {
         key0 = be / 3u;
@@ -1325,7 +1322,8 @@ struct RunList {
 // register sets that alternate between steps (nothing copied out of a load's
 // destination).  Returns the final states, bit r set for E (:723-729).
 template <class E>
-__device__ uint32_t viterbi_fwd_runs(const GrpZvT<true>& v, const DevImage& im, const uint32_t* runs, uint32_t n) {
+__device__ uint32_t viterbi_fwd_runs(const GrpZvT<true>& v, const DevImage& im, const uint32_t* runs, uint32_t n,
+                                     uint32_t& nt) {
     // rune cursor: position q and run r of the current, next and next-but-one rune
     uint32_t q0 = 0, r0 = 0, q1 = 0, r1 = 0, q2 = 0, r2 = 0, t = 0;
     auto rs_of = [&](uint32_t r) { return v.wb + (runs[r * 64u] & 0xFFFFu); };
@@ -1365,11 +1363,13 @@ __device__ uint32_t viterbi_fwd_runs(const GrpZvT<true>& v, const DevImage& im, 
         }
         uint32_t cB, cM, cE, cS;
         double pB, pM, pE, pS;
-        route2(vE + T_EB, vS + T_SB, &cB, &pB);  // B <- E, S
-        route2(vB + T_BM, vM + T_MM, &cM, &pM);  // M <- B, M
-        route2(vB + T_BE, vM + T_ME, &cE, &pE);  // E <- B, M
-        route2(vE + T_ES, vS + T_SS, &cS, &pS);  // S <- E, S
+        uint32_t tt = 0;  // (a run's first rune takes no route: its values are the previous run's)
+        route2(vE + T_EB, vS + T_SB, &cB, &pB, tt);  // B <- E, S
+        route2(vB + T_BM, vM + T_MM, &cM, &pM, tt);  // M <- B, M
+        route2(vB + T_BE, vM + T_ME, &cE, &pE, tt);  // E <- B, M
+        route2(vE + T_ES, vS + T_SS, &cS, &pS, tt);  // S <- E, S
         const bool first = t == 0;
+        nt += first ? 0u : tt;
         vB = (first ? START_B : pB) + ec[0];
         vM = (first ? JB_MIN_FLOAT : pM) + ec[1];
         vE = (first ? JB_MIN_FLOAT : pE) + ec[2];
@@ -1397,10 +1397,9 @@ __device__ uint32_t viterbi_fwd_runs(const GrpZvT<true>& v, const DevImage& im, 
 // reference panics (a rune on the chosen path with no DAG edge: cutDAG slices
 // with tail index -1).
 template <bool HMM, class V, class E>
-__device__ bool zh_fwd(const V& v, const DevImage& im, uint32_t bs, uint32_t be, E& em, uint32_t ablate,
-                       RunList* rl) {
+__device__ bool zh_fwd(const V& v, const DevImage& im, uint32_t bs, uint32_t be, E& em, RunList* rl) {
     auto run_end = [&](uint32_t rs, uint32_t re, uint32_t m) {
-        if ((ablate & 32u) || m == 1u) em.token(rs, re);  // a single rune is always "S" (:672-674)
+        if (m == 1u) em.token(rs, re);  // a single rune is always "S" (:672-674)
         else if (rl && rl->n < kZhRuns) {
             rl->t[rl->n * 64u] = (rs - rl->wb) | ((re - rl->wb) << 16);
             rl->n++;
@@ -1435,9 +1434,9 @@ __device__ bool zh_fwd(const V& v, const DevImage& im, uint32_t bs, uint32_t be,
 // The forward walk over all of a lane's blocks in one loop (a lane's trip
 // count is its total piece count, not the per-block maximum over the wave).
 template <bool HMM, class V, class E, class Src>
-__device__ bool zh_fwd_lane(const V& v, const DevImage& im, const Src& src, E& em, uint32_t ablate, RunList* rl) {
+__device__ bool zh_fwd_lane(const V& v, const DevImage& im, const Src& src, E& em, RunList* rl) {
     auto run_end = [&](uint32_t rs, uint32_t re, uint32_t m) {
-        if ((ablate & 32u) || m == 1u) em.token(rs, re);  // a single rune is always "S" (:672-674)
+        if (m == 1u) em.token(rs, re);  // a single rune is always "S" (:672-674)
         else if (rl && rl->n < kZhRuns) {
             rl->t[rl->n * 64u] = (rs - rl->wb) | ((re - rl->wb) << 16);
             rl->n++;
@@ -1507,11 +1506,11 @@ __device__ void zh_chunk_main(const uint8_t* __restrict__ text, const DevImage& 
                               const uint64_t* __restrict__ erec, double* __restrict__ gbest, uint8_t* bls,
                               double* ring, uint32_t* rb32, uint32_t* runs, const TblSrc& src, uint32_t wb,
                               uint32_t lane,
-                              uint32_t* __restrict__ counters, uint32_t ablate, uint64_t* st) {
+                              uint32_t* __restrict__ counters, uint32_t winw, uint32_t& nties, uint64_t* st) {
     const GrpZvT<A3> v{text, bls, wb};
     uint32_t steps;
     if constexpr (A3) steps = zh_dp_a3(v, im, erec, gbest, ring, src);
-    else steps = zh_dp(v, im, erec, gbest, ring, src, ablate);
+    else steps = zh_dp(v, im, erec, gbest, ring, src);
     wave_sync();  // ring dead: its space takes the window's token bitmaps
     if (st) {
         const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -1525,19 +1524,19 @@ __device__ void zh_chunk_main(const uint8_t* __restrict__ text, const DevImage& 
     }
     uint32_t* sb = rb32;
     uint32_t* eb = rb32 + kZhWinWords;
-    for (uint32_t k = lane; k < kZhWinWords; k += 64u) {
+    for (uint32_t k = lane; k < winw; k += 64u) {
         sb[k] = 0u;
         eb[k] = 0u;
     }
     wave_sync();
-    if (!(ablate & 4u)) {
+    {
         LdsEmitter le(sb, eb, wb >> 5);
         bool ok;
         RunList rl{runs, wb, 0u};
         RunList* const rlp = (HMM && A3) ? &rl : nullptr;
-        ok = zh_fwd_lane<HMM>(v, im, src, le, ablate, rlp);
+        ok = zh_fwd_lane<HMM>(v, im, src, le, rlp);
         if constexpr (HMM && A3) {
-            const uint32_t stb = viterbi_fwd_runs<LdsEmitter>(v, im, runs, rl.n);
+            const uint32_t stb = viterbi_fwd_runs<LdsEmitter>(v, im, runs, rl.n, le.ties);
             for (uint32_t r = 0; r < kZhRuns; r++)
                 if (r < rl.n) {
                     const uint32_t x = runs[r * 64u];
@@ -1547,6 +1546,7 @@ __device__ void zh_chunk_main(const uint8_t* __restrict__ text, const DevImage& 
                 }
         }
         le.flush();
+        nties += le.ties;
         if (!ok) atomicOr(counters + CNT_ERR, 1u);
     }
     wave_sync();
@@ -1566,7 +1566,7 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
                                             double* __restrict__ gbest,
                                             uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
                                             uint2* __restrict__ longblk, uint32_t grp,
-                                            uint32_t ablate, uint64_t* __restrict__ dbg) {
+                                            uint32_t diag, uint64_t* __restrict__ dbg) {
     __shared__ uint8_t s_bl[4][kZhWin / 3u + 4u];
     __shared__ double s_rb[4][kZhRing * 64];  // DP ring, then the window's token bitmaps
     __shared__ uint32_t s_tbl[4][kZhChunk];   // the chunk's blocks as found, then as dealt to the lanes
@@ -1580,17 +1580,18 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
     const uint32_t nblk = counters[CNT_NBLK], nzh = counters[CNT_NZH];
     const uint32_t ngroups = (uint32_t)((nbytes + grp - 1u) / grp);  // (grp <= kZhGroupBytes)
     const uint32_t ntiles = (uint32_t)((nbytes + kTileBytes - 1u) / kTileBytes);
+    const uint32_t winw = (grp + (kZhWin - kZhGroupBytes)) / 32u + 1u;  // token words of a window (<= kZhWinWords)
     Emitter em(sbits, ebits);
-    em.off = (ablate & 128u) != 0;
     // diagnostic per-wave clocks (JB_ABLATE bit 8): [0] setup [1] DP [2] forward+Viterbi+flush [3] chunks
     // [4] sum of lane DP steps [5] sum of per-chunk max lane DP steps [6] blocks past the window [7] scratch
     uint64_t stv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #if JB_STAMPS
-    uint64_t* st = (ablate & 0x100u) ? stv : nullptr;
+    uint64_t* st = (diag & 0x100u) ? stv : nullptr;
 #else
     uint64_t* const st = nullptr;  // built without the diagnostic clocks (make STAMPS=1)
 #endif
     const uint64_t tk0 = st ? __builtin_amdgcn_s_memtime() : 0;
+    uint32_t nties = 0;  // Viterbi route ties of the in-window blocks (em.ties: the others)
     for (;;) {
         uint32_t g = 0;
         if (lane == 0) g = atomicAdd(counters + CNT_WORK, 1u);
@@ -1704,18 +1705,17 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
             }
             if (all3)
                 zh_chunk_main<HMM, true>(text, im, erec, gbest, s_bl[wv], ring, rb32, s_runs[wv] + lane, src, wb, lane,
-                                         counters, ablate,
-                                         st);
+                                         counters, winw, nties, st);
             else
                 zh_chunk_main<HMM, false>(text, im, erec, gbest, s_bl[wv], ring, rb32, s_runs[wv] + lane, src, wb,
-                                          lane, counters, ablate, st);
+                                          lane, counters, winw, nties, st);
             // the window's token words: consecutive words per lane, one OR each (edge
             // words are shared with neighbouring groups and with k_nonzh)
-            if (!em.off) {
+            {
                 const uint32_t w0 = wb >> 5;
                 const uint32_t* sb = rb32;
                 const uint32_t* eb = rb32 + kZhWinWords;
-                for (uint32_t k = lane; k < kZhWinWords; k += 64u) {
+                for (uint32_t k = lane; k < winw; k += 64u) {
                     const uint32_t a = sb[k], b = eb[k];
                     if (a) atomicOr(sbits + w0 + k, a);
                     if (b) atomicOr(ebits + w0 + k, b);
@@ -1731,8 +1731,8 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
                     longblk[li] = make_uint2(bsi[i], bei[i]);
                 } else if (out[i]) {
                     const GlbZv gv{text, gbl};
-                    zh_dp(gv, im, erec, gbest, ring, OneSrc{bsi[i], bei[i]}, ablate);
-                    if (!(ablate & 4u) && !zh_fwd<HMM>(gv, im, bsi[i], bei[i], em, ablate, nullptr))
+                    zh_dp(gv, im, erec, gbest, ring, OneSrc{bsi[i], bei[i]});
+                    if (!zh_fwd<HMM>(gv, im, bsi[i], bei[i], em, nullptr))
                         atomicOr(counters + CNT_ERR, 1u);
                 }
             }
@@ -1745,6 +1745,12 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
         }
     }
     em.flush();
+    {
+        uint32_t t = nties + em.ties;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) t += (uint32_t)__shfl_xor((int)t, d, 64);
+        if (lane == 0 && t) atomicAdd(counters + CNT_TIES, t);
+    }
     if (st) {
         // lane DP steps summed over the wave
         uint64_t sum = stv[4];
@@ -1821,9 +1827,11 @@ __global__ __launch_bounds__(64) void k_zh_long(const uint8_t* __restrict__ text
         if (__any(any4)) {  // the general one-lane path (k_zh's)
             if (lane == 0) {
                 const GlbZv gv{text, gbl};
-                zh_dp(gv, im, erec, gbest, s_ring + lane, OneSrc{bs, be}, 0u);
-                if (!zh_fwd<HMM>(gv, im, bs, be, em, 0u, nullptr)) atomicOr(counters + CNT_ERR, 1u);
+                zh_dp(gv, im, erec, gbest, s_ring + lane, OneSrc{bs, be});
+                if (!zh_fwd<HMM>(gv, im, bs, be, em, nullptr)) atomicOr(counters + CNT_ERR, 1u);
                 em.flush();
+                if (em.ties) atomicAdd(counters + CNT_TIES, em.ties);
+                em.ties = 0;
             }
             __syncthreads();
             continue;
@@ -1991,9 +1999,6 @@ __global__ __launch_bounds__(64) void k_zh_long(const uint8_t* __restrict__ text
             }
         };
         stage(0u);
-#if JB_X_NOPATH  // diagnostic: DP only (wrong results)
-        p = n;
-#endif
         while (p < n) {
             if (p - flo >= fm) stage(p);
             const uint32_t Ln = L.b[p - flo];
@@ -2014,10 +2019,10 @@ __global__ __launch_bounds__(64) void k_zh_long(const uint8_t* __restrict__ text
                 } else {
                     uint32_t cB, cM, cE, cS;
                     double pB, pM, pE, pS;
-                    route2(vE + T_EB, vS + T_SB, &cB, &pB);  // B <- E, S
-                    route2(vB + T_BM, vM + T_MM, &cM, &pM);  // M <- B, M
-                    route2(vB + T_BE, vM + T_ME, &cE, &pE);  // E <- B, M
-                    route2(vE + T_ES, vS + T_SS, &cS, &pS);  // S <- E, S
+                    route2(vE + T_EB, vS + T_SB, &cB, &pB, em.ties);  // B <- E, S
+                    route2(vB + T_BM, vM + T_MM, &cM, &pM, em.ties);  // M <- B, M
+                    route2(vB + T_BE, vM + T_ME, &cE, &pE, em.ties);  // E <- B, M
+                    route2(vE + T_ES, vS + T_SS, &cS, &pS, em.ties);  // S <- E, S
                     vB = pB + e[0];
                     vM = pM + e[1];
                     vE = pE + e[2];
@@ -2036,6 +2041,8 @@ __global__ __launch_bounds__(64) void k_zh_long(const uint8_t* __restrict__ text
         }
         if (HMM && run_n && !bad) run_end(n);
         em.flush();
+        if (lane == 0u && em.ties) atomicAdd(counters + CNT_TIES, em.ties);  // (every lane ran the same chain)
+        em.ties = 0;
         if (bad && lane == 0u) atomicOr(counters + CNT_ERR, 1u);
         __syncthreads();
     }
@@ -2246,8 +2253,6 @@ __global__ void k_doc_tok(const uint64_t* __restrict__ doc_off, uint32_t ndocs, 
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-uint32_t g_ablate = 0;  // diagnostic ablations (JB_ABLATE); results are wrong when non-zero
-
 template <bool HMM>
 static uint32_t occ_zh() {
     int n = 0;
@@ -2271,12 +2276,13 @@ uint32_t nonzh_blocks_per_cu() {
     } while (0)
 
 hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text, uint64_t nbytes,
-                        const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, uint32_t grid_zh, uint32_t grid_nz,
+                        const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, const LaunchCfg& lc,
                         hipStream_t stream, KernelTimer* timer) {
+    const uint32_t grid_zh = lc.grid_zh, grid_nz = lc.grid_nz, diag = lc.diag;
     const uint64_t nwords = (nbytes + 31) / 32;
     const uint32_t ntiles = (uint32_t)((nbytes + kTileBytes - 1) / kTileBytes);
     // k_zh work unit: a small batch gets small groups, so that enough waves share it
-    const uint32_t grp = nbytes < kZhSmallBatch ? kZhGroupSmall : kZhGroupBytes;
+    const uint32_t grp = lc.zh_group ? lc.zh_group : zh_group_for(nbytes);
     const uint32_t nttiles = (uint32_t)((nwords + kTokTileWords - 1) / kTokTileWords);
     hipError_t e;
     if ((e = hipMemsetAsync(w.counters, 0, CNT_NWORDS * sizeof(uint32_t) + sizeof(uint64_t), stream))) return e;
@@ -2291,7 +2297,7 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                                d_doc_off, ndocs, nbytes, w.docbits));
     JB_TIMED(K_MARK_WALK, hipLaunchKernelGGL(k_mark_walk, dim3(ntiles), dim3(256), 0, stream, d_text, nbytes,
                                              w.docbits, im, w.lanemask, w.tile_cnt, w.erec + kErecPad,
-                                             w.tile4, w.alnum16, w.sbits, w.ebits, g_ablate, w.dbg_walk));
+                                             w.tile4, w.alnum16, w.sbits, w.ebits, diag, w.dbg_walk));
     JB_TIMED(K_SCAN_BLOCKS, hipLaunchKernelGGL(k_sup, dim3((ntiles + 255) / 256), dim3(256), 0, stream, w.tile_cnt,
                                                ntiles, w.supb));
     JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL(k_blocks_write, dim3((ntiles + kBwTiles - 1) / kBwTiles), dim3(256), 0,
@@ -2300,11 +2306,11 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     if (hmm)
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
                                           w.gstart, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
-                                          w.longblk, grp, g_ablate, w.dbg));
+                                          w.longblk, grp, diag, w.dbg));
     else
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
                                           w.gstart, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
-                                          w.longblk, grp, g_ablate, w.dbg));
+                                          w.longblk, grp, diag, w.dbg));
     if (hmm)
         JB_TIMED(K_ZH_LONG, hipLaunchKernelGGL((k_zh_long<true>), dim3(kZhLongGrid), dim3(64), 0, stream, d_text, im,
                                                w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters, w.sbits,

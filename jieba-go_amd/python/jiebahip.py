@@ -29,7 +29,7 @@ EXPORTS = [
     "jb_cut_device",
     "jb_add_word", "jb_dict_get", "jb_dict_size", "jb_save", "jb_profile_enable", "jb_profile_read",
     "jb_profile_reset", "jb_image_build", "jb_image_free", "jb_image_save", "jb_image_dict_info", "jb_image_lookup",
-    "jb_image_stats", "jb_image_emit", "jb_go_log",
+    "jb_image_stats", "jb_image_emit", "jb_go_log", "jb_shard_bounds", "jb_last_stats",
 ]
 
 
@@ -45,6 +45,11 @@ class jb_config(C.Structure):
         ("size_override", C.c_int64), ("emit_path", C.c_char_p), ("emit_buf", C.c_char_p), ("emit_len", C.c_size_t),
         ("device", C.c_int), ("ndevices", C.c_int),
     ]
+
+
+class jb_stats(C.Structure):
+    _fields_ = [("tokens", C.c_uint64), ("blocks", C.c_uint64), ("zh_blocks", C.c_uint64),
+                ("long_blocks", C.c_uint64), ("viterbi_ties", C.c_uint64)]
 
 
 class jb_spans(C.Structure):
@@ -107,6 +112,8 @@ def lib():
         L.jb_image_emit.restype = C.c_double
         L.jb_go_log.argtypes = [C.c_double]
         L.jb_go_log.restype = C.c_double
+        L.jb_shard_bounds.argtypes = [vp, C.c_uint32, C.c_uint32, vp]
+        L.jb_last_stats.argtypes = [vp, C.POINTER(jb_stats)]
         _lib = L
     return _lib
 
@@ -313,6 +320,15 @@ class Tokenizer:
                                    int(hmm), C.c_void_p(stream_ptr), C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
         return a.value, b.value, c.value, d.value
 
+    def last_stats(self):
+        """Counters of the last pipeline run (jb_last_stats); synchronises."""
+        st = jb_stats()
+        _check(lib().jb_last_stats(self.h, C.byref(st)))
+        return {k: getattr(st, k) for k, _ in jb_stats._fields_}
+
+    def last_ties(self):
+        return self.last_stats()["viterbi_ties"]
+
     # -- dictionary ------------------------------------------------------
     def AddWord(self, word, freq):
         """Tokenizer.AddWord (tokenizer.go:372) without the reference's deadlock."""
@@ -372,6 +388,14 @@ def loaded_runtime():
     except OSError:
         pass
     return sorted(out)
+
+
+def shard_bounds(doc_off, nparts):
+    """jb_shard_bounds: the document ranges jb_cut_batch gives each device."""
+    doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
+    cut = np.zeros(nparts + 1, np.uint32)
+    _check(lib().jb_shard_bounds(doc_off.ctypes.data, len(doc_off) - 1, nparts, cut.ctypes.data))
+    return [int(x) for x in cut]
 
 
 def go_log(x):

@@ -153,6 +153,43 @@ def test_docs_corpus(full, hmm):
     _cmp_batch(tk, o, buf, off, hmm, f"docs hmm={hmm}")
 
 
+@pytest.mark.parametrize("group", [1024, 3072, 6144])
+def test_docs_corpus_zh_groups(syn_full, group, monkeypatch):
+    """k_zh picks its group size by batch size (1 KiB under 16 MiB, 6 KiB at the
+    headline's size); JB_ZH_GROUP (read at jb_open) forces one, so the large-batch
+    group runs here on a small batch, both HMM settings, bit-exact."""
+    dp, ep, s = syn_full
+    monkeypatch.setenv("JB_ZH_GROUP", str(group))
+    tk, o = _pair(dp, ep)
+    monkeypatch.delenv("JB_ZH_GROUP")
+    buf, off, nr = s.corpus(synth.KIND_DOCS, 2000 + group, target_bytes=6 << 20)
+    for hmm in (False, True):
+        _cmp_batch(tk, o, buf, off, hmm, f"docs group={group} hmm={hmm}")
+    sbuf, soff, _ = s.corpus(synth.KIND_SENTENCES, 50, max_docs=3000, target_bytes=1 << 30)
+    _cmp_batch(tk, o, sbuf, soff, True, f"sentences group={group}")
+    tk.close()
+
+
+def test_graph_replay_after_add_word(syn_small):
+    """A batch cut twice is replayed from a captured HIP graph; AddWord re-uploads
+    the image (new device buffers), so the next cut must not replay the old graph."""
+    dp, ep, s = syn_small
+    tk, o = _pair(dp, ep)
+    buf, off, nr = s.corpus(synth.KIND_DOCS, 31, target_bytes=1 << 20)
+    for _ in range(3):  # direct, captured, replayed
+        _cmp_batch(tk, o, buf, off, True, "before AddWord")
+    text = bytes(np.asarray(buf)[: int(off[1])]).decode("utf-8")
+    import re
+    word = re.search("[\u4e00-\u9fa5]{4}", text).group(0)  # 4 adjacent Han runes of the first document
+    tk.AddWord(word, 10_000_000)
+    o.add_term(word, 10_000_000)
+    for _ in range(3):
+        _cmp_batch(tk, o, buf, off, True, "after AddWord")
+    gs, ge, _ = tk.cut_batch(buf, off, True)
+    assert any(bytes(np.asarray(buf)[a:b]).decode("utf-8") == word for a, b in zip(gs[:5000], ge[:5000]))
+    tk.close()
+
+
 @pytest.mark.parametrize("kind", [synth.KIND_LONG_PUNCT, synth.KIND_LONG_OOV])
 def test_long_document(full, kind):
     """Config 5: one 1M-rune document (5a punctuated, 5b long OOV runs)."""
@@ -360,3 +397,48 @@ def test_cut_batch_into_caller_arrays(small):
         assert np.array_equal(ts, gs) and np.array_equal(te, ge) and np.array_equal(td, gd)
         ts2, te2, td2, _ = tk.cut_batch_into(buf, off, hmm, out)  # reuse
         assert np.array_equal(ts2, gs) and np.array_equal(td2, gd)
+
+
+def _tie_emissions():
+    """Emissions under which the 3-rune HMM run 甲乙丙 has an exact route tie
+    vE + T_EB == vS + T_SB > minFloat at its third rune (state B, Q12), found by
+    stepping eS(乙) one ulp at a time (float64 adds as in tokenizer.go:686-716)."""
+    import math
+    START_B, START_S = -0.26268660809250016, -1.4652633398537678  # tokenizer.go:629-632
+    T_BE, T_SS, T_EB, T_SB = -0.51082562376599, -0.6658631448798212, -0.5897149736854513, -0.7211965654669841
+    eB0, eS0, eE1 = -3.0, -4.0, -5.0
+    vE1 = ((START_B + eB0) + T_BE) + eE1
+    a = vE1 + T_EB
+    pS = (START_S + eS0) + T_SS
+    x = (a - T_SB) - pS
+    for _ in range(4096):
+        if (pS + x) + T_SB == a:
+            break
+        x = math.nextafter(x, -math.inf if (pS + x) + T_SB > a else math.inf)
+    else:
+        raise AssertionError("no exact tie found")
+    return {"B": {"甲": eB0, "乙": -6.0, "丙": -2.5, "词": -3.0}, "E": {"乙": eE1, "丙": -2.0, "语": -3.0},
+            "M": {"乙": -7.0}, "S": {"甲": eS0, "乙": x, "丙": -3.5}}
+
+
+def test_viterbi_ties_counted(tmp_path):
+    """Exact stateTransitionRoute ties (tokenizer.go:748-753, resolved in Go map
+    order) are counted on the GPU (jb_last_stats) exactly as the oracle counts
+    them, in each Viterbi code path: k_zh's deferred runs (all-3-byte window),
+    its general path (a 4-byte Han rune in the window) and k_zh_long (a block
+    of >= 8 KiB); the cut itself is bit-exact."""
+    import json
+    dp, ep = tmp_path / "d.txt", tmp_path / "e.json"
+    dp.write_text("词 5\n词语 1000\n", encoding="utf-8")
+    ep.write_text(json.dumps(_tie_emissions(), ensure_ascii=False), encoding="utf-8")
+    texts = ["甲乙丙", "x，甲乙丙。", "\U00020000，甲乙丙", "词语" * 1400 + "甲乙丙"]
+    for t in texts:
+        tk, o = _pair(str(dp), str(ep))
+        buf, off = _batch_of([t])
+        _cmp_batch(tk, o, buf, off, True, t[:8])
+        st = tk.last_stats()
+        assert o.ties >= 1, t[:8]
+        assert st["viterbi_ties"] == o.ties, (t[:8], st, o.ties)
+        if len(t) > 4000:
+            assert st["long_blocks"] == 1
+        tk.close()

@@ -19,24 +19,65 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, dict_path, emit_path, buf, off, out_dir):
-    import torch
+class OracleCutter:
+    """Stands in for bench.GpuCutter on CPU (test only): the rank's "device"
+    output is the oracle's, optionally with one token corrupted."""
+
+    def __init__(self, o, buf, off, hmm, corrupt=False):
+        self.o, self.buf, self.off, self.hmm, self.corrupt = o, buf, off, hmm, corrupt
+        self.steps = 0
+
+    def step(self):
+        self.steps += 1
+
+    def sync(self):
+        pass
+
+    def profile(self, steps):
+        return {}, None
+
+    def results(self):
+        s, e, d = self.o.cut_batch(self.buf, self.off, bool(self.hmm), nthreads=2)
+        s = s.copy()
+        if self.corrupt and len(s):
+            s[len(s) // 2] += 1
+        return s, e, d
+
+    def ties(self):
+        return 0
+
+
+def _worker(rank, world, port, dict_path, emit_path, corpus_mib, corrupt_rank, out_dir):
+    import json
+    import types
+    import bench
     import oracle as O
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    sub, soff, d0, base = shard.shard_of(buf, off, world, rank)
-    o = O.Oracle.from_files(dict_path, emit_path, 0)
-    s, e, dt = o.cut_batch(sub, soff, True)
+    args = types.SimpleNamespace(workload="docs", corpus_mib=corpus_mib, nwords=20_000, hmm=1, steps=3, warmup=1,
+                                 no_profile=True, no_parity=False, cpu1_sample_mib=0, dict_kind="txt")
+    seen = {}
+
+    def make_cutter(buf, off, hmm):
+        c = OracleCutter(O.Oracle.from_files(dict_path, emit_path, 0), buf, off, hmm, corrupt=rank == corrupt_rank)
+        seen["c"] = c
+        return c
+
+    out = bench.run(args, world, rank, dist, "cpu", make_cutter, lambda: O.Oracle.from_files(dict_path, emit_path, 0))
+    c = seen["c"]
+    s, e, d = c.o.cut_batch(c.buf, c.off, True, nthreads=2)
     parts = [None] * world
-    dist.all_gather_object(parts, (s, e, dt, base))
-    # job-level aggregates as bench.py computes them
-    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    w = torch.tensor([float(len(sub) - 16)], dtype=torch.float64)
-    dist.all_reduce(w, op=dist.ReduceOp.SUM)
+    dist.all_gather_object(parts, (s, e, d, len(c.off) - 1, c.steps))
     if rank == 0:
-        S, E, DT = shard.merge(parts)
-        np.savez(os.path.join(out_dir, "merged.npz"), s=S, e=E, dt=DT, tmax=t.item(), wsum=w.item())
+        line = out[0]
+        with open(os.path.join(out_dir, "line.json"), "w") as f:
+            json.dump(line, f)
+        np.savez(os.path.join(out_dir, "parts.npz"),
+                 **{f"s{r}": p[0] for r, p in enumerate(parts)}, **{f"e{r}": p[1] for r, p in enumerate(parts)},
+                 **{f"d{r}": p[2] for r, p in enumerate(parts)},
+                 nd=np.array([p[3] for p in parts]), steps=np.array([p[4] for p in parts]))
+    else:
+        assert out is None
     dist.barrier()
     dist.destroy_process_group()
 
@@ -53,16 +94,56 @@ def test_shard_bounds_cover_and_balance():
         assert max(per) - min(per) <= 2 * 5000
 
 
-def test_two_ranks_gloo_equals_single_process(syn_small):
+def test_library_shard_bounds_equal_python():
+    """jb_shard_bounds (the partition jb_cut_batch gives each device of a ctx)
+    and shard.shard_bounds (bench.py's per-rank partition) are the same rule."""
+    import jiebahip as J
+    rng = np.random.default_rng(5)
+    cases = [np.zeros(1, np.uint64), np.array([0, 10], np.uint64), np.array([7, 7, 7, 20], np.uint64)]
+    for n in (1, 2, 3, 17, 1000):
+        sizes = rng.integers(0, 3000, size=n)
+        sizes[rng.random(n) < 0.2] = 0  # empty documents
+        cases.append((np.concatenate([[0], np.cumsum(sizes)]) + rng.integers(0, 50)).astype(np.uint64))
+    big = np.cumsum(np.full(9, 1 << 40, np.uint64))  # offsets past 2^32
+    cases.append(np.concatenate([[0], big]).astype(np.uint64))
+    for off in cases:
+        for parts in (1, 2, 3, 4, 8, 13):
+            assert J.shard_bounds(off, parts) == shard.shard_bounds(off, parts), (len(off), parts)
+    with pytest.raises(J.JbError):
+        J.shard_bounds(np.array([0, 5, 3], np.uint64), 2)  # not monotonic
+
+
+@pytest.mark.parametrize("corrupt_rank", [-1, 1])
+def test_bench_two_ranks_gloo(syn_small, corrupt_rank):
+    """bench.run's N > 1 path on CPU over gloo, world size 2: each rank takes its
+    jb_shard_bounds range of the fixed corpus, times its steps, checks its whole
+    shard against the oracle; rank 0's line carries the max-over-ranks time and
+    the job-level sums.  The per-rank outputs merged in rank order equal one
+    process cutting the whole corpus, and one corrupted token on rank 1 makes
+    the job's parity fail."""
+    import json
     import oracle as O
     import synth
     dp, ep, s = syn_small
-    buf, off, nr = s.corpus(synth.KIND_DOCS, 40, target_bytes=300_000)
+    mib = 0.75
     with tempfile.TemporaryDirectory() as out:
-        mp.start_processes(_worker, args=(2, _free_port(), dp, ep, buf, off, out), nprocs=2, join=True,
+        mp.start_processes(_worker, args=(2, _free_port(), dp, ep, mib, corrupt_rank, out), nprocs=2, join=True,
                            start_method="spawn")
-        m = np.load(os.path.join(out, "merged.npz"))
-        o = O.Oracle.from_files(dp, ep, 0)
-        s1, e1, d1 = o.cut_batch(buf, off, True)
-        assert np.array_equal(m["s"], s1) and np.array_equal(m["e"], e1) and np.array_equal(m["dt"], d1)
-        assert m["tmax"] == 2.0 and m["wsum"] == float(off[-1])
+        with open(os.path.join(out, "line.json")) as f:
+            line = json.load(f)
+        parts = np.load(os.path.join(out, "parts.npz"))
+    buf, off, nr = s.corpus_parallel(synth.KIND_DOCS, 0, target_bytes=int(mib * (1 << 20)), threads=2)
+    cut = shard.shard_bounds(off, 2)
+    assert list(parts["nd"]) == [cut[1] - cut[0], cut[2] - cut[1]] and list(parts["steps"]) == [4, 4]
+    merged = shard.merge([(parts[f"s{r}"], parts[f"e{r}"], parts[f"d{r}"], int(off[cut[r]])) for r in range(2)])
+    o = O.Oracle.from_files(dp, ep, 0)
+    s1, e1, d1 = o.cut_batch(buf, off, True, nthreads=4)
+    assert np.array_equal(merged[0], s1) and np.array_equal(merged[1], e1) and np.array_equal(merged[2], d1)
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["config"]["corpus_bytes"] == int(off[-1]) and line["config"]["corpus_docs"] == len(off) - 1
+    assert line["config"]["corpus_chars"] == nr
+    assert line["parity"]["bytes"] == int(off[-1]) and line["parity"]["tokens"] == len(s1)
+    assert line["parity"]["bit_exact"] == (corrupt_rank < 0)
+    assert line["parity"]["mismatches"] == (0 if corrupt_rank < 0 else 1)
+    assert line["cpu_baseline"] is None  # (rank 0 at N = 1 only)
+    assert abs(line["value"] - nr * 3 / (line["ms_per_step"] * 3e-3)) / line["value"] < 0.05  # (ms rounded)
