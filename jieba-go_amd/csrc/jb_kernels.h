@@ -69,6 +69,10 @@ struct Work {
     uint2* longblk;        // (start, end) of each long zh block (k_zh -> k_zh_long)
     uint32_t* tile4;       // per tile: a 4-byte Han rune starts in it
     uint8_t* gbl;          // per Han rune: chosen piece length, then Viterbi back-pointers / labels
+                           // (+512 bytes: k_zh_long reads 256-slot windows)
+    uint32_t* lpath;       // long blocks: 1 bit per Han rune slot, a piece of the chosen path starts here
+    uint32_t* lflag;       // per long block: 1 when k_long_tail cuts it (all-3-byte, path complete)
+    uint8_t* lbp;          // long blocks: Viterbi back-pointers / labels per slot (k_long_tail)
     double* gbest;         // per Han rune: best proba, kept only for blocks with an edge > 8 runes
     uint32_t* tok_start;
     uint32_t* tok_end;
@@ -83,7 +87,7 @@ struct Work {
 // Kernel ids for per-launch timing.
 enum KernelId {
     K_DOCBITS = 0, K_MARK_WALK, K_SCAN_BLOCKS, K_BLOCKS_WRITE, K_ZH, K_NONZH,
-    K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_ZH_LONG, K_NUM
+    K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_ZH_LONG, K_LONG_TAIL, K_NUM
 };
 extern const char* const kKernelNames[K_NUM];
 

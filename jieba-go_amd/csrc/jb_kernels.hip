@@ -35,7 +35,7 @@ namespace jb {
 
 const char* const kKernelNames[K_NUM] = {"k_docbits", "k_mark_walk", "k_scan_blocks", "k_blocks_write",
                                          "k_zh", "k_nonzh", "k_tok_count", "k_scan_tok",
-                                         "k_tok_write", "k_doc_tok", "k_zh_long"};
+                                         "k_tok_write", "k_doc_tok", "k_zh_long", "k_long_tail"};
 
 // newJiebaHMM literals (tokenizer.go:629-652)
 #define START_B (-0.26268660809250016)
@@ -1775,25 +1775,41 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// k_zh_long: the long zh blocks (>= kZhLongMin bytes; e.g. an unpunctuated
-// document), one wave each.  Their DP, path and Viterbi are serial chains
-// (bit-exact float64 order forbids reassociating them), so the wave runs each
-// chain as one uniform program on all lanes at once, from LDS: windows of
-// kLW runes are staged cooperatively (records and their weights for the DP,
-// piece lengths and emissions for the path and the Viterbi), then every lane
-// steps through the window with the same values (broadcast LDS reads, no
-// divergence), so the next refill is again a parallel, coalesced load.  One
-// lane's walk over global memory took a memory round trip per rune.
-// All-3-byte blocks only; a block with a 4-byte Han rune takes the one-lane
-// path of k_zh.
+// Long zh blocks (>= kZhLongMin bytes; e.g. an unpunctuated document, BASELINE
+// config 5b).  Their DP is one serial chain: best(i) is built from best(i+L)
+// with float64 adds in the reference's order (:519-529), which must not be
+// re-associated, so no two runes' values can be computed in parallel.  What
+// is NOT serial is everything after it: findDagPath only follows the chosen
+// lengths, and the HMM runs between multi-rune pieces are independent of
+// each other (:229-253).  So:
+//   k_zh_long  one wave per long block: (1) the DP, backwards, run as a
+//              uniform program (every lane computes the same values, the
+//              chain branches on scalars: each rune's record is classified
+//              when its block of 64 is loaded);
+//              (2) the path: a scalar walk p += L(p) from rune 0 over the
+//              chosen lengths, marking piece starts in the `lpath` bitmap.
+//   k_long_tail  many waves: one lane per 64 runes turns the marked pieces
+//              into tokens and runs the Viterbi (+ cutHMM) of every run of
+//              single-rune pieces that starts in its range.
+// All-3-byte blocks only; a long block with a 4-byte Han rune takes k_zh's
+// one-lane path inside k_zh_long.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kLW = 1024;  // runes per staged window
-constexpr uint32_t kZhLongGrid = 64;   // k_zh_long waves (persistent over the long-block list)
-struct LongLds {
-    uint64_t rec[kLW];      // DP: records
-    double wt[kLW][4];      // DP: weights; path: emissions B, M, E, S
-    double best[kLW + 64];  // DP: best values of the window, then 64 carried from the window after it
-    uint8_t b[kLW];         // DP: piece lengths; path: lengths, then back-pointers / labels
+constexpr uint32_t kZhLongGrid = 64;  // k_zh_long waves (persistent over the long-block list)
+constexpr uint32_t kTailRunes = 64;   // k_long_tail: runes per lane
+
+// double from lane j of a uniform-in-register value (readlane: no memory access)
+__device__ __forceinline__ double rl64(double v, uint32_t j) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, j), hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), j);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// DP classes of a rune's record (staged with it): the chain branches on them.
+enum : uint32_t {
+    kDpWalk = 0,  // record overflowed: walk the trie here (rare)
+    kDpOne = 1,   // the single edge L = 1: best = w + best(i+1)
+    kDpTwo = 2,   // edges L = 1 and L2 (meta bits 4..7)
+    kDpFold = 3,  // anything else: the general fold
 };
 
 template <bool HMM>
@@ -1801,19 +1817,13 @@ __global__ __launch_bounds__(64) void k_zh_long(const uint8_t* __restrict__ text
                                                 const uint64_t* __restrict__ erec, uint8_t* __restrict__ gbl,
                                                 double* __restrict__ gbest, const uint2* __restrict__ longblk,
                                                 uint32_t* __restrict__ counters, uint32_t* __restrict__ sbits,
-                                                uint32_t* __restrict__ ebits, double* __restrict__ ring_g) {
-    __shared__ LongLds L;
+                                                uint32_t* __restrict__ ebits, uint32_t* __restrict__ lpath,
+                                                uint32_t* __restrict__ lflag) {
+    __shared__ double s_best[256];  // best(i) at i & 255 (edges are at most 255 runes)
     __shared__ double s_ring[kZhRing * 64];
-    // LDS pointers typed as such: the lambdas below would otherwise see generic
-    // pointers and the compiler would emit flat loads
-    typedef uint8_t __attribute__((address_space(3))) LU8;
-    typedef double __attribute__((address_space(3))) LF64;
-    LU8* const Lb = (LU8*)L.b;
-    LF64* const Lbest = (LF64*)L.best;
     const uint32_t lane = threadIdx.x;
     const uint32_t nlong = counters[CNT_NLONG];
     Emitter em(sbits, ebits);
-    em.off = lane != 0u;  // every lane runs the chains; lane 0 writes the tokens
     for (uint32_t bi = blockIdx.x; bi < nlong; bi += gridDim.x) {
         const uint2 bb = longblk[bi];
         const uint32_t bs = bb.x, be = bb.y;
@@ -1824,8 +1834,9 @@ __global__ __launch_bounds__(64) void k_zh_long(const uint8_t* __restrict__ text
                      (x.z & (x.z << 1) & (x.z << 2) & (x.z << 3)) | (x.w & (x.w << 1) & (x.w << 2) & (x.w << 3))) &
                     0x80808080u;
         }
-        if (__any(any4)) {  // the general one-lane path (k_zh's)
+        if (__any(any4)) {  // the general one-lane path (k_zh's); k_long_tail skips the block
             if (lane == 0) {
+                lflag[bi] = 0u;
                 const GlbZv gv{text, gbl};
                 zh_dp(gv, im, erec, gbest, s_ring + lane, OneSrc{bs, be});
                 if (!zh_fwd<HMM>(gv, im, bs, be, em, nullptr)) atomicOr(counters + CNT_ERR, 1u);
@@ -1837,216 +1848,274 @@ __global__ __launch_bounds__(64) void k_zh_long(const uint8_t* __restrict__ text
             continue;
         }
         const uint32_t n = (be - bs) / 3u, s0 = bs / 3u;  // rune i: bytes bs + 3i, slot s0 + i
-        // ---- DP (calcDagProba + maxIndexProba, tokenizer.go:502-578), backwards by window ----
-        bool bad = false;
-        for (uint32_t hi = n; hi > 0u;) {
-            const uint32_t lo = hi > kLW ? hi - kLW : 0u, m = hi - lo;
-            for (uint32_t k = lane; k < m; k += 64u) L.rec[k] = erec[s0 + lo + k];
-            __syncthreads();
-            for (uint32_t k = lane; k < m; k += 64u) rec_weights(im, L.rec[k], L.wt[k]);
-            __syncthreads();
-            auto best_at = [&](uint32_t j) -> double {  // best(j), j > i (j < n)
-                if (j - lo < m + 64u) return Lbest[j - lo];
-                return *reinterpret_cast<const volatile double*>(gbest + s0 + j);
-            };
-            // The window's best values sit at best[k], the carried ones right after them at
-            // best[m ..], so best(i + L) is best[k + L] for any L <= 64 (one LDS read, no
-            // branch); best(i + 1), the value the chain just made, stays in a register.
-            {
-                double cv = 0.0;
-                if (lane < 64u && hi + lane < n) cv = L.best[kLW + lane];
-                __syncthreads();
-                if (lane < 64u) L.best[m + lane] = cv;
-                __syncthreads();
-            }
-            double b1 = (hi < n) ? L.best[m] : 0.0;
-            for (uint32_t i = hi; i-- > lo;) {
-                const uint32_t k = i - lo, c = n - i;
-                const uint64_t rc = L.rec[k];
-                uint32_t mm = (uint32_t)rc & 0xFFu;
-                DpFold f;
-                if (mm) {
-#pragma unroll
-                    for (int e = 0; e < 4; e++) {
-                        if (mm == 0u) break;
-                        const uint32_t Ln = (uint32_t)__builtin_ctz(mm) + 1u;
-                        mm &= mm - 1u;
-                        const double bl = L.best[k + Ln];
-                        const double nb = (Ln == c) ? 0.0 : (Ln == 1u ? b1 : bl);
-                        const double pp = L.wt[k][e] + nb;
-                        if (pp >= f.prevP) {
-                            f.bestL = Ln;
-                            f.bestP = pp;
-                        }
-                        f.prevP = pp;
-                        f.lastL = Ln;
-                    }
-                } else {  // overflowed record (rare): walk the rune here, every item folded
-                    auto item = [&](uint32_t Ln, double wt) {
-                        const double pp = wt + ((Ln == c) ? 0.0 : best_at(i + Ln));
-                        if (pp >= f.prevP) {
-                            f.bestL = Ln;
-                            f.bestP = pp;
-                        }
-                        f.prevP = pp;
-                        f.lastL = Ln;
-                    };
-                    auto dec3 = [&](uint32_t q) {
-                        const uint32_t x = ld4(text, q);
-                        return ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
-                    };
-                    const uint32_t q = bs + 3u * i;
-                    uint32_t id = rune_code(im, dec3(q));
-                    uint64_t cc = im.cells[id];
-                    if (jb_cell_check(cc) != JB_CHECK_ROOT) {
-                        item(1u, im.wtab[JB_WIDX_ABSENT]);
-                    } else if (jb_cell_fc(cc) == JB_FC_ZERO) {
-                        item(1u, im.wtab[jb_cell_widx(cc)]);
-                    } else {
-                        if (jb_cell_fc(cc) == JB_FC_POS) item(1u, im.wtab[jb_cell_widx(cc)]);
-                        uint32_t qq = q + 3u, len = 1;
-                        bool go = jb_cell_hc(cc) != 0u;
-                        while (go && qq < be) {
-                            const uint32_t tt = dat_slot(im, cc, dec3(qq));
-                            const uint64_t ch = im.cells[tt];
-                            if (!dat_hit(ch, id)) break;  // (:475-478)
-                            ++len;
-                            qq += 3u;
-                            if (jb_cell_fc(ch) == JB_FC_POS) item(len, im.wtab[jb_cell_widx(ch)]);
-                            go = jb_cell_hc(ch) != 0u;
-                            id = tt;
-                            cc = ch;
-                        }
-                    }
-                }
-                f.finish();
-                L.best[k] = f.bestP;
-                L.b[k] = (uint8_t)f.bestL;
-                b1 = f.bestP;
-            }
-            __syncthreads();
-            for (uint32_t k = lane; k < m; k += 64u) {
-                gbl[s0 + lo + k] = L.b[k];
-                gbest[s0 + lo + k] = L.best[k];
-            }
-            const double carry = lane < m ? L.best[lane] : 0.0;
-            __syncthreads();
-            if (lane < m) L.best[kLW + lane] = carry;
-            __syncthreads();
-            hi = lo;
+        // clear the block's bits of the path bitmap (its end words may be shared with a neighbour)
+        for (uint32_t w = (s0 >> 5) + lane; w <= (s0 + n - 1u) >> 5; w += 64u) {
+            const uint32_t lo = max(s0, w << 5), hi = min(s0 + n, (w << 5) + 32u);  // slots [lo, hi) of word w
+            const uint32_t m = (hi - lo == 32u ? ~0u : ((1u << (hi - lo)) - 1u)) << (lo & 31u);
+            atomicAnd(lpath + w, ~m);
         }
-        // ---- path (findDagPath, :552-562) + HMM runs (viterbi + cutHMM, :668-756, 273-285) ----
-        // Window [flo, flo + fm) holds piece lengths (then back-pointers) and emissions.
-        uint32_t flo = 0, fm = 0;
-        auto stage = [&](uint32_t from) {  // (uniform)
-            __syncthreads();
-            flo = from;
-            fm = min(kLW, n - from);
-            for (uint32_t k = lane; k < fm; k += 64u) {
-                Lb[k] = gbl[s0 + flo + k];
-                if (HMM) {
-                    const uint32_t x = ld4(text, bs + 3u * (flo + k));
-                    const uint32_t r = ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
-                    load_emit(im, r, L.wt[k]);
-                }
-            }
-            __syncthreads();
+        // ---- DP (calcDagProba + maxIndexProba, tokenizer.go:502-578), backwards ----
+        // Blocks of 64 runes, lane j holding rune 64B + j's record and the weights of
+        // its edges in registers (loaded two blocks ahead: records, then weights); the
+        // chain reads them with readlane, so nothing but the 256-entry best ring in
+        // LDS (best(i+L) for L >= 3, written by one lane) is a memory access on it.
+        s_best[n & 255u] = 0.0;  // best(n): the {n, 0.0} sentinel (:522-525)
+        double b1 = 0.0, b2 = 0.0;  // best(i+1), best(i+2) of the rune i up next
+        const int32_t Btop = (int32_t)((n - 1u) >> 6);
+        auto load_rec = [&](int32_t B) -> uint64_t {
+            const uint32_t i = 64u * (uint32_t)B + lane;
+            return (B >= 0 && i < n) ? erec[s0 + i] : 0ull;
         };
-        // slot bytes (piece length / back-pointer / label): LDS inside the window, else HBM
-        auto getb = [&](uint32_t j) -> uint32_t {  // (volatile: two loads, not one flat load of either)
-            if (j - flo < fm) return Lb[j - flo];
-            return *reinterpret_cast<const volatile uint8_t*>(gbl + s0 + j);
+        auto meta_of = [](uint64_t rc) -> uint32_t {
+            const uint32_t mk = (uint32_t)rc & 0xFFu;
+            if (mk == 0u) return kDpWalk;
+            if (mk == 1u) return kDpOne;
+            if ((mk & 1u) && __popc(mk) == 2) return kDpTwo | (((uint32_t)__builtin_ctz(mk & ~1u) + 1u) << 4);
+            return kDpFold;
         };
-        auto setb = [&](uint32_t j, uint32_t v) {
-            if (j - flo < fm) Lb[j - flo] = (uint8_t)v;
-            gbl[s0 + j] = (uint8_t)v;  // (every lane: its own later reads see its own store)
-        };
-        auto token = [&](uint32_t a, uint32_t e) { em.token(bs + 3u * a, bs + 3u * e); };  // runes [a, e)
-        uint32_t p = 0, run_s = 0, run_n = 0;
-        double vB = 0, vM = 0, vE = 0, vS = 0;
-        auto run_end = [&](uint32_t re) {  // the run of single-rune pieces [run_s, re)
-            const uint32_t m = re - run_s;
-            if (m == 1u) {  // always "S" (:672-674)
-                token(run_s, re);
-                return;
-            }
-            uint32_t st = vE > vS ? (uint32_t)JB_E : (uint32_t)JB_S;  // (:723-729)
-            uint32_t t = m - 1u, reset = 0, jt = re - 1u;
-            for (;;) {
-                if (t == 0u) {
-                    setb(jt, st);
-                    break;
+        uint64_t rc = load_rec(Btop);
+        double w[4];
+        rec_weights(im, rc, w);
+        uint64_t rc1 = load_rec(Btop - 1);  // the next block's records
+        for (int32_t B = Btop; B >= 0; B--) {
+            double w1n[4];  // the next block's weights, in flight during this block
+            rec_weights(im, rc1, w1n);
+            const uint64_t rc2 = load_rec(B - 2);
+            const uint32_t meta_v = meta_of(rc);
+            const uint32_t rlo = (uint32_t)rc, rhi = (uint32_t)(rc >> 32);
+            uint32_t blv = 0;  // chosen lengths, lane j = rune 64B + j
+            const uint32_t base = 64u * (uint32_t)B;
+            for (uint32_t j = min(63u, n - 1u - base) + 1u; j-- > 0u;) {
+                const uint32_t i = base + j;
+                const uint32_t meta = __builtin_amdgcn_readlane(meta_v, j);
+                const uint32_t cls = meta & 15u;
+                const double w0 = rl64(w[0], j);
+                double P;
+                uint32_t BL;
+                if (cls == kDpOne) {  // one item: it is the answer whether or not it qualifies (:573-576)
+                    P = w0 + b1;
+                    BL = 1u;
+                } else if (cls == kDpTwo) {  // items L = 1 then L2: the second wins unless it is smaller
+                    const uint32_t L2 = meta >> 4;  // and the first qualifies (>= minFloat)
+                    const double v2 = L2 == 2u ? b2 : s_best[(i + L2) & 255u];
+                    const double pp2 = rl64(w[1], j) + v2;
+                    const double pp1 = w0 + b1;
+                    const bool second = (pp2 >= pp1) | !(pp1 >= JB_MIN_FLOAT);
+                    P = second ? pp2 : pp1;
+                    BL = second ? L2 : 1u;
+                } else {
+                    DpFold f;
+                    if (cls == kDpFold) {
+                        const uint64_t r = ((uint64_t)__builtin_amdgcn_readlane(rhi, j) << 32) |
+                                           __builtin_amdgcn_readlane(rlo, j);
+                        uint32_t mm = (uint32_t)r & 0xFFu;
+#pragma unroll
+                        for (int e = 0; e < 4; e++) {
+                            if (mm == 0u) break;
+                            const uint32_t Ln = (uint32_t)__builtin_ctz(mm) + 1u;
+                            mm &= mm - 1u;
+                            const double nb = Ln == 1u ? b1 : (Ln == 2u ? b2 : s_best[(i + Ln) & 255u]);
+                            const double pp = rl64(w[e], j) + nb;
+                            if (pp >= f.prevP) {
+                                f.bestL = Ln;
+                                f.bestP = pp;
+                            }
+                            f.prevP = pp;
+                            f.lastL = Ln;
+                        }
+                    } else {  // overflowed record: walk the rune here, every item folded
+                        auto item = [&](uint32_t Ln, double wt) {  // (Ln <= 255: best(i+Ln) is in the ring)
+                            const double pp = wt + (Ln == 1u ? b1 : s_best[(i + Ln) & 255u]);
+                            if (pp >= f.prevP) {
+                                f.bestL = Ln;
+                                f.bestP = pp;
+                            }
+                            f.prevP = pp;
+                            f.lastL = Ln;
+                        };
+                        auto dec3 = [&](uint32_t q) {
+                            const uint32_t x = ld4(text, q);
+                            return ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
+                        };
+                        const uint32_t q = bs + 3u * i;
+                        uint32_t id = rune_code(im, dec3(q));
+                        uint64_t cc = im.cells[id];
+                        if (jb_cell_check(cc) != JB_CHECK_ROOT) {
+                            item(1u, im.wtab[JB_WIDX_ABSENT]);
+                        } else if (jb_cell_fc(cc) == JB_FC_ZERO) {
+                            item(1u, im.wtab[jb_cell_widx(cc)]);
+                        } else {
+                            if (jb_cell_fc(cc) == JB_FC_POS) item(1u, im.wtab[jb_cell_widx(cc)]);
+                            uint32_t qq = q + 3u, len = 1;
+                            bool go = jb_cell_hc(cc) != 0u;
+                            while (go && qq < be) {
+                                const uint32_t tt = dat_slot(im, cc, dec3(qq));
+                                const uint64_t ch = im.cells[tt];
+                                if (!dat_hit(ch, id)) break;  // (:475-478)
+                                ++len;
+                                qq += 3u;
+                                if (jb_cell_fc(ch) == JB_FC_POS) item(len, im.wtab[jb_cell_widx(ch)]);
+                                go = jb_cell_hc(ch) != 0u;
+                                id = tt;
+                                cc = ch;
+                            }
+                        }
+                    }
+                    f.finish();
+                    P = f.bestP;
+                    BL = f.bestL;
                 }
-                const uint32_t code = (getb(jt) >> (2u * st)) & 3u;
-                setb(jt, st);
-                if (code == 2u) {
-                    reset = t;
-                    break;
-                }
-                st = (st == JB_B || st == JB_S) ? 2u + code : code;
-                --t;
-                --jt;
+                if (lane == 0u) s_best[i & 255u] = P;
+                blv = lane == j ? BL : blv;
+                b2 = b1;
+                b1 = P;
             }
-            uint32_t ja = run_s, jb = jt, ts = run_s;
-            for (uint32_t k = 0; k < m - reset; k++) {
-                const uint32_t lab = getb(jb);
-                ++ja;
-                ++jb;
-                if (lab >= (uint32_t)JB_E) {
-                    token(ts, ja);
-                    ts = ja;
-                }
-            }
-        };
-        stage(0u);
+            if (base + lane < n) gbl[s0 + base + lane] = (uint8_t)blv;
+            rc = rc1;
+            rc1 = rc2;
+#pragma unroll
+            for (int e = 0; e < 4; e++) w[e] = w1n[e];
+        }
+        // ---- path (findDagPath, :552-562): p += L(p) from rune 0, marking piece starts ----
+        __threadfence();  // gbl and the cleared bitmap words, before the reads below
+        uint32_t p = 0, wslot = s0 - 1024u, dw = 0, bword = 0xFFFFFFFFu, bits = 0;  // (first trip loads)
+        bool bad = false;
+        const uint32_t* gbl32 = reinterpret_cast<const uint32_t*>(gbl);
         while (p < n) {
-            if (p - flo >= fm) stage(p);
-            const uint32_t Ln = L.b[p - flo];
+            const uint32_t sl = s0 + p;
+            if (sl - wslot >= 256u) {  // lane j holds the lengths of slots wslot + 4j .. + 3
+                wslot = sl & ~3u;
+                dw = __hip_atomic_load(gbl32 + (wslot >> 2) + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            const uint32_t d = __builtin_amdgcn_readlane(dw, (sl - wslot) >> 2);
+            const uint32_t Ln = (d >> (8u * (sl & 3u))) & 0xFFu;
             if (Ln == 0u) {  // tail index -1: cutDAG's slice panics in the reference
                 bad = true;
                 break;
             }
-            if (!HMM) {
-                token(p, p + Ln);
-            } else if (Ln == 1u) {
-                const double* e = L.wt[p - flo];
-                if (run_n == 0u) {
-                    run_s = p;
-                    vB = START_B + e[0];
-                    vM = JB_MIN_FLOAT + e[1];
-                    vE = JB_MIN_FLOAT + e[2];
-                    vS = START_S + e[3];
-                } else {
-                    uint32_t cB, cM, cE, cS;
-                    double pB, pM, pE, pS;
-                    route2(vE + T_EB, vS + T_SB, &cB, &pB, em.ties);  // B <- E, S
-                    route2(vB + T_BM, vM + T_MM, &cM, &pM, em.ties);  // M <- B, M
-                    route2(vB + T_BE, vM + T_ME, &cE, &pE, em.ties);  // E <- B, M
-                    route2(vE + T_ES, vS + T_SS, &cS, &pS, em.ties);  // S <- E, S
-                    vB = pB + e[0];
-                    vM = pM + e[1];
-                    vE = pE + e[2];
-                    vS = pS + e[3];
-                    setb(p, cB | (cM << 2) | (cE << 4) | (cS << 6));
-                }
-                run_n++;
-            } else {
-                if (run_n) {
-                    run_end(p);
-                    run_n = 0;
-                }
-                token(p, p + Ln);
+            if ((sl >> 5) != bword) {
+                if (bits && lane == 0u) atomicOr(lpath + bword, bits);
+                bword = sl >> 5;
+                bits = 0;
             }
+            bits |= 1u << (sl & 31u);
             p += Ln;
         }
-        if (HMM && run_n && !bad) run_end(n);
-        em.flush();
-        if (lane == 0u && em.ties) atomicAdd(counters + CNT_TIES, em.ties);  // (every lane ran the same chain)
-        em.ties = 0;
+        if (bits && lane == 0u) atomicOr(lpath + bword, bits);
+        if (lane == 0u) lflag[bi] = bad ? 0u : 1u;
         if (bad && lane == 0u) atomicOr(counters + CNT_ERR, 1u);
         __syncthreads();
     }
-    (void)ring_g;
+}
+
+// Viterbi (tokenizer.go:668-730) + cutHMM (:273-285) of the run of single-rune
+// pieces [q, r) (rune indices of a long block, all 3-byte): back-pointers in
+// bp (slot bytes), the final state from v[E] > v[S] (:723-729).
+template <class E>
+__device__ void long_viterbi(const uint8_t* __restrict__ text, const DevImage& im, uint32_t bs, uint32_t s0,
+                             uint32_t q, uint32_t r, uint8_t* __restrict__ bp, E& em) {
+    auto rune_at = [&](uint32_t j) {
+        const uint32_t x = ld4(text, bs + 3u * j);
+        return ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
+    };
+    double e[4], en[4];
+    load_emit(im, rune_at(q), e);
+    double vB = START_B + e[0], vM = JB_MIN_FLOAT + e[1], vE = JB_MIN_FLOAT + e[2], vS = START_S + e[3];
+    if (q + 1u < r) load_emit(im, rune_at(q + 1u), e);
+    for (uint32_t j = q + 1u; j < r; j++) {
+        if (j + 1u < r) load_emit(im, rune_at(j + 1u), en);  // next rune's emissions, in flight
+        uint32_t cB, cM, cE, cS;
+        double pB, pM, pE, pS;
+        route2(vE + T_EB, vS + T_SB, &cB, &pB, em.ties);  // B <- E, S
+        route2(vB + T_BM, vM + T_MM, &cM, &pM, em.ties);  // M <- B, M
+        route2(vB + T_BE, vM + T_ME, &cE, &pE, em.ties);  // E <- B, M
+        route2(vE + T_ES, vS + T_SS, &cS, &pS, em.ties);  // S <- E, S
+        vB = pB + e[0];
+        vM = pM + e[1];
+        vE = pE + e[2];
+        vS = pS + e[3];
+        bp[s0 + j] = (uint8_t)(cB | (cM << 2) | (cE << 4) | (cS << 6));
+        e[0] = en[0]; e[1] = en[1]; e[2] = en[2]; e[3] = en[3];
+    }
+    // traceback from the final state; a "" route restarts the path there (:715),
+    // and cutHMM labels runes from the run start (:273-285)
+    const uint32_t m = r - q;
+    uint32_t st = vE > vS ? (uint32_t)JB_E : (uint32_t)JB_S;
+    uint32_t t = m - 1u, reset = 0, jt = r - 1u;
+    for (;;) {
+        if (t == 0u) {
+            bp[s0 + jt] = (uint8_t)st;
+            break;
+        }
+        const uint32_t code = (bp[s0 + jt] >> (2u * st)) & 3u;
+        bp[s0 + jt] = (uint8_t)st;
+        if (code == 2u) {
+            reset = t;
+            break;
+        }
+        st = (st == JB_B || st == JB_S) ? 2u + code : code;  // B,S <- {E,S}; M,E <- {B,M}
+        --t;
+        --jt;
+    }
+    uint32_t ja = q, jb = jt, ts = q;
+    for (uint32_t k = 0; k < m - reset; k++) {
+        const uint32_t lab = bp[s0 + jb];
+        ++ja;
+        ++jb;
+        if (lab >= (uint32_t)JB_E) {
+            em.token(bs + 3u * ts, bs + 3u * ja);
+            ts = ja;
+        }
+    }
+}
+
+// k_long_tail: the pieces k_zh_long marked in `lpath`, one lane per kTailRunes
+// runes of a long block (the lane owns the pieces and runs that START there).
+template <bool HMM>
+__global__ __launch_bounds__(256) void k_long_tail(const uint8_t* __restrict__ text, DevImage im,
+                                                   const uint8_t* __restrict__ gbl, const uint2* __restrict__ longblk,
+                                                   const uint32_t* __restrict__ lflag, uint32_t* __restrict__ counters,
+                                                   const uint32_t* __restrict__ lpath, uint8_t* __restrict__ bp,
+                                                   uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits) {
+    const uint32_t nlong = counters[CNT_NLONG];
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+    Emitter em(sbits, ebits);
+    for (uint32_t bi = 0; bi < nlong; bi++) {
+        if (!lflag[bi]) continue;  // cut by the one-lane path, or the reference panics
+        const uint2 bb = longblk[bi];
+        const uint32_t bs = bb.x, n = (bb.y - bb.x) / 3u, s0 = bs / 3u;
+        auto start = [&](uint32_t j) { return ((lpath[(s0 + j) >> 5] >> ((s0 + j) & 31u)) & 1u) != 0u; };
+        auto len = [&](uint32_t j) { return (uint32_t)gbl[s0 + j]; };
+        for (uint32_t c = gid; c * kTailRunes < n; c += nth) {
+            const uint32_t c0 = c * kTailRunes, c1 = min(n, c0 + kTailRunes);
+            uint32_t q = c0;
+            // a run that began before c0 belongs to the lane that owns its start
+            if (HMM && q > 0u && start(q - 1u) && len(q - 1u) == 1u)
+                while (q < n && start(q) && len(q) == 1u) q++;
+            while (q < c1) {
+                if (!start(q)) {
+                    q++;
+                    continue;
+                }
+                const uint32_t Ln = len(q);
+                if (!HMM || Ln > 1u) {
+                    em.token(bs + 3u * q, bs + 3u * (q + Ln));
+                    q += Ln;
+                    continue;
+                }
+                uint32_t r = q + 1u;
+                while (r < n && start(r) && len(r) == 1u) r++;
+                if (r - q == 1u) em.token(bs + 3u * q, bs + 3u * r);  // a single rune is always "S" (:672-674)
+                else long_viterbi(text, im, bs, s0, q, r, bp, em);
+                q = r;
+            }
+        }
+    }
+    em.flush();
+    uint32_t t = em.ties;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) t += (uint32_t)__shfl_xor((int)t, d, 64);
+    if ((threadIdx.x & 63u) == 0u && t) atomicAdd(counters + CNT_TIES, t);
 }
 
 // ---------------------------------------------------------------------------
@@ -2311,14 +2380,26 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
                                           w.gstart, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
                                           w.longblk, grp, diag, w.dbg));
-    if (hmm)
-        JB_TIMED(K_ZH_LONG, hipLaunchKernelGGL((k_zh_long<true>), dim3(kZhLongGrid), dim3(64), 0, stream, d_text, im,
-                                               w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters, w.sbits,
-                                               w.ebits, nullptr));
-    else
-        JB_TIMED(K_ZH_LONG, hipLaunchKernelGGL((k_zh_long<false>), dim3(kZhLongGrid), dim3(64), 0, stream, d_text, im,
-                                               w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters, w.sbits,
-                                               w.ebits, nullptr));
+    {
+        // k_long_tail: one lane per kTailRunes runes of the long blocks (at most nbytes / 3 runes)
+        const uint64_t lanes = nbytes / 3u / kTailRunes + 1u;
+        const uint32_t gtail = (uint32_t)std::min<uint64_t>(1024u, (lanes + 255u) / 256u);
+        if (hmm) {
+            JB_TIMED(K_ZH_LONG, hipLaunchKernelGGL((k_zh_long<true>), dim3(kZhLongGrid), dim3(64), 0, stream, d_text, im,
+                                                   w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters, w.sbits,
+                                                   w.ebits, w.lpath, w.lflag));
+            JB_TIMED(K_LONG_TAIL, hipLaunchKernelGGL((k_long_tail<true>), dim3(gtail), dim3(256), 0, stream, d_text, im,
+                                                     w.gbl, w.longblk, w.lflag, w.counters, w.lpath, w.lbp, w.sbits,
+                                                     w.ebits));
+        } else {
+            JB_TIMED(K_ZH_LONG, hipLaunchKernelGGL((k_zh_long<false>), dim3(kZhLongGrid), dim3(64), 0, stream, d_text,
+                                                   im, w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters,
+                                                   w.sbits, w.ebits, w.lpath, w.lflag));
+            JB_TIMED(K_LONG_TAIL, hipLaunchKernelGGL((k_long_tail<false>), dim3(gtail), dim3(256), 0, stream, d_text,
+                                                     im, w.gbl, w.longblk, w.lflag, w.counters, w.lpath, w.lbp, w.sbits,
+                                                     w.ebits));
+        }
+    }
     JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3(grid_nz), dim3(256), 0, stream, d_text, w.blk, w.alnum16,
                                          w.counters, w.sbits, w.ebits));
     JB_TIMED(K_TOK_COUNT, hipLaunchKernelGGL((k_tok<false>), dim3(nttiles), dim3(256), 0, stream, w.sbits, w.ebits,

@@ -180,7 +180,10 @@ def test_graph_replay_after_add_word(syn_small):
         _cmp_batch(tk, o, buf, off, True, "before AddWord")
     text = bytes(np.asarray(buf)[: int(off[1])]).decode("utf-8")
     import re
-    word = re.search("[\u4e00-\u9fa5]{4}", text).group(0)  # 4 adjacent Han runes of the first document
+    # two adjacent Han runes whose first is a word (AddWord adds no prefixes, so the
+    # walk reaches the new word only through a key, tokenizer.go:475-478,580-585)
+    word = next(m.group(0) for m in re.finditer("(?=([\u4e00-\u9fa5]{2}))", text)
+                for m in [re.match(".*", m.group(1))] if (o.get(m.group(0)[0]) or 0) > 0 and o.get(m.group(0)) is None)
     tk.AddWord(word, 10_000_000)
     o.add_term(word, 10_000_000)
     for _ in range(3):
@@ -355,7 +358,8 @@ def test_record_overflow_paths(tmp_path, syn_small, kind):
                 else:
                     parts.append(rng.choice(["，", "。", " ab12 ", "\n"]))
             texts.append("".join(parts))
-        texts.append("".join(seqs))  # one long block through every chain
+        texts.append("".join(seqs))  # one block through every chain
+        texts.append("".join(seqs) * 6)  # the same as a long block (k_zh_long's overflow walks)
         buf, off = _batch_of(texts)
         for hmm in (False, True):
             _cmp_batch(tk, o, buf, off, hmm, f"overflow kind={kind} hmm={hmm}")
