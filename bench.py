@@ -241,7 +241,7 @@ def roofline_of(kernels, units, traffic_of):
     """Algorithmic bytes: 1 B read per byte of a kernel's units +
     2 output bits per byte = 1.25 B per unit byte.  Units: every input byte for
     k_mark_walk (it classifies and walks the whole batch), the Han bytes for
-    k_zh / k_zh_long (DP + Viterbi over zh blocks)."""
+    k_zh / k_long_dp (DP + Viterbi over zh blocks)."""
     out = {}
     for kname, u in units.items():
         kk = kernels.get(kname)
@@ -335,8 +335,8 @@ def run(args, world, rank, dist, agg_dev, make_cutter, open_oracle, log=print):
     if rank != 0:
         return None
     units = {"k_mark_walk": float(nbytes), "k_zh": float(hbytes)}
-    if args.workload == "long-oov":  # one unpunctuated block: its Han bytes all go through k_zh_long
-        units["k_zh_long"] = float(hbytes)
+    if args.workload == "long-oov":  # one unpunctuated block: its Han bytes all go through the k_long_* chain
+        units["k_long_dp"] = float(hbytes)
     wkey = f"{args.workload}:{nbytes}:{'hmm' if args.hmm else 'nohmm'}:{args.dict_kind}"
     rooflines = roofline_of(kernels, units, lambda k: load_pmc_traffic(k, wkey))
     roof = None

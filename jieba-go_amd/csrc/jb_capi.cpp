@@ -427,7 +427,7 @@ static int upload_image(Device* d, const Image& img) {
 static void free_work(Work* w) {
     dfree(w->docbits); dfree(w->tile_cnt); dfree(w->tile_off);
     dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->supb); dfree(w->supt); dfree(w->blk); dfree(w->alnum16); dfree(w->erec); dfree(w->lanemask);
-    dfree(w->gbl); dfree(w->lpath); dfree(w->lflag); dfree(w->lbp); dfree(w->gbest); dfree(w->gstart); dfree(w->tile4); dfree(w->longblk);
+    dfree(w->gbl); dfree(w->lsegb); dfree(w->lseg); dfree(w->lpath); dfree(w->lflag); dfree(w->lbp); dfree(w->gbest); dfree(w->gstart); dfree(w->tile4); dfree(w->longblk);
     dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters); dfree(w->dbg); dfree(w->dbg_walk);
     *w = Work{};
 }
@@ -461,6 +461,8 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.gbl, nb / 3 + 8 + 512));
     HIPCHK(hipMalloc(&w.lpath, (nb / 3 / 32 + 4) * 4));
     HIPCHK(hipMalloc(&w.lflag, (nb / kZhLongMin + 2) * 4));
+    HIPCHK(hipMalloc(&w.lsegb, (nb / kZhLongMin + 2) * 4));
+    HIPCHK(hipMalloc(&w.lseg, (nb / (3 * kSeg) + nb / kZhLongMin + 4) * sizeof(uint4)));
     HIPCHK(hipMalloc(&w.lbp, nb / 3 + 64));
     HIPCHK(hipMalloc(&w.gstart, (nb / kZhGroupSmall + 4) * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.tile4, ntiles * 4));
@@ -1099,7 +1101,7 @@ extern "C" int jb_last_stats(jb_ctx* ctx, jb_stats* out) {
         if (!d->w.counters) continue;
         HIPCHK(hipSetDevice(d->ordinal));
         HIPCHK(hipDeviceSynchronize());  // (jb_cut_device may have queued on a caller's stream)
-        uint32_t c[CNT_NWORDS + 2];
+        uint32_t c[CNT_CLEAR];
         HIPCHK(hipMemcpy(c, d->w.counters, sizeof c, hipMemcpyDeviceToHost));
         uint64_t ntok;
         memcpy(&ntok, c + CNT_NWORDS, 8);

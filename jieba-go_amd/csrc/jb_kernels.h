@@ -29,9 +29,11 @@ enum {
     CNT_NTOKE = 3,  // token ends (== CNT_NTOK when consistent)
     CNT_ERR = 4,    // bit 0: a zh block reached a tail index -1 (the reference panics)
     CNT_WORK = 5,   // k_zh work counter: next group (kZhGroupBytes of text)
-    CNT_NLONG = 6,  // long zh blocks k_zh left to k_zh_long
     CNT_TIES = 7,   // exact Viterbi route ties (Q12)
-    CNT_NWORDS = 8  // u32 slots reserved; u64 token count lives at byte offset 32
+    CNT_NWORDS = 8, // u64 token count lives at u32 slots 8-9 (byte offset 32)
+    CNT_NLONG = 10, // long zh blocks k_zh left to k_long_* (u64 with CNT_NLSEG: one atomic)
+    CNT_NLSEG = 11, // their 64-rune segments
+    CNT_CLEAR = 12  // u32 slots cleared per batch
 };
 
 constexpr int kTileBytes = 4096;       // k_blocks: 256 threads x 16 bytes
@@ -46,7 +48,8 @@ constexpr uint32_t kErecPad = 8;  // erec slots before slot 0 (k_zh reads a few 
 constexpr uint32_t kZhGroupBytes = JB_ZH_GROUP;
 constexpr uint32_t kZhGroupSmall = 1024;
 constexpr uint64_t kZhSmallBatch = 16ull << 20;
-constexpr uint32_t kZhLongMin = 8192;  // zh blocks of at least this many bytes go to k_zh_long
+constexpr uint32_t kZhLongMin = 8192;  // zh blocks of at least this many bytes go to k_long_*
+constexpr uint32_t kSeg = 64;          // runes per segment of a long block (k_long_seg/path/tail)
 inline uint32_t zh_group_for(uint64_t nbytes) { return nbytes < kZhSmallBatch ? kZhGroupSmall : kZhGroupBytes; }
 
 // Per-call device workspace, sized for `nbytes` of text.
@@ -66,12 +69,14 @@ struct Work {
     uint64_t* erec;        // per Han rune (slot = byte / 3): packed DAG edges (k_mark_walk -> k_zh)
     uint32_t* lanemask;    // per 16 bytes: block starts | Han block starts << 16
     uint2* gstart;         // per k_zh group g: (blocks, zh blocks) that start before g * group bytes
-    uint2* longblk;        // (start, end) of each long zh block (k_zh -> k_zh_long)
+    uint2* longblk;        // (start, end) of each long zh block (k_zh -> k_long_*)
+    uint32_t* lsegb;       // per long block: its first segment (ascending with the block index)
+    uint4* lseg;           // per segment: speculative path exit, -, path bits lo, hi (k_long_seg -> k_long_path)
     uint32_t* tile4;       // per tile: a 4-byte Han rune starts in it
     uint8_t* gbl;          // per Han rune: chosen piece length, then Viterbi back-pointers / labels
                            // (+512 bytes: k_zh_long reads 256-slot windows)
     uint32_t* lpath;       // long blocks: 1 bit per Han rune slot, a piece of the chosen path starts here
-    uint32_t* lflag;       // per long block: 1 when k_long_tail cuts it (all-3-byte, path complete)
+    uint32_t* lflag;       // per long block: 0 cut by k_long_dp's one-lane path (or no path), 2 DP done, 1 path done
     uint8_t* lbp;          // long blocks: Viterbi back-pointers / labels per slot (k_long_tail)
     double* gbest;         // per Han rune: best proba, kept only for blocks with an edge > 8 runes
     uint32_t* tok_start;
@@ -87,7 +92,7 @@ struct Work {
 // Kernel ids for per-launch timing.
 enum KernelId {
     K_DOCBITS = 0, K_MARK_WALK, K_SCAN_BLOCKS, K_BLOCKS_WRITE, K_ZH, K_NONZH,
-    K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_ZH_LONG, K_LONG_TAIL, K_NUM
+    K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_LONG_DP, K_LONG_SEG, K_LONG_PATH, K_LONG_TAIL, K_NUM
 };
 extern const char* const kKernelNames[K_NUM];
 

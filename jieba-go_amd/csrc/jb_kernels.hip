@@ -25,6 +25,8 @@
 // built with -ffp-contract=off and without fast-math (±Inf must propagate).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "jb_kernels.h"
 
 #ifndef JB_STAMPS
@@ -35,7 +37,8 @@ namespace jb {
 
 const char* const kKernelNames[K_NUM] = {"k_docbits", "k_mark_walk", "k_scan_blocks", "k_blocks_write",
                                          "k_zh", "k_nonzh", "k_tok_count", "k_scan_tok",
-                                         "k_tok_write", "k_doc_tok", "k_zh_long", "k_long_tail"};
+                                         "k_tok_write", "k_doc_tok", "k_long_dp", "k_long_seg", "k_long_path",
+                                         "k_long_tail"};
 
 // newJiebaHMM literals (tokenizer.go:629-652)
 #define START_B (-0.26268660809250016)
@@ -1565,7 +1568,7 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
                                             const uint64_t* __restrict__ erec, uint8_t* __restrict__ gbl,
                                             double* __restrict__ gbest,
                                             uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
-                                            uint2* __restrict__ longblk, uint32_t grp,
+                                            uint2* __restrict__ longblk, uint32_t* __restrict__ lsegb, uint32_t grp,
                                             uint32_t diag, uint64_t* __restrict__ dbg) {
     __shared__ uint8_t s_bl[4][kZhWin / 3u + 4u];
     __shared__ double s_rb[4][kZhRing * 64];  // DP ring, then the window's token bitmaps
@@ -1726,9 +1729,13 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
 #pragma unroll
             for (int i = 0; i < 3; i++) {
                 if (st) stv[6] += __popcll(__ballot(out[i]));
-                if (out[i] && bei[i] - bsi[i] >= kZhLongMin) {  // k_zh_long cuts it with a whole wave
-                    const uint32_t li = atomicAdd(counters + CNT_NLONG, 1u);
-                    longblk[li] = make_uint2(bsi[i], bei[i]);
+                if (out[i] && bei[i] - bsi[i] >= kZhLongMin) {  // the k_long_* kernels cut it
+                    // block index and first segment from one atomic, so lsegb ascends with the index
+                    const uint32_t nsg = ((bei[i] - bsi[i]) / 3u + kSeg - 1u) / kSeg;
+                    const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long*>(counters + CNT_NLONG),
+                                                             ((unsigned long long)nsg << 32) | 1ull);
+                    longblk[(uint32_t)old] = make_uint2(bsi[i], bei[i]);
+                    lsegb[(uint32_t)old] = (uint32_t)(old >> 32);
                 } else if (out[i]) {
                     const GlbZv gv{text, gbl};
                     zh_dp(gv, im, erec, gbest, ring, OneSrc{bsi[i], bei[i]});
@@ -1776,235 +1783,485 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
 
 // ---------------------------------------------------------------------------
 // Long zh blocks (>= kZhLongMin bytes; e.g. an unpunctuated document, BASELINE
-// config 5b).  Their DP is one serial chain: best(i) is built from best(i+L)
-// with float64 adds in the reference's order (:519-529), which must not be
-// re-associated, so no two runes' values can be computed in parallel.  What
-// is NOT serial is everything after it: findDagPath only follows the chosen
-// lengths, and the HMM runs between multi-rune pieces are independent of
-// each other (:229-253).  So:
-//   k_zh_long  one wave per long block: (1) the DP, backwards, run as a
-//              uniform program (every lane computes the same values, the
-//              chain branches on scalars: each rune's record is classified
-//              when its block of 64 is loaded);
-//              (2) the path: a scalar walk p += L(p) from rune 0 over the
-//              chosen lengths, marking piece starts in the `lpath` bitmap.
-//   k_long_tail  many waves: one lane per 64 runes turns the marked pieces
-//              into tokens and runs the Viterbi (+ cutHMM) of every run of
-//              single-rune pieces that starts in its range.
-// All-3-byte blocks only; a long block with a 4-byte Han rune takes k_zh's
-// one-lane path inside k_zh_long.
+// config 5b), all 3-byte runes.  Their DP is one serial chain: best(i) is built
+// from best(i+L) with float64 adds in the reference's order (:519-529), which
+// must not be re-associated, so no two runes' values can be computed in
+// parallel.  Everything around the chain is parallel:
+//   k_long_dp    one workgroup per long block.  Waves 1-3 turn each rune's DAG
+//                record into a descriptor in LDS (its item weights and the LDS
+//                addresses of the best values they add to), two windows of 256
+//                runes ahead of the chain, and copy finished best values to
+//                HBM.  Wave 0 runs the chain on one lane, from LDS only, one
+//                step software-pipelined and without a branch.
+//   k_long_seg   one lane per 64-rune segment: the chosen lengths (maxIndexProba
+//                over the same sums again, from the best values in HBM) and a
+//                speculative path walked from the segment's first rune.
+//   k_long_path  one wave per long block: findDagPath's true path through the
+//                segments (:552-562).  Where it enters a segment off the
+//                speculative path it walks until the two meet (within a few
+//                pieces, in practice) and fixes the segment's path bits.
+//   k_long_tail  one lane per segment: tokens of the marked pieces, and the
+//                Viterbi (+ cutHMM) of every run of single-rune pieces that
+//                starts there (the runs are independent, :229-253).
+// A long block with a 4-byte Han rune takes k_zh's one-lane path in k_long_dp.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kZhLongGrid = 64;  // k_zh_long waves (persistent over the long-block list)
-constexpr uint32_t kTailRunes = 64;   // k_long_tail: runes per lane
+constexpr uint32_t kLongGrid = 64;    // k_long_dp workgroups (persistent over the long-block list)
+constexpr uint32_t kLdWin = 256;      // runes per descriptor window
+constexpr uint32_t kLdDesc = 1024;    // descriptor ring: 4 windows
+constexpr uint32_t kLdRing = 512;     // best-value ring (edges are at most 255 runes)
+constexpr uint32_t kLdSide = 256;     // items of slow runes, per window
+constexpr uint32_t kLdWalk = 0xFFFFFFFFu;  // descriptor flag: the chain walks the rune itself
+static_assert(kSeg == 64u, "segments are one 64-bit mask");
 
-// double from lane j of a uniform-in-register value (readlane: no memory access)
-__device__ __forceinline__ double rl64(double v, uint32_t j) {
-    const uint64_t u = (uint64_t)__double_as_longlong(v);
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, j), hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), j);
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-
-// DP classes of a rune's record (staged with it): the chain branches on them.
-enum : uint32_t {
-    kDpWalk = 0,  // record overflowed: walk the trie here (rare)
-    kDpOne = 1,   // the single edge L = 1: best = w + best(i+1)
-    kDpTwo = 2,   // edges L = 1 and L2 (meta bits 4..7)
-    kDpFold = 3,  // anything else: the general fold
+// A rune's DP step in LDS.  Fast form (flag 0): items L = 1 < L2 < L3 < L4,
+// absent ones with a NaN weight (their sums are NaN, every compare with them
+// is false and fmax drops them).
+struct LDesc {
+    double w[4];    // item weights, ascending L
+    uint32_t a[3];  // byte offsets in the best ring of best(i + L_k), k = 2..4
+    uint32_t flag;  // 0: fast; 1 | off << 1 | m << 16: m items at side[off]; kLdWalk
+};
+struct LItem {
+    double w;
+    uint32_t L, pad;
+};
+struct LongLds {
+    double ring[kLdRing];  // best(i) at i & 511
+    LDesc desc[kLdDesc];   // rune i at i & 1023
+    LItem side[4][kLdSide];
+    uint32_t sidecnt[4], wslow[4];
 };
 
+// DAG items (L, weight) of rune i of an all-3-byte block [bs, be), ascending L
+// (buildDag's pieces and calcDagProba's pieceFreq, :462-497,511-519): from the
+// rune's record, or by walking the trie when the record overflowed.
+template <class F>
+__device__ __forceinline__ void long_items(const uint8_t* __restrict__ text, const DevImage& im,
+                                           const uint64_t* __restrict__ erec, uint32_t bs, uint32_t be, uint32_t i,
+                                           F&& f) {
+    const uint32_t q = bs + 3u * i;
+    const uint64_t rc = erec[q / 3u];
+    uint32_t mk = (uint32_t)rc & 0xFFu;
+    if (mk) {
+        for (int k = 0; k < 4 && mk; k++) {
+            const uint32_t L = (uint32_t)__builtin_ctz(mk) + 1u;
+            mk &= mk - 1u;
+            f(L, im.wtab[(uint32_t)(rc >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u)]);
+        }
+        return;
+    }
+    auto dec3 = [&](uint32_t p) {
+        const uint32_t x = ld4(text, p);
+        return ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
+    };
+    uint32_t id = rune_code(im, dec3(q));
+    uint64_t cc = im.cells[id];
+    if (jb_cell_check(cc) != JB_CHECK_ROOT) {  // not a key: the rune alone, tf 1.0 (:468-471,515-518)
+        f(1u, im.wtab[JB_WIDX_ABSENT]);
+        return;
+    }
+    if (jb_cell_fc(cc) == JB_FC_ZERO) {  // count == 0: the rune alone, Log(0) (:468-471)
+        f(1u, im.wtab[jb_cell_widx(cc)]);
+        return;
+    }
+    if (jb_cell_fc(cc) == JB_FC_POS) f(1u, im.wtab[jb_cell_widx(cc)]);
+    uint32_t qq = q + 3u, len = 1;
+    bool go = jb_cell_hc(cc) != 0u;
+    while (go && qq < be) {
+        const uint32_t tt = dat_slot(im, cc, dec3(qq));
+        const uint64_t ch = im.cells[tt];
+        if (!dat_hit(ch, id)) break;  // (:475-478)
+        ++len;
+        qq += 3u;
+        if (jb_cell_fc(ch) == JB_FC_POS) f(len, im.wtab[jb_cell_widx(ch)]);
+        go = jb_cell_hc(ch) != 0u;
+        id = tt;
+        cc = ch;
+    }
+}
+
+// maxIndexProba's rule on one item (:565-578), for a DpFold
+__device__ __forceinline__ void fold_item(DpFold& f, uint32_t L, double pp) {
+    if (pp >= f.prevP) {
+        f.bestL = L;
+        f.bestP = pp;
+    }
+    f.prevP = pp;
+    f.lastL = L;
+}
+
+// bits of a 64-rune mask at slot `slot` of a slot bitmap (up to 3 words)
+__device__ __forceinline__ void bits64_or(uint32_t* __restrict__ bm, uint32_t slot, uint64_t m) {
+    const uint32_t w = slot >> 5, sh = slot & 31u;
+    const uint32_t x0 = (uint32_t)(m << sh);
+    const uint32_t x1 = sh ? (uint32_t)(m >> (32u - sh)) : (uint32_t)(m >> 32);
+    const uint32_t x2 = sh ? (uint32_t)(m >> (64u - sh)) : 0u;
+    if (x0) atomicOr(bm + w, x0);
+    if (x1) atomicOr(bm + w + 1u, x1);
+    if (x2) atomicOr(bm + w + 2u, x2);
+}
+__device__ __forceinline__ void bits64_clear(uint32_t* __restrict__ bm, uint32_t slot, uint64_t m) {
+    const uint32_t w = slot >> 5, sh = slot & 31u;
+    const uint32_t x0 = (uint32_t)(m << sh);
+    const uint32_t x1 = sh ? (uint32_t)(m >> (32u - sh)) : (uint32_t)(m >> 32);
+    const uint32_t x2 = sh ? (uint32_t)(m >> (64u - sh)) : 0u;
+    if (x0) atomicAnd(bm + w, ~x0);
+    if (x1) atomicAnd(bm + w + 1u, ~x1);
+    if (x2) atomicAnd(bm + w + 2u, ~x2);
+}
+
+// the long block that segment g belongs to (lsegb: first segment of each block, ascending)
+__device__ __forceinline__ uint32_t long_block_of(const uint32_t* __restrict__ lsegb, uint32_t nlong, uint32_t g) {
+    uint32_t lo = 0, hi = nlong;
+    while (hi - lo > 1u) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (lsegb[mid] <= g) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
 template <bool HMM>
-__global__ __launch_bounds__(64) void k_zh_long(const uint8_t* __restrict__ text, DevImage im,
-                                                const uint64_t* __restrict__ erec, uint8_t* __restrict__ gbl,
-                                                double* __restrict__ gbest, const uint2* __restrict__ longblk,
-                                                uint32_t* __restrict__ counters, uint32_t* __restrict__ sbits,
-                                                uint32_t* __restrict__ ebits, uint32_t* __restrict__ lpath,
-                                                uint32_t* __restrict__ lflag) {
-    __shared__ double s_best[256];  // best(i) at i & 255 (edges are at most 255 runes)
-    __shared__ double s_ring[kZhRing * 64];
-    const uint32_t lane = threadIdx.x;
+__global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ text, DevImage im,
+                                                 const uint64_t* __restrict__ erec, uint8_t* __restrict__ gbl,
+                                                 double* __restrict__ gbest, const uint2* __restrict__ longblk,
+                                                 uint32_t* __restrict__ counters, uint32_t* __restrict__ sbits,
+                                                 uint32_t* __restrict__ ebits, uint32_t* __restrict__ lpath,
+                                                 uint32_t* __restrict__ lflag) {
+    __shared__ LongLds S;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const uint32_t nlong = counters[CNT_NLONG];
-    Emitter em(sbits, ebits);
+    const char* const rb = reinterpret_cast<const char*>(S.ring);
     for (uint32_t bi = blockIdx.x; bi < nlong; bi += gridDim.x) {
         const uint2 bb = longblk[bi];
         const uint32_t bs = bb.x, be = bb.y;
         bool any4 = false;  // a 4-byte Han rune (lead >= 0xF0) anywhere in the block
-        for (uint32_t a = (bs & ~15u) + 16u * lane; a < be; a += 1024u) {
+        for (uint32_t a = (bs & ~15u) + 16u * tid; a < be; a += 4096u) {
             const uint4 x = *reinterpret_cast<const uint4*>(text + a);
             any4 |= ((x.x & (x.x << 1) & (x.x << 2) & (x.x << 3)) | (x.y & (x.y << 1) & (x.y << 2) & (x.y << 3)) |
                      (x.z & (x.z << 1) & (x.z << 2) & (x.z << 3)) | (x.w & (x.w << 1) & (x.w << 2) & (x.w << 3))) &
                     0x80808080u;
         }
-        if (__any(any4)) {  // the general one-lane path (k_zh's); k_long_tail skips the block
-            if (lane == 0) {
+        if (__syncthreads_or(any4)) {  // the general one-lane path (k_zh's); the later kernels skip the block
+            if (tid == 0) {
                 lflag[bi] = 0u;
+                Emitter em(sbits, ebits);
                 const GlbZv gv{text, gbl};
-                zh_dp(gv, im, erec, gbest, s_ring + lane, OneSrc{bs, be});
+                zh_dp(gv, im, erec, gbest, S.ring, OneSrc{bs, be});
                 if (!zh_fwd<HMM>(gv, im, bs, be, em, nullptr)) atomicOr(counters + CNT_ERR, 1u);
                 em.flush();
                 if (em.ties) atomicAdd(counters + CNT_TIES, em.ties);
-                em.ties = 0;
             }
             __syncthreads();
             continue;
         }
         const uint32_t n = (be - bs) / 3u, s0 = bs / 3u;  // rune i: bytes bs + 3i, slot s0 + i
-        // clear the block's bits of the path bitmap (its end words may be shared with a neighbour)
-        for (uint32_t w = (s0 >> 5) + lane; w <= (s0 + n - 1u) >> 5; w += 64u) {
-            const uint32_t lo = max(s0, w << 5), hi = min(s0 + n, (w << 5) + 32u);  // slots [lo, hi) of word w
+        const int32_t J = (int32_t)((n + kLdWin - 1u) / kLdWin);  // windows; runes [n, 256 J) are dummies
+        // the block's bits of the path bitmap (its end words may be shared with a neighbour)
+        for (uint32_t w = (s0 >> 5) + tid; w <= (s0 + n - 1u) >> 5; w += 256u) {
+            const uint32_t lo = max(s0, w << 5), hi = min(s0 + n, (w << 5) + 32u);
             const uint32_t m = (hi - lo == 32u ? ~0u : ((1u << (hi - lo)) - 1u)) << (lo & 31u);
             atomicAnd(lpath + w, ~m);
         }
-        // ---- DP (calcDagProba + maxIndexProba, tokenizer.go:502-578), backwards ----
-        // Blocks of 64 runes, lane j holding rune 64B + j's record and the weights of
-        // its edges in registers (loaded two blocks ahead: records, then weights); the
-        // chain reads them with readlane, so nothing but the 256-entry best ring in
-        // LDS (best(i+L) for L >= 3, written by one lane) is a memory access on it.
-        s_best[n & 255u] = 0.0;  // best(n): the {n, 0.0} sentinel (:522-525)
-        double b1 = 0.0, b2 = 0.0;  // best(i+1), best(i+2) of the rune i up next
-        const int32_t Btop = (int32_t)((n - 1u) >> 6);
-        auto load_rec = [&](int32_t B) -> uint64_t {
-            const uint32_t i = 64u * (uint32_t)B + lane;
-            return (B >= 0 && i < n) ? erec[s0 + i] : 0ull;
-        };
-        auto meta_of = [](uint64_t rc) -> uint32_t {
-            const uint32_t mk = (uint32_t)rc & 0xFFu;
-            if (mk == 0u) return kDpWalk;
-            if (mk == 1u) return kDpOne;
-            if ((mk & 1u) && __popc(mk) == 2) return kDpTwo | (((uint32_t)__builtin_ctz(mk & ~1u) + 1u) << 4);
-            return kDpFold;
-        };
-        uint64_t rc = load_rec(Btop);
-        double w[4];
-        rec_weights(im, rc, w);
-        uint64_t rc1 = load_rec(Btop - 1);  // the next block's records
-        for (int32_t B = Btop; B >= 0; B--) {
-            double w1n[4];  // the next block's weights, in flight during this block
-            rec_weights(im, rc1, w1n);
-            const uint64_t rc2 = load_rec(B - 2);
-            const uint32_t meta_v = meta_of(rc);
-            const uint32_t rlo = (uint32_t)rc, rhi = (uint32_t)(rc >> 32);
-            uint32_t blv = 0;  // chosen lengths, lane j = rune 64B + j
-            const uint32_t base = 64u * (uint32_t)B;
-            for (uint32_t j = min(63u, n - 1u - base) + 1u; j-- > 0u;) {
-                const uint32_t i = base + j;
-                const uint32_t meta = __builtin_amdgcn_readlane(meta_v, j);
-                const uint32_t cls = meta & 15u;
-                const double w0 = rl64(w[0], j);
-                double P;
-                uint32_t BL;
-                if (cls == kDpOne) {  // one item: it is the answer whether or not it qualifies (:573-576)
-                    P = w0 + b1;
-                    BL = 1u;
-                } else if (cls == kDpTwo) {  // items L = 1 then L2: the second wins unless it is smaller
-                    const uint32_t L2 = meta >> 4;  // and the first qualifies (>= minFloat)
-                    const double v2 = L2 == 2u ? b2 : s_best[(i + L2) & 255u];
-                    const double pp2 = rl64(w[1], j) + v2;
-                    const double pp1 = w0 + b1;
-                    const bool second = (pp2 >= pp1) | !(pp1 >= JB_MIN_FLOAT);
-                    P = second ? pp2 : pp1;
-                    BL = second ? L2 : 1u;
-                } else {
-                    DpFold f;
-                    if (cls == kDpFold) {
-                        const uint64_t r = ((uint64_t)__builtin_amdgcn_readlane(rhi, j) << 32) |
-                                           __builtin_amdgcn_readlane(rlo, j);
-                        uint32_t mm = (uint32_t)r & 0xFFu;
-#pragma unroll
-                        for (int e = 0; e < 4; e++) {
-                            if (mm == 0u) break;
-                            const uint32_t Ln = (uint32_t)__builtin_ctz(mm) + 1u;
-                            mm &= mm - 1u;
-                            const double nb = Ln == 1u ? b1 : (Ln == 2u ? b2 : s_best[(i + Ln) & 255u]);
-                            const double pp = rl64(w[e], j) + nb;
-                            if (pp >= f.prevP) {
-                                f.bestL = Ln;
-                                f.bestP = pp;
-                            }
-                            f.prevP = pp;
-                            f.lastL = Ln;
-                        }
-                    } else {  // overflowed record: walk the rune here, every item folded
-                        auto item = [&](uint32_t Ln, double wt) {  // (Ln <= 255: best(i+Ln) is in the ring)
-                            const double pp = wt + (Ln == 1u ? b1 : s_best[(i + Ln) & 255u]);
-                            if (pp >= f.prevP) {
-                                f.bestL = Ln;
-                                f.bestP = pp;
-                            }
-                            f.prevP = pp;
-                            f.lastL = Ln;
-                        };
-                        auto dec3 = [&](uint32_t q) {
-                            const uint32_t x = ld4(text, q);
-                            return ((x & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
-                        };
-                        const uint32_t q = bs + 3u * i;
-                        uint32_t id = rune_code(im, dec3(q));
-                        uint64_t cc = im.cells[id];
-                        if (jb_cell_check(cc) != JB_CHECK_ROOT) {
-                            item(1u, im.wtab[JB_WIDX_ABSENT]);
-                        } else if (jb_cell_fc(cc) == JB_FC_ZERO) {
-                            item(1u, im.wtab[jb_cell_widx(cc)]);
-                        } else {
-                            if (jb_cell_fc(cc) == JB_FC_POS) item(1u, im.wtab[jb_cell_widx(cc)]);
-                            uint32_t qq = q + 3u, len = 1;
-                            bool go = jb_cell_hc(cc) != 0u;
-                            while (go && qq < be) {
-                                const uint32_t tt = dat_slot(im, cc, dec3(qq));
-                                const uint64_t ch = im.cells[tt];
-                                if (!dat_hit(ch, id)) break;  // (:475-478)
-                                ++len;
-                                qq += 3u;
-                                if (jb_cell_fc(ch) == JB_FC_POS) item(len, im.wtab[jb_cell_widx(ch)]);
-                                go = jb_cell_hc(ch) != 0u;
-                                id = tt;
-                                cc = ch;
-                            }
-                        }
-                    }
-                    f.finish();
-                    P = f.bestP;
-                    BL = f.bestL;
-                }
-                if (lane == 0u) s_best[i & 255u] = P;
-                blv = lane == j ? BL : blv;
-                b2 = b1;
-                b1 = P;
-            }
-            if (base + lane < n) gbl[s0 + base + lane] = (uint8_t)blv;
-            rc = rc1;
-            rc1 = rc2;
-#pragma unroll
-            for (int e = 0; e < 4; e++) w[e] = w1n[e];
+        if (tid < 4u) {
+            S.sidecnt[tid] = 0u;
+            S.wslow[tid] = 0u;
         }
-        // ---- path (findDagPath, :552-562): p += L(p) from rune 0, marking piece starts ----
-        __threadfence();  // gbl and the cleared bitmap words, before the reads below
-        uint32_t p = 0, wslot = s0 - 1024u, dw = 0, bword = 0xFFFFFFFFu, bits = 0;  // (first trip loads)
-        bool bad = false;
-        const uint32_t* gbl32 = reinterpret_cast<const uint32_t*>(gbl);
-        while (p < n) {
-            const uint32_t sl = s0 + p;
-            if (sl - wslot >= 256u) {  // lane j holds the lengths of slots wslot + 4j .. + 3
-                wslot = sl & ~3u;
-                dw = __hip_atomic_load(gbl32 + (wslot >> 2) + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0u) lflag[bi] = 2u;  // DP done here; k_long_path sets 1 (path found) or 0
+        __syncthreads();
+        // descriptors of window jw (buffer jw & 3) by threads t, t + nt, ...
+        auto fill = [&](int32_t jw, uint32_t t, uint32_t nt) {
+            const uint32_t b = (uint32_t)jw & 3u;
+            for (uint32_t r = t; r < kLdWin; r += nt) {
+                const int32_t i = jw * (int32_t)kLdWin + (int32_t)r;
+                LDesc& d = S.desc[(uint32_t)i & (kLdDesc - 1u)];
+                const double nan = __builtin_nan("");
+                if (i < 0 || (uint32_t)i >= n) {  // past the block: best = 0.0 + 0.0 (so best(n) = 0.0, :522-525)
+                    d.w[0] = 0.0;
+                    d.w[1] = d.w[2] = d.w[3] = nan;
+                    d.a[0] = d.a[1] = d.a[2] = 0u;
+                    d.flag = 0u;
+                    continue;
+                }
+                uint32_t m = 0, L[4] = {0, 0, 0, 0};
+                double w[4] = {nan, nan, nan, nan};
+                long_items(text, im, erec, bs, be, (uint32_t)i, [&](uint32_t Lk, double wk) {
+#pragma unroll
+                    for (uint32_t k = 0; k < 4u; k++) {  // (no dynamic register index: no scratch)
+                        L[k] = m == k ? Lk : L[k];
+                        w[k] = m == k ? wk : w[k];
+                    }
+                    m++;
+                });
+                if (m >= 1u && m <= 4u && L[0] == 1u) {
+#pragma unroll
+                    for (int k = 0; k < 4; k++) d.w[k] = w[k];
+#pragma unroll
+                    for (int k = 1; k < 4; k++) d.a[k - 1] = (uint32_t)k < m ? (((uint32_t)i + L[k]) & (kLdRing - 1u)) * 8u : 0u;
+                    d.flag = 0u;
+                } else {  // more than 4 items, or none, or no L = 1 item (a negative count)
+                    const uint32_t off = atomicAdd(&S.sidecnt[b], m);
+                    if (off + m <= kLdSide) {
+                        uint32_t k = 0;
+                        long_items(text, im, erec, bs, be, (uint32_t)i, [&](uint32_t Lk, double wk) {
+                            S.side[b][off + k].w = wk;
+                            S.side[b][off + k].L = Lk;
+                            k++;
+                        });
+                        d.flag = 1u | (off << 1) | (m << 16);
+                    } else {
+                        d.flag = kLdWalk;
+                    }
+                    d.a[0] = d.a[1] = d.a[2] = 0u;
+                    atomicOr(&S.wslow[b], 1u);
+                }
             }
-            const uint32_t d = __builtin_amdgcn_readlane(dw, (sl - wslot) >> 2);
-            const uint32_t Ln = (d >> (8u * (sl & 3u))) & 0xFFu;
-            if (Ln == 0u) {  // tail index -1: cutDAG's slice panics in the reference
-                bad = true;
+        };
+        auto copy = [&](int32_t jw, uint32_t t, uint32_t nt) {  // finished best values of window jw -> gbest
+            for (uint32_t r = t; r < kLdWin; r += nt) {
+                const uint32_t i = (uint32_t)jw * kLdWin + r;
+                if (i < n) gbest[s0 + i] = S.ring[i & (kLdRing - 1u)];
+            }
+        };
+        fill(J - 1, tid, 256u);
+        fill(J - 2, tid, 256u);
+        if (tid == 0u) S.ring[n & (kLdRing - 1u)] = 0.0;
+        __syncthreads();
+        if (wave == 0u) {
+            // ---- the chain (calcDagProba + maxIndexProba, :502-578), lane 0 ----
+            // Step s: issue rune s-3's descriptor and rune s-1's ring reads, then
+            // fold rune s.  The reference's rule over items p1..p4 (:565-578) is
+            // "the last k with p_k >= p_(k-1)" (p_0 = minFloat).  With L1 = 1 and
+            // NaN for absent items that is: p4 if p4 >= p3, else p3 if p3 >= p2,
+            // else max(p1, p2) (p1 < minFloat only when p1 = -Inf, and then
+            // p2 >= p1 whenever item 2 exists; equal values are the same value).
+            double W[4][4], RV[2][3];
+            uint32_t A[4][3], F[4];
+            double b1 = 0.0;  // best(s + 1)
+            auto ld_desc = [&](uint32_t set, uint32_t off) {  // off: byte offset in S.desc
+                const char* p = reinterpret_cast<const char*>(S.desc) + off;
+                const double2 x = *reinterpret_cast<const double2*>(p);
+                const double2 y = *reinterpret_cast<const double2*>(p + 16);
+                const uint4 z = *reinterpret_cast<const uint4*>(p + 32);
+                W[set][0] = x.x;
+                W[set][1] = x.y;
+                W[set][2] = y.x;
+                W[set][3] = y.y;
+                A[set][0] = z.x;
+                A[set][1] = z.y;
+                A[set][2] = z.z;
+                F[set] = z.w;
+            };
+            auto ld_ring = [&](uint32_t rs, uint32_t set) {
+#pragma unroll
+                for (int k = 0; k < 3; k++) RV[rs][k] = *reinterpret_cast<const double*>(rb + A[set][k]);
+            };
+            const int32_t top = (int32_t)kLdWin * J - 1;
+            if (lane == 0u) {
+                ld_desc(3u, ((uint32_t)top & (kLdDesc - 1u)) * 48u);
+                ld_desc(2u, ((uint32_t)(top - 1) & (kLdDesc - 1u)) * 48u);
+                ld_desc(1u, ((uint32_t)(top - 2) & (kLdDesc - 1u)) * 48u);
+                ld_ring(1u, 3u);
+            }
+            auto run = [&](auto chk, int32_t j) {
+                constexpr bool CHK = decltype(chk)::value;
+                const uint32_t b = (uint32_t)j & 3u;
+                for (int32_t g = (int32_t)kLdWin * j + (int32_t)kLdWin - 4; g >= (int32_t)kLdWin * j; g -= 4) {
+                    // runes s = g + 3 - u, u = 0..3: descriptor set s & 3 = 3 - u, ring set s & 1
+                    const uint32_t dcur = ((uint32_t)g & (kLdDesc - 1u)) * 48u;
+                    const uint32_t dnxt = ((uint32_t)(g - 4) & (kLdDesc - 1u)) * 48u;
+                    char* const rw = reinterpret_cast<char*>(S.ring) + ((uint32_t)g & (kLdRing - 1u)) * 8u;
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t cs = (uint32_t)(3 - u) & 3u, c1 = (uint32_t)(2 - u) & 3u,
+                                       c3 = (uint32_t)(0 - u) & 3u;
+                        const uint32_t rs = (uint32_t)(3 - u) & 1u, r1 = (uint32_t)(2 - u) & 1u;
+                        // rune s - 3 is g - u: slot g (u = 0) or g - 4 + (4 - u)
+                        ld_desc(c3, u == 0 ? dcur : dnxt + (uint32_t)(4 - u) * 48u);
+                        ld_ring(r1, c1);
+                        double P;
+                        if (CHK && F[cs] != 0u) {
+                            const uint32_t s = (uint32_t)(g + 3 - u), fl = F[cs];
+                            DpFold f;
+                            if (fl == kLdWalk) {
+                                long_items(text, im, erec, bs, be, s, [&](uint32_t L, double wt) {
+                                    fold_item(f, L, wt + S.ring[(s + L) & (kLdRing - 1u)]);
+                                });
+                            } else {
+                                const uint32_t m = fl >> 16, off = (fl >> 1) & 0x7FFFu;
+                                for (uint32_t k = 0; k < m; k++) {
+                                    const LItem it = S.side[b][off + k];
+                                    fold_item(f, it.L, it.w + S.ring[(s + it.L) & (kLdRing - 1u)]);
+                                }
+                            }
+                            f.finish();
+                            P = f.bestP;
+                        } else {
+                            const double p1 = W[cs][0] + b1;
+                            const double p2 = W[cs][1] + RV[rs][0];
+                            const double p3 = W[cs][2] + RV[rs][1];
+                            const double p4 = W[cs][3] + RV[rs][2];
+                            const double R = __builtin_fmax(p1, p2);
+                            const bool k3 = p3 >= p2, k4 = p4 >= p3;
+                            const double p34 = k4 ? p4 : p3;
+                            P = (k3 || k4) ? p34 : R;
+                        }
+                        *reinterpret_cast<double*>(rw + (uint32_t)(3 - u) * 8u) = P;
+                        b1 = P;
+                        // keep each step's loads a whole step ahead of their use: the
+                        // scheduler would otherwise hoist the next step's adds up to
+                        // its just-issued ring reads and wait for them
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+            };
+            for (int32_t j = J - 1; j >= 0; --j) {
+                if (lane == 0u) {
+                    if (S.wslow[j & 3]) run(std::true_type{}, j);
+                    else run(std::false_type{}, j);
+                }
+                __syncthreads();
+            }
+        } else {
+            const uint32_t ht = tid - 64u;  // helper thread 0..191
+            for (int32_t j = J - 1; j >= 0; --j) {
+                if (ht == 0u) {  // buffer of window j - 3 (last used by window j + 1, done): filled next trip
+                    S.sidecnt[(uint32_t)(j - 3) & 3u] = 0u;
+                    S.wslow[(uint32_t)(j - 3) & 3u] = 0u;
+                }
+                fill(j - 2, ht, 192u);
+                if (j + 1 < J) copy(j + 1, ht, 192u);
+                __syncthreads();
+            }
+            copy(0, ht, 192u);
+        }
+        __syncthreads();
+    }
+}
+
+// k_long_seg: one lane per 64-rune segment of a long block that k_long_dp ran
+// the chain for.  The chosen lengths are maxIndexProba over the same sums
+// w + best(i + L) the chain formed (the same float64 adds of the same values),
+// so they are the chain's choices.  Then a speculative path from the segment's
+// first rune, its bits into `lpath` and its exit into lseg.
+__global__ __launch_bounds__(256) void k_long_seg(const uint8_t* __restrict__ text, DevImage im,
+                                                  const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
+                                                  const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ counters,
+                                                  const uint32_t* __restrict__ lflag, const double* __restrict__ gbest,
+                                                  uint8_t* __restrict__ gbl, uint32_t* __restrict__ lpath,
+                                                  uint4* __restrict__ lseg) {
+    __shared__ uint8_t s_bl[256][kSeg];
+    const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG];
+    uint8_t* const my = s_bl[threadIdx.x];
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < nseg; g += gridDim.x * blockDim.x) {
+        const uint32_t bi = long_block_of(lsegb, nlong, g);
+        if (lflag[bi] != 2u) continue;
+        const uint2 bb = longblk[bi];
+        const uint32_t bs = bb.x, be = bb.y, n = (be - bs) / 3u, s0 = bs / 3u;
+        const uint32_t a = (g - lsegb[bi]) * kSeg, lim = min(a + kSeg, n);
+        for (uint32_t i = a; i < lim; i++) {
+            DpFold f;
+            long_items(text, im, erec, bs, be, i, [&](uint32_t L, double wt) {
+                fold_item(f, L, wt + (i + L == n ? 0.0 : gbest[s0 + i + L]));
+            });
+            f.finish();
+            my[i - a] = (uint8_t)f.bestL;
+            gbl[s0 + i] = (uint8_t)f.bestL;
+        }
+        uint64_t bits = 0;
+        uint32_t p = a;
+        bool stuck = false;
+        while (p < lim) {
+            const uint32_t L = my[p - a];
+            if (L == 0u) {  // tail index -1 (cutDAG panics if the true path comes here)
+                stuck = true;
                 break;
             }
-            if ((sl >> 5) != bword) {
-                if (bits && lane == 0u) atomicOr(lpath + bword, bits);
-                bword = sl >> 5;
-                bits = 0;
-            }
-            bits |= 1u << (sl & 31u);
-            p += Ln;
+            bits |= 1ull << (p - a);
+            p += L;
         }
-        if (bits && lane == 0u) atomicOr(lpath + bword, bits);
-        if (lane == 0u) lflag[bi] = bad ? 0u : 1u;
-        if (bad && lane == 0u) atomicOr(counters + CNT_ERR, 1u);
-        __syncthreads();
+        lseg[g] = make_uint4(stuck ? 0xFFFFFFFFu : p, 0u, (uint32_t)bits, (uint32_t)(bits >> 32));
+        bits64_or(lpath, s0 + a, bits);
+    }
+}
+
+// k_long_path: one wave per long block.  E is the true path's next piece start
+// (findDagPath, :552-562).  Segment by segment: where E is on the speculative
+// path, the rest of the segment's path is the speculative one (from E on it is
+// the same walk); otherwise walk from E until the walk meets a speculative
+// piece start (from there on it is the same walk) or leaves the segment.  The
+// speculative bits before the meeting point are cleared, the walked ones set.
+__global__ __launch_bounds__(64) void k_long_path(const uint2* __restrict__ longblk, const uint32_t* __restrict__ lsegb,
+                                                  uint32_t* __restrict__ counters, uint32_t* __restrict__ lflag,
+                                                  const uint8_t* __restrict__ gbl, const uint4* __restrict__ lseg,
+                                                  uint32_t* __restrict__ lpath) {
+    __shared__ uint32_t s_bl32[kSeg * kSeg / 4u];  // chosen lengths of 64 segments
+    const uint8_t* const s_bl = reinterpret_cast<const uint8_t*>(s_bl32);
+    const uint32_t lane = threadIdx.x;
+    const uint32_t nlong = counters[CNT_NLONG];
+    for (uint32_t bi = blockIdx.x; bi < nlong; bi += gridDim.x) {
+        if (lflag[bi] != 2u) continue;
+        const uint2 bb = longblk[bi];
+        const uint32_t n = (bb.y - bb.x) / 3u, s0 = bb.x / 3u, sb = lsegb[bi];
+        const uint32_t nsg = (n + kSeg - 1u) / kSeg;
+        uint32_t E = 0;
+        bool bad = false;
+        for (uint32_t b0 = 0; b0 < nsg && !bad; b0 += 64u) {
+            const uint4 rec = b0 + lane < nsg ? lseg[sb + b0 + lane] : make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t nw = min(kSeg * kSeg / 4u, (n - b0 * kSeg + 3u) / 4u);  // (gbl has 512 bytes of slack)
+            for (uint32_t k = lane; k < nw; k += 64u) s_bl32[k] = ld4(gbl, (uint64_t)s0 + b0 * kSeg + 4u * k);
+            __syncthreads();
+            const uint32_t top = min(64u, nsg - b0);
+            for (uint32_t t = 0; t < top; t++) {
+                const uint32_t a = (b0 + t) * kSeg, lim = min(a + kSeg, n);
+                const uint32_t ex = __builtin_amdgcn_readlane(rec.x, t);
+                const uint64_t bits = ((uint64_t)__builtin_amdgcn_readlane(rec.w, t) << 32) | __builtin_amdgcn_readlane(rec.z, t);
+                if (E >= lim) {  // a piece spans the whole segment: no start in it
+                    if (bits && lane == 0u) bits64_clear(lpath, s0 + a, bits);
+                    continue;
+                }
+                uint32_t mrel, En;
+                uint64_t tb = 0;
+                if ((bits >> (E - a)) & 1u) {
+                    mrel = E - a;
+                    En = ex;
+                } else {
+                    uint32_t q = E;
+                    while (q < lim && !((bits >> (q - a)) & 1u)) {
+                        const uint32_t L = s_bl[q - b0 * kSeg];
+                        if (L == 0u) {
+                            bad = true;
+                            break;
+                        }
+                        tb |= 1ull << (q - a);
+                        q += L;
+                    }
+                    if (bad) break;
+                    if (q >= lim) {
+                        mrel = kSeg;
+                        En = q;
+                    } else {
+                        mrel = q - a;
+                        En = ex;
+                    }
+                }
+                const uint64_t clr = mrel >= kSeg ? bits : bits & ((1ull << mrel) - 1ull);
+                if (lane == 0u) {
+                    if (clr) bits64_clear(lpath, s0 + a, clr);
+                    if (tb) bits64_or(lpath, s0 + a, tb);
+                }
+                if (En == 0xFFFFFFFFu) {  // joined a speculative walk that reached a rune with no piece
+                    bad = true;
+                    break;
+                }
+                E = En;
+            }
+            __syncthreads();
+        }
+        if (lane == 0u) {
+            lflag[bi] = bad ? 0u : 1u;
+            if (bad) atomicOr(counters + CNT_ERR, 1u);
+        }
     }
 }
 
@@ -2069,46 +2326,45 @@ __device__ void long_viterbi(const uint8_t* __restrict__ text, const DevImage& i
     }
 }
 
-// k_long_tail: the pieces k_zh_long marked in `lpath`, one lane per kTailRunes
-// runes of a long block (the lane owns the pieces and runs that START there).
+// k_long_tail: one lane per segment of a long block whose path k_long_path
+// marked in `lpath` (the lane owns the pieces and runs that START there).
 template <bool HMM>
 __global__ __launch_bounds__(256) void k_long_tail(const uint8_t* __restrict__ text, DevImage im,
                                                    const uint8_t* __restrict__ gbl, const uint2* __restrict__ longblk,
-                                                   const uint32_t* __restrict__ lflag, uint32_t* __restrict__ counters,
-                                                   const uint32_t* __restrict__ lpath, uint8_t* __restrict__ bp,
-                                                   uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits) {
-    const uint32_t nlong = counters[CNT_NLONG];
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+                                                   const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ lflag,
+                                                   uint32_t* __restrict__ counters, const uint32_t* __restrict__ lpath,
+                                                   uint8_t* __restrict__ bp, uint32_t* __restrict__ sbits,
+                                                   uint32_t* __restrict__ ebits) {
+    const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG];
     Emitter em(sbits, ebits);
-    for (uint32_t bi = 0; bi < nlong; bi++) {
-        if (!lflag[bi]) continue;  // cut by the one-lane path, or the reference panics
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < nseg; g += gridDim.x * blockDim.x) {
+        const uint32_t bi = long_block_of(lsegb, nlong, g);
+        if (lflag[bi] != 1u) continue;  // cut by the one-lane path, or the reference panics
         const uint2 bb = longblk[bi];
         const uint32_t bs = bb.x, n = (bb.y - bb.x) / 3u, s0 = bs / 3u;
         auto start = [&](uint32_t j) { return ((lpath[(s0 + j) >> 5] >> ((s0 + j) & 31u)) & 1u) != 0u; };
         auto len = [&](uint32_t j) { return (uint32_t)gbl[s0 + j]; };
-        for (uint32_t c = gid; c * kTailRunes < n; c += nth) {
-            const uint32_t c0 = c * kTailRunes, c1 = min(n, c0 + kTailRunes);
-            uint32_t q = c0;
-            // a run that began before c0 belongs to the lane that owns its start
-            if (HMM && q > 0u && start(q - 1u) && len(q - 1u) == 1u)
-                while (q < n && start(q) && len(q) == 1u) q++;
-            while (q < c1) {
-                if (!start(q)) {
-                    q++;
-                    continue;
-                }
-                const uint32_t Ln = len(q);
-                if (!HMM || Ln > 1u) {
-                    em.token(bs + 3u * q, bs + 3u * (q + Ln));
-                    q += Ln;
-                    continue;
-                }
-                uint32_t r = q + 1u;
-                while (r < n && start(r) && len(r) == 1u) r++;
-                if (r - q == 1u) em.token(bs + 3u * q, bs + 3u * r);  // a single rune is always "S" (:672-674)
-                else long_viterbi(text, im, bs, s0, q, r, bp, em);
-                q = r;
+        const uint32_t c0 = (g - lsegb[bi]) * kSeg, c1 = min(n, c0 + kSeg);
+        uint32_t q = c0;
+        // a run that began before c0 belongs to the lane that owns its start
+        if (HMM && q > 0u && start(q - 1u) && len(q - 1u) == 1u)
+            while (q < n && start(q) && len(q) == 1u) q++;
+        while (q < c1) {
+            if (!start(q)) {
+                q++;
+                continue;
             }
+            const uint32_t Ln = len(q);
+            if (!HMM || Ln > 1u) {
+                em.token(bs + 3u * q, bs + 3u * (q + Ln));
+                q += Ln;
+                continue;
+            }
+            uint32_t r = q + 1u;
+            while (r < n && start(r) && len(r) == 1u) r++;
+            if (r - q == 1u) em.token(bs + 3u * q, bs + 3u * r);  // a single rune is always "S" (:672-674)
+            else long_viterbi(text, im, bs, s0, q, r, bp, em);
+            q = r;
         }
     }
     em.flush();
@@ -2354,7 +2610,7 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     const uint32_t grp = lc.zh_group ? lc.zh_group : zh_group_for(nbytes);
     const uint32_t nttiles = (uint32_t)((nwords + kTokTileWords - 1) / kTokTileWords);
     hipError_t e;
-    if ((e = hipMemsetAsync(w.counters, 0, CNT_NWORDS * sizeof(uint32_t) + sizeof(uint64_t), stream))) return e;
+    if ((e = hipMemsetAsync(w.counters, 0, CNT_CLEAR * sizeof(uint32_t), stream))) return e;
     // (k_mark_walk clears the token bitmaps tile by tile)
     if ((e = hipMemsetAsync(w.docbits, 0, (nwords + 2) * 4, stream))) return e;
     if (nbytes == 0) {
@@ -2375,30 +2631,37 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     if (hmm)
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
                                           w.gstart, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
-                                          w.longblk, grp, diag, w.dbg));
+                                          w.longblk, w.lsegb, grp, diag, w.dbg));
     else
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
                                           w.gstart, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
-                                          w.longblk, grp, diag, w.dbg));
+                                          w.longblk, w.lsegb, grp, diag, w.dbg));
     {
-        // k_long_tail: one lane per kTailRunes runes of the long blocks (at most nbytes / 3 runes)
-        const uint64_t lanes = nbytes / 3u / kTailRunes + 1u;
-        const uint32_t gtail = (uint32_t)std::min<uint64_t>(1024u, (lanes + 255u) / 256u);
-        if (hmm) {
-            JB_TIMED(K_ZH_LONG, hipLaunchKernelGGL((k_zh_long<true>), dim3(kZhLongGrid), dim3(64), 0, stream, d_text, im,
+        // long blocks: the chain, then one lane per 64-rune segment (at most
+        // nbytes / 192 + nbytes / kZhLongMin segments), one wave per block
+        const uint64_t segs = nbytes / (3u * kSeg) + nbytes / kZhLongMin + 2u;
+        const uint32_t gseg = (uint32_t)std::min<uint64_t>(1024u, (segs + 255u) / 256u);
+        if (hmm)
+            JB_TIMED(K_LONG_DP, hipLaunchKernelGGL((k_long_dp<true>), dim3(kLongGrid), dim3(256), 0, stream, d_text, im,
                                                    w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters, w.sbits,
                                                    w.ebits, w.lpath, w.lflag));
-            JB_TIMED(K_LONG_TAIL, hipLaunchKernelGGL((k_long_tail<true>), dim3(gtail), dim3(256), 0, stream, d_text, im,
-                                                     w.gbl, w.longblk, w.lflag, w.counters, w.lpath, w.lbp, w.sbits,
-                                                     w.ebits));
-        } else {
-            JB_TIMED(K_ZH_LONG, hipLaunchKernelGGL((k_zh_long<false>), dim3(kZhLongGrid), dim3(64), 0, stream, d_text,
-                                                   im, w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters,
-                                                   w.sbits, w.ebits, w.lpath, w.lflag));
-            JB_TIMED(K_LONG_TAIL, hipLaunchKernelGGL((k_long_tail<false>), dim3(gtail), dim3(256), 0, stream, d_text,
-                                                     im, w.gbl, w.longblk, w.lflag, w.counters, w.lpath, w.lbp, w.sbits,
-                                                     w.ebits));
-        }
+        else
+            JB_TIMED(K_LONG_DP, hipLaunchKernelGGL((k_long_dp<false>), dim3(kLongGrid), dim3(256), 0, stream, d_text, im,
+                                                   w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters, w.sbits,
+                                                   w.ebits, w.lpath, w.lflag));
+        JB_TIMED(K_LONG_SEG, hipLaunchKernelGGL(k_long_seg, dim3(gseg), dim3(256), 0, stream, d_text, im,
+                                                w.erec + kErecPad, w.longblk, w.lsegb, w.counters, w.lflag, w.gbest,
+                                                w.gbl, w.lpath, w.lseg));
+        JB_TIMED(K_LONG_PATH, hipLaunchKernelGGL(k_long_path, dim3(kLongGrid), dim3(64), 0, stream, w.longblk, w.lsegb,
+                                                 w.counters, w.lflag, w.gbl, w.lseg, w.lpath));
+        if (hmm)
+            JB_TIMED(K_LONG_TAIL, hipLaunchKernelGGL((k_long_tail<true>), dim3(gseg), dim3(256), 0, stream, d_text, im,
+                                                     w.gbl, w.longblk, w.lsegb, w.lflag, w.counters, w.lpath, w.lbp,
+                                                     w.sbits, w.ebits));
+        else
+            JB_TIMED(K_LONG_TAIL, hipLaunchKernelGGL((k_long_tail<false>), dim3(gseg), dim3(256), 0, stream, d_text, im,
+                                                     w.gbl, w.longblk, w.lsegb, w.lflag, w.counters, w.lpath, w.lbp,
+                                                     w.sbits, w.ebits));
     }
     JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3(grid_nz), dim3(256), 0, stream, d_text, w.blk, w.alnum16,
                                          w.counters, w.sbits, w.ebits));

@@ -367,6 +367,39 @@ def test_record_overflow_paths(tmp_path, syn_small, kind):
         tk.close()
 
 
+@pytest.mark.parametrize("kind", [J.JB_DICT_TXT, J.JB_DICT_PREFIX])
+def test_long_blocks_many(tmp_path, syn_small, kind):
+    """The k_long_* kernels: several long blocks in one batch, sharing path-bitmap
+    words across a 1-byte gap and across a document boundary; edges longer than
+    a 64-rune segment (a piece spans whole segments); runes with more than 4
+    items (the chain's side list) and windows whose items overflow it (the chain
+    walks the trie itself)."""
+    _, ep, _ = syn_small
+    rng = random.Random(5)
+    pool = [chr(c) for c in range(0x4E00, 0x4E00 + 300)]
+    lines = [f"{'丁' * k} {10 + k}" for k in range(1, 21)]  # every 丁 starts up to 20 items
+    longw = []
+    for _ in range(30):  # 65..200-rune words; every prefix is a key, the word itself the likeliest
+        w = "".join(rng.choice(pool) for _ in range(rng.randint(65, 200)))
+        longw.append(w)
+        lines += [f"{w[:k]} {rng.randint(1, 3) if k < len(w) else 10 ** 6}" for k in range(1, len(w) + 1)]
+    dp = tmp_path / "dict.txt"
+    dp.write_text("\n".join(lines) + "\n", encoding="utf-8")
+    tk, o = _pair(str(dp), ep, kind=kind, size_override=60101967 if kind == J.JB_DICT_PREFIX else 0)
+    try:
+        a = "".join(rng.choice(longw) for _ in range(40))
+        b = "丁" * 3000
+        c = "".join(rng.choice([rng.choice(longw), "丁" * rng.randint(1, 30),
+                                "".join(rng.choice(pool) for _ in range(rng.randint(1, 40)))]) for _ in range(300))
+        texts = [a + "x" + c, b, c + "。" + a, "短文本，中文", b[:2800] + a[:3000], "丁乙" * 1500]
+        buf, off = _batch_of(texts)
+        for hmm in (False, True):
+            _cmp_batch(tk, o, buf, off, hmm, f"long blocks kind={kind} hmm={hmm}")
+            assert tk.last_stats()["long_blocks"] >= 6
+    finally:
+        tk.close()
+
+
 def test_synthetic_golden_vectors(syn_golden):
     """The GPU path reproduces the committed golden vectors (oracle output frozen in tests/golden)."""
     g, docs, dp, ep = syn_golden
