@@ -427,7 +427,7 @@ static int upload_image(Device* d, const Image& img) {
 static void free_work(Work* w) {
     dfree(w->docbits); dfree(w->tile_cnt); dfree(w->tile_off);
     dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->supb); dfree(w->supt); dfree(w->blk); dfree(w->alnum16); dfree(w->erec); dfree(w->lanemask);
-    dfree(w->gbl); dfree(w->lsegb); dfree(w->lseg); dfree(w->lpath); dfree(w->lflag); dfree(w->lbp); dfree(w->gbest); dfree(w->gstart); dfree(w->tile4); dfree(w->longblk);
+    dfree(w->gbl); dfree(w->lsegb); dfree(w->lent); dfree(w->lflag); dfree(w->lbp); dfree(w->gbest); dfree(w->gstart); dfree(w->tile4); dfree(w->longblk);
     dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters); dfree(w->dbg); dfree(w->dbg_walk);
     *w = Work{};
 }
@@ -459,10 +459,9 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.erec, (nb / 3 + 8 + kErecPad) * 8));
     HIPCHK(hipMalloc(&w.lanemask, ntiles * 256 * 4));
     HIPCHK(hipMalloc(&w.gbl, nb / 3 + 8 + 512));
-    HIPCHK(hipMalloc(&w.lpath, (nb / 3 / 32 + 4) * 4));
     HIPCHK(hipMalloc(&w.lflag, (nb / kZhLongMin + 2) * 4));
     HIPCHK(hipMalloc(&w.lsegb, (nb / kZhLongMin + 2) * 4));
-    HIPCHK(hipMalloc(&w.lseg, (nb / (3 * kSeg) + nb / kZhLongMin + 4) * sizeof(uint4)));
+    HIPCHK(hipMalloc(&w.lent, (nb / (3 * kSeg) + nb / kZhLongMin + 4) * 4));
     HIPCHK(hipMalloc(&w.lbp, nb / 3 + 64));
     HIPCHK(hipMalloc(&w.gstart, (nb / kZhGroupSmall + 4) * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.tile4, ntiles * 4));
@@ -636,6 +635,17 @@ static int launch(Device* d, const uint8_t* d_text, uint64_t nbytes, const uint6
         fprintf(stderr, "[jb] k_mark_walk clocks/wave: mark %.0f (staging %.0f) entries %.0f (loads %.0f) walk %.0f "
                         "tail %.0f; trips/wave %.2f\n",
                 b[0] / m, b[6] / m, b[1] / m, b[7] / m, b[2] / m, b[3] / m, b[4] / m);
+        std::vector<uint64_t> sl(64 * 8);
+        HIPCHK(hipMemcpyAsync(sl.data(), d->w.dbg + 65536 * 4, sl.size() * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (int i = 0; i < 64; i++)
+            if (sl[i * 8 + 2])
+                fprintf(stderr, "[jb] k_long_dp wg %d: chain run %llu bar %llu windows %llu slow %llu | "
+                                "helpers run %llu bar %llu\n", i,
+                        (unsigned long long)sl[i * 8], (unsigned long long)sl[i * 8 + 1],
+                        (unsigned long long)sl[i * 8 + 2], (unsigned long long)sl[i * 8 + 3],
+                        (unsigned long long)sl[i * 8 + 4], (unsigned long long)sl[i * 8 + 5]);
+        HIPCHK(hipMemsetAsync(d->w.dbg + 65536 * 4, 0, sl.size() * 8, s));
     }
     return JB_OK;
 }

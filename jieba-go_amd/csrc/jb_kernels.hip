@@ -1806,6 +1806,7 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
 // A long block with a 4-byte Han rune takes k_zh's one-lane path in k_long_dp.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kLongGrid = 64;    // k_long_dp workgroups (persistent over the long-block list)
+constexpr uint32_t kDbgLong = 65536u * 4u;  // k_long_dp's diagnostic clocks in the debug buffer (u64 index)
 constexpr uint32_t kLdWin = 256;      // runes per descriptor window
 constexpr uint32_t kLdDesc = 1024;    // descriptor ring: 4 windows
 constexpr uint32_t kLdRing = 512;     // best-value ring (edges are at most 255 runes)
@@ -1828,6 +1829,7 @@ struct LItem {
 struct LongLds {
     double ring[kLdRing];  // best(i) at i & 511
     LDesc desc[kLdDesc];   // rune i at i & 1023
+    uint8_t cls[kLdDesc];  // rune i's step form: 0 one item, 1 two, 2 three or four, 3 slow
     LItem side[4][kLdSide];
     uint32_t sidecnt[4], wslow[4];
 };
@@ -1880,6 +1882,14 @@ __device__ __forceinline__ void long_items(const uint8_t* __restrict__ text, con
     }
 }
 
+// max of two float64 sums that are never NaN: one v_max_f64 (fmax would add a
+// canonicalizing v_max_f64 of an operand the compiler cannot prove canonical)
+__device__ __forceinline__ double max_f64(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // maxIndexProba's rule on one item (:565-578), for a DpFold
 __device__ __forceinline__ void fold_item(DpFold& f, uint32_t L, double pp) {
     if (pp >= f.prevP) {
@@ -1888,26 +1898,6 @@ __device__ __forceinline__ void fold_item(DpFold& f, uint32_t L, double pp) {
     }
     f.prevP = pp;
     f.lastL = L;
-}
-
-// bits of a 64-rune mask at slot `slot` of a slot bitmap (up to 3 words)
-__device__ __forceinline__ void bits64_or(uint32_t* __restrict__ bm, uint32_t slot, uint64_t m) {
-    const uint32_t w = slot >> 5, sh = slot & 31u;
-    const uint32_t x0 = (uint32_t)(m << sh);
-    const uint32_t x1 = sh ? (uint32_t)(m >> (32u - sh)) : (uint32_t)(m >> 32);
-    const uint32_t x2 = sh ? (uint32_t)(m >> (64u - sh)) : 0u;
-    if (x0) atomicOr(bm + w, x0);
-    if (x1) atomicOr(bm + w + 1u, x1);
-    if (x2) atomicOr(bm + w + 2u, x2);
-}
-__device__ __forceinline__ void bits64_clear(uint32_t* __restrict__ bm, uint32_t slot, uint64_t m) {
-    const uint32_t w = slot >> 5, sh = slot & 31u;
-    const uint32_t x0 = (uint32_t)(m << sh);
-    const uint32_t x1 = sh ? (uint32_t)(m >> (32u - sh)) : (uint32_t)(m >> 32);
-    const uint32_t x2 = sh ? (uint32_t)(m >> (64u - sh)) : 0u;
-    if (x0) atomicAnd(bm + w, ~x0);
-    if (x1) atomicAnd(bm + w + 1u, ~x1);
-    if (x2) atomicAnd(bm + w + 2u, ~x2);
 }
 
 // the long block that segment g belongs to (lsegb: first segment of each block, ascending)
@@ -1926,9 +1916,12 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                                                  const uint64_t* __restrict__ erec, uint8_t* __restrict__ gbl,
                                                  double* __restrict__ gbest, const uint2* __restrict__ longblk,
                                                  uint32_t* __restrict__ counters, uint32_t* __restrict__ sbits,
-                                                 uint32_t* __restrict__ ebits, uint32_t* __restrict__ lpath,
-                                                 uint32_t* __restrict__ lflag) {
+                                                 uint32_t* __restrict__ ebits, uint32_t* __restrict__ lflag,
+                                                 uint64_t* __restrict__ dbg) {
     __shared__ LongLds S;
+#if JB_STAMPS
+    uint64_t st_run = 0, st_bar = 0, st_n = 0, st_slow = 0;  // diagnostic clocks (wave 0 and wave 1, lane 0)
+#endif
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const uint32_t nlong = counters[CNT_NLONG];
     const char* const rb = reinterpret_cast<const char*>(S.ring);
@@ -1957,17 +1950,11 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
         }
         const uint32_t n = (be - bs) / 3u, s0 = bs / 3u;  // rune i: bytes bs + 3i, slot s0 + i
         const int32_t J = (int32_t)((n + kLdWin - 1u) / kLdWin);  // windows; runes [n, 256 J) are dummies
-        // the block's bits of the path bitmap (its end words may be shared with a neighbour)
-        for (uint32_t w = (s0 >> 5) + tid; w <= (s0 + n - 1u) >> 5; w += 256u) {
-            const uint32_t lo = max(s0, w << 5), hi = min(s0 + n, (w << 5) + 32u);
-            const uint32_t m = (hi - lo == 32u ? ~0u : ((1u << (hi - lo)) - 1u)) << (lo & 31u);
-            atomicAnd(lpath + w, ~m);
-        }
         if (tid < 4u) {
             S.sidecnt[tid] = 0u;
             S.wslow[tid] = 0u;
         }
-        if (tid == 0u) lflag[bi] = 2u;  // DP done here; k_long_path sets 1 (path found) or 0
+        if (tid == 0u) lflag[bi] = 2u;  // DP done here; k_long_path sets 1 (entries found)
         __syncthreads();
         // descriptors of window jw (buffer jw & 3) by threads t, t + nt, ...
         auto fill = [&](int32_t jw, uint32_t t, uint32_t nt) {
@@ -1976,7 +1963,9 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                 const int32_t i = jw * (int32_t)kLdWin + (int32_t)r;
                 LDesc& d = S.desc[(uint32_t)i & (kLdDesc - 1u)];
                 const double nan = __builtin_nan("");
+                uint8_t& cl = S.cls[(uint32_t)i & (kLdDesc - 1u)];
                 if (i < 0 || (uint32_t)i >= n) {  // past the block: best = 0.0 + 0.0 (so best(n) = 0.0, :522-525)
+                    cl = 0u;
                     d.w[0] = 0.0;
                     d.w[1] = d.w[2] = d.w[3] = nan;
                     d.a[0] = d.a[1] = d.a[2] = 0u;
@@ -1999,7 +1988,9 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
 #pragma unroll
                     for (int k = 1; k < 4; k++) d.a[k - 1] = (uint32_t)k < m ? (((uint32_t)i + L[k]) & (kLdRing - 1u)) * 8u : 0u;
                     d.flag = 0u;
+                    cl = m == 1u ? 0u : (m == 2u ? 1u : 2u);
                 } else {  // more than 4 items, or none, or no L = 1 item (a negative count)
+                    cl = 3u;
                     const uint32_t off = atomicAdd(&S.sidecnt[b], m);
                     if (off + m <= kLdSide) {
                         uint32_t k = 0;
@@ -2063,10 +2054,15 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                 ld_desc(1u, ((uint32_t)(top - 2) & (kLdDesc - 1u)) * 48u);
                 ld_ring(1u, 3u);
             }
+            // step forms of the 4 runes of the group up next (one LDS word, a group ahead)
+            uint32_t cwn = 0;
+            if (lane == 0u) cwn = *reinterpret_cast<const uint32_t*>(S.cls + ((uint32_t)(top - 3) & (kLdDesc - 1u)));
             auto run = [&](auto chk, int32_t j) {
                 constexpr bool CHK = decltype(chk)::value;
                 const uint32_t b = (uint32_t)j & 3u;
                 for (int32_t g = (int32_t)kLdWin * j + (int32_t)kLdWin - 4; g >= (int32_t)kLdWin * j; g -= 4) {
+                    const uint32_t cw = __builtin_amdgcn_readfirstlane(cwn);
+                    cwn = *reinterpret_cast<const uint32_t*>(S.cls + ((uint32_t)(g - 4) & (kLdDesc - 1u)));
                     // runes s = g + 3 - u, u = 0..3: descriptor set s & 3 = 3 - u, ring set s & 1
                     const uint32_t dcur = ((uint32_t)g & (kLdDesc - 1u)) * 48u;
                     const uint32_t dnxt = ((uint32_t)(g - 4) & (kLdDesc - 1u)) * 48u;
@@ -2080,7 +2076,8 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                         ld_desc(c3, u == 0 ? dcur : dnxt + (uint32_t)(4 - u) * 48u);
                         ld_ring(r1, c1);
                         double P;
-                        if (CHK && F[cs] != 0u) {
+                        const uint32_t cl = (cw >> (8 * (3 - u))) & 3u;  // rune s = g + 3 - u: byte 3 - u
+                        if (CHK && cl == 3u) {
                             const uint32_t s = (uint32_t)(g + 3 - u), fl = F[cs];
                             DpFold f;
                             if (fl == kLdWalk) {
@@ -2096,12 +2093,16 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                             }
                             f.finish();
                             P = f.bestP;
+                        } else if (cl == 0u) {  // one item: it is the answer (:573-576)
+                            P = W[cs][0] + b1;
+                        } else if (cl == 1u) {  // two: the second unless it is smaller
+                            P = max_f64(W[cs][0] + b1, W[cs][1] + RV[rs][0]);
                         } else {
                             const double p1 = W[cs][0] + b1;
                             const double p2 = W[cs][1] + RV[rs][0];
                             const double p3 = W[cs][2] + RV[rs][1];
                             const double p4 = W[cs][3] + RV[rs][2];
-                            const double R = __builtin_fmax(p1, p2);
+                            const double R = max_f64(p1, p2);  // (items 1, 2 exist: no NaN)
                             const bool k3 = p3 >= p2, k4 = p4 >= p3;
                             const double p34 = k4 ? p4 : p3;
                             P = (k3 || k4) ? p34 : R;
@@ -2116,11 +2117,23 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                 }
             };
             for (int32_t j = J - 1; j >= 0; --j) {
+#if JB_STAMPS
+                const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
                 if (lane == 0u) {
                     if (S.wslow[j & 3]) run(std::true_type{}, j);
                     else run(std::false_type{}, j);
                 }
+#if JB_STAMPS
+                const uint64_t t1 = __builtin_amdgcn_s_memtime();
+                st_slow += S.wslow[j & 3] ? 1u : 0u;
+#endif
                 __syncthreads();
+#if JB_STAMPS
+                st_run += t1 - t0;
+                st_bar += __builtin_amdgcn_s_memtime() - t1;
+                st_n++;
+#endif
             }
         } else {
             const uint32_t ht = tid - 64u;  // helper thread 0..191
@@ -2129,27 +2142,51 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                     S.sidecnt[(uint32_t)(j - 3) & 3u] = 0u;
                     S.wslow[(uint32_t)(j - 3) & 3u] = 0u;
                 }
+#if JB_STAMPS
+                const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
                 fill(j - 2, ht, 192u);
                 if (j + 1 < J) copy(j + 1, ht, 192u);
+#if JB_STAMPS
+                const uint64_t t1 = __builtin_amdgcn_s_memtime();
+#endif
                 __syncthreads();
+#if JB_STAMPS
+                st_run += t1 - t0;
+                st_bar += __builtin_amdgcn_s_memtime() - t1;
+                st_n++;
+#endif
             }
             copy(0, ht, 192u);
         }
         __syncthreads();
     }
+#if JB_STAMPS
+    if (lane == 0u && wave < 2u) {  // [0..3] chain: run, barrier, windows, slow windows; [4..7] helper wave 1
+        uint64_t* o = dbg + kDbgLong + blockIdx.x * 8u + wave * 4u;
+        o[0] = st_run;
+        o[1] = st_bar;
+        o[2] = st_n;
+        o[3] = st_slow;
+    }
+#else
+    (void)dbg;
+#endif
 }
 
 // k_long_seg: one lane per 64-rune segment of a long block that k_long_dp ran
 // the chain for.  The chosen lengths are maxIndexProba over the same sums
 // w + best(i + L) the chain formed (the same float64 adds of the same values),
-// so they are the chain's choices.  Then a speculative path from the segment's
-// first rune, its bits into `lpath` and its exit into lseg.
+// so they are the chain's choices.  Then, backwards over the segment, each
+// rune's exit code: where findDagPath, entering the segment at that rune, first
+// lands at or past the segment's end (its offset past the end, 0..254), or
+// 0xFF when that is the end itself and the last piece before it is one rune
+// (so the next segment knows a run of single-rune pieces enters it).
 __global__ __launch_bounds__(256) void k_long_seg(const uint8_t* __restrict__ text, DevImage im,
                                                   const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
                                                   const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ counters,
                                                   const uint32_t* __restrict__ lflag, const double* __restrict__ gbest,
-                                                  uint8_t* __restrict__ gbl, uint32_t* __restrict__ lpath,
-                                                  uint4* __restrict__ lseg) {
+                                                  uint8_t* __restrict__ gbl, uint8_t* __restrict__ lcode) {
     __shared__ uint8_t s_bl[256][kSeg];
     const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG];
     uint8_t* const my = s_bl[threadIdx.x];
@@ -2168,35 +2205,26 @@ __global__ __launch_bounds__(256) void k_long_seg(const uint8_t* __restrict__ te
             my[i - a] = (uint8_t)f.bestL;
             gbl[s0 + i] = (uint8_t)f.bestL;
         }
-        uint64_t bits = 0;
-        uint32_t p = a;
-        bool stuck = false;
-        while (p < lim) {
-            const uint32_t L = my[p - a];
-            if (L == 0u) {  // tail index -1 (cutDAG panics if the true path comes here)
-                stuck = true;
-                break;
-            }
-            bits |= 1ull << (p - a);
-            p += L;
+        for (uint32_t p = lim; p-- > a;) {
+            // (a rune with no piece walks on as if it had one: if the true path
+            // comes to it, k_long_tail reports it)
+            const uint32_t L = max(1u, (uint32_t)my[p - a]), q = p + L;
+            const uint8_t c = q >= lim ? (L == 1u ? (uint8_t)0xFFu : (uint8_t)(q - lim)) : my[q - a];
+            my[p - a] = c;
+            lcode[s0 + p] = c;
         }
-        lseg[g] = make_uint4(stuck ? 0xFFFFFFFFu : p, 0u, (uint32_t)bits, (uint32_t)(bits >> 32));
-        bits64_or(lpath, s0 + a, bits);
     }
 }
 
-// k_long_path: one wave per long block.  E is the true path's next piece start
-// (findDagPath, :552-562).  Segment by segment: where E is on the speculative
-// path, the rest of the segment's path is the speculative one (from E on it is
-// the same walk); otherwise walk from E until the walk meets a speculative
-// piece start (from there on it is the same walk) or leaves the segment.  The
-// speculative bits before the meeting point are cleared, the walked ones set.
+// k_long_path: one wave per long block: findDagPath (:552-562) hop by hop over
+// the segments, one exit-code lookup per segment, staged 64 segments at a time
+// in LDS.  Per segment: the offset of the path's first piece start in it (0xFF:
+// none, a piece spans the segment) and whether a one-rune piece ends there.
 __global__ __launch_bounds__(64) void k_long_path(const uint2* __restrict__ longblk, const uint32_t* __restrict__ lsegb,
-                                                  uint32_t* __restrict__ counters, uint32_t* __restrict__ lflag,
-                                                  const uint8_t* __restrict__ gbl, const uint4* __restrict__ lseg,
-                                                  uint32_t* __restrict__ lpath) {
-    __shared__ uint32_t s_bl32[kSeg * kSeg / 4u];  // chosen lengths of 64 segments
-    const uint8_t* const s_bl = reinterpret_cast<const uint8_t*>(s_bl32);
+                                                  const uint32_t* __restrict__ counters, uint32_t* __restrict__ lflag,
+                                                  const uint8_t* __restrict__ lcode, uint32_t* __restrict__ lent) {
+    __shared__ uint32_t s_c32[kSeg * kSeg / 4u];  // exit codes of 64 segments
+    const uint8_t* const s_c = reinterpret_cast<const uint8_t*>(s_c32);
     const uint32_t lane = threadIdx.x;
     const uint32_t nlong = counters[CNT_NLONG];
     for (uint32_t bi = blockIdx.x; bi < nlong; bi += gridDim.x) {
@@ -2204,64 +2232,24 @@ __global__ __launch_bounds__(64) void k_long_path(const uint2* __restrict__ long
         const uint2 bb = longblk[bi];
         const uint32_t n = (bb.y - bb.x) / 3u, s0 = bb.x / 3u, sb = lsegb[bi];
         const uint32_t nsg = (n + kSeg - 1u) / kSeg;
-        uint32_t E = 0;
-        bool bad = false;
-        for (uint32_t b0 = 0; b0 < nsg && !bad; b0 += 64u) {
-            const uint4 rec = b0 + lane < nsg ? lseg[sb + b0 + lane] : make_uint4(0u, 0u, 0u, 0u);
-            const uint32_t nw = min(kSeg * kSeg / 4u, (n - b0 * kSeg + 3u) / 4u);  // (gbl has 512 bytes of slack)
-            for (uint32_t k = lane; k < nw; k += 64u) s_bl32[k] = ld4(gbl, (uint64_t)s0 + b0 * kSeg + 4u * k);
+        uint32_t E = 0, single = 0;
+        for (uint32_t b0 = 0; b0 < nsg; b0 += 64u) {
+            const uint32_t base = b0 * kSeg, top = min(n, base + kSeg * kSeg);
+            const uint32_t nw = (top - base + 3u) / 4u;  // (lcode has 512 bytes of slack)
+            for (uint32_t k = lane; k < nw; k += 64u) s_c32[k] = ld4(lcode, (uint64_t)s0 + base + 4u * k);
             __syncthreads();
-            const uint32_t top = min(64u, nsg - b0);
-            for (uint32_t t = 0; t < top; t++) {
-                const uint32_t a = (b0 + t) * kSeg, lim = min(a + kSeg, n);
-                const uint32_t ex = __builtin_amdgcn_readlane(rec.x, t);
-                const uint64_t bits = ((uint64_t)__builtin_amdgcn_readlane(rec.w, t) << 32) | __builtin_amdgcn_readlane(rec.z, t);
-                if (E >= lim) {  // a piece spans the whole segment: no start in it
-                    if (bits && lane == 0u) bits64_clear(lpath, s0 + a, bits);
-                    continue;
-                }
-                uint32_t mrel, En;
-                uint64_t tb = 0;
-                if ((bits >> (E - a)) & 1u) {
-                    mrel = E - a;
-                    En = ex;
-                } else {
-                    uint32_t q = E;
-                    while (q < lim && !((bits >> (q - a)) & 1u)) {
-                        const uint32_t L = s_bl[q - b0 * kSeg];
-                        if (L == 0u) {
-                            bad = true;
-                            break;
-                        }
-                        tb |= 1ull << (q - a);
-                        q += L;
-                    }
-                    if (bad) break;
-                    if (q >= lim) {
-                        mrel = kSeg;
-                        En = q;
-                    } else {
-                        mrel = q - a;
-                        En = ex;
-                    }
-                }
-                const uint64_t clr = mrel >= kSeg ? bits : bits & ((1ull << mrel) - 1ull);
-                if (lane == 0u) {
-                    if (clr) bits64_clear(lpath, s0 + a, clr);
-                    if (tb) bits64_or(lpath, s0 + a, tb);
-                }
-                if (En == 0xFFFFFFFFu) {  // joined a speculative walk that reached a rune with no piece
-                    bad = true;
-                    break;
-                }
-                E = En;
+            uint32_t ent = 0xFFFFFFFFu;  // lane t: segment b0 + t
+            while (E < top) {
+                const uint32_t seg = E / kSeg, lim = min(seg * kSeg + kSeg, n);
+                const uint32_t c = s_c[E - base];
+                ent = lane == seg - b0 ? ((E - seg * kSeg) | (single << 8)) : ent;
+                single = c == 0xFFu;
+                E = lim + (single ? 0u : c);
             }
+            if (b0 + lane < nsg) lent[sb + b0 + lane] = ent;
             __syncthreads();
         }
-        if (lane == 0u) {
-            lflag[bi] = bad ? 0u : 1u;
-            if (bad) atomicOr(counters + CNT_ERR, 1u);
-        }
+        if (lane == 0u) lflag[bi] = 1u;
     }
 }
 
@@ -2326,48 +2314,52 @@ __device__ void long_viterbi(const uint8_t* __restrict__ text, const DevImage& i
     }
 }
 
-// k_long_tail: one lane per segment of a long block whose path k_long_path
-// marked in `lpath` (the lane owns the pieces and runs that START there).
+// k_long_tail: one lane per segment of a long block, from the entry
+// k_long_path found: the pieces that start in the segment become tokens, and
+// every run of one-rune pieces that starts there gets its Viterbi (+ cutHMM);
+// a run that entered from the previous segment belongs to that segment's lane.
 template <bool HMM>
 __global__ __launch_bounds__(256) void k_long_tail(const uint8_t* __restrict__ text, DevImage im,
                                                    const uint8_t* __restrict__ gbl, const uint2* __restrict__ longblk,
                                                    const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ lflag,
-                                                   uint32_t* __restrict__ counters, const uint32_t* __restrict__ lpath,
+                                                   uint32_t* __restrict__ counters, const uint32_t* __restrict__ lent,
                                                    uint8_t* __restrict__ bp, uint32_t* __restrict__ sbits,
                                                    uint32_t* __restrict__ ebits) {
     const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG];
     Emitter em(sbits, ebits);
+    bool bad = false;
     for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < nseg; g += gridDim.x * blockDim.x) {
         const uint32_t bi = long_block_of(lsegb, nlong, g);
-        if (lflag[bi] != 1u) continue;  // cut by the one-lane path, or the reference panics
+        if (lflag[bi] != 1u) continue;  // cut by the one-lane path
+        const uint32_t ent = lent[g];
+        if (ent == 0xFFFFFFFFu) continue;  // no piece starts here
         const uint2 bb = longblk[bi];
         const uint32_t bs = bb.x, n = (bb.y - bb.x) / 3u, s0 = bs / 3u;
-        auto start = [&](uint32_t j) { return ((lpath[(s0 + j) >> 5] >> ((s0 + j) & 31u)) & 1u) != 0u; };
         auto len = [&](uint32_t j) { return (uint32_t)gbl[s0 + j]; };
         const uint32_t c0 = (g - lsegb[bi]) * kSeg, c1 = min(n, c0 + kSeg);
-        uint32_t q = c0;
-        // a run that began before c0 belongs to the lane that owns its start
-        if (HMM && q > 0u && start(q - 1u) && len(q - 1u) == 1u)
-            while (q < n && start(q) && len(q) == 1u) q++;
+        uint32_t q = c0 + (ent & 0xFFu);
+        if (HMM && (ent >> 8))  // a run of one-rune pieces enters: its owner cuts it
+            while (q < n && len(q) == 1u) q++;
         while (q < c1) {
-            if (!start(q)) {
-                q++;
-                continue;
-            }
             const uint32_t Ln = len(q);
+            if (Ln == 0u) {  // tail index -1: cutDAG's slice panics in the reference
+                bad = true;
+                break;
+            }
             if (!HMM || Ln > 1u) {
                 em.token(bs + 3u * q, bs + 3u * (q + Ln));
                 q += Ln;
                 continue;
             }
             uint32_t r = q + 1u;
-            while (r < n && start(r) && len(r) == 1u) r++;
+            while (r < n && len(r) == 1u) r++;
             if (r - q == 1u) em.token(bs + 3u * q, bs + 3u * r);  // a single rune is always "S" (:672-674)
             else long_viterbi(text, im, bs, s0, q, r, bp, em);
             q = r;
         }
     }
     em.flush();
+    if (bad) atomicOr(counters + CNT_ERR, 1u);
     uint32_t t = em.ties;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) t += (uint32_t)__shfl_xor((int)t, d, 64);
@@ -2644,23 +2636,23 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         if (hmm)
             JB_TIMED(K_LONG_DP, hipLaunchKernelGGL((k_long_dp<true>), dim3(kLongGrid), dim3(256), 0, stream, d_text, im,
                                                    w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters, w.sbits,
-                                                   w.ebits, w.lpath, w.lflag));
+                                                   w.ebits, w.lflag, w.dbg));
         else
             JB_TIMED(K_LONG_DP, hipLaunchKernelGGL((k_long_dp<false>), dim3(kLongGrid), dim3(256), 0, stream, d_text, im,
                                                    w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters, w.sbits,
-                                                   w.ebits, w.lpath, w.lflag));
+                                                   w.ebits, w.lflag, w.dbg));
         JB_TIMED(K_LONG_SEG, hipLaunchKernelGGL(k_long_seg, dim3(gseg), dim3(256), 0, stream, d_text, im,
                                                 w.erec + kErecPad, w.longblk, w.lsegb, w.counters, w.lflag, w.gbest,
-                                                w.gbl, w.lpath, w.lseg));
+                                                w.gbl, w.lbp));
         JB_TIMED(K_LONG_PATH, hipLaunchKernelGGL(k_long_path, dim3(kLongGrid), dim3(64), 0, stream, w.longblk, w.lsegb,
-                                                 w.counters, w.lflag, w.gbl, w.lseg, w.lpath));
+                                                 w.counters, w.lflag, w.lbp, w.lent));
         if (hmm)
             JB_TIMED(K_LONG_TAIL, hipLaunchKernelGGL((k_long_tail<true>), dim3(gseg), dim3(256), 0, stream, d_text, im,
-                                                     w.gbl, w.longblk, w.lsegb, w.lflag, w.counters, w.lpath, w.lbp,
+                                                     w.gbl, w.longblk, w.lsegb, w.lflag, w.counters, w.lent, w.lbp,
                                                      w.sbits, w.ebits));
         else
             JB_TIMED(K_LONG_TAIL, hipLaunchKernelGGL((k_long_tail<false>), dim3(gseg), dim3(256), 0, stream, d_text, im,
-                                                     w.gbl, w.longblk, w.lsegb, w.lflag, w.counters, w.lpath, w.lbp,
+                                                     w.gbl, w.longblk, w.lsegb, w.lflag, w.counters, w.lent, w.lbp,
                                                      w.sbits, w.ebits));
     }
     JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3(grid_nz), dim3(256), 0, stream, d_text, w.blk, w.alnum16,
