@@ -67,6 +67,15 @@ typedef struct {
     size_t emit_len;
     int device;              /* first HIP device ordinal */
     int ndevices;            /* >= 1: documents are sharded over devices device..device+ndevices-1 */
+    /* Optional caller-computed logarithms: log_vals[i] is the caller's
+     * math.Log(float64(log_keys[i])).  calcDagProba's weights math.Log(tf) - math.Log(pd.size)
+     * (tokenizer.go:503,515-519) use these values for the frequencies and the size they
+     * cover, and the library's restatement of Go's math.Log (jb_go_log) for the rest, so a
+     * Go caller that passes math.Log results gets the reference's weights by construction.
+     * The keys a dictionary needs are listed by jb_image_log_keys.  nlog = 0: none. */
+    const int64_t *log_keys;
+    const double *log_vals;
+    size_t nlog;
 } jb_config;
 
 typedef struct {
@@ -126,6 +135,14 @@ int jb_shard_bounds(const uint64_t *doc_off, uint32_t ndocs, uint32_t nparts, ui
  * :376 + :581).  freq < 1 takes suggestFreq's value (tokenizer.go:589-614). */
 int jb_add_word(jb_ctx *ctx, const char *word, size_t len, int64_t freq);
 
+/* suggestFreq (tokenizer.go:589-614): the frequency AddWord(word, freq < 1) would store. */
+int jb_suggest_freq(jb_ctx *ctx, const char *word, size_t len, int64_t *freq);
+
+/* Add caller-computed logarithms (as jb_config.log_keys/log_vals) to ctx's table: they
+ * apply from the next image build, i.e. the next jb_add_word.  A Go AddWord passes
+ * math.Log of the new frequency and of the new pd.size before calling jb_add_word. */
+int jb_add_log(jb_ctx *ctx, const int64_t *keys, const double *vals, size_t n);
+
 /* Dictionary introspection (prefixDictionary.termFreq / size, tokenizer.go:382-383). */
 int jb_dict_get(jb_ctx *ctx, const char *word, size_t len, int64_t *freq); /* 1 found, 0 absent */
 int64_t jb_dict_size(jb_ctx *ctx);
@@ -169,6 +186,11 @@ int jb_image_stats(const jb_image *img, uint64_t *nodes, uint64_t *cap, uint32_t
                    int64_t *size, double *w_absent);
 /* emitP[state][string(rune)] as the device sees it (minFloat if absent). */
 double jb_image_emit(const jb_image *img, int state, uint32_t rune);
+/* The x whose math.Log(float64(x)) the image's weights use (every frequency of a key a
+ * Han run can spell, 1 for absent pieces, and pd.size), ascending and distinct: what a
+ * caller fills jb_config.log_keys with.  *n receives the count; returns JB_ELIMIT when
+ * it exceeds cap (keys may be NULL with cap 0 to ask for the count). */
+int jb_image_log_keys(const jb_image *img, int64_t *keys, size_t cap, size_t *n);
 /* Go math.Log as used for the weights (src/math/log.go algorithm). */
 double jb_go_log(double x);
 

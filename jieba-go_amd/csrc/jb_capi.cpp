@@ -276,13 +276,16 @@ extern "C" int jb_image_build(const jb_config* cfg, jb_image** out) {
         dl = dbuf.size();
     }
     if (!d && dl) return fail(JB_EINVAL, "no dictionary given");
+    if (cfg->nlog && (!cfg->log_keys || !cfg->log_vals)) return fail(JB_EINVAL, "nlog > 0 without log_keys/log_vals");
     auto im = std::make_unique<jb_image>();
     im->dict_kind = kind;
+    for (size_t i = 0; i < cfg->nlog; i++) im->dict.log_of[cfg->log_keys[i]] = cfg->log_vals[i];
     std::string err;
     if (kind == JB_DICT_IMAGE) {
         if ((rc = load_image(d ? d : "", dl, &im->dict, &im->emit, &im->img, &err))) return fail(rc, "%s", err.c_str());
-        if (cfg->size_override > 0 && cfg->size_override != im->dict.size) {
-            im->dict.size = cfg->size_override;
+        for (size_t i = 0; i < cfg->nlog; i++) im->dict.log_of[cfg->log_keys[i]] = cfg->log_vals[i];
+        if ((cfg->size_override > 0 && cfg->size_override != im->dict.size) || cfg->nlog) {  // reweigh
+            if (cfg->size_override > 0) im->dict.size = cfg->size_override;
             if ((rc = build_image(im->dict, im->emit, &im->img, &err))) return fail(rc, "%s", err.c_str());
         }
         *out = im.release();
@@ -380,6 +383,15 @@ extern "C" double jb_image_emit(const jb_image* img, int state, uint32_t rune) {
     if (!img || state < 0 || state > 3 || rune >= 0x110000u) return JB_MIN_FLOAT;
     const Image& m = img->img;
     return m.emit[(size_t)jb_row(m.pagemap.data(), rune) * 4 + state];
+}
+
+extern "C" int jb_image_log_keys(const jb_image* img, int64_t* keys, size_t cap, size_t* n) {
+    if (!img || !n || (cap && !keys)) return fail(JB_EINVAL, "jb_image_log_keys: null argument");
+    const std::vector<int64_t> k = weight_log_keys(img->dict);
+    *n = k.size();
+    if (k.size() > cap) return cap ? fail(JB_ELIMIT, "%zu log keys do not fit %zu", k.size(), cap) : JB_ELIMIT;
+    std::copy(k.begin(), k.end(), keys);
+    return JB_OK;
 }
 
 extern "C" double jb_go_log(double x) { return go_log(x); }
@@ -1068,6 +1080,19 @@ static int suggest_freq(jb_ctx* ctx, const char* word, size_t len, int64_t* out)
     auto it = dict.term_freq.find(std::string(word, len));
     if (it != dict.term_freq.end()) b = it->second;
     *out = a > b ? a : b;
+    return JB_OK;
+}
+
+extern "C" int jb_suggest_freq(jb_ctx* ctx, const char* word, size_t len, int64_t* freq) {
+    if (!ctx || !freq || (!word && len)) return fail(JB_EINVAL, "jb_suggest_freq: null argument");
+    std::shared_lock<std::shared_mutex> rl(ctx->lock);
+    return suggest_freq(ctx, word ? word : "", len, freq);
+}
+
+extern "C" int jb_add_log(jb_ctx* ctx, const int64_t* keys, const double* vals, size_t n) {
+    if (!ctx || (n && (!keys || !vals))) return fail(JB_EINVAL, "jb_add_log: null argument");
+    std::unique_lock<std::shared_mutex> wl(ctx->lock);
+    for (size_t i = 0; i < n; i++) ctx->im->dict.log_of[keys[i]] = vals[i];
     return JB_OK;
 }
 

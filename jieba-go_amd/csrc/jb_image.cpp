@@ -449,10 +449,32 @@ int parse_emission(const char* buf, size_t len, Emission* out, std::string* err)
 // ---------------------------------------------------------------------------
 static uint32_t freq_class(int64_t f) { return f > 0 ? JB_FC_POS : (f == 0 ? JB_FC_ZERO : JB_FC_NEG); }
 
+double dict_log(const Dictionary& d, int64_t x) {
+    if (!d.log_of.empty()) {
+        auto it = d.log_of.find(x);
+        if (it != d.log_of.end()) return it->second;
+    }
+    return go_log((double)x);
+}
+
+std::vector<int64_t> weight_log_keys(const Dictionary& d) {
+    std::vector<int64_t> out{1, d.size};
+    std::vector<uint32_t> runes;
+    for (const auto& kv : d.term_freq) {  // the keys build_image keeps
+        if (!valid_runes(kv.first, &runes) || runes.empty()) continue;
+        bool han = true;
+        for (uint32_t r : runes) han = han && jb_is_han(r);
+        if (han) out.push_back(kv.second);
+    }
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+    return out;
+}
+
 int build_image(const Dictionary& d, const Emission& e, Image* img, std::string* err) {
     img->size = d.size;
-    img->total = go_log((double)d.size);       // calcDagProba: total := math.Log(float64(pd.size))
-    img->w_absent = go_log(1.0) - img->total;  // tf := 1.0 when the piece is absent (tokenizer.go:515)
+    img->total = dict_log(d, d.size);         // calcDagProba: total := math.Log(float64(pd.size))
+    img->w_absent = dict_log(d, 1) - img->total;  // tf := 1.0 when the piece is absent (tokenizer.go:515)
 
     // Keys a walk can spell: valid UTF-8, every rune Han.
     struct Key { std::vector<uint32_t> r; int64_t f; };
@@ -495,7 +517,7 @@ int build_image(const Dictionary& d, const Emission& e, Image* img, std::string*
     img->wtab.assign(1, img->w_absent);
     std::unordered_map<uint64_t, uint32_t> widx_of;
     auto wbits = [&](int64_t f) -> uint64_t {
-        const double w = go_log((double)f) - img->total;
+        const double w = dict_log(d, f) - img->total;
         uint64_t bits;
         memcpy(&bits, &w, 8);
         return bits;

@@ -16,7 +16,16 @@ namespace jb {
 struct Dictionary {
     std::unordered_map<std::string, int64_t> term_freq;
     int64_t size = 0;
+    // Caller-supplied math.Log(float64(x)) values (jb_config.log_keys/log_vals,
+    // jb_add_log): the weights use them instead of go_log for these x.
+    std::unordered_map<int64_t, double> log_of;
 };
+
+// math.Log(float64(x)) for the weights (tokenizer.go:503,515-519): the caller's
+// value when it gave one for x, else the restatement go_log.
+double dict_log(const Dictionary& d, int64_t x);
+// The x whose logarithm build_image takes: frequencies of Han-spellable keys, 1, size.
+std::vector<int64_t> weight_log_keys(const Dictionary& d);
 
 // emitP (tokenizer.go:619) restricted to the 4 states the Viterbi reads:
 // single-rune keys only (viterbi looks up string(rune), tokenizer.go:689,708).

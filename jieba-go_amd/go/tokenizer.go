@@ -17,6 +17,7 @@ import "C"
 import (
 	"errors"
 	"log"
+	"math"
 	"runtime"
 	"sync"
 	"unsafe"
@@ -46,6 +47,27 @@ func open(dictPath, emitPath string, kind C.int, size int64) *Tokenizer {
 	cfg.size_override = C.int64_t(size)
 	cfg.device = 0
 	cfg.ndevices = 1
+	// calcDagProba's weights are math.Log(tf) - math.Log(pd.size) (tokenizer.go:503,
+	// 515-519): list the values the dictionary needs, take Go's own math.Log of
+	// each and hand the table to the library, so the weights are Go's bit for bit.
+	var img *C.jb_image
+	if rc := C.jb_image_build(&cfg, &img); rc != C.JB_OK {
+		log.Fatal("jiebahip: ", lastError())
+	}
+	var n C.size_t
+	C.jb_image_log_keys(img, nil, 0, &n)
+	keys := make([]int64, int(n)+1)
+	vals := make([]float64, int(n)+1)
+	if rc := C.jb_image_log_keys(img, (*C.int64_t)(unsafe.Pointer(&keys[0])), n, &n); rc != C.JB_OK {
+		log.Fatal("jiebahip: ", lastError())
+	}
+	C.jb_image_free(img)
+	for i := 0; i < int(n); i++ {
+		vals[i] = math.Log(float64(keys[i]))
+	}
+	cfg.log_keys = (*C.int64_t)(unsafe.Pointer(&keys[0]))
+	cfg.log_vals = (*C.double)(unsafe.Pointer(&vals[0]))
+	cfg.nlog = n
 	var ctx *C.jb_ctx
 	if rc := C.jb_open(&cfg, &ctx); rc != C.JB_OK {
 		// the reference stops the process on load errors (tokenizer.go:397,443,656)
@@ -181,7 +203,19 @@ func (t *Tokenizer) AddWord(word string, freq int) {
 	defer t.mu.Unlock()
 	cw := C.CString(word)
 	defer C.free(unsafe.Pointer(cw))
-	if rc := C.jb_add_word(t.ctx, cw, C.size_t(len(word)), C.int64_t(freq)); rc != C.JB_OK {
+	f := C.int64_t(freq)
+	if freq < 1 {
+		if rc := C.jb_suggest_freq(t.ctx, cw, C.size_t(len(word)), &f); rc != C.JB_OK {
+			log.Fatal("jiebahip: ", lastError())
+		}
+	}
+	// Go's math.Log of the new frequency and of the new pd.size for the rebuild
+	// (addTerm adds freq to pd.size even when the word was present, tokenizer.go:580-585)
+	size := int64(C.jb_dict_size(t.ctx))
+	keys := []int64{int64(f), size + int64(f)}
+	vals := []float64{math.Log(float64(keys[0])), math.Log(float64(keys[1]))}
+	C.jb_add_log(t.ctx, (*C.int64_t)(unsafe.Pointer(&keys[0])), (*C.double)(unsafe.Pointer(&vals[0])), 2)
+	if rc := C.jb_add_word(t.ctx, cw, C.size_t(len(word)), f); rc != C.JB_OK {
 		log.Fatal("jiebahip: ", lastError())
 	}
 }

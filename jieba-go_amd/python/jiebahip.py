@@ -30,6 +30,7 @@ EXPORTS = [
     "jb_add_word", "jb_dict_get", "jb_dict_size", "jb_save", "jb_profile_enable", "jb_profile_read",
     "jb_profile_reset", "jb_image_build", "jb_image_free", "jb_image_save", "jb_image_dict_info", "jb_image_lookup",
     "jb_image_stats", "jb_image_emit", "jb_go_log", "jb_shard_bounds", "jb_last_stats",
+    "jb_suggest_freq", "jb_add_log", "jb_image_log_keys",
 ]
 
 
@@ -44,6 +45,7 @@ class jb_config(C.Structure):
         ("dict_path", C.c_char_p), ("dict_buf", C.c_char_p), ("dict_len", C.c_size_t), ("dict_kind", C.c_int),
         ("size_override", C.c_int64), ("emit_path", C.c_char_p), ("emit_buf", C.c_char_p), ("emit_len", C.c_size_t),
         ("device", C.c_int), ("ndevices", C.c_int),
+        ("log_keys", C.POINTER(C.c_int64)), ("log_vals", C.POINTER(C.c_double)), ("nlog", C.c_size_t),
     ]
 
 
@@ -113,6 +115,9 @@ def lib():
         L.jb_go_log.argtypes = [C.c_double]
         L.jb_go_log.restype = C.c_double
         L.jb_shard_bounds.argtypes = [vp, C.c_uint32, C.c_uint32, vp]
+        L.jb_image_log_keys.argtypes = [vp, vp, C.c_size_t, C.POINTER(C.c_size_t)]
+        L.jb_suggest_freq.argtypes = [vp, cp, C.c_size_t, C.POINTER(C.c_int64)]
+        L.jb_add_log.argtypes = [vp, vp, vp, C.c_size_t]
         L.jb_last_stats.argtypes = [vp, C.POINTER(jb_stats)]
         _lib = L
     return _lib
@@ -129,9 +134,17 @@ def _b(s):
 
 
 def make_config(dict_path=None, emit_path=None, dict_bytes=None, emit_bytes=None, kind=JB_DICT_TXT,
-                size_override=0, device=0, ndevices=1):
+                size_override=0, device=0, ndevices=1, logs=None):
+    """logs: optional {x: math.Log(float64(x))} the caller computed (jb_config.log_keys/log_vals)."""
     cfg = jb_config()
     keep = []
+    if logs:
+        ks = np.ascontiguousarray(list(logs.keys()), np.int64)
+        vs = np.ascontiguousarray([logs[k] for k in logs.keys()], np.float64)
+        keep += [ks, vs]
+        cfg.log_keys = ks.ctypes.data_as(C.POINTER(C.c_int64))
+        cfg.log_vals = vs.ctypes.data_as(C.POINTER(C.c_double))
+        cfg.nlog = len(ks)
     if dict_path is not None:
         cfg.dict_path = os.fsencode(dict_path)
     else:
@@ -203,6 +216,14 @@ class Image:
 
     def save(self, path):
         _check(lib().jb_image_save(self.h, os.fsencode(path)))
+
+    def log_keys(self):
+        """jb_image_log_keys: the x whose math.Log the weights use."""
+        n = C.c_size_t()
+        lib().jb_image_log_keys(self.h, None, 0, C.byref(n))
+        out = np.zeros(max(n.value, 1), np.int64)
+        _check(lib().jb_image_log_keys(self.h, out.ctypes.data, n.value, C.byref(n)))
+        return out[:n.value]
 
     def dict_info(self):
         n, sz = C.c_uint64(), C.c_int64()
@@ -334,6 +355,19 @@ class Tokenizer:
         """Tokenizer.AddWord (tokenizer.go:372) without the reference's deadlock."""
         w = _b(word)
         _check(lib().jb_add_word(self.h, w, len(w), freq))
+
+    def suggest_freq(self, word):
+        """suggestFreq (tokenizer.go:589-614)."""
+        w = _b(word)
+        f = C.c_int64()
+        _check(lib().jb_suggest_freq(self.h, w, len(w), C.byref(f)))
+        return f.value
+
+    def add_log(self, logs):
+        """jb_add_log: caller-computed {x: math.Log(float64(x))} for the next image build."""
+        ks = np.ascontiguousarray(list(logs.keys()), np.int64)
+        vs = np.ascontiguousarray([logs[k] for k in logs.keys()], np.float64)
+        _check(lib().jb_add_log(self.h, ks.ctypes.data, vs.ctypes.data, len(ks)))
 
     def dict_get(self, word):
         w = _b(word)

@@ -479,3 +479,133 @@ def test_viterbi_ties_counted(tmp_path):
         if len(t) > 4000:
             assert st["long_blocks"] == 1
         tk.close()
+
+
+from conftest import ROOT, real_data_dir  # noqa: E402
+
+SENTENCE = "我昨天去上海交通大學與老師討論量子力學"  # tokenizer_test.go:531
+
+
+def _spans_line(line):
+    parts = line.split()
+    n = int(parts[1])
+    v = list(map(int, parts[2:]))
+    assert len(v) == 2 * n
+    return v[0::2], v[1::2]
+
+
+def test_c_abi_smoke_program(syn_small, tmp_path):
+    """A C99 program bound to include/jiebahip.h (what cgo sees): open, Cut, a batch,
+    a batch into caller arrays, AddWord with suggestFreq, Cut again — every span
+    against the oracle."""
+    import subprocess
+    dp, ep, s = syn_small
+    exe = str(tmp_path / "c_abi_smoke")
+    lib = os.path.join(ROOT, "jieba-go_amd", "lib")
+    subprocess.check_call(["gcc", "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror", "-I",
+                           os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "c_abi_smoke.c"), "-L", lib,
+                           "-ljiebahip", "-Wl,-rpath," + lib, "-o", exe])
+    buf, off, _ = s.corpus(synth.KIND_DOCS, 3, target_bytes=20_000)
+    text = SENTENCE.encode() + b" abc 12 " + bytes(buf[:int(off[1])]) + "㐀㐁一二".encode()
+    tf = tmp_path / "text.txt"
+    tf.write_bytes(text)
+    word = "量子力學"
+    r = subprocess.run([exe, dp, ep, str(tf), word], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = {ln.split()[0]: ln for ln in r.stdout.splitlines()}
+    o = O.Oracle.from_files(dp, ep, 0)
+    s1, e1 = o.cut_spans(text, True)
+    assert _spans_line(out["cut"]) == (s1.tolist(), e1.tolist())
+    n = len(text)
+    both = np.frombuffer(text + text + b"\0" * 16, np.uint8)
+    off2 = np.array([0, n, 2 * n], np.uint64)
+    bs, be, bd = o.cut_batch(both, off2, False)
+    assert _spans_line(out["batch"]) == (bs.tolist(), be.tolist())
+    assert list(map(int, out["doc_tok"].split()[1:])) == bd.tolist()
+    hs, he, _ = o.cut_batch(both, off2, True)
+    assert _spans_line(out["into"]) == (hs.tolist(), he.tolist())
+    freq = int(out["freq"].split()[1])
+    o.add_term(word, freq)
+    assert int(out["freq"].split()[3]) == o.size
+    s2, e2 = o.cut_spans(text, True)
+    assert _spans_line(out["cut2"]) == (s2.tolist(), e2.tolist())
+
+
+def test_cpp_tokenizer_mirror(syn_small, tmp_path):
+    """The C++ mirror of the Go Tokenizer API (libjbtok.so): NewTokenizer, Cut,
+    CutParallel, CutBatch, AddWord, Save/FromImage — tokens against the oracle."""
+    import subprocess
+    dp, ep, s = syn_small
+    exe = str(tmp_path / "cpp_tok_smoke")
+    lib = os.path.join(ROOT, "jieba-go_amd", "lib")
+    subprocess.check_call(["g++", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+                           "-I", os.path.join(ROOT, "jieba-go_amd", "host"),
+                           os.path.join(ROOT, "tests", "cpp_tok_smoke.cpp"), "-L", lib, "-ljbtok", "-ljiebahip",
+                           "-Wl,-rpath," + lib, "-o", exe])
+    buf, off, _ = s.corpus(synth.KIND_DOCS, 5, target_bytes=8_000)
+    text = (SENTENCE + " x1 ").encode() + bytes(buf[:int(off[1])])
+    tf = tmp_path / "text.txt"
+    tf.write_bytes(text)
+    word = "交通大學與"
+    r = subprocess.run([exe, dp, str(tf), word, str(tmp_path / "img.jbi")], capture_output=True, timeout=120,
+                       cwd=os.path.dirname(ep))
+    assert r.returncode == 0, r.stderr
+    got = {}
+    for ln in r.stdout.decode("utf-8").splitlines():
+        tag, *toks = ln.split("|")
+        got.setdefault(tag, []).append(toks)
+    o = O.Oracle.from_files(dp, ep, 0)
+    t = text.decode("utf-8")
+    assert got["cut_hmm"][0] == o.cut(t, True)
+    assert got["cut_nohmm"][0] == o.cut(t, False)
+    assert got["cut_parallel"][0] == o.cut(t, True)
+    assert got["batch_doc"] == [o.cut(t, True), [], o.cut(t, True)]
+    tk = J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep))
+    f = tk.suggest_freq(word)
+    tk.close()
+    o.add_term(word, f)
+    assert got["cut_added"][0] == o.cut(t, True)
+    assert got["cut_image"][0] == o.cut(t, True)
+
+
+def test_caller_log_table_gpu(syn_small):
+    """Identity jb_config log table (math.Log values for every key the image uses)
+    keeps bit parity on the GPU; a perturbed table reopens and cuts (CPU tests pin
+    its weights)."""
+    dp, ep, s = syn_small
+    img = J.Image(J.make_config(dict_path=dp, emit_path=ep))
+    keys = [int(x) for x in img.log_keys()]
+    img.close()
+    logs = {k: J.go_log(k) for k in keys}
+    tk = J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep, logs=logs))
+    o = O.Oracle.from_files(dp, ep, 0)
+    buf, off, _ = s.corpus(synth.KIND_DOCS, 11, target_bytes=1 << 20)
+    for hmm in (False, True):
+        _cmp_batch(tk, o, buf, off, hmm, "identity log table")
+    # AddWord with caller logs for the new frequency and size
+    w = "量子力學"
+    f = 77
+    tk.add_log({f: J.go_log(f), tk.size + f: J.go_log(tk.size + f)})
+    tk.AddWord(w, f)
+    o.add_term(w, f)
+    _cmp_batch(tk, o, buf, off, True, "identity log table after AddWord")
+    tk.close()
+
+
+@pytest.mark.skipif(real_data_dir() is None, reason="real jieba data (LFS objects) not present; set JIEBA_DATA_DIR")
+def test_gpu_real_data_kats(kats):
+    """TestCut "cut 1..10" (tokenizer_test.go:28-59) through the HIP path on the
+    genuine dictionary and emission table (sha256-checked), both as
+    NewJiebaTokenizer's map (dict.txt with prefix semantics, size 60,101,967) and,
+    when present, prefix_dictionary.gob itself."""
+    d = real_data_dir()
+    ep = os.path.join(d, "prob_emit.json")
+    tks = [J.Tokenizer(J.make_config(dict_path=os.path.join(d, "dict.txt"), emit_path=ep, kind=J.JB_DICT_PREFIX,
+                                     size_override=J.JIEBA_SIZE))]
+    gp = os.path.join(d, "prefix_dictionary.gob")
+    if os.path.exists(gp):
+        tks.append(J.Tokenizer(J.make_config(dict_path=gp, emit_path=ep, kind=J.JB_DICT_GOB)))
+    for tk in tks:
+        for c in kats["cut_real_data"]["cases"]:
+            assert tk.Cut(c["text"], c["hmm"]) == c["want"], c["name"]
+        tk.close()

@@ -143,3 +143,66 @@ def test_open_without_gpu_fails_loudly(syn_small):
     with pytest.raises(J.JbError) as ei:
         J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep))
     assert ei.value.code == J.JB_EDEVICE
+
+
+def test_caller_log_table(syn_small):
+    """jb_config.log_keys/log_vals: the weights use the caller's
+    math.Log values.  An identity table (the library's own restatement) changes
+    nothing; a perturbed one moves exactly the weights of the keys it covers."""
+    dp, ep, s = syn_small
+    base = J.Image(J.make_config(dict_path=dp, emit_path=ep))
+    keys = [int(x) for x in base.log_keys()]
+    size = base.stats()["size"]
+    assert keys == sorted(set(keys)) and 1 in keys and size in keys
+    ident = J.Image(J.make_config(dict_path=dp, emit_path=ep, logs={k: J.go_log(k) for k in keys}))
+    o = O.Oracle.from_files(dp, ep, 0)
+    items = o.items()
+    words = [k for k in sorted(items) if base.lookup(k) is not None][:3000]
+    assert len(words) > 1000
+    for w in words:
+        assert _bits(base.lookup(w)[1]) == _bits(ident.lookup(w)[1]), w
+    # perturb one frequency's log by one ulp and pd.size's log by another
+    f0 = items[words[7]]
+    bump = {f0: math.nextafter(J.go_log(f0), math.inf), size: math.nextafter(J.go_log(size), -math.inf)}
+    pert = J.Image(J.make_config(dict_path=dp, emit_path=ep, logs=bump))
+    tot = bump[size]
+    assert _bits(pert.stats()["w_absent"]) == _bits(J.go_log(1.0) - tot)
+    for w in words:
+        f = items[w]
+        want = (bump[f] if f in bump else J.go_log(f)) - tot
+        assert _bits(pert.lookup(w)[1]) == _bits(want), w
+    with pytest.raises(J.JbError):
+        cfg = J.make_config(dict_path=dp, emit_path=ep)
+        cfg.nlog = 3  # no arrays
+        J.Image(cfg)
+
+
+def test_c_abi_consumer_compiles_as_c99(tmp_path):
+    """tests/c_abi_smoke.c — what a cgo preamble sees — compiles as strict C99
+    against include/jiebahip.h and links against libjiebahip.so."""
+    import subprocess
+    exe = str(tmp_path / "c_abi_smoke")
+    subprocess.check_call(["gcc", "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror",
+                           "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "c_abi_smoke.c"),
+                           "-L", os.path.join(ROOT, "jieba-go_amd", "lib"), "-ljiebahip",
+                           "-Wl,-rpath," + os.path.join(ROOT, "jieba-go_amd", "lib"), "-o", exe])
+    # without a GPU it must fail loudly at jb_open (exit 2), never fall back to the CPU
+    import torch
+    if not torch.cuda.is_available():
+        r = subprocess.run([exe, "--expect-no-device"], capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_cpp_tokenizer_mirror_compiles(tmp_path):
+    """The C++ mirror (libjbtok.so, host/tokenizer.hpp) builds a consumer program."""
+    import subprocess
+    exe = str(tmp_path / "cpp_tok_smoke")
+    lib = os.path.join(ROOT, "jieba-go_amd", "lib")
+    subprocess.check_call(["g++", "-std=c++17", "-Wall", "-Wextra", "-Werror",
+                           "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "jieba-go_amd", "host"),
+                           os.path.join(ROOT, "tests", "cpp_tok_smoke.cpp"),
+                           "-L", lib, "-ljbtok", "-ljiebahip", "-Wl,-rpath," + lib, "-o", exe])
+    import torch
+    if not torch.cuda.is_available():
+        r = subprocess.run([exe, "--expect-no-device"], capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout + r.stderr
