@@ -539,9 +539,6 @@ static int ensure_span_staging(Device* d, uint64_t ntok) {
     return JB_OK;
 }
 
-#ifndef JB_NZ_PER_CU
-#define JB_NZ_PER_CU 8  // k_nonzh workgroups per CU (persistent grid; 4: 0.075 ms, 8: 0.058)
-#endif
 static int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
     return v && *v ? atoi(v) : dflt;
@@ -556,7 +553,6 @@ static int env_int(const char* name, int dflt) {
 static int init_launch_cfg(Device* d) {
     LaunchCfg& lc = d->lc;
     lc.grid_zh = d->ncu * std::max(zh_blocks_per_cu(true), zh_blocks_per_cu(false));
-    lc.grid_nz = d->ncu * std::max(1u, std::min((uint32_t)JB_NZ_PER_CU, nonzh_blocks_per_cu()));
     const int gz = env_int("JB_GRID_ZH", 0);
     if (gz > 0) lc.grid_zh = (uint32_t)gz;
     const int grp = env_int("JB_ZH_GROUP", 0);
@@ -577,8 +573,8 @@ static int launch(Device* d, const uint8_t* d_text, uint64_t nbytes, const uint6
     static const bool dbg = getenv("JB_DEBUG") != nullptr;
     const LaunchCfg& lc = d->lc;
     if (dbg)
-        fprintf(stderr, "[jb] nbytes=%llu ndocs=%u grid_zh=%u grid_nz=%u zh_group=%u\n", (unsigned long long)nbytes,
-                ndocs, lc.grid_zh, lc.grid_nz, lc.zh_group ? lc.zh_group : zh_group_for(nbytes));
+        fprintf(stderr, "[jb] nbytes=%llu ndocs=%u grid_zh=%u zh_group=%u\n", (unsigned long long)nbytes,
+                ndocs, lc.grid_zh, lc.zh_group ? lc.zh_group : zh_group_for(nbytes));
     static const bool use_graph = env_int("JB_GRAPH", 1) != 0;
     if (use_graph && !d->profile && lc.diag == 0 && s != nullptr) {
         const Device::GraphKey key{d_text, nbytes, d_doc_off, ndocs, hmm, d->work_gen, s};

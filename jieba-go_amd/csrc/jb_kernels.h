@@ -105,7 +105,6 @@ struct KernelTimer {
 // Launch shape of one pipeline run (fixed per device at jb_open).
 struct LaunchCfg {
     uint32_t grid_zh;   // persistent grid of k_zh
-    uint32_t grid_nz;   // persistent grid of k_nonzh
     uint32_t zh_group;  // k_zh group bytes (0: zh_group_for(nbytes))
     uint32_t diag;      // diagnostic clocks (STAMPS builds only; 0 otherwise)
 };
@@ -118,6 +117,5 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
 
 // Resident k_zh workgroups per CU (occupancy API).
 uint32_t zh_blocks_per_cu(bool hmm);
-uint32_t nonzh_blocks_per_cu();
 
 }  // namespace jb

@@ -2425,53 +2425,96 @@ __device__ void nonzh_block(const uint8_t* __restrict__ text, uint32_t bs, uint3
     if (in_run) em.token(run, be);
 }
 
-// One thread per 8 consecutive entries of the block list: the entries and the
-// lane bits under each non-Han block load in one round, and only blocks with a
-// [0-9A-Za-z] byte near them are read (the rest have no tokens, :290-293).
-#ifndef JB_NZ_PER
-#define JB_NZ_PER 8
-#endif
-constexpr uint32_t kNzPer = JB_NZ_PER;
-__global__ __launch_bounds__(256) void k_nonzh(const uint8_t* __restrict__ text, const uint32_t* __restrict__ blk,
-                                               const uint64_t* __restrict__ alnum16,
-                                               const uint32_t* __restrict__ counters, uint32_t* __restrict__ sbits,
+// Bit k set for each byte k of the 16 bytes x that is [0-9A-Za-z] (jb_is_alnum).
+__device__ __forceinline__ uint32_t alnum_mask16(uint4 x) {
+    const uint32_t v[4] = {x.x, x.y, x.z, x.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t f = (jb_bytes_between(v[j], 0x2Fu, 0x3Au) | jb_bytes_between(v[j] | 0x20202020u, 0x60u, 0x7Bu)) >> 7;
+        m |= ((f * 0x204081u) >> 21 & 0xFu) << (4 * j);  // bits 0/8/16/24 -> 0..3
+    }
+    return m;
+}
+
+// The first block start after chunk c (16 bytes each), or nbytes: the rest of c's
+// tile chunk by chunk, then whole tiles by their block counts (tile_cnt.x).
+__device__ uint32_t nz_block_end(const uint32_t* __restrict__ lanemask, const uint2* __restrict__ tile_cnt,
+                                 uint32_t ntiles, uint32_t nbytes, uint32_t c) {
+    const uint32_t nch = ntiles * 256u;
+    uint32_t k = c + 1u;
+    while (k < nch) {
+        if ((k & 255u) == 0u) {
+            uint32_t t = k >> 8;
+            while (t < ntiles && tile_cnt[t].x == 0u) t++;
+            if (t >= ntiles) break;
+            k = t * 256u;
+        }
+        const uint32_t m = lanemask[k] & 0xFFFFu;
+        if (m) return min(nbytes, k * 16u + (uint32_t)__builtin_ctz(m));
+        k++;
+    }
+    return nbytes;
+}
+
+// k_nonzh: cutNonZh (tokenizer.go:289-310) for exactly the non-Han blocks that hold
+// a [0-9A-Za-z] byte; every other non-Han block has no tokens (:290-293).  An alnum
+// byte is never Han, so it always lies in a non-Han block.  One thread per alnum16
+// word (1 KiB of text); for each 16-byte chunk with an alnum byte and each block
+// with an alnum byte there, the thread cuts the block when this chunk holds the
+// block's first alnum byte (the block starts in the chunk, or walking back from it
+// to the block start meets no alnum byte).  Block bounds come from the lane masks
+// of k_mark_walk, so the kernel touches neither the block list nor the Han blocks.
+__global__ __launch_bounds__(256) void k_nonzh(const uint8_t* __restrict__ text, uint32_t nbytes,
+                                               const uint32_t* __restrict__ lanemask,
+                                               const uint2* __restrict__ tile_cnt, uint32_t ntiles,
+                                               const uint64_t* __restrict__ alnum16, uint32_t* __restrict__ sbits,
                                                uint32_t* __restrict__ ebits) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[256][80];
-    const uint32_t nblk = counters[CNT_NBLK];
+    const uint32_t nch = (nbytes + 15u) >> 4, nw = (nch + 63u) >> 6;
     Emitter em(sbits, ebits);
-    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c * kNzPer < nblk; c += gridDim.x * blockDim.x) {
-        const uint32_t i0 = c * kNzPer;
-        uint32_t e[kNzPer + 1];
-        if (i0 + kNzPer <= nblk) {  // blk[nblk] is the end sentinel
-            const uint4 u = *reinterpret_cast<const uint4*>(blk + i0);
-            const uint4 v = *reinterpret_cast<const uint4*>(blk + i0 + 4);
-            e[0] = u.x; e[1] = u.y; e[2] = u.z; e[3] = u.w;
-            e[4] = v.x; e[5] = v.y; e[6] = v.z; e[7] = v.w;
-            e[8] = blk[i0 + kNzPer];
-        } else {
-#pragma unroll
-            for (uint32_t k = 0; k <= kNzPer; k++) e[k] = (i0 + k <= nblk) ? blk[i0 + k] : 0x80000000u;
-        }
-        uint64_t aw[kNzPer];
-#pragma unroll
-        for (uint32_t k = 0; k < kNzPer; k++) aw[k] = alnum16[(e[k] & 0x7FFFFFFFu) >> 10];
-#pragma unroll
-        for (uint32_t k = 0; k < kNzPer; k++) {
-            if ((e[k] >> 31) || i0 + k >= nblk) continue;  // a zh block
-            const uint32_t bs = e[k], be = e[k + 1] & 0x7FFFFFFFu;
-            const uint32_t llast = (be - 1u) >> 4;
-            uint32_t l = bs >> 4;
-            bool maybe = false;
-            uint64_t w = aw[k];
-            for (;;) {
-                const uint32_t lo = l & 63u, hi = min(63u, lo + (llast - l));
-                const uint64_t m = (hi == 63u ? ~0ull : ((2ull << hi) - 1ull)) & (~0ull << lo);
-                maybe = (w & m) != 0ull;
-                l += hi - lo + 1u;
-                if (maybe || l > llast) break;
-                w = alnum16[l >> 6];  // a block over more than one 1 KiB word (rare)
+    for (uint32_t wi = blockIdx.x * blockDim.x + threadIdx.x; wi < nw; wi += gridDim.x * blockDim.x) {
+        uint64_t a = alnum16[wi];
+        while (a) {
+            const uint32_t c = wi * 64u + (uint32_t)__builtin_ctzll(a);
+            a &= a - 1ull;
+            if (c >= nch) break;  // (padding past the batch)
+            const uint32_t c0 = c * 16u;
+            uint32_t A = alnum_mask16(*reinterpret_cast<const uint4*>(text + c0));
+            if (c0 + 16u > nbytes) A &= (1u << (nbytes - c0)) - 1u;
+            const uint32_t bm = lanemask[c] & 0xFFFFu;
+            while (A) {  // a block with an alnum byte in this chunk
+                const uint32_t i = (uint32_t)__builtin_ctz(A);
+                const uint32_t le = bm & ((2u << i) - 1u), after = bm & ~((2u << i) - 1u);
+                A &= after ? ~((1u << __builtin_ctz(after)) - 1u) : 0u;  // the block's bytes of this chunk
+                uint32_t bs;
+                bool own = true;
+                if (le) {
+                    bs = c0 + 31u - (uint32_t)__builtin_clz(le);
+                } else {  // the block began before this chunk: walk back to its start
+                    uint32_t k = c;
+                    bs = 0;
+                    while (k > 0u) {  // (byte 0 starts a block, so the walk ends there at the latest)
+                        --k;
+                        const uint32_t m = lanemask[k] & 0xFFFFu;
+                        const bool al = (alnum16[k >> 6] >> (k & 63u)) & 1ull;
+                        if (m) {
+                            const uint32_t o = 31u - (uint32_t)__builtin_clz(m);
+                            bs = k * 16u + o;
+                            if (al) own = (alnum_mask16(*reinterpret_cast<const uint4*>(text + k * 16u)) >> o) == 0u;
+                            break;
+                        }
+                        if (al) {
+                            own = false;
+                            break;
+                        }
+                    }
+                }
+                if (!own) continue;
+                const uint32_t be = after ? c0 + (uint32_t)__builtin_ctz(after)
+                                          : nz_block_end(lanemask, tile_cnt, ntiles, nbytes, c);
+                nonzh_block(text, bs, be, em, s_win[threadIdx.x]);
             }
-            if (maybe) nonzh_block(text, bs, be, em, s_win[threadIdx.x]);
         }
     }
     em.flush();
@@ -2579,23 +2622,19 @@ static uint32_t occ_zh() {
 
 uint32_t zh_blocks_per_cu(bool hmm) { return hmm ? occ_zh<true>() : occ_zh<false>(); }
 
-uint32_t nonzh_blocks_per_cu() {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_nonzh, 256, 0) != hipSuccess || n <= 0) return 1;
-    return (uint32_t)n;
-}
 
-#define JB_TIMED(id, stmt)                        \
+#define JB_TIMED_ON(id, st, ...)                  \
     do {                                          \
-        if (timer) timer->begin((id), stream);    \
-        stmt;                                     \
-        if (timer) timer->end((id), stream);      \
+        if (timer) timer->begin((id), (st));      \
+        __VA_ARGS__;                              \
+        if (timer) timer->end((id), (st));        \
     } while (0)
+#define JB_TIMED(id, ...) JB_TIMED_ON(id, stream, __VA_ARGS__)
 
 hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text, uint64_t nbytes,
                         const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, const LaunchCfg& lc,
                         hipStream_t stream, KernelTimer* timer) {
-    const uint32_t grid_zh = lc.grid_zh, grid_nz = lc.grid_nz, diag = lc.diag;
+    const uint32_t grid_zh = lc.grid_zh, diag = lc.diag;
     const uint64_t nwords = (nbytes + 31) / 32;
     const uint32_t ntiles = (uint32_t)((nbytes + kTileBytes - 1) / kTileBytes);
     // k_zh work unit: a small batch gets small groups, so that enough waves share it
@@ -2655,8 +2694,12 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                                      w.gbl, w.longblk, w.lsegb, w.lflag, w.counters, w.lent, w.lbp,
                                                      w.sbits, w.ebits));
     }
-    JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3(grid_nz), dim3(256), 0, stream, d_text, w.blk, w.alnum16,
-                                         w.counters, w.sbits, w.ebits));
+    {
+        const uint32_t nw = (uint32_t)((nbytes + 1023u) / 1024u);  // alnum16 words
+        JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3((nw + 255u) / 256u), dim3(256), 0, stream, d_text,
+                                             (uint32_t)nbytes, w.lanemask, w.tile_cnt, ntiles, w.alnum16, w.sbits,
+                                             w.ebits));
+    }
     JB_TIMED(K_TOK_COUNT, hipLaunchKernelGGL((k_tok<false>), dim3(nttiles), dim3(256), 0, stream, w.sbits, w.ebits,
                                              nwords, w.ttile_cnt, w.supt, w.counters, nullptr, nullptr));
     JB_TIMED(K_SCAN_TOK, hipLaunchKernelGGL(k_sup, dim3((nttiles + 255) / 256), dim3(256), 0, stream, w.ttile_cnt,

@@ -609,3 +609,35 @@ def test_gpu_real_data_kats(kats):
         for c in kats["cut_real_data"]["cases"]:
             assert tk.Cut(c["text"], c["hmm"]) == c["want"], c["name"]
         tk.close()
+
+
+def test_nonzh_blocks_across_chunks_and_tiles(small):
+    """cutNonZh (tokenizer.go:289-310) where k_nonzh's block bounds come from the
+    lane masks: alnum bytes at 16-byte chunk edges, non-Han blocks longer than a
+    4 KiB tile with their first alnum byte far from the block start, blocks with
+    no alnum at all (no tokens), several blocks in one chunk, and document
+    boundaries inside non-Han runs."""
+    tk, o, s = small
+    rng = random.Random(77)
+    pieces = ["。", "，", " ", "\t", "…", "abc", "Z9", "1", "中文", "世界", "é", "—", "!!", "x y", "　"]
+    docs = []
+    for n in range(60):
+        k = rng.choice([1, 3, 15, 16, 17, 31, 33, 200, 5000, 9000])
+        parts = []
+        while sum(len(p.encode()) for p in parts) < k:
+            parts.append(rng.choice(pieces))
+        docs.append("".join(parts))
+    # a long punctuation-only run with one alnum byte at its very end, across tiles
+    docs.append("，" * 3000 + "a")
+    docs.append("a" + "，" * 3000)
+    docs.append("。" * 2000)  # no alnum: no tokens
+    docs.append(" " * 4095 + "q" + "中" + " " * 20 + "7")
+    docs.append("x" * 10000)  # one alnum run over several tiles
+    for pad in range(0, 33):  # an alnum run starting at every offset of a chunk
+        docs.append("，" * (pad // 3) + " " * (pad % 3) + "ab12" + "字")
+    buf, off = _batch_of(docs)
+    for hmm in (False, True):
+        _cmp_batch(tk, o, buf, off, hmm, "nonzh edges")
+    # the same texts as one document (blocks spanning the former boundaries)
+    buf1, off1 = _batch_of(["".join(docs)])
+    _cmp_batch(tk, o, buf1, off1, True, "nonzh one document")
