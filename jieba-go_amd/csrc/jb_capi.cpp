@@ -132,6 +132,7 @@ struct Device {
     std::vector<hipEvent_t> ev;  // span pieces landed (host batches)
     uint32_t ncu = 0;
     LaunchCfg lc{};  // launch shape, fixed at jb_open
+    uint64_t last_nbytes = 0;  // batch size of the last pipeline run (jb_last_stats)
     EventTimer timer;
     bool profile = false;
     // replay cache: the whole pipeline captured as one HIP graph for the last
@@ -437,9 +438,9 @@ static int upload_image(Device* d, const Image& img) {
 }
 
 static void free_work(Work* w) {
-    dfree(w->docbits); dfree(w->tile_cnt); dfree(w->tile_off);
-    dfree(w->ttile_cnt); dfree(w->ttile_off); dfree(w->supb); dfree(w->supt); dfree(w->blk); dfree(w->alnum16); dfree(w->erec); dfree(w->lanemask);
-    dfree(w->gbl); dfree(w->lsegb); dfree(w->lent); dfree(w->lflag); dfree(w->lbp); dfree(w->gbest); dfree(w->gstart); dfree(w->tile4); dfree(w->longblk);
+    dfree(w->docbits); dfree(w->tile_cnt);
+    dfree(w->ttile_cnt); dfree(w->supt); dfree(w->alnum16); dfree(w->erec); dfree(w->lanemask);
+    dfree(w->gbl); dfree(w->lsegb); dfree(w->lent); dfree(w->lflag); dfree(w->lbp); dfree(w->gbest); dfree(w->tile4); dfree(w->longblk);
     dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters); dfree(w->dbg); dfree(w->dbg_walk);
     *w = Work{};
 }
@@ -463,10 +464,7 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     w.ebits = w.docbits + 2 * nwords;
     w.bits_stride = nwords;
     HIPCHK(hipMalloc(&w.tile_cnt, ntiles * sizeof(uint2)));
-    HIPCHK(hipMalloc(&w.tile_off, ntiles * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.ttile_cnt, nttiles * sizeof(uint2)));
-    HIPCHK(hipMalloc(&w.ttile_off, nttiles * sizeof(uint2)));
-    HIPCHK(hipMalloc(&w.blk, (nb + 4) * 4));
     HIPCHK(hipMalloc(&w.alnum16, (nb / 1024 + 8) * 8));
     HIPCHK(hipMalloc(&w.erec, (nb / 3 + 8 + kErecPad) * 8));
     HIPCHK(hipMalloc(&w.lanemask, ntiles * 256 * 4));
@@ -475,7 +473,6 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.lsegb, (nb / kZhLongMin + 2) * 4));
     HIPCHK(hipMalloc(&w.lent, (nb / (3 * kSeg) + nb / kZhLongMin + 4) * 4));
     HIPCHK(hipMalloc(&w.lbp, nb / 3 + 64));
-    HIPCHK(hipMalloc(&w.gstart, (nb / kZhGroupSmall + 4) * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.tile4, ntiles * 4));
     HIPCHK(hipMalloc(&w.longblk, (nb / kZhLongMin + 2) * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.gbest, (nb / 3 + 8) * sizeof(double)));
@@ -484,7 +481,6 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.tok_end, (nb + 4) * 4));
     HIPCHK(hipMalloc(&w.doc_tok, ((uint64_t)ndc + 2) * 8));
     HIPCHK(hipMalloc(&w.counters, 64 * 4));
-    HIPCHK(hipMalloc(&w.supb, (ntiles / 256 + 2) * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.supt, (nttiles / 256 + 2) * sizeof(uint2)));
     if (d->lc.diag & 0x100u) {
         HIPCHK(hipMalloc(&w.dbg, 65536 * 8 * 8));
@@ -572,6 +568,7 @@ static int launch(Device* d, const uint8_t* d_text, uint64_t nbytes, const uint6
                   bool hmm, hipStream_t s) {
     static const bool dbg = getenv("JB_DEBUG") != nullptr;
     const LaunchCfg& lc = d->lc;
+    d->last_nbytes = nbytes;
     if (dbg)
         fprintf(stderr, "[jb] nbytes=%llu ndocs=%u grid_zh=%u zh_group=%u\n", (unsigned long long)nbytes,
                 ndocs, lc.grid_zh, lc.zh_group ? lc.zh_group : zh_group_for(nbytes));
@@ -1137,8 +1134,16 @@ extern "C" int jb_last_stats(jb_ctx* ctx, jb_stats* out) {
         uint64_t ntok;
         memcpy(&ntok, c + CNT_NWORDS, 8);
         out->tokens += ntok;
-        out->blocks += c[CNT_NBLK];
-        out->zh_blocks += c[CNT_NZH];
+        // blocks: the per-tile counts k_mark_walk left in the workspace
+        const uint64_t ntiles = (d->last_nbytes + kTileBytes - 1) / kTileBytes;
+        if (ntiles) {
+            std::vector<uint2> tc(ntiles);
+            HIPCHK(hipMemcpy(tc.data(), d->w.tile_cnt, ntiles * sizeof(uint2), hipMemcpyDeviceToHost));
+            for (const uint2& t : tc) {
+                out->blocks += t.x;
+                out->zh_blocks += t.y;
+            }
+        }
         out->long_blocks += c[CNT_NLONG];
         out->viterbi_ties += c[CNT_TIES];
     }

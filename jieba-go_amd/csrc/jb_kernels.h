@@ -23,8 +23,6 @@ struct DevImage {
 
 // Device counters (u32 slots unless noted)
 enum {
-    CNT_NBLK = 0,   // all blocks (zh + non-zh)
-    CNT_NZH = 1,    // zh blocks
     CNT_NTOK = 2,   // token starts
     CNT_NTOKE = 3,  // token ends (== CNT_NTOK when consistent)
     CNT_ERR = 4,    // bit 0: a zh block reached a tail index -1 (the reference panics)
@@ -58,17 +56,13 @@ struct Work {
     uint32_t* sbits;       // 1 bit per byte: a token starts here
     uint32_t* ebits;       // 1 bit per byte: a token ends here (last byte)
     uint64_t bits_stride;  // words between docbits, sbits and ebits (one allocation)
-    uint2* supb;           // per 256 k_mark_walk tiles: (blocks, zh blocks) (k_sup)
     uint2* supt;           // per 256 token tiles: (starts, ends) (k_sup)
-    uint2* tile_cnt;       // per k_blocks tile (all, zh) counts, then exclusive offsets
-    uint2* tile_off;
+    uint2* tile_cnt;       // per k_mark_walk tile: (blocks, zh blocks) starting in it
     uint2* ttile_cnt;      // per token tile (starts, ends)
-    uint2* ttile_off;
-    uint32_t* blk;         // block start | zh << 31, then sentinel nbytes
     uint64_t* alnum16;     // 1 bit per 16 bytes of text: some [0-9A-Za-z] byte there
     uint64_t* erec;        // per Han rune (slot = byte / 3): packed DAG edges (k_mark_walk -> k_zh)
-    uint32_t* lanemask;    // per 16 bytes: block starts | Han block starts << 16
-    uint2* gstart;         // per k_zh group g: (blocks, zh blocks) that start before g * group bytes
+    uint32_t* lanemask;    // per 16 bytes: block starts | Han block starts << 16 (k_zh and k_nonzh read
+                           // their blocks from these bits: a block ends at the next start)
     uint2* longblk;        // (start, end) of each long zh block (k_zh -> k_long_*)
     uint32_t* lsegb;       // per long block: its first segment (ascending with the block index)
     uint32_t* lent;        // per segment: offset of the path's first piece start (0xFF none) | one-rune piece ends there << 8
@@ -90,7 +84,7 @@ struct Work {
 
 // Kernel ids for per-launch timing.
 enum KernelId {
-    K_DOCBITS = 0, K_MARK_WALK, K_SCAN_BLOCKS, K_BLOCKS_WRITE, K_ZH, K_NONZH,
+    K_DOCBITS = 0, K_MARK_WALK, K_ZH, K_NONZH,
     K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_LONG_DP, K_LONG_SEG, K_LONG_PATH, K_LONG_TAIL, K_NUM
 };
 extern const char* const kKernelNames[K_NUM];

@@ -35,8 +35,7 @@
 
 namespace jb {
 
-const char* const kKernelNames[K_NUM] = {"k_docbits", "k_mark_walk", "k_scan_blocks", "k_blocks_write",
-                                         "k_zh", "k_nonzh", "k_tok_count", "k_scan_tok",
+const char* const kKernelNames[K_NUM] = {"k_docbits", "k_mark_walk", "k_zh", "k_nonzh", "k_tok_count", "k_scan_tok",
                                          "k_tok_write", "k_doc_tok", "k_long_dp", "k_long_seg", "k_long_path",
                                          "k_long_tail"};
 
@@ -714,57 +713,6 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     }
 }
 
-// k_blocks_write: the lane masks -> block list (start | zh<<31).
-// The thread whose 16 bytes begin a k_zh group (g * grp) also writes
-// gstart[g] = (blocks, zh blocks) that start before it.
-constexpr uint32_t kBwTiles = 4;  // k_blocks_write: tiles per workgroup
-__global__ __launch_bounds__(256) void k_blocks_write(const uint32_t* __restrict__ lanemask,
-                                                      const uint2* __restrict__ tile_cnt,
-                                                      const uint2* __restrict__ supb, uint32_t* __restrict__ blk,
-                                                      uint2* __restrict__ gstart, uint32_t* __restrict__ counters,
-                                                      uint32_t nbytes, uint32_t ntiles, uint32_t grp) {
-    __shared__ uint32_t lds[8];
-    const uint32_t tb = blockIdx.x * kBwTiles;
-    const PrefixLoads pl = pf_load(tile_cnt, supb, tb);
-    uint32_t mm[kBwTiles];
-#pragma unroll
-    for (uint32_t k = 0; k < kBwTiles; k++) mm[k] = tb + k < ntiles ? lanemask[(tb + k) * 256u + threadIdx.x] : 0u;
-    uint2 to = pf_sum(pl, lds);  // blocks (all, zh) before tile tb
-#pragma unroll
-    for (uint32_t k = 0; k < kBwTiles; k++) {
-        const uint32_t t = tb + k;
-        if (t >= ntiles) break;
-        const uint32_t bmask = mm[k] & 0xFFFFu, zmask = mm[k] >> 16;
-        uint32_t tot;
-        const uint32_t ex = block_scan_u32(__popc(bmask) | (__popc(zmask) << 16), lds, &tot);
-        const uint32_t p0 = (t * 256u + threadIdx.x) * 16u;
-        if (p0 % grp == 0u) gstart[p0 / grp] = make_uint2(to.x + (ex & 0xFFFFu), to.y + (ex >> 16));
-        uint32_t ga = to.x + (ex & 0xFFFFu);  // global block rank
-        uint32_t b = bmask;
-        while (b) {
-            const uint32_t kk = __builtin_ctz(b);
-            b &= b - 1u;
-            const bool h = (zmask >> kk) & 1u;
-            blk[ga] = (p0 + kk) | (h ? 0x80000000u : 0u);
-            ga++;
-        }
-        to.x += tot & 0xFFFFu;
-        to.y += tot >> 16;
-    }
-    if (blockIdx.x == gridDim.x - 1u && threadIdx.x == 0) {  // totals and the end sentinel
-        counters[CNT_NBLK] = to.x;
-        counters[CNT_NZH] = to.y;
-        blk[to.x] = nbytes;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_scan2: exclusive scan of n uint2 counts by one 1024-thread workgroup.
-// Rounds of 1024*kScanK entries: each thread loads its kScanK consecutive
-// counts into registers in one batch (16-byte loads, all in flight), the
-// workgroup scans the per-thread sums, then each thread writes its offsets
-// from registers. One HBM round trip per round instead of one per entry.
-// Writes totals to tot[0], tot[1]; optional u64 copy of tot.x; optional sentinel.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kScanK = 16;
 __global__ __launch_bounds__(1024) void k_scan2(const uint2* __restrict__ cnt, uint32_t n, uint2* __restrict__ off,
@@ -839,6 +787,36 @@ __global__ __launch_bounds__(1024) void k_scan2(const uint2* __restrict__ cnt, u
         if (tot64) *tot64 = carry_a;
         if (sentinel_base) sentinel_base[carry_a] = sentinel_val;
     }
+}
+
+// The first block start after chunk c (16 bytes each), or nbytes: the rest of c's
+// tile chunk by chunk, then whole tiles by their block counts (tile_cnt.x).
+__device__ uint32_t nz_block_end(const uint32_t* __restrict__ lanemask, const uint2* __restrict__ tile_cnt,
+                                 uint32_t ntiles, uint32_t nbytes, uint32_t c) {
+    const uint32_t nch = ntiles * 256u;
+    uint32_t k = c + 1u;
+    while (k < nch) {
+        if ((k & 255u) == 0u) {
+            uint32_t t = k >> 8;
+            while (t < ntiles && tile_cnt[t].x == 0u) t++;
+            if (t >= ntiles) break;
+            k = t * 256u;
+        }
+        const uint32_t m = lanemask[k] & 0xFFFFu;
+        if (m) return min(nbytes, k * 16u + (uint32_t)__builtin_ctz(m));
+        k++;
+    }
+    return nbytes;
+}
+
+// The end of the block that starts at byte bs: the next block start of any kind
+// (k_mark_walk's lane masks), or nbytes.
+__device__ uint32_t block_end_at(const uint32_t* __restrict__ lanemask, const uint2* __restrict__ tile_cnt,
+                                 uint32_t ntiles, uint32_t nbytes, uint32_t bs) {
+    const uint32_t c = bs >> 4;
+    const uint32_t above = lanemask[c] & 0xFFFFu & ~((2u << (bs & 15u)) - 1u);
+    if (above) return c * 16u + (uint32_t)__builtin_ctz(above);
+    return nz_block_end(lanemask, tile_cnt, ntiles, nbytes, c);
 }
 
 // ---------------------------------------------------------------------------
@@ -1555,14 +1533,73 @@ __device__ void zh_chunk_main(const uint8_t* __restrict__ text, const DevImage& 
     wave_sync();
 }
 
-#ifdef JB_ZH_WAVES
-#define JB_ZH_ATTR __attribute__((amdgpu_waves_per_eu(JB_ZH_WAVES)))
-#else
-#define JB_ZH_ATTR
+// The next m zh blocks of a k_zh group, in text order, from its lane-mask words
+// staged in LDS (lmv: group word i at lmv[i]; gnw words hold the group's starts,
+// the rest are lookahead for block ends).  Rounds of 64 words, one per lane; rw is
+// the current round, used how many of its zh starts earlier chunks took.  Entries
+// tbl[0..m): in-window blocks as (bs - wb) | (be - wb) << 16, the others as
+// 0x80000000 | (bs - wb).  Returns the new (rw, used).  Not inlined: its registers
+// would otherwise stay allocated across k_zh's DP (3 waves per SIMD instead of 4).
+__device__ __noinline__ uint2 lm_collect(const uint32_t* lmv, uint32_t* tbl, uint32_t lane, uint32_t gw0, uint32_t gnw,
+                                         uint32_t nlw, uint32_t nbytes, uint32_t wb, uint32_t wend, uint32_t m,
+                                         uint32_t rw, uint32_t used) {
+    for (uint32_t have = 0; have < m;) {
+        const uint32_t xa = lmv[rw + lane], xb = lmv[rw + 64u + lane];  // this round and its lookahead
+        const uint32_t bm = xa & 0xFFFFu;
+        const uint32_t zm = (rw + lane < gnw) ? (xa >> 16) : 0u;
+        const uint32_t cz = (uint32_t)__popc(zm);
+        uint32_t incl = cz;  // inclusive prefix over the lanes
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)incl, d, 64);
+            if (lane >= (uint32_t)d) incl += t;
+        }
+        const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
+        // the first block start after this lane's word: in a later lane of this round, else
+        // in the lookahead round, else past it (0xFFFFFFFF: found later) or the batch end
+        const uint64_t la = __ballot(bm != 0u), lb = __ballot((xb & 0xFFFFu) != 0u);
+        const uint64_t later = la & ~((2ull << lane) - 1ull);
+        const uint32_t j = later ? (uint32_t)__builtin_ctzll(later) : (lb ? (uint32_t)__builtin_ctzll(lb) : 0u);
+        const uint32_t lo_a = bm ? (uint32_t)__builtin_ctz(bm) : 0u;
+        const uint32_t lo_b = (xb & 0xFFFFu) ? (uint32_t)__builtin_ctz(xb & 0xFFFFu) : 0u;
+        const uint32_t sa = (uint32_t)__shfl((int)lo_a, (int)j, 64), sb = (uint32_t)__shfl((int)lo_b, (int)j, 64);
+        const uint32_t wr = gw0 + rw;
+        uint32_t nxt = 0xFFFFFFFFu;
+        if (later) nxt = (wr + j) * 16u + sa;
+        else if (lb) nxt = (wr + 64u + j) * 16u + sb;
+        else if (wr + 128u >= nlw) nxt = (uint32_t)nbytes;  // no block starts after this one
+        const uint32_t take = min(total - used, m - have);
+        uint32_t z = zm, r = incl - cz;
+        while (z) {
+            const uint32_t k = (uint32_t)__builtin_ctz(z);
+            z &= z - 1u;
+            if (r >= used && r < used + take) {
+                const uint32_t bs = (wr + lane) * 16u + k;
+                const uint32_t above = bm & ~((2u << k) - 1u);
+                const uint32_t be = above ? (wr + lane) * 16u + (uint32_t)__builtin_ctz(above) : nxt;
+                tbl[have + r - used] = (be <= wend) ? (bs - wb) | ((be - wb) << 16) : (0x80000000u | (bs - wb));
+            }
+            r++;
+        }
+        have += take;
+        used += take;
+        if (used == total) {  // next round
+            rw += 64u;
+            used = 0;
+        }
+    }
+    return make_uint2(rw, used);
+}
+
+// At least 4 waves per SIMD (at most 128 VGPRs): the DP is latency-bound and
+// needs them; left alone the allocator lands just above 128 (3 waves, k_zh +17 %).
+#ifndef JB_ZH_WAVES
+#define JB_ZH_WAVES 4
 #endif
+#define JB_ZH_ATTR __attribute__((amdgpu_waves_per_eu(JB_ZH_WAVES)))
 template <bool HMM>
 __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict__ text, uint64_t nbytes,
-                                            const uint32_t* __restrict__ blk, const uint2* __restrict__ gstart,
+                                            const uint32_t* __restrict__ lanemask, const uint2* __restrict__ tile_cnt,
                                             const uint32_t* __restrict__ tile4,
                                             uint32_t* __restrict__ counters, DevImage im,
                                             const uint64_t* __restrict__ erec, uint8_t* __restrict__ gbl,
@@ -1580,10 +1617,11 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
     uint32_t* rb32 = reinterpret_cast<uint32_t*>(s_rb[wv]);
     uint32_t* tbl = s_tbl[wv];
     uint32_t* hist = s_hist[wv];
-    const uint32_t nblk = counters[CNT_NBLK], nzh = counters[CNT_NZH];
     const uint32_t ngroups = (uint32_t)((nbytes + grp - 1u) / grp);  // (grp <= kZhGroupBytes)
     const uint32_t ntiles = (uint32_t)((nbytes + kTileBytes - 1u) / kTileBytes);
+    const uint32_t nlw = ntiles * 256u;                                  // lane-mask words (16 bytes each)
     const uint32_t winw = (grp + (kZhWin - kZhGroupBytes)) / 32u + 1u;  // token words of a window (<= kZhWinWords)
+    auto lmw = [&](uint32_t w) -> uint32_t { return w < nlw ? lanemask[w] : 0u; };
     Emitter em(sbits, ebits);
     // diagnostic per-wave clocks (JB_ABLATE bit 8): [0] setup [1] DP [2] forward+Viterbi+flush [3] chunks
     // [4] sum of lane DP steps [5] sum of per-chunk max lane DP steps [6] blocks past the window [7] scratch
@@ -1600,10 +1638,32 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
         if (lane == 0) g = atomicAdd(counters + CNT_WORK, 1u);
         g = __builtin_amdgcn_readfirstlane(g);
         if (g >= ngroups) break;
-        const uint2 g0 = gstart[g];
-        const uint2 g1 = (g + 1u < ngroups) ? gstart[g + 1u] : make_uint2(nblk, nzh);
-        if (g0.y >= g1.y) continue;  // no Han block starts here
         const uint32_t wb = g * grp, wend = wb + grp + (kZhWin - kZhGroupBytes);
+        // The group's zh blocks are the Han block starts (lane-mask bits 16-31) in its
+        // words; a block ends at the next block start of any kind (bits 0-15).
+        const uint32_t gw0 = wb >> 4;
+        const uint32_t gnw = (uint32_t)((min((uint64_t)wb + grp, nbytes) - wb + 15u) >> 4);
+        // The group's lane-mask words and those after it (block ends, up to 8 KiB of text)
+        // are staged in the wave's ring area, which is free until the DP.
+        uint32_t* const lmv = rb32;
+        auto stage = [&]() {
+            uint32_t v[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[k] = lmw(gw0 + lane + 64u * (uint32_t)k);
+#pragma unroll
+            for (int k = 0; k < 8; k++) lmv[lane + 64u * (uint32_t)k] = v[k];
+            wave_sync();
+        };
+        stage();
+        uint32_t n = 0;
+        {
+            uint32_t c = 0;
+            for (uint32_t w = lane; w < gnw; w += 64u) c += (uint32_t)__popc(lmv[w] >> 16);
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) c += (uint32_t)__shfl_xor((int)c, d, 64);
+            n = __builtin_amdgcn_readfirstlane(c);
+        }
+        if (n == 0u) continue;  // no Han block starts here
         // all-3-byte window: no 4-byte Han rune starts in the tiles under it
         bool any4 = false;
         {
@@ -1611,35 +1671,19 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
             if (lane <= t1 - t0 && t0 + lane < ntiles) any4 = tile4[t0 + lane] != 0u;
         }
         const bool all3 = __ballot(any4) == 0ull;
-        const uint32_t n = g1.y - g0.y;
         const uint32_t nch = (n + kZhChunk - 1u) / kZhChunk;
         const uint32_t cs = (n + nch - 1u) / nch;  // even chunks
-        uint32_t cur = g0.x;                       // next block (all kinds) to look at
+        uint32_t rw = 0, used = 0;  // current round: group words [rw, rw + 64); zh starts of it already taken
         for (uint32_t c0 = 0; c0 < n; c0 += cs) {
             if (st) stv[7] = __builtin_amdgcn_s_memtime();
             const uint32_t m = min(cs, n - c0);
-            // the chunk's m zh blocks, in order, from the block list (coalesced): in-window
-            // ones as (bs - wb) | (be - wb) << 16, others as 0x80000000 | block index
-            for (uint32_t have = 0; have < m;) {
-                const uint32_t k = cur + lane;
-                uint32_t x = 0, y = 0;
-                if (k < g1.x) {
-                    x = blk[k];
-                    y = blk[k + 1u];
-                }
-                const bool z = (x >> 31) != 0u;
-                const uint64_t zm = __ballot(z);
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(zm >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)zm, 0u));
-                const uint32_t nz = (uint32_t)__popcll(zm);
-                const uint32_t take = min(nz, m - have);
-                if (z && rank < take) {
-                    const uint32_t bs = x & 0x7FFFFFFFu, be = y & 0x7FFFFFFFu;
-                    tbl[have + rank] = (be <= wend) ? (bs - wb) | ((be - wb) << 16) : (0x80000000u | k);
-                }
-                if (take < nz) cur += (uint32_t)__builtin_ctzll(__ballot(z && rank == take));  // first one left
-                else cur = min(cur + 64u, g1.x);
-                have += take;
+            if (c0) stage();  // (the previous chunk's DP and bitmaps used the ring)
+            // the chunk's m zh blocks in text order: in-window ones as (bs - wb) | (be - wb) << 16,
+            // the others as 0x80000000 | (bs - wb) (their end is found later)
+            {
+                const uint2 ru = lm_collect(lmv, tbl, lane, gw0, gnw, nlw, (uint32_t)nbytes, wb, wend, m, rw, used);
+                rw = ru.x;
+                used = ru.y;
             }
             wave_sync();
             // this lane's items k = lane + 64 i of the chunk
@@ -1653,9 +1697,8 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
                 if (k < m) {
                     const uint32_t x = tbl[k];
                     if (x & 0x80000000u) {  // ends past the window (rare)
-                        const uint32_t gi = x & 0x7FFFFFFFu;
-                        bsi[i] = blk[gi] & 0x7FFFFFFFu;
-                        bei[i] = blk[gi + 1u] & 0x7FFFFFFFu;
+                        bsi[i] = wb + (x & 0xFFFFu);
+                        bei[i] = block_end_at(lanemask, tile_cnt, ntiles, (uint32_t)nbytes, bsi[i]);
                         out[i] = true;
                     } else {
                         bsi[i] = wb + (x & 0xFFFFu);
@@ -1806,7 +1849,9 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
 // A long block with a 4-byte Han rune takes k_zh's one-lane path in k_long_dp.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kLongGrid = 64;    // k_long_dp workgroups (persistent over the long-block list)
+#if JB_STAMPS
 constexpr uint32_t kDbgLong = 65536u * 4u;  // k_long_dp's diagnostic clocks in the debug buffer (u64 index)
+#endif
 constexpr uint32_t kLdWin = 256;      // runes per descriptor window
 constexpr uint32_t kLdDesc = 1024;    // descriptor ring: 4 windows
 constexpr uint32_t kLdRing = 512;     // best-value ring (edges are at most 255 runes)
@@ -2437,26 +2482,6 @@ __device__ __forceinline__ uint32_t alnum_mask16(uint4 x) {
     return m;
 }
 
-// The first block start after chunk c (16 bytes each), or nbytes: the rest of c's
-// tile chunk by chunk, then whole tiles by their block counts (tile_cnt.x).
-__device__ uint32_t nz_block_end(const uint32_t* __restrict__ lanemask, const uint2* __restrict__ tile_cnt,
-                                 uint32_t ntiles, uint32_t nbytes, uint32_t c) {
-    const uint32_t nch = ntiles * 256u;
-    uint32_t k = c + 1u;
-    while (k < nch) {
-        if ((k & 255u) == 0u) {
-            uint32_t t = k >> 8;
-            while (t < ntiles && tile_cnt[t].x == 0u) t++;
-            if (t >= ntiles) break;
-            k = t * 256u;
-        }
-        const uint32_t m = lanemask[k] & 0xFFFFu;
-        if (m) return min(nbytes, k * 16u + (uint32_t)__builtin_ctz(m));
-        k++;
-    }
-    return nbytes;
-}
-
 // k_nonzh: cutNonZh (tokenizer.go:289-310) for exactly the non-Han blocks that hold
 // a [0-9A-Za-z] byte; every other non-Han block has no tokens (:290-293).  An alnum
 // byte is never Han, so it always lies in a non-Han block.  One thread per alnum16
@@ -2654,18 +2679,13 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     JB_TIMED(K_MARK_WALK, hipLaunchKernelGGL(k_mark_walk, dim3(ntiles), dim3(256), 0, stream, d_text, nbytes,
                                              w.docbits, im, w.lanemask, w.tile_cnt, w.erec + kErecPad,
                                              w.tile4, w.alnum16, w.sbits, w.ebits, diag, w.dbg_walk));
-    JB_TIMED(K_SCAN_BLOCKS, hipLaunchKernelGGL(k_sup, dim3((ntiles + 255) / 256), dim3(256), 0, stream, w.tile_cnt,
-                                               ntiles, w.supb));
-    JB_TIMED(K_BLOCKS_WRITE, hipLaunchKernelGGL(k_blocks_write, dim3((ntiles + kBwTiles - 1) / kBwTiles), dim3(256), 0,
-                                                stream, w.lanemask, w.tile_cnt, w.supb, w.blk, w.gstart, w.counters,
-                                                (uint32_t)nbytes, ntiles, grp));
     if (hmm)
-        JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
-                                          w.gstart, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
+        JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes,
+                                          w.lanemask, w.tile_cnt, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
                                           w.longblk, w.lsegb, grp, diag, w.dbg));
     else
-        JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes, w.blk,
-                                          w.gstart, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
+        JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes,
+                                          w.lanemask, w.tile_cnt, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
                                           w.longblk, w.lsegb, grp, diag, w.dbg));
     {
         // long blocks: the chain, then one lane per 64-rune segment (at most
