@@ -376,6 +376,7 @@ def run(args, world, rank, dist, agg_dev, make_cutter, open_oracle, log=print):
         "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
         "ms_per_step_kernel_by_kernel": round(prof_ms, 4) if prof_ms else None,
         "gen_s": round(gen_s, 2),
+        "workload_key": wkey,
     }
     return line, (sbuf, soff, cutter)
 

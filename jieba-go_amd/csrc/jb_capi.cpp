@@ -483,7 +483,7 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.counters, 64 * 4));
     HIPCHK(hipMalloc(&w.supt, (nttiles / 256 + 2) * sizeof(uint2)));
     if (d->lc.diag & 0x100u) {
-        HIPCHK(hipMalloc(&w.dbg, 65536 * 8 * 8));
+        HIPCHK(hipMalloc(&w.dbg, 65536 * 16 * 8));
         HIPCHK(hipMalloc(&w.dbg_walk, ntiles * 4 * 8 * 8));
         HIPCHK(hipMemset(w.dbg_walk, 0, ntiles * 4 * 8 * 8));
     }
@@ -610,22 +610,23 @@ static int launch(Device* d, const uint8_t* d_text, uint64_t nbytes, const uint6
     if (e != hipSuccess) return fail(JB_EDEVICE, "pipeline launch: %s", hipGetErrorString(e));
     if ((lc.diag & 0x100u) && d->w.dbg) {  // diagnostic: per-wave clocks of k_zh (STAMPS builds)
         const uint32_t nwv = std::min<uint32_t>(lc.grid_zh * 4u, 65536u);
-        std::vector<uint64_t> st((size_t)nwv * 8);
+        std::vector<uint64_t> st((size_t)nwv * 16);
         HIPCHK(hipMemcpyAsync(st.data(), d->w.dbg, st.size() * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        double a[16] = {0};
         double n = 0;
         for (uint32_t i = 0; i < nwv; i++)
-            if (st[i * 8 + 3]) {
-                for (int k = 0; k < 8; k++) a[k] += (double)st[i * 8 + k];
+            if (st[i * 16 + 3]) {
+                for (int k = 0; k < 16; k++) a[k] += (double)st[i * 16 + k];
                 n++;
             }
         if (n == 0) n = 1;
-        fprintf(stderr, "[jb] k_zh clocks/wave: setup %.0f dp %.0f fwd+vit %.0f total %.0f; chunks/wave %.1f; "
-                        "lane DP steps %.0f vs 64*max %.0f (DP lane use %.2f); blocks past the window per chunk %.3f\n",
-                a[0] / n, a[1] / n, a[2] / n, a[6] / n, a[3] / n, a[4] / n, 64.0 * a[5] / n,
+        fprintf(stderr, "[jb] k_zh clocks/wave: setup %.0f dp %.0f fwd walk %.0f viterbi fwd %.0f back+flush+rest %.0f "
+                        "total %.0f; chunks/wave %.1f; lane DP steps %.0f vs 64*max %.0f (DP lane use %.2f); blocks past "
+                        "the window per chunk %.3f\n",
+                a[0] / n, a[1] / n, a[8] / n, a[9] / n, a[2] / n, a[6] / n, a[3] / n, a[4] / n, 64.0 * a[5] / n,
                 a[4] / (64.0 * a[5] + 1e-9), a[7] / (a[3] + 1e-9));
-        HIPCHK(hipMemsetAsync(d->w.dbg, 0, (size_t)nwv * 64, s));
+        HIPCHK(hipMemsetAsync(d->w.dbg, 0, (size_t)nwv * 128, s));
         const uint64_t nww = (nbytes + kTileBytes - 1) / kTileBytes * 4;
         std::vector<uint64_t> sw(nww * 8);
         HIPCHK(hipMemcpyAsync(sw.data(), d->w.dbg_walk, sw.size() * 8, hipMemcpyDeviceToHost, s));

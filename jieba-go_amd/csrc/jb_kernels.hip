@@ -1194,12 +1194,20 @@ __device__ uint32_t zh_dp(const V& v, const DevImage& im, const uint64_t* __rest
     return steps;
 }
 
-// All-3-byte form, software-pipelined.  Rune k steps back has slot s - k, so
-// per step, in this issue order: the weights of the NEXT rune (its record
-// came two steps ago), then the record of the rune three back, then the fold
-// of this rune with the weights loaded one step ago.  vmcnt retires loads in
-// issue order, so this order is what lets each load have a whole step: the
-// fold's wait does not cover the record load issued after the weights.
+// All-3-byte form, software-pipelined.  Rune k steps back has slot s - k.  Per
+// step, in this issue order: the weights of the NEXT rune (its record landed
+// long ago), then, every other step, the record pair of the runes four and five
+// back, then the fold of this rune with the weights loaded one step ago.
+// Records come two per 16-byte load into two register pairs X and Y that
+// alternate, so a pair is loaded three steps before its first use; vmcnt
+// retires loads in issue order and the pair is issued after the weights, so
+// the next step's wait for those weights does not wait for it, and it has two
+// whole steps to land (with one pair register set a record had one step: the
+// DP waited for an HBM round trip every other step).  Four step kinds cycle:
+//   0: A_X  uses X.lo = E(s-1), reloads X = (E(s-5), E(s-4))
+//   1: B_Y  uses Y.hi = E(s-1)
+//   2: A_Y  uses Y.lo = E(s-1), reloads Y = (E(s-5), E(s-4))
+//   3: B_X  uses X.hi = E(s-1)
 template <class Src>
 __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const uint64_t* __restrict__ erec,
                              double* __restrict__ gbest, double* ring, const Src& src) {
@@ -1207,34 +1215,52 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
     if (!src.next(j, bs, be)) return 0;
     uint32_t key0 = 0, steps = 0, q = 0, c = 1, s = 0, mc = 0;
     bool longm = false;
-    // Records come two per load: slots (k, k+1) = runes two apart going back.
-    // A steps load the pair of the next-but-one and next-but-two runes; B steps
-    // load none.  Slots before a block (or before the text: erec has 8 slots of
-    // padding in front) are garbage that `more` masks at the use.
-    uint64_t lo = 0, hi = 0;  // the last pair: lo = the rune further back
-    auto pair = [&](uint32_t k) {  // slots k, k+1 in one 16-byte load
+    // Slots before a block (or before the text: erec has kErecPad slots of padding in
+    // front) are garbage that `more` masks at the use.
+    uint64_t xl = 0, xh = 0, yl = 0, yh = 0;
+    auto ld_pair = [&](uint32_t k, uint64_t& lo, uint64_t& hi) {  // slots k, k+1 in one 16-byte load
         typedef uint64_t u64x2 __attribute__((ext_vector_type(2), aligned(8)));
         const u64x2 x = *reinterpret_cast<const u64x2*>(erec + (int32_t)k);
         lo = x.x;
         hi = x.y;
     };
-    auto setup = [&]() {
+    auto setup = [&]() {  // (re)start at the last rune of [bs, be)
         key0 = be / 3u;
         q = be - 3u;
         c = 1;
         s = q / 3u;
         ring[0] = 0.0;  // best(n), the {n, 0.0} sentinel (rec_fold_s)
     };
-    // One rune.  r1: the next rune's record (landed a step ago); wc: this rune's
-    // weights (loaded a step ago); wn: gets the next rune's.  Weight registers
-    // alternate between the two steps, so nothing is copied out of a load's
-    // destination (a copy would wait for the load).
-    auto step = [&](const bool A, double (&wc)[4], double (&wn)[4]) -> bool {
+    // The pairs a step of kind P at slot s (the block's last rune) and the steps after it read.
+    auto prime = [&](const int P, double (&wn)[4]) {
+        const uint64_t rc = erec[s];
+        if (P == 0) {
+            ld_pair(s - 1u, xl, xh);
+            ld_pair(s - 3u, yl, yh);
+        } else if (P == 1) {
+            ld_pair(s - 2u, yl, yh);
+            ld_pair(s - 4u, xl, xh);
+        } else if (P == 2) {
+            ld_pair(s - 1u, yl, yh);
+            ld_pair(s - 3u, xl, xh);
+        } else {
+            ld_pair(s - 2u, xl, xh);
+            ld_pair(s - 4u, yl, yh);
+        }
+        mc = (uint32_t)rc & 0xFFu;
+        rec_weights(im, rc, wn);
+    };
+    // One rune.  wc: this rune's weights (loaded a step ago); wn: gets the next rune's.
+    // Weight registers alternate between steps, so nothing is copied out of a
+    // load's destination (a copy would wait for the load).
+    auto step = [&](const int P, double (&wc)[4], double (&wn)[4]) -> bool {
         const bool more = q > bs;
-        const uint64_t r1v = more ? (A ? lo : hi) : 0ull;  // (the next rune exists)
-        if (A) pair(s - 3u);  // runes t+3, t+2 (first: vmcnt retires in order)
+        const uint64_t nx = P == 0 ? xl : (P == 1 ? yh : (P == 2 ? yl : xh));
+        const uint64_t r1v = more ? nx : 0ull;  // the next rune's record (when it exists)
         const uint32_t mn = (uint32_t)r1v & 0xFFu;
         rec_weights(im, r1v, wn);
+        if (P == 0) ld_pair(s - 5u, xl, xh);
+        if (P == 2) ld_pair(s - 5u, yl, yh);
         DpFold f;
         rec_fold_s(mc, wc, f, c, ring);
         if (mc == 0u) dp_walk_rune(v, im, q, be, f, c, ring, longm, gbest, key0);  // overflowed record (rare)
@@ -1256,28 +1282,18 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
             if (!src.next(j, bs, be)) return true;
             longm = false;
         }
-        // (re)start at the last rune of [bs, be); the next step is the other kind
         setup();
-        if (A) {  // next: B, which wants hi = E(s-1); the A after it wants lo = E(s-2)
-            pair(s - 2u);
-            const uint64_t rc = erec[s];
-            mc = (uint32_t)rc & 0xFFu;
-            rec_weights(im, rc, wn);
-        } else {  // next: A, which wants lo = E(s-1)
-            pair(s - 1u);
-            mc = (uint32_t)hi & 0xFFu;
-            rec_weights(im, hi, wn);
-        }
+        prime((P + 1) & 3, wn);  // the next step is the next kind
         return false;
     };
     double wa[4], wb[4];
-    setup();  // first block: the next step is an A
-    pair(s - 1u);
-    mc = (uint32_t)hi & 0xFFu;
-    rec_weights(im, hi, wa);
+    setup();
+    prime(0, wa);
     for (;;) {
-        if (step(true, wa, wb)) break;
-        if (step(false, wb, wa)) break;
+        if (step(0, wa, wb)) break;
+        if (step(1, wb, wa)) break;
+        if (step(2, wa, wb)) break;
+        if (step(3, wb, wa)) break;
     }
     return steps;
 }
@@ -1516,8 +1532,18 @@ __device__ void zh_chunk_main(const uint8_t* __restrict__ text, const DevImage& 
         RunList rl{runs, wb, 0u};
         RunList* const rlp = (HMM && A3) ? &rl : nullptr;
         ok = zh_fwd_lane<HMM>(v, im, src, le, rlp);
+        if (st) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            st[8] += t - st[7];
+            st[7] = t;
+        }
         if constexpr (HMM && A3) {
             const uint32_t stb = viterbi_fwd_runs<LdsEmitter>(v, im, runs, rl.n, le.ties);
+            if (st) {
+                const uint64_t t = __builtin_amdgcn_s_memtime();
+                st[9] += t - st[7];
+                st[7] = t;
+            }
             for (uint32_t r = 0; r < kZhRuns; r++)
                 if (r < rl.n) {
                     const uint32_t x = runs[r * 64u];
@@ -1625,7 +1651,7 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
     Emitter em(sbits, ebits);
     // diagnostic per-wave clocks (JB_ABLATE bit 8): [0] setup [1] DP [2] forward+Viterbi+flush [3] chunks
     // [4] sum of lane DP steps [5] sum of per-chunk max lane DP steps [6] blocks past the window [7] scratch
-    uint64_t stv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t stv[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // [8] forward walk [9] Viterbi forward half
 #if JB_STAMPS
     uint64_t* st = (diag & 0x100u) ? stv : nullptr;
 #else
@@ -1811,7 +1837,9 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
             sum += ((uint64_t)hi << 32) | lo;
         }
         if (lane == 0) {
-            uint64_t* o = dbg + (blockIdx.x * 4u + wv) * 8u;
+            uint64_t* o = dbg + (blockIdx.x * 4u + wv) * 16u;
+            o[8] = stv[8];
+            o[9] = stv[9];
             o[0] = stv[0];
             o[1] = stv[1];
             o[2] = stv[2];

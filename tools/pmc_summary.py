@@ -7,7 +7,9 @@ prescribes (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) counts 64-B requests
 and reads 1/2 of a wide coalesced stream's bytes on gfx950 -> x2; WRITE_SIZE
 (KiB) is exact for 16-B/lane stores.  Both raw and corrected values are kept.
 
-usage: pmc_summary.py <pmc dir with p*/run_counter_collection.csv> <out.json> [bytes_per_launch_note]
+usage: pmc_summary.py <pmc dir with p*/run_counter_collection.csv> <out.json> [note ...]
+The workload key (bench.py's docs:<bytes>:hmm:prefix form, which bench.py matches
+before it uses the traffic) is taken from the passes' bench lines (p1.json).
 """
 import csv
 import glob
@@ -49,8 +51,14 @@ def main():
         res[k] = e
     meta = {"source": d, "note": " ".join(sys.argv[3:]),
             "method": "rocprofv3 --kernel-trace --pmc, one counter group per run; FETCH_SIZE x2 (gfx950)"}
+    wkey = None
+    try:
+        with open(os.path.join(d, "p1.json")) as f:
+            wkey = json.loads(f.read().strip().splitlines()[-1]).get("workload_key")
+    except (OSError, ValueError, IndexError):
+        pass
     with open(out, "w") as f:
-        json.dump({"meta": meta, "kernels": res}, f, indent=1)
+        json.dump({"meta": meta, "workload_key": wkey, "kernels": res}, f, indent=1)
     for k, e in sorted(res.items(), key=lambda x: -x[1]["mean_ms_profiled"]):
         print(f"{k:22s} ms={e['mean_ms_profiled']:.3f} " + " ".join(
             f"{c}={e[c]:.4g}" for c in ("hbm_bytes_per_launch", "l2_hit_rate", "TCC_EA0_RDREQ_sum", "TCC_HIT_sum",
