@@ -713,82 +713,6 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     }
 }
 
-// ---------------------------------------------------------------------------
-constexpr uint32_t kScanK = 16;
-__global__ __launch_bounds__(1024) void k_scan2(const uint2* __restrict__ cnt, uint32_t n, uint2* __restrict__ off,
-                                                uint32_t* __restrict__ tot, uint64_t* __restrict__ tot64,
-                                                uint32_t* __restrict__ sentinel_base, uint32_t sentinel_val) {
-    __shared__ uint32_t la[16], lz[16];
-    const uint32_t t = threadIdx.x;
-    const uint32_t lane = t & 63u, wid = t >> 6;
-    uint32_t carry_a = 0, carry_z = 0;
-    for (uint32_t r0 = 0; r0 < n; r0 += 1024u * kScanK) {
-        const uint32_t b = r0 + t * kScanK;
-        uint2 c[kScanK];
-        if (b + kScanK <= n) {
-            const uint4* p = reinterpret_cast<const uint4*>(cnt + b);
-#pragma unroll
-            for (uint32_t k = 0; k < kScanK / 2; k++) {
-                const uint4 v = p[k];
-                c[2 * k] = make_uint2(v.x, v.y);
-                c[2 * k + 1] = make_uint2(v.z, v.w);
-            }
-        } else {
-#pragma unroll
-            for (uint32_t k = 0; k < kScanK; k++) c[k] = (b + k < n) ? cnt[b + k] : make_uint2(0u, 0u);
-        }
-        uint32_t sa = 0, sz = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kScanK; k++) { sa += c[k].x; sz += c[k].y; }
-        uint32_t xa = sa, xz = sz;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t ya = __shfl_up(xa, d, 64), yz = __shfl_up(xz, d, 64);
-            if (lane >= (uint32_t)d) { xa += ya; xz += yz; }
-        }
-        __syncthreads();  // la/lz reuse across rounds
-        if (lane == 63) { la[wid] = xa; lz[wid] = xz; }
-        __syncthreads();
-        uint32_t ba = carry_a, bz = carry_z, ta = 0, tz = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 16; k++) {
-            const uint32_t va = la[k], vz = lz[k];
-            if (k < wid) { ba += va; bz += vz; }
-            ta += va;
-            tz += vz;
-        }
-        ba += xa - sa;
-        bz += xz - sz;
-        if (b + kScanK <= n) {
-            uint4* q = reinterpret_cast<uint4*>(off + b);
-#pragma unroll
-            for (uint32_t k = 0; k < kScanK / 2; k++) {
-                uint4 v;
-                v.x = ba; v.y = bz;
-                ba += c[2 * k].x; bz += c[2 * k].y;
-                v.z = ba; v.w = bz;
-                ba += c[2 * k + 1].x; bz += c[2 * k + 1].y;
-                q[k] = v;
-            }
-        } else {
-#pragma unroll
-            for (uint32_t k = 0; k < kScanK; k++) {
-                if (b + k < n) off[b + k] = make_uint2(ba, bz);
-                ba += c[k].x;
-                bz += c[k].y;
-            }
-        }
-        carry_a += ta;
-        carry_z += tz;
-    }
-    if (t == 0) {
-        tot[0] = carry_a;
-        tot[1] = carry_z;
-        if (tot64) *tot64 = carry_a;
-        if (sentinel_base) sentinel_base[carry_a] = sentinel_val;
-    }
-}
-
 // The first block start after chunk c (16 bytes each), or nbytes: the rest of c's
 // tile chunk by chunk, then whole tiles by their block counts (tile_cnt.x).
 __device__ uint32_t nz_block_end(const uint32_t* __restrict__ lanemask, const uint2* __restrict__ tile_cnt,
