@@ -1583,10 +1583,17 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
 #endif
     const uint64_t tk0 = st ? __builtin_amdgcn_s_memtime() : 0;
     uint32_t nties = 0;  // Viterbi route ties of the in-window blocks (em.ties: the others)
-    for (;;) {
-        uint32_t g = 0;
-        if (lane == 0) g = atomicAdd(counters + CNT_WORK, 1u);
-        g = __builtin_amdgcn_readfirstlane(g);
+    // Wave w takes group w first, then the next unclaimed one from the counter: only
+    // waves that finished a group touch the counter (4096 waves all claiming their
+    // first group on one address cost ~80 us on a one-sentence batch).
+    const uint32_t nwv = gridDim.x * (blockDim.x >> 6);
+    uint32_t g = blockIdx.x * (blockDim.x >> 6) + wv;
+    auto next_group = [&]() -> uint32_t {
+        uint32_t x = 0;
+        if (lane == 0) x = atomicAdd(counters + CNT_WORK, 1u);
+        return nwv + __builtin_amdgcn_readfirstlane(x);
+    };
+    for (;; ) {
         if (g >= ngroups) break;
         const uint32_t wb = g * grp, wend = wb + grp + (kZhWin - kZhGroupBytes);
         // The group's zh blocks are the Han block starts (lane-mask bits 16-31) in its
@@ -1613,7 +1620,10 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
             for (int d = 32; d >= 1; d >>= 1) c += (uint32_t)__shfl_xor((int)c, d, 64);
             n = __builtin_amdgcn_readfirstlane(c);
         }
-        if (n == 0u) continue;  // no Han block starts here
+        if (n == 0u) {  // no Han block starts here
+            g = next_group();
+            continue;
+        }
         // all-3-byte window: no 4-byte Han rune starts in the tiles under it
         bool any4 = false;
         {
@@ -1743,6 +1753,7 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
                 stv[7] = t;
             }
         }
+        g = next_group();
     }
     em.flush();
     {
@@ -2611,12 +2622,15 @@ uint32_t zh_blocks_per_cu(bool hmm) { return hmm ? occ_zh<true>() : occ_zh<false
 hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text, uint64_t nbytes,
                         const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, const LaunchCfg& lc,
                         hipStream_t stream, KernelTimer* timer) {
-    const uint32_t grid_zh = lc.grid_zh, diag = lc.diag;
+    const uint32_t diag = lc.diag;
     const uint64_t nwords = (nbytes + 31) / 32;
     const uint32_t ntiles = (uint32_t)((nbytes + kTileBytes - 1) / kTileBytes);
     // k_zh work unit: a small batch gets small groups, so that enough waves share it
     const uint32_t grp = lc.zh_group ? lc.zh_group : zh_group_for(nbytes);
     const uint32_t nttiles = (uint32_t)((nwords + kTokTileWords - 1) / kTokTileWords);
+    // k_zh: a persistent grid, but no more 4-wave workgroups than the batch has groups
+    const uint64_t ngroups = (nbytes + grp - 1) / grp;
+    const uint32_t grid_zh = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(lc.grid_zh, (ngroups + 3) / 4));
     hipError_t e;
     if ((e = hipMemsetAsync(w.counters, 0, CNT_CLEAR * sizeof(uint32_t), stream))) return e;
     // (k_mark_walk clears the token bitmaps tile by tile)
