@@ -699,7 +699,9 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     if (stamps) c3 = __builtin_amdgcn_s_memtime();
     __syncthreads();
     // records out in entry (= text) order: consecutive lanes, mostly consecutive slots
-    for (uint32_t i = threadIdx.x; i < nent; i += 256u) erec[(t0 + ent_pos(s_e[i])) / 3u] = s_c[i];
+    // (non-temporal: k_zh reads them on another XCD; kept out of this L2, where the trie's hot lines live)
+    for (uint32_t i = threadIdx.x; i < nent; i += 256u)
+        __builtin_nontemporal_store(s_c[i], erec + (t0 + ent_pos(s_e[i])) / 3u);
     if (stamps && (threadIdx.x & 63u) == 0) {  // per-wave phase clocks, summed on the host
         uint64_t* o = dbg + ((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * 8u;
         o[0] = c1 - c0;
