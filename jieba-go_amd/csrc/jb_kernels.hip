@@ -2579,8 +2579,8 @@ __global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits,
     }
     if (staged) {
         __syncthreads();
-        for (uint32_t k = threadIdx.x; k < ts; k += 256u) tok_start[to.x + k] = s_s[k];
-        for (uint32_t k = threadIdx.x; k < te; k += 256u) tok_end[to.y + k] = s_e[k];
+        for (uint32_t k = threadIdx.x; k < ts; k += 256u) __builtin_nontemporal_store(s_s[k], tok_start + to.x + k);
+        for (uint32_t k = threadIdx.x; k < te; k += 256u) __builtin_nontemporal_store(s_e[k], tok_end + to.y + k);
     }
 }
 
