@@ -391,7 +391,7 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     const uint64_t lastw = (nbytes + 31) >> 5;
     {  // clear the tile's words of the token bitmaps (k_zh and k_nonzh OR into them): no memset pass
         const uint64_t wz = (t0 >> 5) + (threadIdx.x & 127u);
-        if (wz < lastw + 2u) (threadIdx.x < 128u ? sbits : ebits)[wz] = 0u;
+        if (wz < lastw + 2u) __builtin_nontemporal_store(0u, (threadIdx.x < 128u ? sbits : ebits) + wz);
     }
     if (threadIdx.x < kTileBytes / 32 + 3) {
         const uint64_t wi = (t0 >> 5) + threadIdx.x;
@@ -495,7 +495,7 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     if (nbytes < p0 + 16) valid = nbytes > p0 ? ((1u << (uint32_t)(nbytes - p0)) - 1u) << 4 : 0u;
     const uint32_t bs = ~covered & valid & ((uint32_t)M | (hanb ^ (hanb << 1)));
     const uint32_t bmask = (bs >> 4) & 0xFFFFu, zmask = ((bs & hanb) >> 4) & 0xFFFFu;
-    lanemask[blockIdx.x * 256u + threadIdx.x] = bmask | (zmask << 16);
+    __builtin_nontemporal_store(bmask | (zmask << 16), lanemask + blockIdx.x * 256u + threadIdx.x);  // (read on other XCDs)
     uint32_t tot;
     block_scan_u32(__popc(bmask) | (__popc(zmask) << 16), lds, &tot);
     if (threadIdx.x == 0) tile_cnt[blockIdx.x] = make_uint2(tot & 0xFFFFu, tot >> 16);
