@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.."
 OUT=gpurun_out/${TAG:-pmc2}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu --no-profile --no-e2e}
+ARGS=${BENCH_ARGS:---steps 3 --warmup 1 --no-parity --no-profile --no-e2e}
 i=0
 while IFS= read -r grp; do
   [ -z "$grp" ] && continue
