@@ -641,3 +641,38 @@ def test_nonzh_blocks_across_chunks_and_tiles(small):
     # the same texts as one document (blocks spanning the former boundaries)
     buf1, off1 = _batch_of(["".join(docs)])
     _cmp_batch(tk, o, buf1, off1, True, "nonzh one document")
+
+
+@pytest.mark.parametrize("group", [1024, 6144])
+def test_zh_blocks_from_lane_masks(syn_small, group, monkeypatch):
+    """k_zh takes its groups' Han blocks from k_mark_walk's lane masks: groups with
+    more Han blocks than one chunk (single-rune blocks between commas), blocks that
+    end past the lookahead round but inside the window (1-7 KiB Han runs), blocks
+    that end exactly at group and batch ends, and documents that end inside a run."""
+    monkeypatch.setenv("JB_ZH_GROUP", str(group))
+    dp, ep, s = syn_small
+    tk, o = _pair(dp, ep)
+    rng = random.Random(group)
+    han = "的一是在不了有和人这中大为上个国我以要他时来用们生到作地于出就分对成会可主发年动同工也能下过子说产种面而方后多定行学法所民得经十三之进着等部度家电力里如水化高自二理起小物现实加量都两体制机当使点从业本去把性好应开它合还因由其些然前外天政四日那社义事平形相全表间样与关各重新线内数正心反你明看原又么利比或但质气第向道命此变条只没结解问意建月公无系军很情者最立代想已通并提直题党程展五果料象员革位入常文总次品式活设及管特件长求老头基资边流路级少图山统接知较将组见计别她手角期根论运农指几九区强放决西被干做必战先回则任取据处队南给色光门即保治北造百规热领七海口东导器压志世金增争济阶油思术极交受联什认六共权收证改清己美再采转更单风切打白教速花带安场身车例真务具万每目至达走积示议声报斗完类八离华名确才科张信马节话米整空元况今集温传土许步群广石记需段研界拉林律叫且究观越织装影算低持音众书布复容儿须际商非验连断深难近矿千周委素技备半办青省列习响约支般史感劳便团往酸历市克何除消构府称太准精值号率族维划选标写存候毛亲快效斯院查江型眼王按格养易置派层片始却专状育厂京识适属圆包火住调满县局照参红细引听该铁价严"
+    docs = []
+    # dense: single-rune Han blocks between commas (more blocks than one chunk per group)
+    docs.append("，".join(rng.choice(han) for _ in range(6000)))
+    # long runs of 300..2500 runes (0.9-7.5 KiB) at varied offsets, punctuation between
+    for k in range(12):
+        pad = "a" * rng.randrange(0, 40)
+        docs.append(pad + "".join(rng.choice(han) for _ in range(rng.randrange(300, 2500))) + "。")
+    # runs ending exactly at group boundaries (3-byte runes: group/3 runes, with offsets)
+    for off in (0, 1, 2, 32):
+        docs.append("x" * off + "".join(rng.choice(han) for _ in range(group // 3)) + "，" + "".join(
+            rng.choice(han) for _ in range(50)))
+    # a document that ends inside a Han run (the next document starts Han as well)
+    docs.append("".join(rng.choice(han) for _ in range(700)))
+    docs.append("".join(rng.choice(han) for _ in range(40)))
+    buf, off = _batch_of(docs)
+    for hmm in (False, True):
+        _cmp_batch(tk, o, buf, off, hmm, f"lane-mask blocks group={group}")
+    # the same as one batch padded to a multiple of the group size
+    tail = (-int(off[-1])) % group
+    buf2, off2 = _batch_of(docs + ["中" * (tail // 3) + "a" * (tail % 3)])
+    _cmp_batch(tk, o, buf2, off2, True, f"lane-mask blocks group={group}, batch end at a group end")
+    tk.close()
