@@ -7,16 +7,18 @@
 //                 tokenizer.go:21,154-155,165-210); then the trie walk (DAG
 //                 edges) of every Han rune of the tile, one walk per lane at a
 //                 time from an LDS entry list (buildDag, :462-497)
-//   k_blocks_write  block list (start | zh<<31); its offsets from per-tile counts
-//                 and 256-tile sums that k_mark_walk adds up with atomics
-//   k_zh          one lane per Han block: backward max-prob DP over those edges +
-//                 forward path + BMES Viterbi on singleton runs
+//   k_zh          per 6 KiB group (1 KiB in small batches): its Han blocks from the
+//                 block-start masks, dealt to lanes by length; backward max-prob DP
+//                 over the edges + forward path + BMES Viterbi on singleton runs
 //                                               (cutZh/cutDAG/buildDag/calcDagProba/
 //                                                findDagPath/maxIndexProba/viterbi/cutHMM,
 //                                                tokenizer.go:221-285,462-578,668-756)
-//   k_nonzh       one lane per non-Han block: alnum runs, single runes, spaces
-//                 dropped, no-alnum blocks dropped (cutNonZh, tokenizer.go:289-310)
-//   k_tok<0>/k_tok<1>  token start/end bitmaps -> counts (+ 256-tile sums) -> (start, end) spans
+//   k_long_*      Han blocks of 8 KiB or more (one serial DP chain each)
+//   k_nonzh       the non-Han blocks with an alnum byte, from the alnum16 bits and
+//                 the masks: alnum runs, single runes, spaces dropped (cutNonZh,
+//                 tokenizer.go:289-310; blocks without alnum have no tokens)
+//   k_tok<0>/k_tok<1>  token start/end bitmaps -> counts (+ 256-tile sums, k_sup)
+//                 -> (start, end) spans
 //   k_doc_tok     per document first token (Cut per document)
 //
 // Output format on the device: two bitmaps, 1 bit per input byte each (token
@@ -749,7 +751,7 @@ __device__ uint32_t block_end_at(const uint32_t* __restrict__ lanemask, const ui
 // k_zh: Han blocks (cutZh, tokenizer.go:221-255), balanced over a wave's lanes.
 //
 // Work unit: a group = the zh blocks that start in one kZhGroupBytes span of
-// text (gstart[] from k_blocks_write), dequeued by whole waves.  The group's
+// text (read from k_mark_walk's block-start masks), taken by whole waves.  The group's
 // blocks (in chunks of at most kZhChunk) are ranked by length and dealt to
 // the 64 lanes in a snake (lane i gets ranks i, 127-i, 128+i, ...), so every
 // lane carries about the same number of runes.  Per lane, one flattened
