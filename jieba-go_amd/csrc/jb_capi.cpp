@@ -129,6 +129,13 @@ struct Device {
     uint64_t* h_misc = nullptr;  // doc offsets in / doc_tok out (u64)
     uint64_t h_misc_cap = 0;
     uint32_t* h_cnt = nullptr;   // counters (64 u32)
+    // k_small's pinned, mapped host buffers (coherent: the kernel reads and writes them directly)
+    uint8_t* h_sin = nullptr;    // text (kSmallBytes + 128), then u64 doc offsets (kSmallDocs + 1)
+    uint32_t* h_sout = nullptr;  // header, spans, doc_tok (kSmallOutBytes)
+    uint8_t* d_sin = nullptr;    // their device addresses
+    uint32_t* d_sout = nullptr;
+    bool last_small = false;     // the last batch took k_small (jb_last_stats reads small_hdr)
+    uint32_t small_hdr[kSmallHdr] = {0};
     std::vector<hipEvent_t> ev;  // span pieces landed (host batches)
     uint32_t ncu = 0;
     LaunchCfg lc{};  // launch shape, fixed at jb_open
@@ -561,6 +568,10 @@ static int init_launch_cfg(Device* d) {
 #if JB_STAMPS
     lc.diag = (uint32_t)env_int("JB_STAMPS", 0) ? 0x100u : 0u;
 #endif
+    const int sm = env_int("JB_SMALL", (int)kSmallBytes);
+    if (sm < 0 || sm > (int)kSmallBytes)
+        return fail(JB_EINVAL, "JB_SMALL=%d: want 0 (off) .. %u bytes", sm, kSmallBytes);
+    lc.small_max = (uint32_t)sm;
     return JB_OK;
 }
 
@@ -569,6 +580,7 @@ static int launch(Device* d, const uint8_t* d_text, uint64_t nbytes, const uint6
     static const bool dbg = getenv("JB_DEBUG") != nullptr;
     const LaunchCfg& lc = d->lc;
     d->last_nbytes = nbytes;
+    d->last_small = false;
     if (dbg)
         fprintf(stderr, "[jb] nbytes=%llu ndocs=%u grid_zh=%u zh_group=%u\n", (unsigned long long)nbytes,
                 ndocs, lc.grid_zh, lc.zh_group ? lc.zh_group : zh_group_for(nbytes));
@@ -696,7 +708,7 @@ extern "C" void jb_close(jb_ctx* ctx) {
         free_work(&d->w);
         dfree(d->text); dfree(d->doc_off); dfree(d->pagemap); dfree(d->emit); dfree(d->cells); dfree(d->code);
         dfree(d->wtab); dfree(d->l1row);
-        hfree(d->h_text); hfree(d->h_span); hfree(d->h_misc); hfree(d->h_cnt);
+        hfree(d->h_text); hfree(d->h_span); hfree(d->h_misc); hfree(d->h_cnt); hfree(d->h_sin); hfree(d->h_sout);
         for (hipEvent_t e : d->ev) (void)hipEventDestroy(e);
         (void)hipStreamDestroy(d->stream);
     }
@@ -709,6 +721,55 @@ extern "C" const char* jb_last_error(void) { return g_err.c_str(); }
 // cutting
 // ---------------------------------------------------------------------------
 static const uint64_t kChunkBytes = 1ull << 30;  // device offsets are u32 with a zh flag bit
+
+// A batch of at most lc.small_max bytes and kSmallDocs documents (a single Cut
+// call, BASELINE config 1): one k_small launch that reads the text and offsets
+// from mapped pinned host memory and writes the spans there, then one sync.
+// text/doc_off are the batch's (doc_off[0..nd] absolute, base = doc_off[0]).
+static int cut_small(Device* d, const uint8_t* text, const uint64_t* doc_off, uint32_t nd, bool hmm,
+                     SpanBuf* out) {
+    const uint64_t base = doc_off[0], nbytes = doc_off[nd] - base;
+    if (!d->h_sin) {
+        const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+        HIPCHK(hipHostMalloc(&d->h_sin, kSmallBytes + 128 + 8 * (kSmallDocs + 1), fl));
+        HIPCHK(hipHostMalloc(&d->h_sout, kSmallOutBytes, fl));
+        HIPCHK(hipHostGetDevicePointer((void**)&d->d_sin, d->h_sin, 0));
+        HIPCHK(hipHostGetDevicePointer((void**)&d->d_sout, d->h_sout, 0));
+    }
+    if (nbytes) memcpy(d->h_sin, text + base, nbytes);
+    memset(d->h_sin + nbytes, 0, 16);
+    uint64_t* const hoff = reinterpret_cast<uint64_t*>(d->h_sin + kSmallBytes + 128);
+    for (uint32_t k = 0; k <= nd; k++) hoff[k] = doc_off[k] - base;
+    const hipError_t e = run_small(d->dim, d->d_sin, (uint32_t)nbytes,
+                                   reinterpret_cast<const uint64_t*>(d->d_sin + kSmallBytes + 128), nd, hmm,
+                                   d->d_sout, d->stream);
+    if (e != hipSuccess) return fail(JB_EDEVICE, "k_small launch: %s", hipGetErrorString(e));
+    HIPCHK(hipStreamSynchronize(d->stream));
+    const uint32_t* h = d->h_sout;
+    memcpy(d->small_hdr, h, sizeof d->small_hdr);
+    d->last_small = true;
+    if (h[SM_ERR]) return fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)");
+    if (h[SM_NTOK] != h[SM_NTOKE])
+        return fail(JB_EDEVICE, "internal: %u token starts vs %u ends", h[SM_NTOK], h[SM_NTOKE]);
+    const uint32_t nt = h[SM_NTOK];
+    const uint32_t* hs = h + kSmallHdr;
+    const uint32_t* he = hs + kSmallBytes;
+    const uint64_t* dt = reinterpret_cast<const uint64_t*>(he + kSmallBytes);
+    const bool write = out->reserve(out->n + nt);
+    if (!write && !out->external) return fail(JB_ENOMEM, "out of host memory for %u tokens", nt);
+    if (write) {
+        for (uint32_t k = 0; k < nt; k++) {
+            out->s[out->n + k] = base + hs[k];
+            out->e[out->n + k] = base + he[k];
+        }
+    } else {  // caller arrays too small: count the rest, write nothing more
+        out->needed = out->n + nt;
+        out->cap = 0;
+    }
+    out->n += nt;
+    for (uint32_t k = 0; k < nd; k++) out->per_doc.push_back(dt[k + 1] - dt[k]);
+    return JB_OK;
+}
 
 // Cut documents [d0, d1) of a host batch on one device; appends spans to `out`.
 // Host text goes through pinned staging (full-speed DMA), spans come back into
@@ -728,6 +789,11 @@ static int cut_range(jb_ctx* ctx, Device* d, const uint8_t* text, const uint64_t
         const uint64_t base = doc_off[a], nbytes = doc_off[b] - base;
         const uint32_t nd = b - a;
         int rc;
+        if (d->lc.small_max && nbytes <= d->lc.small_max && nd <= kSmallDocs) {
+            if ((rc = cut_small(d, text, doc_off + a, nd, hmm, out))) return rc;
+            a = b;
+            continue;
+        }
         if ((rc = ensure_staging(d, nbytes, nd))) return rc;
         if ((rc = ensure_work(d, nbytes, nd))) return rc;
         static const bool tdbg = getenv("JB_DEBUG") != nullptr;
@@ -1127,6 +1193,13 @@ extern "C" int jb_last_stats(jb_ctx* ctx, jb_stats* out) {
     std::shared_lock<std::shared_mutex> rl(ctx->lock);
     for (auto& d : ctx->devs) {
         std::lock_guard<std::mutex> g(d->mu);
+        if (d->last_small) {  // k_small's counters came back with its spans
+            out->tokens += d->small_hdr[SM_NTOK];
+            out->blocks += d->small_hdr[SM_BLOCKS];
+            out->zh_blocks += d->small_hdr[SM_ZHBLOCKS];
+            out->viterbi_ties += d->small_hdr[SM_TIES];
+            continue;
+        }
         if (!d->w.counters) continue;
         HIPCHK(hipSetDevice(d->ordinal));
         HIPCHK(hipDeviceSynchronize());  // (jb_cut_device may have queued on a caller's stream)

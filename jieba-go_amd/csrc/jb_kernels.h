@@ -101,6 +101,7 @@ struct LaunchCfg {
     uint32_t grid_zh;   // persistent grid of k_zh
     uint32_t zh_group;  // k_zh group bytes (0: zh_group_for(nbytes))
     uint32_t diag;      // diagnostic clocks (STAMPS builds only; 0 otherwise)
+    uint32_t small_max; // host batches up to this many bytes take k_small (0: never)
 };
 
 // Enqueue the whole Cut pipeline on `stream`.  Returns hipSuccess or the first
@@ -108,6 +109,19 @@ struct LaunchCfg {
 hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text, uint64_t nbytes,
                         const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, const LaunchCfg& lc,
                         hipStream_t stream, KernelTimer* timer);
+
+// One-workgroup path for small batches (k_small): the text and document offsets
+// are read from `text`/`doc_off` (device or mapped pinned host memory; text
+// readable 16 bytes past nbytes), the results written to `out`:
+//   u32 header[kSmallHdr] (SM_*), u32 tok_start[kSmallBytes], u32 tok_end[kSmallBytes],
+//   u64 doc_tok[ndocs + 1]
+constexpr uint32_t kSmallBytes = 4096;  // 256 threads x 16 bytes
+constexpr uint32_t kSmallDocs = 4096;
+constexpr uint32_t kSmallHdr = 16;
+constexpr uint64_t kSmallOutBytes = 4ull * (kSmallHdr + 2ull * kSmallBytes) + 8ull * (kSmallDocs + 1ull);
+enum { SM_NTOK = 0, SM_NTOKE, SM_ERR, SM_TIES, SM_BLOCKS, SM_ZHBLOCKS };
+hipError_t run_small(const DevImage& im, const uint8_t* text, uint32_t nbytes, const uint64_t* doc_off,
+                     uint32_t ndocs, bool hmm, uint32_t* out, hipStream_t stream);
 
 // Resident k_zh workgroups per CU (occupancy API).
 uint32_t zh_blocks_per_cu(bool hmm);

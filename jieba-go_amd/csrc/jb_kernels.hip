@@ -2603,8 +2603,396 @@ __global__ void k_doc_tok(const uint64_t* __restrict__ doc_off, uint32_t ndocs, 
 }
 
 // ---------------------------------------------------------------------------
+// k_small: a whole small batch (<= kSmallBytes of text) in one workgroup, for
+// single Cut calls (tokenizer.go:151-162; BASELINE config 1).  The eleven-kernel
+// pipeline costs a dozen launches for a sentence; here one launch reads the
+// text and document offsets straight from the caller's pinned host buffer,
+// keeps everything in LDS and writes the spans back into pinned host memory.
+// Same rules as the pipeline, in phases separated by barriers:
+//   1  text -> LDS; document starts; per lead byte the Go utf8.DecodeRune width
+//      (bounded by the document end) and Han-ness (zh regex, :21)
+//   2  rune starts (bytes no valid sequence covers), block starts (document
+//      starts and changes of Han-ness: splitText, :154-155,165-210)
+//   3  the Han runes and the blocks in text order (workgroup scans)
+//   4  per Han rune (one thread each): dense code and emissions -> LDS
+//   5  per Han rune: its trie walk (buildDag, :462-497) -> up to 4 edges
+//      (length, end byte, weight) in LDS; more edges: the DP walks it again
+//   6  per block (one thread each): Han blocks get the backward DP
+//      (calcDagProba + maxIndexProba, :502-578), the forward path (findDagPath,
+//      :552-562) and the Viterbi of single-rune runs (:228-253,668-756), all
+//      from LDS; other blocks get cutNonZh (:289-310)
+//   7  token bitmaps -> spans, per-document first tokens, counters
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSmallSlots = kSmallBytes / 3u + 2u;
+constexpr uint32_t kSmallWords = kSmallBytes / 32u + 2u;
+
+struct SmallLds {
+    alignas(16) uint8_t txt[kSmallBytes + 128];
+    uint8_t wd[kSmallBytes + 16];  // per byte: DecodeRune width at a lead byte (1 otherwise)
+    uint32_t docb[kSmallWords];    // document starts
+    uint32_t rsb[kSmallWords];     // rune starts
+    uint32_t hsb[kSmallWords];     // Han rune starts
+    uint32_t bsb[kSmallWords];     // block starts
+    uint32_t sb[kSmallWords];      // token first bytes
+    uint32_t eb[kSmallWords];      // token last bytes
+    uint32_t swp[kSmallWords];     // token starts before each word
+    uint32_t scan[8];
+    uint32_t nh, nblk, nzh, err, ties;
+    uint16_t hpos[kSmallSlots];     // Han rune starts, text order
+    uint16_t blist[kSmallBytes + 2];  // block starts, text order
+    // per Han rune, at slot = byte / 3 (Han runes are >= 3 bytes)
+    uint32_t scode[kSmallSlots];
+    uint8_t sn[kSmallSlots];  // edges held (0xFF: more than 4, walked again by the DP)
+    uint8_t sbl[kSmallSlots];  // chosen piece length, then Viterbi back-pointers / labels
+    uint8_t sL[kSmallSlots][4];
+    uint16_t se[kSmallSlots][4];  // end byte of each edge
+    double sw[kSmallSlots][4];
+    double sbest[kSmallSlots];
+    double sem[kSmallSlots][4];  // emissions B, M, E, S
+};
+static_assert(sizeof(SmallLds) <= 163840u, "k_small: one workgroup's LDS");
+
+struct SmlZv {  // text and slots in LDS (viterbi_back, z_prev)
+    static constexpr bool all3 = false;
+    const uint8_t* tx;
+    uint8_t* bls;
+    __device__ __forceinline__ uint32_t b(uint32_t q) const { return tx[q]; }
+    __device__ __forceinline__ uint32_t x4(uint32_t q) const { return lds4(tx, q); }
+    __device__ __forceinline__ uint8_t& bl(uint32_t q) const { return bls[q / 3u]; }
+};
+
+__device__ __forceinline__ bool sm_bit(const uint32_t* b, uint32_t p) { return (b[p >> 5] >> (p & 31u)) & 1u; }
+
+// The trie walk from the Han rune at p (dp_walk_rune's rules, :462-497): f(L, end
+// byte, weight) for each DAG edge in ascending L.  The walk goes on while the
+// next rune is a Han rune of the same block.
+template <class F>
+__device__ __forceinline__ void sm_walk(const SmallLds& s, const DevImage& im, uint32_t p, F&& f) {
+    uint32_t id = s.scode[p / 3u];
+    uint64_t cc = im.cells[id];
+    const uint32_t w0 = s.wd[p];
+    if (jb_cell_check(cc) != JB_CHECK_ROOT) {  // not a key: the rune alone, tf 1.0 (:468-471,515-518)
+        f(1u, p + w0, im.wtab[JB_WIDX_ABSENT]);
+        return;
+    }
+    if (jb_cell_fc(cc) == JB_FC_ZERO) {  // count == 0: the rune alone, Log(0) (:468-471)
+        f(1u, p + w0, im.wtab[jb_cell_widx(cc)]);
+        return;
+    }
+    if (jb_cell_fc(cc) == JB_FC_POS) f(1u, p + w0, im.wtab[jb_cell_widx(cc)]);
+    uint32_t qq = p + w0, len = 1;
+    bool go = jb_cell_hc(cc) != 0u;
+    while (go && sm_bit(s.hsb, qq) && !sm_bit(s.bsb, qq)) {
+        const uint32_t tt = dat_slot_k(cc, s.scode[qq / 3u]);
+        const uint64_t ch = im.cells[tt];
+        if (!dat_hit(ch, id)) break;  // (:475-478)
+        ++len;
+        qq += s.wd[qq];
+        if (jb_cell_fc(ch) == JB_FC_POS) f(len, qq, im.wtab[jb_cell_widx(ch)]);
+        go = jb_cell_hc(ch) != 0u;
+        id = tt;
+        cc = ch;
+    }
+}
+
+// viterbi_run (:668-756 + cutHMM :273-285) with the emissions from LDS
+template <class E>
+__device__ void sm_viterbi(const SmlZv& v, const SmallLds& s, uint32_t rs, uint32_t re, uint32_t m, E& em) {
+    if (m == 1) {  // always "S" for a single rune (:672-674)
+        em.token(rs, re);
+        return;
+    }
+    const double* e = s.sem[rs / 3u];
+    double vB = START_B + e[0], vM = JB_MIN_FLOAT + e[1], vE = JB_MIN_FLOAT + e[2], vS = START_S + e[3];
+    uint32_t q = rs + s.wd[rs];
+    while (q < re) {
+        uint32_t cB, cM, cE, cS;
+        double pB, pM, pE, pS;
+        route2(vE + T_EB, vS + T_SB, &cB, &pB, em.ties);  // B <- E, S
+        route2(vB + T_BM, vM + T_MM, &cM, &pM, em.ties);  // M <- B, M
+        route2(vB + T_BE, vM + T_ME, &cE, &pE, em.ties);  // E <- B, M
+        route2(vE + T_ES, vS + T_SS, &cS, &pS, em.ties);  // S <- E, S
+        e = s.sem[q / 3u];
+        vB = pB + e[0];
+        vM = pM + e[1];
+        vE = pE + e[2];
+        vS = pS + e[3];
+        v.bl(q) = (uint8_t)(cB | (cM << 2) | (cE << 4) | (cS << 6));
+        q += s.wd[q];
+    }
+    viterbi_back(v, rs, re, m, vE > vS ? (uint32_t)JB_E : (uint32_t)JB_S, em);  // (:723-729)
+}
+
+// cutNonZh for the block [bs, be) from LDS (nonzh_block's rules, :289-310)
+template <class E>
+__device__ void sm_nonzh(const uint8_t* tx, uint32_t bs, uint32_t be, E& em) {
+    bool has = false;  // alnum.FindAllIndex found nothing -> no tokens (:290-293)
+    for (uint32_t p = bs; p < be && !has; p++) has = jb_is_alnum(tx[p]);
+    if (!has) return;
+    uint32_t p = bs, run = 0;
+    bool in_run = false;
+    while (p < be) {
+        const uint32_t x = lds4(tx, p);
+        if (jb_is_alnum(x & 0xFFu)) {  // alnum runs are kept whole
+            if (!in_run) {
+                in_run = true;
+                run = p;
+            }
+            p++;
+            continue;
+        }
+        if (in_run) {
+            em.token(run, p);
+            in_run = false;
+        }
+        uint32_t r;
+        const uint32_t w = jb_decode(x, min(4u, be - p), &r);
+        if (!jb_is_space(r)) em.token(p, p + w);  // one token per rune; spaces dropped
+        p += w;
+    }
+    if (in_run) em.token(run, be);
+}
+
+// out: u32 header[kSmallHdr] (SM_*), then tok_start[kSmallBytes], tok_end[kSmallBytes],
+// then doc_tok u64[ndocs + 1].  text is readable 16 bytes past nbytes.
+template <bool HMM>
+__global__ __launch_bounds__(256) void k_small(const uint8_t* __restrict__ text, uint32_t nbytes,
+                                               const uint64_t* __restrict__ doc_off, uint32_t ndocs, DevImage im,
+                                               uint32_t* __restrict__ out) {
+    __shared__ SmallLds s;
+    const uint32_t t = threadIdx.x;
+    const uint32_t nw = (nbytes + 31u) / 32u;
+    // 1. text (zero past nbytes), bitmaps cleared
+    for (uint32_t i = t; i < (kSmallBytes + 128u) / 16u; i += 256u) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (16u * i < nbytes) {
+            v = *reinterpret_cast<const uint4*>(text + 16u * i);
+            uint32_t* w = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t b = 16u * i + 4u * (uint32_t)k;
+                if (b + 4u > nbytes) w[k] = b >= nbytes ? 0u : w[k] & ((1u << (8u * (nbytes - b))) - 1u);
+            }
+        }
+        *reinterpret_cast<uint4*>(s.txt + 16u * i) = v;
+    }
+    for (uint32_t i = t; i < kSmallWords; i += 256u) {
+        s.docb[i] = s.rsb[i] = s.hsb[i] = s.bsb[i] = s.sb[i] = s.eb[i] = 0u;
+    }
+    if (t == 0) s.err = s.ties = s.nzh = 0u;
+    __syncthreads();
+    for (uint32_t d = t; d < ndocs; d += 256u) {
+        const uint64_t o = doc_off[d];
+        if (o < nbytes) atomicOr(&s.docb[o >> 5], 1u << (o & 31u));
+    }
+    __syncthreads();
+    // widths at lead bytes: thread t owns bytes [16t, 16t + 16)
+    const uint32_t p0 = 16u * t;
+    uint32_t hanm = 0;  // Han lead bytes of the thread's 16
+    for (uint32_t k = 0; k < 16u; k++) {
+        const uint32_t p = p0 + k;
+        uint32_t w = 1;
+        if (p < nbytes && s.txt[p] >= 0xC0u) {
+            uint32_t lim = min(4u, nbytes - p);
+            for (uint32_t j = 1; j < lim; j++)
+                if (sm_bit(s.docb, p + j)) {
+                    lim = j;
+                    break;
+                }
+            uint32_t r;
+            w = dec_lead(lds4(s.txt, p), lim, &r);
+            if (w >= 3u && han_cp(r)) hanm |= 1u << k;
+        }
+        s.wd[p] = (uint8_t)w;
+    }
+    __syncthreads();
+    // 2. rune starts: bytes that no valid sequence of the 3 bytes before covers
+    uint32_t rs16 = 0;
+    for (uint32_t k = 0; k < 16u; k++) {
+        const uint32_t p = p0 + k;
+        if (p >= nbytes) break;
+        const bool cov = (p >= 1u && s.wd[p - 1u] >= 2u) || (p >= 2u && s.wd[p - 2u] >= 3u) ||
+                         (p >= 3u && s.wd[p - 3u] >= 4u);
+        if (!cov) rs16 |= 1u << k;
+    }
+    if (rs16) atomicOr(&s.rsb[p0 >> 5], rs16 << (p0 & 31u));
+    if (hanm) atomicOr(&s.hsb[p0 >> 5], hanm << (p0 & 31u));
+    __syncthreads();
+    uint32_t bs16 = 0;
+    for (uint32_t m = rs16; m; m &= m - 1u) {
+        const uint32_t k = (uint32_t)__builtin_ctz(m), p = p0 + k;
+        bool st = p == 0u || sm_bit(s.docb, p);
+        if (!st) {  // Han-ness of the previous rune (it starts at most 4 bytes back)
+            uint32_t q = p - 1u;
+            while (!sm_bit(s.rsb, q)) q--;
+            st = sm_bit(s.hsb, q) != ((hanm >> k) & 1u);
+        }
+        if (st) bs16 |= 1u << k;
+    }
+    if (bs16) atomicOr(&s.bsb[p0 >> 5], bs16 << (p0 & 31u));
+    __syncthreads();
+    // 3. Han runes and blocks in text order
+    {
+        uint32_t tot;
+        const uint32_t hb = block_scan_u32((uint32_t)__popc(hanm), s.scan, &tot);
+        uint32_t i = hb;
+        for (uint32_t m = hanm; m; m &= m - 1u) s.hpos[i++] = (uint16_t)(p0 + (uint32_t)__builtin_ctz(m));
+        if (t == 0) s.nh = tot;
+        const uint32_t bb = block_scan_u32((uint32_t)__popc(bs16), s.scan, &tot);
+        i = bb;
+        uint32_t nz = 0;
+        for (uint32_t m = bs16; m; m &= m - 1u) {
+            const uint32_t k = (uint32_t)__builtin_ctz(m);
+            s.blist[i++] = (uint16_t)(p0 + k);
+            nz += (hanm >> k) & 1u;
+        }
+        if (nz) atomicAdd(&s.nzh, nz);
+        if (t == 0) s.nblk = tot;
+    }
+    __syncthreads();
+    const uint32_t nh = s.nh, nblk = s.nblk;
+    // 4. codes (and emissions) of the Han runes
+    for (uint32_t h = t; h < nh; h += 256u) {
+        const uint32_t p = s.hpos[h];
+        uint32_t r;
+        (void)dec_lead(lds4(s.txt, p), 4u, &r);
+        const uint32_t row = jb_row(im.pagemap, r);
+        s.scode[p / 3u] = im.code[row];
+        if (HMM) {
+            const double2* ep = reinterpret_cast<const double2*>(im.emit) + (size_t)row * 2u;
+            const double2 a = ep[0], b = ep[1];
+            double* e = s.sem[p / 3u];
+            e[0] = a.x; e[1] = a.y; e[2] = b.x; e[3] = b.y;
+        }
+    }
+    __syncthreads();
+    // 5. DAG edges of every Han rune
+    for (uint32_t h = t; h < nh; h += 256u) {
+        const uint32_t p = s.hpos[h], sl = p / 3u;
+        uint32_t n = 0;
+        sm_walk(s, im, p, [&](uint32_t L, uint32_t e, double w) {
+            if (n < 4u) {
+                s.sL[sl][n] = (uint8_t)L;
+                s.se[sl][n] = (uint16_t)e;
+                s.sw[sl][n] = w;
+            }
+            n++;
+        });
+        s.sn[sl] = n <= 4u ? (uint8_t)n : (uint8_t)0xFFu;
+    }
+    __syncthreads();
+    // 6. blocks, one thread each
+    LdsEmitter em(s.sb, s.eb, 0u);
+    const SmlZv v{s.txt, s.sbl};
+    for (uint32_t k = t; k < nblk; k += 256u) {
+        const uint32_t bs = s.blist[k], be = k + 1u < nblk ? s.blist[k + 1u] : nbytes;
+        if (!sm_bit(s.hsb, bs)) {
+            sm_nonzh(s.txt, bs, be, em);
+            continue;
+        }
+        // backward DP (calcDagProba, :502-548): best(i) from best(i + L); best(n) = 0.0
+        uint32_t q = z_prev(v, be, bs);
+        for (;;) {
+            const uint32_t sl = q / 3u;
+            DpFold f;
+            auto item = [&](uint32_t L, uint32_t e, double w) {
+                const double pp = w + (e == be ? 0.0 : s.sbest[e / 3u]);  // pieceProba (:519-529)
+                if (pp >= f.prevP) {  // maxIndexProba (:565-578)
+                    f.bestL = L;
+                    f.bestP = pp;
+                }
+                f.prevP = pp;
+                f.lastL = L;
+            };
+            const uint32_t n = s.sn[sl];
+            if (n == 0xFFu) {
+                sm_walk(s, im, q, item);
+            } else {
+                for (uint32_t j = 0; j < n; j++) item(s.sL[sl][j], s.se[sl][j], s.sw[sl][j]);
+            }
+            f.finish();
+            s.sbest[sl] = f.bestP;
+            s.sbl[sl] = (uint8_t)f.bestL;
+            if (q == bs) break;
+            q = z_prev(v, q, bs);
+        }
+        // forward path (findDagPath, :552-562) + HMM runs (cutZh, :221-255)
+        uint32_t p = bs, run_s = 0, run_n = 0;
+        bool ok = true;
+        while (p < be) {
+            const uint32_t L = s.sbl[p / 3u];
+            if (L == 0) {  // tail index -1: cutDAG's slice panics in the reference
+                ok = false;
+                break;
+            }
+            uint32_t pe = p;
+            for (uint32_t j = 0; j < L; j++) pe += s.wd[pe];
+            if (!HMM) {
+                em.token(p, pe);
+            } else if (L == 1) {
+                if (run_n == 0) run_s = p;
+                run_n++;
+            } else {
+                if (run_n) {
+                    sm_viterbi(v, s, run_s, p, run_n, em);
+                    run_n = 0;
+                }
+                em.token(p, pe);
+            }
+            p = pe;
+        }
+        if (!ok) {
+            s.err = 1u;
+            continue;
+        }
+        if (HMM && run_n) sm_viterbi(v, s, run_s, be, run_n, em);
+    }
+    em.flush();
+    if (em.ties) atomicAdd(&s.ties, em.ties);
+    __syncthreads();
+    // 7. spans, per-document first tokens, counters
+    const uint32_t sw_ = t < nw ? s.sb[t] : 0u, ew = t < nw ? s.eb[t] : 0u;
+    uint32_t ts, te;
+    const uint32_t xs = block_scan_u32((uint32_t)__popc(sw_), s.scan, &ts);
+    const uint32_t xe = block_scan_u32((uint32_t)__popc(ew), s.scan, &te);
+    uint32_t* const os = out + kSmallHdr;
+    uint32_t* const oe = os + kSmallBytes;
+    if (t < nw) {
+        s.swp[t] = xs;
+        uint32_t g = xs;
+        for (uint32_t m = sw_; m; m &= m - 1u) os[g++] = 32u * t + (uint32_t)__builtin_ctz(m);
+        g = xe;
+        for (uint32_t m = ew; m; m &= m - 1u) oe[g++] = 32u * t + (uint32_t)__builtin_ctz(m) + 1u;
+    }
+    __syncthreads();
+    uint64_t* const dt = reinterpret_cast<uint64_t*>(oe + kSmallBytes);
+    for (uint32_t d = t; d <= ndocs; d += 256u) {
+        const uint64_t o = doc_off[d];
+        uint32_t c = ts;
+        if (o < nbytes) c = s.swp[o >> 5] + (uint32_t)__popc(s.sb[o >> 5] & ((1u << (o & 31u)) - 1u));
+        dt[d] = c;
+    }
+    if (t == 0) {
+        out[SM_NTOK] = ts;
+        out[SM_NTOKE] = te;
+        out[SM_ERR] = s.err;
+        out[SM_TIES] = s.ties;
+        out[SM_BLOCKS] = nblk;
+        out[SM_ZHBLOCKS] = s.nzh;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
+hipError_t run_small(const DevImage& im, const uint8_t* text, uint32_t nbytes, const uint64_t* doc_off,
+                     uint32_t ndocs, bool hmm, uint32_t* out, hipStream_t stream) {
+    if (nbytes > kSmallBytes || ndocs > kSmallDocs) return hipErrorInvalidValue;
+    if (hmm) hipLaunchKernelGGL((k_small<true>), dim3(1), dim3(256), 0, stream, text, nbytes, doc_off, ndocs, im, out);
+    else hipLaunchKernelGGL((k_small<false>), dim3(1), dim3(256), 0, stream, text, nbytes, doc_off, ndocs, im, out);
+    return hipGetLastError();
+}
+
 template <bool HMM>
 static uint32_t occ_zh() {
     int n = 0;

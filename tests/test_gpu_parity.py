@@ -363,6 +363,12 @@ def test_record_overflow_paths(tmp_path, syn_small, kind):
         buf, off = _batch_of(texts)
         for hmm in (False, True):
             _cmp_batch(tk, o, buf, off, hmm, f"overflow kind={kind} hmm={hmm}")
+        # the same texts in batches of at most 4 KiB (k_small: its DP walks runes
+        # with more than 4 edges again, edges up to the longest key)
+        for i, docs in enumerate(_small_batches(texts)):
+            bufs, offs = _batch_of(docs)
+            for hmm in (False, True):
+                _cmp_batch(tk, o, bufs, offs, hmm, f"overflow small batch {i} kind={kind} hmm={hmm}")
     finally:
         tk.close()
 
@@ -676,3 +682,67 @@ def test_zh_blocks_from_lane_masks(syn_small, group, monkeypatch):
     buf2, off2 = _batch_of(docs + ["中" * (tail // 3) + "a" * (tail % 3)])
     _cmp_batch(tk, o, buf2, off2, True, f"lane-mask blocks group={group}, batch end at a group end")
     tk.close()
+
+
+def _small_batches(texts, limit=4096, max_docs=4096):
+    """Group texts (in order) into batches of at most `limit` bytes and `max_docs`
+    documents: the batches a one-workgroup k_small launch takes whole."""
+    out, cur, size = [], [], 0
+    for t in texts:
+        b = t.encode("utf-8") if isinstance(t, str) else t
+        if len(b) > limit:
+            continue
+        if cur and (size + len(b) > limit or len(cur) >= max_docs):
+            out.append(cur)
+            cur, size = [], 0
+        cur.append(b)
+        size += len(b)
+    if cur:
+        out.append(cur)
+    return out
+
+
+def test_small_batches_one_workgroup(syn_small, monkeypatch):
+    """Batches of at most 4 KiB (a single Cut call, BASELINE config 1) take k_small:
+    one workgroup, text and offsets read from mapped pinned host memory, the whole
+    Cut path in LDS.  Against the oracle and against the eleven-kernel pipeline
+    (JB_SMALL=0, read at jb_open), bit-exact, with the same block, Han-block, token
+    and Viterbi-tie counts: edge texts, invalid UTF-8 split by documents, random
+    mixed scripts, empty documents, dense Han up to the 4096-byte limit, 4-byte Han
+    runes, and batches just past the limits (which take the pipeline)."""
+    dp, ep, s = syn_small
+    tk, o = _pair(dp, ep)
+    monkeypatch.setenv("JB_SMALL", "0")
+    tp = J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep))
+    monkeypatch.delenv("JB_SMALL")
+    rng = random.Random(4096)
+    texts = list(EDGE_TEXTS)
+    pieces = [x.encode() for x in ("中", "文", "a", " ", "　", "𠀀", "，", "ab12", "é")] + \
+        [b"\xe4", b"\xb8\xad", b"\xf0\x9f", b"\x80", b"\xc2", b"\xff", b"\xed\xa0\x80"]
+    texts += [b"".join(rng.choice(pieces) for _ in range(rng.randint(0, 16))) for _ in range(600)]
+    alphabet = [chr(c) for c in range(0x4E00, 0x4E00 + 3000, 3)] + ["㐀", "㒐", "a", "Z", "9", " ", "，", "。",
+                                                                    "　", "ス", "한", "\n", "𠀀", "々"]
+    texts += ["".join(rng.choice(alphabet) for _ in range(rng.randint(0, 300))) for _ in range(300)]
+    batches = _small_batches(texts)
+    batches += [[("丁" * 1365).encode()], [("一丁" * 682).encode() + b"ab"], [("𠀀" * 1024).encode()],
+                [b""] * 4096, [b""] * 100 + ["中文".encode()] + [b""] * 100, [b"x" * 4096],
+                [("中" * 1365 + "a").encode()],                      # 4097 bytes: pipeline
+                [b""] * 4097]                                          # 4097 documents: pipeline
+    n_small = 0
+    for i, docs in enumerate(batches):
+        buf, off = _batch_of(docs)
+        small = int(off[-1]) <= 4096 and len(docs) <= 4096
+        n_small += small
+        for hmm in (False, True):
+            _cmp_batch(tk, o, buf, off, hmm, f"small batch {i} hmm={hmm}")
+            st = tk.last_stats()
+            _cmp_batch(tp, o, buf, off, hmm, f"pipeline batch {i} hmm={hmm}")
+            sp = tp.last_stats()
+            if int(off[-1]):
+                for k in ("tokens", "blocks", "zh_blocks", "viterbi_ties"):
+                    assert st[k] == sp[k], (i, hmm, k, st, sp)
+    assert n_small >= 20
+    # the reference's benchmark sentence through Cut
+    assert tk.Cut(SENTENCE, True) == o.cut(SENTENCE, True) == tp.Cut(SENTENCE, True)
+    tk.close()
+    tp.close()
