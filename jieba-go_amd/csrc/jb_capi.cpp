@@ -135,6 +135,8 @@ struct Device {
     uint8_t* d_sin = nullptr;    // their device addresses
     uint32_t* d_sout = nullptr;
     bool last_small = false;     // the last batch took k_small (jb_last_stats reads small_hdr)
+    hipStream_t sstream = nullptr;  // k_small's stream, masked to one CU (its code stays in that I-cache)
+    uint32_t small_seq = 0;         // k_small calls: the kernel writes this number last
     uint32_t small_hdr[kSmallHdr] = {0};
     std::vector<hipEvent_t> ev;  // span pieces landed (host batches)
     uint32_t ncu = 0;
@@ -689,6 +691,16 @@ extern "C" int jb_open(const jb_config* cfg, jb_ctx** out) {
         HIPCHK(hipGetDeviceProperties(&prop, d->ordinal));
         d->ncu = (uint32_t)prop.multiProcessorCount;
         HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        {
+            // k_small runs one workgroup per call: pinned to one CU (JB_SMALL_CU, default 0) it
+            // finds its 21 KB of code in that CU's instruction cache (and the trie's hot lines
+            // in that XCD's L2) instead of fetching them cold on whichever CU the dispatcher picks
+            const int cu = env_int("JB_SMALL_CU", 0);
+            if (cu < 0 || cu >= (int)d->ncu) return fail(JB_EINVAL, "JB_SMALL_CU=%d: %u CUs", cu, d->ncu);
+            std::vector<uint32_t> mask((d->ncu + 31) / 32, 0u);
+            mask[cu / 32] = 1u << (cu % 32);
+            HIPCHK(hipExtStreamCreateWithCUMask(&d->sstream, (uint32_t)mask.size(), mask.data()));
+        }
         if ((rc = upload_image(d.get(), img->img))) return rc;
         if ((rc = init_launch_cfg(d.get()))) return rc;
         ctx->devs.push_back(std::move(d));
@@ -702,6 +714,7 @@ extern "C" void jb_close(jb_ctx* ctx) {
     for (auto& d : ctx->devs) {
         (void)hipSetDevice(d->ordinal);
         (void)hipStreamSynchronize(d->stream);
+        if (d->sstream) (void)hipStreamSynchronize(d->sstream);
         d->timer.reset();
         if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
         d->gexec = nullptr;
@@ -711,6 +724,7 @@ extern "C" void jb_close(jb_ctx* ctx) {
         hfree(d->h_text); hfree(d->h_span); hfree(d->h_misc); hfree(d->h_cnt); hfree(d->h_sin); hfree(d->h_sout);
         for (hipEvent_t e : d->ev) (void)hipEventDestroy(e);
         (void)hipStreamDestroy(d->stream);
+        if (d->sstream) (void)hipStreamDestroy(d->sstream);
     }
     delete ctx;
 }
@@ -736,18 +750,44 @@ static int cut_small(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         HIPCHK(hipHostGetDevicePointer((void**)&d->d_sin, d->h_sin, 0));
         HIPCHK(hipHostGetDevicePointer((void**)&d->d_sout, d->h_sout, 0));
     }
+    const auto c0 = std::chrono::steady_clock::now();
     if (nbytes) memcpy(d->h_sin, text + base, nbytes);
     memset(d->h_sin + nbytes, 0, 16);
     uint64_t* const hoff = reinterpret_cast<uint64_t*>(d->h_sin + kSmallBytes + 128);
     for (uint32_t k = 0; k <= nd; k++) hoff[k] = doc_off[k] - base;
+    // the kernel writes the call's sequence number after everything else (system-scope
+    // release); spinning on it returns as soon as the results are in host memory
+    const uint32_t seq = ++d->small_seq;
+    volatile uint32_t* done = d->h_sout + SM_DONE;
     const hipError_t e = run_small(d->dim, d->d_sin, (uint32_t)nbytes,
                                    reinterpret_cast<const uint64_t*>(d->d_sin + kSmallBytes + 128), nd, hmm,
-                                   d->d_sout, d->stream);
+                                   d->d_sout, seq, d->sstream);
     if (e != hipSuccess) return fail(JB_EDEVICE, "k_small launch: %s", hipGetErrorString(e));
-    HIPCHK(hipStreamSynchronize(d->stream));
+    const auto c1 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0; *done != seq; spin++) {
+        if ((spin & 1023u) != 1023u) continue;
+        const hipError_t q = hipStreamQuery(d->sstream);
+        if (q == hipErrorNotReady) continue;
+        if (q != hipSuccess) return fail(JB_EDEVICE, "k_small: %s", hipGetErrorString(q));
+        if (*done != seq) return fail(JB_EDEVICE, "k_small finished without its completion word");
+        break;
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    const auto c2 = std::chrono::steady_clock::now();
     const uint32_t* h = d->h_sout;
     memcpy(d->small_hdr, h, sizeof d->small_hdr);
     d->last_small = true;
+    static const bool dbg = getenv("JB_DEBUG") != nullptr;
+    if (dbg) {  // k_small's phase clocks (10 ns ticks from its start)
+        auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+            return std::chrono::duration<double, std::micro>(b - a).count();
+        };
+        fprintf(stderr, "[jb] k_small %llu bytes: stage+launch %.2f us, sync %.2f us; phases (us):",
+                (unsigned long long)nbytes, us(c0, c1), us(c1, c2));
+        for (int k = 0; k < 15; k++) fprintf(stderr, " %.2f", h[SM_CLK + k] * 0.01);
+        fprintf(stderr, "; %u clocks", h[SM_CLK + 15]);
+        fprintf(stderr, "\n");
+    }
     if (h[SM_ERR]) return fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)");
     if (h[SM_NTOK] != h[SM_NTOKE])
         return fail(JB_EDEVICE, "internal: %u token starts vs %u ends", h[SM_NTOK], h[SM_NTOKE]);

@@ -115,13 +115,14 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
 // readable 16 bytes past nbytes), the results written to `out`:
 //   u32 header[kSmallHdr] (SM_*), u32 tok_start[kSmallBytes], u32 tok_end[kSmallBytes],
 //   u64 doc_tok[ndocs + 1]
-constexpr uint32_t kSmallBytes = 4096;  // 256 threads x 16 bytes
+constexpr uint32_t kSmallBytes = 4096;  // 1024 threads x 4 bytes
 constexpr uint32_t kSmallDocs = 4096;
-constexpr uint32_t kSmallHdr = 16;
+constexpr uint32_t kSmallHdr = 32;
 constexpr uint64_t kSmallOutBytes = 4ull * (kSmallHdr + 2ull * kSmallBytes) + 8ull * (kSmallDocs + 1ull);
-enum { SM_NTOK = 0, SM_NTOKE, SM_ERR, SM_TIES, SM_BLOCKS, SM_ZHBLOCKS };
+enum { SM_NTOK = 0, SM_NTOKE, SM_ERR, SM_TIES, SM_BLOCKS, SM_ZHBLOCKS, SM_DONE, SM_CLK = 8 };  // SM_CLK..+10: phase clocks (10 ns ticks)
+// out[SM_DONE] = seq is the kernel's last write (after a system-scope release).
 hipError_t run_small(const DevImage& im, const uint8_t* text, uint32_t nbytes, const uint64_t* doc_off,
-                     uint32_t ndocs, bool hmm, uint32_t* out, hipStream_t stream);
+                     uint32_t ndocs, bool hmm, uint32_t* out, uint32_t seq, hipStream_t stream);
 
 // Resident k_zh workgroups per CU (occupancy API).
 uint32_t zh_blocks_per_cu(bool hmm);

@@ -2636,19 +2636,21 @@ struct SmallLds {
     uint32_t sb[kSmallWords];      // token first bytes
     uint32_t eb[kSmallWords];      // token last bytes
     uint32_t swp[kSmallWords];     // token starts before each word
-    uint32_t scan[8];
+    uint32_t scan[16];
     uint32_t nh, nblk, nzh, err, ties;
+    uint16_t doff[kSmallDocs + 1];  // document offsets
     uint16_t hpos[kSmallSlots];     // Han rune starts, text order
     uint16_t blist[kSmallBytes + 2];  // block starts, text order
     // per Han rune, at slot = byte / 3 (Han runes are >= 3 bytes)
-    uint32_t scode[kSmallSlots];
-    uint8_t sn[kSmallSlots];  // edges held (0xFF: more than 4, walked again by the DP)
-    uint8_t sbl[kSmallSlots];  // chosen piece length, then Viterbi back-pointers / labels
-    uint8_t sL[kSmallSlots][4];
-    uint16_t se[kSmallSlots][4];  // end byte of each edge
-    double sw[kSmallSlots][4];
+    uint32_t scode[kSmallSlots];  // dense rune code, at slot = byte / 3 (Han runes are >= 3 bytes)
+    uint16_t hord[kSmallSlots];   // Han ordinal, at the slot
+    // per Han rune, by ordinal h (the runes of a block have consecutive ordinals)
+    uint32_t rlw[kSmallSlots];       // DAG edge lengths, a byte each, ascending (0: none); 0xFF: more than 4
+    alignas(16) double rw[kSmallSlots][4];  // their weights (pieceFreq, :511-519)
     double sbest[kSmallSlots];
-    double sem[kSmallSlots][4];  // emissions B, M, E, S
+    uint8_t sL[kSmallSlots];         // chosen piece length (0: none, the reference panics)
+    uint8_t sbl[kSmallSlots];        // Viterbi back-pointers, then labels
+    alignas(16) double sem[kSmallSlots][4];  // emissions B, M, E, S
 };
 static_assert(sizeof(SmallLds) <= 163840u, "k_small: one workgroup's LDS");
 
@@ -2695,39 +2697,72 @@ __device__ __forceinline__ void sm_walk(const SmallLds& s, const DevImage& im, u
     }
 }
 
-// viterbi_run (:668-756 + cutHMM :273-285) with the emissions from LDS
+// viterbi_run (:668-756) + viterbi_back + cutHMM (:273-285) for the m runes with
+// ordinals [ha, ha + m) ending at byte re, everything by ordinal from LDS
 template <class E>
-__device__ void sm_viterbi(const SmlZv& v, const SmallLds& s, uint32_t rs, uint32_t re, uint32_t m, E& em) {
+__device__ void sm_viterbi(SmallLds& s, uint32_t ha, uint32_t re, uint32_t m, E& em) {
+    const uint32_t rs = s.hpos[ha];
     if (m == 1) {  // always "S" for a single rune (:672-674)
         em.token(rs, re);
         return;
     }
-    const double* e = s.sem[rs / 3u];
+    const double* e = s.sem[ha];
     double vB = START_B + e[0], vM = JB_MIN_FLOAT + e[1], vE = JB_MIN_FLOAT + e[2], vS = START_S + e[3];
-    uint32_t q = rs + s.wd[rs];
-    while (q < re) {
+    for (uint32_t h = ha + 1u; h < ha + m; h++) {
         uint32_t cB, cM, cE, cS;
         double pB, pM, pE, pS;
         route2(vE + T_EB, vS + T_SB, &cB, &pB, em.ties);  // B <- E, S
         route2(vB + T_BM, vM + T_MM, &cM, &pM, em.ties);  // M <- B, M
         route2(vB + T_BE, vM + T_ME, &cE, &pE, em.ties);  // E <- B, M
         route2(vE + T_ES, vS + T_SS, &cS, &pS, em.ties);  // S <- E, S
-        e = s.sem[q / 3u];
+        e = s.sem[h];
         vB = pB + e[0];
         vM = pM + e[1];
         vE = pE + e[2];
         vS = pS + e[3];
-        v.bl(q) = (uint8_t)(cB | (cM << 2) | (cE << 4) | (cS << 6));
-        q += s.wd[q];
+        s.sbl[h] = (uint8_t)(cB | (cM << 2) | (cE << 4) | (cS << 6));
     }
-    viterbi_back(v, rs, re, m, vE > vS ? (uint32_t)JB_E : (uint32_t)JB_S, em);  // (:723-729)
+    // traceback (:715-729): stops at the first "" route, and cutHMM then labels the
+    // runes from the run start (viterbi_back)
+    uint32_t st = vE > vS ? (uint32_t)JB_E : (uint32_t)JB_S, t = m - 1u, reset = 0, h = ha + m - 1u;
+    for (;;) {
+        if (t == 0) {
+            s.sbl[h] = (uint8_t)st;
+            break;
+        }
+        const uint32_t code = (s.sbl[h] >> (2u * st)) & 3u;
+        s.sbl[h] = (uint8_t)st;
+        if (code == 2u) {
+            reset = t;
+            break;
+        }
+        st = (st == JB_B || st == JB_S) ? 2u + code : code;  // B,S <- {E,S}; M,E <- {B,M}
+        --t;
+        --h;
+    }
+    uint32_t ts = rs;
+    for (uint32_t k = 0; k < m - reset; k++) {
+        const uint32_t lab = s.sbl[h + k];
+        const uint32_t qa = ha + k + 1u < ha + m ? s.hpos[ha + k + 1u] : re;  // end of rune k
+        if (lab >= (uint32_t)JB_E) {
+            em.token(ts, qa);
+            ts = qa;
+        }
+    }
 }
 
-// cutNonZh for the block [bs, be) from LDS (nonzh_block's rules, :289-310)
+// cutNonZh for the block [bs, be) from LDS (nonzh_block's rules, :289-310), four
+// bytes per LDS read
 template <class E>
 __device__ void sm_nonzh(const uint8_t* tx, uint32_t bs, uint32_t be, E& em) {
     bool has = false;  // alnum.FindAllIndex found nothing -> no tokens (:290-293)
-    for (uint32_t p = bs; p < be && !has; p++) has = jb_is_alnum(tx[p]);
+    for (uint32_t a = bs & ~3u; a < be && !has; a += 16u) {
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; k++) {
+            const uint32_t b = a + 4u * k;
+            has |= jb_any_alnum4(*reinterpret_cast<const uint32_t*>(tx + b) & nz_keep(b, bs, be));
+        }
+    }
     if (!has) return;
     uint32_t p = bs, run = 0;
     bool in_run = false;
@@ -2738,7 +2773,10 @@ __device__ void sm_nonzh(const uint8_t* tx, uint32_t bs, uint32_t be, E& em) {
                 in_run = true;
                 run = p;
             }
-            p++;
+            // the run's bytes of this word: the leading alnum bytes of x
+            uint32_t k = 1;
+            while (k < 4u && p + k < be && jb_is_alnum((x >> (8u * k)) & 0xFFu)) k++;
+            p += k;
             continue;
         }
         if (in_run) {
@@ -2754,51 +2792,62 @@ __device__ void sm_nonzh(const uint8_t* tx, uint32_t bs, uint32_t be, E& em) {
 }
 
 // out: u32 header[kSmallHdr] (SM_*), then tok_start[kSmallBytes], tok_end[kSmallBytes],
-// then doc_tok u64[ndocs + 1].  text is readable 16 bytes past nbytes.
+// then doc_tok u64[ndocs + 1].  text is readable 16 bytes past nbytes.  1024
+// threads (16 waves, 4 per SIMD): with one wave per SIMD every phase ran as one
+// long dependent instruction chain, so the byte phases take 4 bytes per thread.
+constexpr uint32_t kSmallThreads = 1024;
+constexpr uint32_t kSmallPer = kSmallBytes / kSmallThreads;  // bytes per thread in the byte phases
+static_assert(kSmallPer == 4u, "a thread's bytes are one 4-bit field of a 32-bit word");
+
 template <bool HMM>
-__global__ __launch_bounds__(256) void k_small(const uint8_t* __restrict__ text, uint32_t nbytes,
-                                               const uint64_t* __restrict__ doc_off, uint32_t ndocs, DevImage im,
-                                               uint32_t* __restrict__ out) {
+__global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restrict__ text, uint32_t nbytes,
+                                                         const uint64_t* __restrict__ doc_off, uint32_t ndocs,
+                                                         DevImage im, uint32_t* __restrict__ out, uint32_t seq) {
     __shared__ SmallLds s;
     const uint32_t t = threadIdx.x;
     const uint32_t nw = (nbytes + 31u) / 32u;
-    // 1. text (zero past nbytes), bitmaps cleared
-    for (uint32_t i = t; i < (kSmallBytes + 128u) / 16u; i += 256u) {
+    uint64_t clk[16];  // phase clocks (100 MHz), thread 0: header words SM_CLK..
+    uint64_t cyc0 = 0;
+    if (t == 0) {
+        clk[0] = __builtin_amdgcn_s_memrealtime();
+        cyc0 = __builtin_amdgcn_s_memtime();
+    }
+    // 1. text (zero past nbytes) and document offsets -> LDS (one round trip), bitmaps cleared
+    if (t < (kSmallBytes + 128u) / 16u) {
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (16u * i < nbytes) {
-            v = *reinterpret_cast<const uint4*>(text + 16u * i);
+        if (16u * t < nbytes) {
+            v = *reinterpret_cast<const uint4*>(text + 16u * t);
             uint32_t* w = reinterpret_cast<uint32_t*>(&v);
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const uint32_t b = 16u * i + 4u * (uint32_t)k;
+                const uint32_t b = 16u * t + 4u * (uint32_t)k;
                 if (b + 4u > nbytes) w[k] = b >= nbytes ? 0u : w[k] & ((1u << (8u * (nbytes - b))) - 1u);
             }
         }
-        *reinterpret_cast<uint4*>(s.txt + 16u * i) = v;
+        *reinterpret_cast<uint4*>(s.txt + 16u * t) = v;
     }
-    for (uint32_t i = t; i < kSmallWords; i += 256u) {
-        s.docb[i] = s.rsb[i] = s.hsb[i] = s.bsb[i] = s.sb[i] = s.eb[i] = 0u;
-    }
+    for (uint32_t d = t; d <= ndocs; d += kSmallThreads) s.doff[d] = (uint16_t)min(doc_off[d], (uint64_t)nbytes);
+    if (t < kSmallWords) s.docb[t] = s.rsb[t] = s.hsb[t] = s.bsb[t] = s.sb[t] = s.eb[t] = 0u;
     if (t == 0) s.err = s.ties = s.nzh = 0u;
     __syncthreads();
-    for (uint32_t d = t; d < ndocs; d += 256u) {
-        const uint64_t o = doc_off[d];
+    if (t == 0) clk[1] = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t d = t; d < ndocs; d += kSmallThreads) {
+        const uint32_t o = s.doff[d];
         if (o < nbytes) atomicOr(&s.docb[o >> 5], 1u << (o & 31u));
     }
     __syncthreads();
-    // widths at lead bytes: thread t owns bytes [16t, 16t + 16)
-    const uint32_t p0 = 16u * t;
-    uint32_t hanm = 0;  // Han lead bytes of the thread's 16
-    for (uint32_t k = 0; k < 16u; k++) {
+    if (t == 0) clk[2] = __builtin_amdgcn_s_memrealtime();
+    // widths at lead bytes: thread t owns bytes [4t, 4t + 4)
+    const uint32_t p0 = kSmallPer * t, sh = p0 & 31u;
+    uint32_t hanm = 0;  // Han lead bytes of the thread's 4
+#pragma unroll
+    for (uint32_t k = 0; k < kSmallPer; k++) {
         const uint32_t p = p0 + k;
         uint32_t w = 1;
         if (p < nbytes && s.txt[p] >= 0xC0u) {
-            uint32_t lim = min(4u, nbytes - p);
-            for (uint32_t j = 1; j < lim; j++)
-                if (sm_bit(s.docb, p + j)) {
-                    lim = j;
-                    break;
-                }
+            // bounded by the document end: the first document start in p+1 .. p+3
+            const uint32_t nx = (uint32_t)(((((uint64_t)s.docb[(p >> 5) + 1u] << 32) | s.docb[p >> 5]) >> (p & 31u)) >> 1);
+            const uint32_t lim = min(min(4u, nbytes - p), nx ? (uint32_t)__builtin_ctz(nx) + 1u : 4u);
             uint32_t r;
             w = dec_lead(lds4(s.txt, p), lim, &r);
             if (w >= 3u && han_cp(r)) hanm |= 1u << k;
@@ -2806,20 +2855,22 @@ __global__ __launch_bounds__(256) void k_small(const uint8_t* __restrict__ text,
         s.wd[p] = (uint8_t)w;
     }
     __syncthreads();
+    if (t == 0) clk[3] = __builtin_amdgcn_s_memrealtime();
     // 2. rune starts: bytes that no valid sequence of the 3 bytes before covers
-    uint32_t rs16 = 0;
-    for (uint32_t k = 0; k < 16u; k++) {
+    uint32_t rs4 = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kSmallPer; k++) {
         const uint32_t p = p0 + k;
-        if (p >= nbytes) break;
         const bool cov = (p >= 1u && s.wd[p - 1u] >= 2u) || (p >= 2u && s.wd[p - 2u] >= 3u) ||
                          (p >= 3u && s.wd[p - 3u] >= 4u);
-        if (!cov) rs16 |= 1u << k;
+        if (p < nbytes && !cov) rs4 |= 1u << k;
     }
-    if (rs16) atomicOr(&s.rsb[p0 >> 5], rs16 << (p0 & 31u));
-    if (hanm) atomicOr(&s.hsb[p0 >> 5], hanm << (p0 & 31u));
+    if (rs4) atomicOr(&s.rsb[p0 >> 5], rs4 << sh);
+    if (hanm) atomicOr(&s.hsb[p0 >> 5], hanm << sh);
     __syncthreads();
-    uint32_t bs16 = 0;
-    for (uint32_t m = rs16; m; m &= m - 1u) {
+    if (t == 0) clk[4] = __builtin_amdgcn_s_memrealtime();
+    uint32_t bs4 = 0;
+    for (uint32_t m = rs4; m; m &= m - 1u) {
         const uint32_t k = (uint32_t)__builtin_ctz(m), p = p0 + k;
         bool st = p == 0u || sm_bit(s.docb, p);
         if (!st) {  // Han-ness of the previous rune (it starts at most 4 bytes back)
@@ -2827,32 +2878,38 @@ __global__ __launch_bounds__(256) void k_small(const uint8_t* __restrict__ text,
             while (!sm_bit(s.rsb, q)) q--;
             st = sm_bit(s.hsb, q) != ((hanm >> k) & 1u);
         }
-        if (st) bs16 |= 1u << k;
+        if (st) bs4 |= 1u << k;
     }
-    if (bs16) atomicOr(&s.bsb[p0 >> 5], bs16 << (p0 & 31u));
-    __syncthreads();
-    // 3. Han runes and blocks in text order
+    if (bs4) atomicOr(&s.bsb[p0 >> 5], bs4 << sh);
+    // 3. Han runes and blocks in text order: one scan of both counts (Han runes in
+    // the low half: at most kSmallSlots; blocks in the high half: at most kSmallBytes)
     {
         uint32_t tot;
-        const uint32_t hb = block_scan_u32((uint32_t)__popc(hanm), s.scan, &tot);
-        uint32_t i = hb;
-        for (uint32_t m = hanm; m; m &= m - 1u) s.hpos[i++] = (uint16_t)(p0 + (uint32_t)__builtin_ctz(m));
-        if (t == 0) s.nh = tot;
-        const uint32_t bb = block_scan_u32((uint32_t)__popc(bs16), s.scan, &tot);
-        i = bb;
+        const uint32_t x = block_scan_u32((uint32_t)__popc(hanm) | ((uint32_t)__popc(bs4) << 16), s.scan, &tot);
+        uint32_t i = x & 0xFFFFu;
+        for (uint32_t m = hanm; m; m &= m - 1u) {
+            const uint32_t p = p0 + (uint32_t)__builtin_ctz(m);
+            s.hord[p / 3u] = (uint16_t)i;
+            s.hpos[i++] = (uint16_t)p;
+        }
+        i = x >> 16;
         uint32_t nz = 0;
-        for (uint32_t m = bs16; m; m &= m - 1u) {
+        for (uint32_t m = bs4; m; m &= m - 1u) {
             const uint32_t k = (uint32_t)__builtin_ctz(m);
             s.blist[i++] = (uint16_t)(p0 + k);
             nz += (hanm >> k) & 1u;
         }
         if (nz) atomicAdd(&s.nzh, nz);
-        if (t == 0) s.nblk = tot;
+        if (t == 0) {
+            s.nh = tot & 0xFFFFu;
+            s.nblk = tot >> 16;
+        }
     }
     __syncthreads();
+    if (t == 0) clk[5] = __builtin_amdgcn_s_memrealtime();
     const uint32_t nh = s.nh, nblk = s.nblk;
     // 4. codes (and emissions) of the Han runes
-    for (uint32_t h = t; h < nh; h += 256u) {
+    for (uint32_t h = t; h < nh; h += kSmallThreads) {
         const uint32_t p = s.hpos[h];
         uint32_t r;
         (void)dec_lead(lds4(s.txt, p), 4u, &r);
@@ -2861,135 +2918,173 @@ __global__ __launch_bounds__(256) void k_small(const uint8_t* __restrict__ text,
         if (HMM) {
             const double2* ep = reinterpret_cast<const double2*>(im.emit) + (size_t)row * 2u;
             const double2 a = ep[0], b = ep[1];
-            double* e = s.sem[p / 3u];
+            double* e = s.sem[h];
             e[0] = a.x; e[1] = a.y; e[2] = b.x; e[3] = b.y;
         }
     }
     __syncthreads();
+    if (t == 0) clk[6] = __builtin_amdgcn_s_memrealtime();
     // 5. DAG edges of every Han rune
-    for (uint32_t h = t; h < nh; h += 256u) {
-        const uint32_t p = s.hpos[h], sl = p / 3u;
-        uint32_t n = 0;
-        sm_walk(s, im, p, [&](uint32_t L, uint32_t e, double w) {
+    for (uint32_t h = t; h < nh; h += kSmallThreads) {
+        const uint32_t p = s.hpos[h];
+        uint32_t n = 0, lw = 0;
+        sm_walk(s, im, p, [&](uint32_t L, uint32_t, double w) {
             if (n < 4u) {
-                s.sL[sl][n] = (uint8_t)L;
-                s.se[sl][n] = (uint16_t)e;
-                s.sw[sl][n] = w;
+                lw |= L << (8u * n);
+                s.rw[h][n] = w;
             }
             n++;
         });
-        s.sn[sl] = n <= 4u ? (uint8_t)n : (uint8_t)0xFFu;
+        s.rlw[h] = n <= 4u ? lw : 0xFFu;
     }
     __syncthreads();
+    if (t == 0) clk[7] = __builtin_amdgcn_s_memrealtime();
     // 6. blocks, one thread each
     LdsEmitter em(s.sb, s.eb, 0u);
-    const SmlZv v{s.txt, s.sbl};
-    for (uint32_t k = t; k < nblk; k += 256u) {
+    const SmlZv v{s.txt, s.sbl};  // (z_prev only)
+    if (t == 0) clk[12] = clk[13] = clk[14] = 0;
+    if (t == 0) clk[15] = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t k = t; k < nblk; k += kSmallThreads) {
         const uint32_t bs = s.blist[k], be = k + 1u < nblk ? s.blist[k + 1u] : nbytes;
         if (!sm_bit(s.hsb, bs)) {
             sm_nonzh(s.txt, bs, be, em);
             continue;
         }
-        // backward DP (calcDagProba, :502-548): best(i) from best(i + L); best(n) = 0.0
-        uint32_t q = z_prev(v, be, bs);
+        // backward DP (calcDagProba, :502-548) over the block's runes, ordinals [h0, h1):
+        // best(h) from best(h + L), best(h1) = 0.0.  The next rune's record is read
+        // while this one folds; best(h + 1) stays in a register, the others come from LDS.
+        const uint32_t h0 = s.hord[bs / 3u], h1 = s.hord[z_prev(v, be, bs) / 3u] + 1u;
+        uint32_t h = h1 - 1u;
+        uint32_t lw = s.rlw[h];
+        double w0 = s.rw[h][0], w1 = s.rw[h][1], w2 = s.rw[h][2], w3 = s.rw[h][3];
+        double bnx = 0.0;
         for (;;) {
-            const uint32_t sl = q / 3u;
-            DpFold f;
-            auto item = [&](uint32_t L, uint32_t e, double w) {
-                const double pp = w + (e == be ? 0.0 : s.sbest[e / 3u]);  // pieceProba (:519-529)
-                if (pp >= f.prevP) {  // maxIndexProba (:565-578)
-                    f.bestL = L;
-                    f.bestP = pp;
-                }
-                f.prevP = pp;
-                f.lastL = L;
+            const uint32_t hp = h > h0 ? h - 1u : h;
+            const uint32_t lwn = s.rlw[hp];
+            const double n0 = s.rw[hp][0], n1 = s.rw[hp][1], n2 = s.rw[hp][2], n3 = s.rw[hp][3];
+            double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT;  // maxIndexProba's state (:565-578)
+            uint32_t bestL = 0, lastL = 0;
+            auto item = [&](uint32_t L, double w, double nb) {
+                const double pp = w + (h + L == h1 ? 0.0 : (L == 1u ? bnx : nb));  // pieceProba (:519-529)
+                const bool take = pp >= prevP;
+                bestL = take ? L : bestL;
+                bestP = take ? pp : bestP;
+                prevP = pp;
+                lastL = L;
             };
-            const uint32_t n = s.sn[sl];
-            if (n == 0xFFu) {
-                sm_walk(s, im, q, item);
+            if (lw == 0xFFu) {  // more than 4 edges: walk the rune again
+                sm_walk(s, im, s.hpos[h], [&](uint32_t L, uint32_t, double w) { item(L, w, s.sbest[h + L]); });
             } else {
-                for (uint32_t j = 0; j < n; j++) item(s.sL[sl][j], s.se[sl][j], s.sw[sl][j]);
+                const uint32_t L0 = lw & 0xFFu, L1 = (lw >> 8) & 0xFFu, L2 = (lw >> 16) & 0xFFu, L3 = lw >> 24;
+                const double b0 = s.sbest[h + L0], b1 = s.sbest[h + L1], b2 = s.sbest[h + L2], b3 = s.sbest[h + L3];
+                if (L0) item(L0, w0, b0);
+                if (L1) item(L1, w1, b1);
+                if (L2) item(L2, w2, b2);
+                if (L3) item(L3, w3, b3);
             }
-            f.finish();
-            s.sbest[sl] = f.bestP;
-            s.sbl[sl] = (uint8_t)f.bestL;
-            if (q == bs) break;
-            q = z_prev(v, q, bs);
+            if (bestL == 0) {  // no item qualified: the last item (or none: tail -1)
+                bestL = lastL;
+                bestP = prevP;
+            }
+            s.sbest[h] = bestP;
+            s.sL[h] = (uint8_t)bestL;
+            if (h == h0) break;
+            bnx = bestP;
+            h = hp;
+            lw = lwn;
+            w0 = n0; w1 = n1; w2 = n2; w3 = n3;
         }
+        if (t == 0) clk[12] = __builtin_amdgcn_s_memrealtime();
         // forward path (findDagPath, :552-562) + HMM runs (cutZh, :221-255)
-        uint32_t p = bs, run_s = 0, run_n = 0;
+        uint32_t run_h = 0, run_n = 0;
         bool ok = true;
-        while (p < be) {
-            const uint32_t L = s.sbl[p / 3u];
+        for (h = h0; h < h1;) {
+            const uint32_t L = s.sL[h], p = s.hpos[h];
             if (L == 0) {  // tail index -1: cutDAG's slice panics in the reference
                 ok = false;
                 break;
             }
-            uint32_t pe = p;
-            for (uint32_t j = 0; j < L; j++) pe += s.wd[pe];
+            const uint32_t pe = h + L < h1 ? s.hpos[h + L] : be;
             if (!HMM) {
                 em.token(p, pe);
             } else if (L == 1) {
-                if (run_n == 0) run_s = p;
+                if (run_n == 0) run_h = h;
                 run_n++;
             } else {
                 if (run_n) {
-                    sm_viterbi(v, s, run_s, p, run_n, em);
+                    sm_viterbi(s, run_h, p, run_n, em);
                     run_n = 0;
                 }
                 em.token(p, pe);
             }
-            p = pe;
+            h += L;
         }
         if (!ok) {
             s.err = 1u;
             continue;
         }
-        if (HMM && run_n) sm_viterbi(v, s, run_s, be, run_n, em);
+        if (HMM && run_n) sm_viterbi(s, run_h, be, run_n, em);
+        if (t == 0) clk[13] = __builtin_amdgcn_s_memrealtime();
     }
     em.flush();
+    if (t == 0) clk[14] = __builtin_amdgcn_s_memrealtime();
     if (em.ties) atomicAdd(&s.ties, em.ties);
     __syncthreads();
-    // 7. spans, per-document first tokens, counters
+    if (t == 0) clk[8] = __builtin_amdgcn_s_memrealtime();
+    // 7. spans, per-document first tokens, counters (starts in the low half of one
+    // scan, ends in the high half: at most kSmallBytes each)
     const uint32_t sw_ = t < nw ? s.sb[t] : 0u, ew = t < nw ? s.eb[t] : 0u;
-    uint32_t ts, te;
-    const uint32_t xs = block_scan_u32((uint32_t)__popc(sw_), s.scan, &ts);
-    const uint32_t xe = block_scan_u32((uint32_t)__popc(ew), s.scan, &te);
+    uint32_t tot;
+    const uint32_t x = block_scan_u32((uint32_t)__popc(sw_) | ((uint32_t)__popc(ew) << 16), s.scan, &tot);
+    const uint32_t ts = tot & 0xFFFFu, te = tot >> 16;
+    if (t == 0) clk[9] = __builtin_amdgcn_s_memrealtime();
     uint32_t* const os = out + kSmallHdr;
     uint32_t* const oe = os + kSmallBytes;
     if (t < nw) {
-        s.swp[t] = xs;
-        uint32_t g = xs;
+        s.swp[t] = x & 0xFFFFu;
+        uint32_t g = x & 0xFFFFu;
         for (uint32_t m = sw_; m; m &= m - 1u) os[g++] = 32u * t + (uint32_t)__builtin_ctz(m);
-        g = xe;
+        g = x >> 16;
         for (uint32_t m = ew; m; m &= m - 1u) oe[g++] = 32u * t + (uint32_t)__builtin_ctz(m) + 1u;
     }
     __syncthreads();
+    if (t == 0) clk[10] = __builtin_amdgcn_s_memrealtime();
     uint64_t* const dt = reinterpret_cast<uint64_t*>(oe + kSmallBytes);
-    for (uint32_t d = t; d <= ndocs; d += 256u) {
-        const uint64_t o = doc_off[d];
+    for (uint32_t d = t; d <= ndocs; d += kSmallThreads) {
+        const uint32_t o = s.doff[d];
         uint32_t c = ts;
         if (o < nbytes) c = s.swp[o >> 5] + (uint32_t)__popc(s.sb[o >> 5] & ((1u << (o & 31u)) - 1u));
         dt[d] = c;
     }
     if (t == 0) {
+        clk[11] = __builtin_amdgcn_s_memrealtime();
         out[SM_NTOK] = ts;
         out[SM_NTOKE] = te;
         out[SM_ERR] = s.err;
         out[SM_TIES] = s.ties;
         out[SM_BLOCKS] = nblk;
         out[SM_ZHBLOCKS] = s.nzh;
+        for (int k = 1; k < 16; k++) out[SM_CLK + k - 1] = (uint32_t)(clk[k] - clk[0]);
+        out[SM_CLK + 15] = (uint32_t)(__builtin_amdgcn_s_memtime() - cyc0);  // shader clock cycles
     }
+    // every thread's writes reach host memory before the completion word
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(out + SM_DONE, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 hipError_t run_small(const DevImage& im, const uint8_t* text, uint32_t nbytes, const uint64_t* doc_off,
-                     uint32_t ndocs, bool hmm, uint32_t* out, hipStream_t stream) {
+                     uint32_t ndocs, bool hmm, uint32_t* out, uint32_t seq, hipStream_t stream) {
     if (nbytes > kSmallBytes || ndocs > kSmallDocs) return hipErrorInvalidValue;
-    if (hmm) hipLaunchKernelGGL((k_small<true>), dim3(1), dim3(256), 0, stream, text, nbytes, doc_off, ndocs, im, out);
-    else hipLaunchKernelGGL((k_small<false>), dim3(1), dim3(256), 0, stream, text, nbytes, doc_off, ndocs, im, out);
+    if (hmm)
+        hipLaunchKernelGGL((k_small<true>), dim3(1), dim3(kSmallThreads), 0, stream, text, nbytes, doc_off, ndocs, im,
+                           out, seq);
+    else
+        hipLaunchKernelGGL((k_small<false>), dim3(1), dim3(kSmallThreads), 0, stream, text, nbytes, doc_off, ndocs,
+                           im, out, seq);
     return hipGetLastError();
 }
 
