@@ -2649,7 +2649,8 @@ struct SmallLds {
     alignas(16) double rw[kSmallSlots][4];  // their weights (pieceFreq, :511-519)
     double sbest[kSmallSlots];
     uint8_t sL[kSmallSlots];         // chosen piece length (0: none, the reference panics)
-    uint8_t sbl[kSmallSlots];        // Viterbi back-pointers, then labels
+    uint8_t sbl[kSmallSlots];        // Viterbi labels (traceback)
+    uint8_t bp4[kSmallSlots][4];     // Viterbi back-pointer of each state (quad lane = state)
     alignas(16) double sem[kSmallSlots][4];  // emissions B, M, E, S
 };
 static_assert(sizeof(SmallLds) <= 163840u, "k_small: one workgroup's LDS");
@@ -2697,31 +2698,50 @@ __device__ __forceinline__ void sm_walk(const SmallLds& s, const DevImage& im, u
     }
 }
 
+// A float64 from another lane of the quad (DPP quad_perm; ctrl = src lane of lanes 0..3, 2 bits each)
+template <int CTRL>
+__device__ __forceinline__ double quad_perm_f64(double x) {
+    const long long i = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_mov_dpp((int)i, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(i >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
 // viterbi_run (:668-756) + viterbi_back + cutHMM (:273-285) for the m runes with
-// ordinals [ha, ha + m) ending at byte re, everything by ordinal from LDS
+// ordinals [ha, ha + m) ending at byte re, by the four lanes of a quad: lane s holds
+// state s (B, M, E, S: HMMstates order, :685) and takes its two candidates
+// (stateChange, :24-29) from the other lanes with DPP, so a rune is one short
+// chain instead of four serial routes.  Lane 0 then runs the traceback and emits.
 template <class E>
-__device__ void sm_viterbi(SmallLds& s, uint32_t ha, uint32_t re, uint32_t m, E& em) {
+__device__ void sm_viterbi(SmallLds& s, uint32_t ha, uint32_t re, uint32_t m, E& em, uint32_t ql) {
     const uint32_t rs = s.hpos[ha];
     if (m == 1) {  // always "S" for a single rune (:672-674)
-        em.token(rs, re);
+        if (ql == 0) em.token(rs, re);
         return;
     }
-    const double* e = s.sem[ha];
-    double vB = START_B + e[0], vM = JB_MIN_FLOAT + e[1], vE = JB_MIN_FLOAT + e[2], vS = START_S + e[3];
+    // B <- (E, S), M <- (B, M), E <- (B, M), S <- (E, S)
+    const double ta = ql == 0 ? T_EB : (ql == 1 ? T_BM : (ql == 2 ? T_BE : T_ES));
+    const double tb = ql == 0 ? T_SB : (ql == 1 ? T_MM : (ql == 2 ? T_ME : T_SS));
+    double vv = (ql == 0 ? START_B : (ql == 3 ? START_S : JB_MIN_FLOAT)) + s.sem[ha][ql];
+    double en = s.sem[ha + 1u][ql];
+    uint32_t nt = 0;
     for (uint32_t h = ha + 1u; h < ha + m; h++) {
-        uint32_t cB, cM, cE, cS;
-        double pB, pM, pE, pS;
-        route2(vE + T_EB, vS + T_SB, &cB, &pB, em.ties);  // B <- E, S
-        route2(vB + T_BM, vM + T_MM, &cM, &pM, em.ties);  // M <- B, M
-        route2(vB + T_BE, vM + T_ME, &cE, &pE, em.ties);  // E <- B, M
-        route2(vE + T_ES, vS + T_SS, &cS, &pS, em.ties);  // S <- E, S
-        e = s.sem[h];
-        vB = pB + e[0];
-        vM = pM + e[1];
-        vE = pE + e[2];
-        vS = pS + e[3];
-        s.sbl[h] = (uint8_t)(cB | (cM << 2) | (cE << 4) | (cS << 6));
+        const double enn = s.sem[h + 1u][ql];  // (past the run: a harmless read)
+        const double a = quad_perm_f64<2 | (0 << 2) | (0 << 4) | (2 << 6)>(vv) + ta;
+        const double b = quad_perm_f64<3 | (1 << 2) | (1 << 4) | (3 << 6)>(vv) + tb;
+        // stateTransitionRoute (:736-756): strict '>' against minFloat, code 2 = no route
+        uint32_t c = 2u;
+        double best = JB_MIN_FLOAT;
+        if (a > best) { c = 0u; best = a; }
+        if (b > best) { c = 1u; best = b; }
+        nt += (a == b && a > JB_MIN_FLOAT) ? 1u : 0u;
+        vv = best + en;
+        s.bp4[h][ql] = (uint8_t)c;
+        en = enn;
     }
+    em.ties += nt;
+    const double vE = quad_perm_f64<0xAA>(vv), vS = quad_perm_f64<0xFF>(vv);
+    if (ql != 0) return;
     // traceback (:715-729): stops at the first "" route, and cutHMM then labels the
     // runes from the run start (viterbi_back)
     uint32_t st = vE > vS ? (uint32_t)JB_E : (uint32_t)JB_S, t = m - 1u, reset = 0, h = ha + m - 1u;
@@ -2730,7 +2750,7 @@ __device__ void sm_viterbi(SmallLds& s, uint32_t ha, uint32_t re, uint32_t m, E&
             s.sbl[h] = (uint8_t)st;
             break;
         }
-        const uint32_t code = (s.sbl[h] >> (2u * st)) & 3u;
+        const uint32_t code = s.bp4[h][st];
         s.sbl[h] = (uint8_t)st;
         if (code == 2u) {
             reset = t;
@@ -2939,15 +2959,17 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
     }
     __syncthreads();
     if (t == 0) clk[7] = __builtin_amdgcn_s_memrealtime();
-    // 6. blocks, one thread each
+    // 6. blocks, one quad of lanes each (the Viterbi takes all four; the rest is
+    // run alike by the four lanes and written by lane 0)
     LdsEmitter em(s.sb, s.eb, 0u);
+    const uint32_t ql = t & 3u;
     const SmlZv v{s.txt, s.sbl};  // (z_prev only)
     if (t == 0) clk[12] = clk[13] = clk[14] = 0;
     if (t == 0) clk[15] = __builtin_amdgcn_s_memrealtime();
-    for (uint32_t k = t; k < nblk; k += kSmallThreads) {
+    for (uint32_t k = t >> 2; k < nblk; k += kSmallThreads / 4u) {
         const uint32_t bs = s.blist[k], be = k + 1u < nblk ? s.blist[k + 1u] : nbytes;
         if (!sm_bit(s.hsb, bs)) {
-            sm_nonzh(s.txt, bs, be, em);
+            if (ql == 0) sm_nonzh(s.txt, bs, be, em);
             continue;
         }
         // backward DP (calcDagProba, :502-548) over the block's runes, ordinals [h0, h1):
@@ -3006,24 +3028,24 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
             }
             const uint32_t pe = h + L < h1 ? s.hpos[h + L] : be;
             if (!HMM) {
-                em.token(p, pe);
+                if (ql == 0) em.token(p, pe);
             } else if (L == 1) {
                 if (run_n == 0) run_h = h;
                 run_n++;
             } else {
                 if (run_n) {
-                    sm_viterbi(s, run_h, p, run_n, em);
+                    sm_viterbi(s, run_h, p, run_n, em, ql);
                     run_n = 0;
                 }
-                em.token(p, pe);
+                if (ql == 0) em.token(p, pe);
             }
             h += L;
         }
         if (!ok) {
-            s.err = 1u;
+            if (ql == 0) s.err = 1u;
             continue;
         }
-        if (HMM && run_n) sm_viterbi(s, run_h, be, run_n, em);
+        if (HMM && run_n) sm_viterbi(s, run_h, be, run_n, em, ql);
         if (t == 0) clk[13] = __builtin_amdgcn_s_memrealtime();
     }
     em.flush();
