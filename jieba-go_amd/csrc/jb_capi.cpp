@@ -751,17 +751,28 @@ static int cut_small(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         HIPCHK(hipHostGetDevicePointer((void**)&d->d_sout, d->h_sout, 0));
     }
     const auto c0 = std::chrono::steady_clock::now();
-    if (nbytes) memcpy(d->h_sin, text + base, nbytes);
-    memset(d->h_sin + nbytes, 0, 16);
-    uint64_t* const hoff = reinterpret_cast<uint64_t*>(d->h_sin + kSmallBytes + 128);
-    for (uint32_t k = 0; k <= nd; k++) hoff[k] = doc_off[k] - base;
+    // a batch that fits the kernel arguments travels in them (the kernel reads them from
+    // the kernarg segment instead of host memory over PCIe); others go through h_sin
+    const bool inl = nbytes <= kSmallInline && nd <= kSmallInlineDocs;
+    SmallInline in;
+    memset(&in, 0, sizeof in);
+    if (inl) {
+        if (nbytes) memcpy(in.txt, text + base, nbytes);
+        for (uint32_t k = 0; k <= nd; k++) in.doff[k] = (uint16_t)(doc_off[k] - base);
+    } else {
+        if (nbytes) memcpy(d->h_sin, text + base, nbytes);
+        memset(d->h_sin + nbytes, 0, 16);
+        uint64_t* const hoff = reinterpret_cast<uint64_t*>(d->h_sin + kSmallBytes + 128);
+        for (uint32_t k = 0; k <= nd; k++) hoff[k] = doc_off[k] - base;
+    }
     // the kernel writes the call's sequence number after everything else (system-scope
     // release); spinning on it returns as soon as the results are in host memory
     const uint32_t seq = ++d->small_seq;
     volatile uint32_t* done = d->h_sout + SM_DONE;
-    const hipError_t e = run_small(d->dim, d->d_sin, (uint32_t)nbytes,
-                                   reinterpret_cast<const uint64_t*>(d->d_sin + kSmallBytes + 128), nd, hmm,
-                                   d->d_sout, seq, d->sstream);
+    const hipError_t e =
+        run_small(d->dim, inl ? nullptr : d->d_sin, (uint32_t)nbytes,
+                  inl ? nullptr : reinterpret_cast<const uint64_t*>(d->d_sin + kSmallBytes + 128), nd, hmm,
+                  d->d_sout, seq, in, d->sstream);
     if (e != hipSuccess) return fail(JB_EDEVICE, "k_small launch: %s", hipGetErrorString(e));
     const auto c1 = std::chrono::steady_clock::now();
     for (uint32_t spin = 0; *done != seq; spin++) {

@@ -120,9 +120,19 @@ constexpr uint32_t kSmallDocs = 4096;
 constexpr uint32_t kSmallHdr = 32;
 constexpr uint64_t kSmallOutBytes = 4ull * (kSmallHdr + 2ull * kSmallBytes) + 8ull * (kSmallDocs + 1ull);
 enum { SM_NTOK = 0, SM_NTOKE, SM_ERR, SM_TIES, SM_BLOCKS, SM_ZHBLOCKS, SM_DONE, SM_CLK = 8 };  // SM_CLK..+10: phase clocks (10 ns ticks)
+// A batch small enough to travel in the kernel arguments (text == nullptr): the
+// kernel then reads it from the kernarg segment instead of host memory over PCIe.
+constexpr uint32_t kSmallInline = 224;  // text bytes (zero-padded)
+constexpr uint32_t kSmallInlineDocs = 7;
+struct alignas(16) SmallInline {
+    uint8_t txt[kSmallInline];
+    uint16_t doff[kSmallInlineDocs + 1];  // document offsets, doff[ndocs] = nbytes
+    uint32_t pad[4];
+};
 // out[SM_DONE] = seq is the kernel's last write (after a system-scope release).
 hipError_t run_small(const DevImage& im, const uint8_t* text, uint32_t nbytes, const uint64_t* doc_off,
-                     uint32_t ndocs, bool hmm, uint32_t* out, uint32_t seq, hipStream_t stream);
+                     uint32_t ndocs, bool hmm, uint32_t* out, uint32_t seq, const SmallInline& in,
+                     hipStream_t stream);
 
 // Resident k_zh workgroups per CU (occupancy API).
 uint32_t zh_blocks_per_cu(bool hmm);

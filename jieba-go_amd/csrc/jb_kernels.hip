@@ -2812,9 +2812,9 @@ __device__ void sm_nonzh(const uint8_t* tx, uint32_t bs, uint32_t be, E& em) {
 }
 
 // out: u32 header[kSmallHdr] (SM_*), then tok_start[kSmallBytes], tok_end[kSmallBytes],
-// then doc_tok u64[ndocs + 1].  text is readable 16 bytes past nbytes.  1024
-// threads (16 waves, 4 per SIMD): with one wave per SIMD every phase ran as one
-// long dependent instruction chain, so the byte phases take 4 bytes per thread.
+// then doc_tok u64[ndocs + 1].  text is readable 16 bytes past nbytes.  Up to 1024
+// threads, 4 bytes each in the byte phases (16 bytes each ran every phase as one long
+// dependent instruction chain per wave); a batch gets as many waves as its bytes need.
 constexpr uint32_t kSmallThreads = 1024;
 constexpr uint32_t kSmallPer = kSmallBytes / kSmallThreads;  // bytes per thread in the byte phases
 static_assert(kSmallPer == 4u, "a thread's bytes are one 4-bit field of a 32-bit word");
@@ -2822,7 +2822,8 @@ static_assert(kSmallPer == 4u, "a thread's bytes are one 4-bit field of a 32-bit
 template <bool HMM>
 __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restrict__ text, uint32_t nbytes,
                                                          const uint64_t* __restrict__ doc_off, uint32_t ndocs,
-                                                         DevImage im, uint32_t* __restrict__ out, uint32_t seq) {
+                                                         DevImage im, uint32_t* __restrict__ out, uint32_t seq,
+                                                         SmallInline in) {
     __shared__ SmallLds s;
     const uint32_t t = threadIdx.x;
     const uint32_t nw = (nbytes + 31u) / 32u;
@@ -2832,26 +2833,30 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
         clk[0] = __builtin_amdgcn_s_memrealtime();
         cyc0 = __builtin_amdgcn_s_memtime();
     }
-    // 1. text (zero past nbytes) and document offsets -> LDS (one round trip), bitmaps cleared
-    if (t < (kSmallBytes + 128u) / 16u) {
+    const uint32_t nt = blockDim.x;  // a multiple of 64 with 4 * nt >= nbytes (run_small)
+    // 1. text (zero past nbytes, up to 64 bytes on) and document offsets -> LDS (one
+    // round trip), bitmaps cleared
+    const uint8_t* const src = text ? text : in.txt;  // (inline: zero-padded by the host)
+    for (uint32_t i = t; i < min((kSmallBytes + 128u) / 16u, (nbytes + 79u) / 16u); i += nt) {
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (16u * t < nbytes) {
-            v = *reinterpret_cast<const uint4*>(text + 16u * t);
+        if (16u * i < nbytes) {
+            v = *reinterpret_cast<const uint4*>(src + 16u * i);
             uint32_t* w = reinterpret_cast<uint32_t*>(&v);
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const uint32_t b = 16u * t + 4u * (uint32_t)k;
+                const uint32_t b = 16u * i + 4u * (uint32_t)k;
                 if (b + 4u > nbytes) w[k] = b >= nbytes ? 0u : w[k] & ((1u << (8u * (nbytes - b))) - 1u);
             }
         }
-        *reinterpret_cast<uint4*>(s.txt + 16u * t) = v;
+        *reinterpret_cast<uint4*>(s.txt + 16u * i) = v;
     }
-    for (uint32_t d = t; d <= ndocs; d += kSmallThreads) s.doff[d] = (uint16_t)min(doc_off[d], (uint64_t)nbytes);
-    if (t < kSmallWords) s.docb[t] = s.rsb[t] = s.hsb[t] = s.bsb[t] = s.sb[t] = s.eb[t] = 0u;
+    for (uint32_t d = t; d <= ndocs; d += nt)
+        s.doff[d] = doc_off ? (uint16_t)min(doc_off[d], (uint64_t)nbytes) : in.doff[d];
+    for (uint32_t i = t; i < kSmallWords; i += nt) s.docb[i] = s.rsb[i] = s.hsb[i] = s.bsb[i] = s.sb[i] = s.eb[i] = 0u;
     if (t == 0) s.err = s.ties = s.nzh = 0u;
     __syncthreads();
     if (t == 0) clk[1] = __builtin_amdgcn_s_memrealtime();
-    for (uint32_t d = t; d < ndocs; d += kSmallThreads) {
+    for (uint32_t d = t; d < ndocs; d += nt) {
         const uint32_t o = s.doff[d];
         if (o < nbytes) atomicOr(&s.docb[o >> 5], 1u << (o & 31u));
     }
@@ -2929,7 +2934,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
     if (t == 0) clk[5] = __builtin_amdgcn_s_memrealtime();
     const uint32_t nh = s.nh, nblk = s.nblk;
     // 4. codes (and emissions) of the Han runes
-    for (uint32_t h = t; h < nh; h += kSmallThreads) {
+    for (uint32_t h = t; h < nh; h += nt) {
         const uint32_t p = s.hpos[h];
         uint32_t r;
         (void)dec_lead(lds4(s.txt, p), 4u, &r);
@@ -2945,7 +2950,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
     __syncthreads();
     if (t == 0) clk[6] = __builtin_amdgcn_s_memrealtime();
     // 5. DAG edges of every Han rune
-    for (uint32_t h = t; h < nh; h += kSmallThreads) {
+    for (uint32_t h = t; h < nh; h += nt) {
         const uint32_t p = s.hpos[h];
         uint32_t n = 0, lw = 0;
         sm_walk(s, im, p, [&](uint32_t L, uint32_t, double w) {
@@ -2966,7 +2971,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
     const SmlZv v{s.txt, s.sbl};  // (z_prev only)
     if (t == 0) clk[12] = clk[13] = clk[14] = 0;
     if (t == 0) clk[15] = __builtin_amdgcn_s_memrealtime();
-    for (uint32_t k = t >> 2; k < nblk; k += kSmallThreads / 4u) {
+    for (uint32_t k = t >> 2; k < nblk; k += nt / 4u) {
         const uint32_t bs = s.blist[k], be = k + 1u < nblk ? s.blist[k + 1u] : nbytes;
         if (!sm_bit(s.hsb, bs)) {
             if (ql == 0) sm_nonzh(s.txt, bs, be, em);
@@ -3072,7 +3077,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
     __syncthreads();
     if (t == 0) clk[10] = __builtin_amdgcn_s_memrealtime();
     uint64_t* const dt = reinterpret_cast<uint64_t*>(oe + kSmallBytes);
-    for (uint32_t d = t; d <= ndocs; d += kSmallThreads) {
+    for (uint32_t d = t; d <= ndocs; d += nt) {
         const uint32_t o = s.doff[d];
         uint32_t c = ts;
         if (o < nbytes) c = s.swp[o >> 5] + (uint32_t)__popc(s.sb[o >> 5] & ((1u << (o & 31u)) - 1u));
@@ -3099,14 +3104,20 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
 // host side
 // ---------------------------------------------------------------------------
 hipError_t run_small(const DevImage& im, const uint8_t* text, uint32_t nbytes, const uint64_t* doc_off,
-                     uint32_t ndocs, bool hmm, uint32_t* out, uint32_t seq, hipStream_t stream) {
+                     uint32_t ndocs, bool hmm, uint32_t* out, uint32_t seq, const SmallInline& in,
+                     hipStream_t stream) {
     if (nbytes > kSmallBytes || ndocs > kSmallDocs) return hipErrorInvalidValue;
+    if ((!text || !doc_off) && (text || doc_off || nbytes > kSmallInline || ndocs > kSmallInlineDocs))
+        return hipErrorInvalidValue;
+    // as many waves as the byte phases need (4 bytes per thread): a sentence is one
+    // wave, whose barriers and scans cost next to nothing
+    const uint32_t nt = std::max(64u, (nbytes + 4u * 64u - 1u) / (4u * 64u) * 64u);
     if (hmm)
-        hipLaunchKernelGGL((k_small<true>), dim3(1), dim3(kSmallThreads), 0, stream, text, nbytes, doc_off, ndocs, im,
-                           out, seq);
+        hipLaunchKernelGGL((k_small<true>), dim3(1), dim3(nt), 0, stream, text, nbytes, doc_off, ndocs, im, out, seq,
+                           in);
     else
-        hipLaunchKernelGGL((k_small<false>), dim3(1), dim3(kSmallThreads), 0, stream, text, nbytes, doc_off, ndocs,
-                           im, out, seq);
+        hipLaunchKernelGGL((k_small<false>), dim3(1), dim3(nt), 0, stream, text, nbytes, doc_off, ndocs, im, out, seq,
+                           in);
     return hipGetLastError();
 }
 
