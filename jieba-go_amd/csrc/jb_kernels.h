@@ -122,7 +122,7 @@ constexpr uint64_t kSmallOutBytes = 4ull * (kSmallHdr + 2ull * kSmallBytes) + 8u
 enum { SM_NTOK = 0, SM_NTOKE, SM_ERR, SM_TIES, SM_BLOCKS, SM_ZHBLOCKS, SM_DONE, SM_CLK = 8 };  // SM_CLK..+10: phase clocks (10 ns ticks)
 // A batch small enough to travel in the kernel arguments (text == nullptr): the
 // kernel then reads it from the kernarg segment instead of host memory over PCIe.
-constexpr uint32_t kSmallInline = 224;  // text bytes (zero-padded)
+constexpr uint32_t kSmallInline = 96;  // text bytes (zero-padded)
 constexpr uint32_t kSmallInlineDocs = 7;
 struct alignas(16) SmallInline {
     uint8_t txt[kSmallInline];

@@ -724,9 +724,10 @@ def test_small_batches_one_workgroup(syn_small, monkeypatch):
                                                                     "　", "ス", "한", "\n", "𠀀", "々"]
     texts += ["".join(rng.choice(alphabet) for _ in range(rng.randint(0, 300))) for _ in range(300)]
     batches = _small_batches(texts)
-    # batches of at most 224 bytes and 7 documents travel in the kernel arguments
-    short = [t for t in texts[len(EDGE_TEXTS):] if len(t if isinstance(t, bytes) else t.encode()) <= 60]
-    batches += [short[i:i + 3] for i in range(0, 90, 3)] + _small_batches(short[:300], limit=224, max_docs=7)
+    # batches of at most 96 bytes and 7 documents travel in the kernel arguments
+    short = [t for t in texts[len(EDGE_TEXTS):] if len(t if isinstance(t, bytes) else t.encode()) <= 30]
+    batches += [short[i:i + 3] for i in range(0, 90, 3)] + _small_batches(short[:300], limit=96, max_docs=7)
+    batches += [[("中" * 32).encode()], [("中" * 31).encode() + b"abc"], [b"x" * 97]]  # 96, 96 and 97 bytes
     batches += [[("丁" * 1365).encode()], [("一丁" * 682).encode() + b"ab"], [("𠀀" * 1024).encode()],
                 [b""] * 4096, [b""] * 100 + ["中文".encode()] + [b""] * 100, [b"x" * 4096],
                 [("中" * 1365 + "a").encode()],                      # 4097 bytes: pipeline
