@@ -480,7 +480,7 @@ def main():
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
                 "data": "the reference's benchmark sentence", "config": {
                     "workload": f"config 1: Cut({SENTENCE!r}, hmm=true) through jb_cut, one call at a time "
-                                "(host string in, one k_small launch reading it from mapped pinned host memory, "
+                                "(host string in, one k_small launch with the text in its kernel arguments, "
                                 "spans back in pinned host memory), 19 runes / 57 bytes",
                     "parallelism": "one call"},
                 "vs_reference_ns_per_op": round(REF_SENTENCE_NS / med, 3),
