@@ -1045,16 +1045,26 @@ __device__ __forceinline__ void rec_fold(uint32_t m, const double w[4], DpFold& 
     }
 }
 
+// A record's edge lengths (its 8-bit mask's set bits + 1, ascending, a byte each,
+// 0 = no edge), from a 256-entry LDS table that k_zh fills at its start.
+__shared__ uint32_t s_ltab[256];
+__device__ __forceinline__ uint32_t ltab_entry(uint32_t m) {
+    uint32_t v = 0, k = 0;
+    for (uint32_t b = 0; b < 8u && k < 4u; b++)
+        if ((m >> b) & 1u) v |= (b + 1u) << (8u * k++);
+    return v;
+}
+
 // The same with the {n, 0.0} sentinel kept in the ring: the caller writes 0.0
 // to slot 0 when a block (re)starts at c = 1, so the edge with L == c reads
 // best(n) = 0.0 from slot (c - L) & 7 = 0, which step 8 is the first to
-// overwrite (after its reads).  No per-edge select for the sentinel.
-__device__ __forceinline__ void rec_fold_s(uint32_t m, const double w[4], DpFold& f, uint32_t c, const double* ring) {
+// overwrite (after its reads).  No per-edge select for the sentinel.  lp: the
+// record's lengths (s_ltab), looked up a step ahead.
+__device__ __forceinline__ void rec_fold_s(uint32_t lp, const double w[4], DpFold& f, uint32_t c, const double* ring) {
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const bool has = m != 0u;
-        const uint32_t L = has ? (uint32_t)__builtin_ctz(m) + 1u : 1u;
-        m &= m - 1u;
+        const uint32_t L = (lp >> (8 * k)) & 0xFFu;
+        const bool has = L != 0u;
         const double pp = w[k] + ring[((c - L) & (kZhRing - 1u)) * 64u];
         const bool take = has && pp >= f.prevP;
         f.bestL = take ? L : f.bestL;
@@ -1141,7 +1151,7 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
                              double* __restrict__ gbest, double* ring, const Src& src) {
     uint32_t j = 0, bs = 0, be = 0;
     if (!src.next(j, bs, be)) return 0;
-    uint32_t key0 = 0, steps = 0, q = 0, c = 1, s = 0, mc = 0;
+    uint32_t key0 = 0, steps = 0, q = 0, c = 1, s = 0, mc = 0, lc = 0;
     bool longm = false;
     // Slots before a block (or before the text: erec has kErecPad slots of padding in
     // front) are garbage that `more` masks at the use.
@@ -1176,6 +1186,7 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
             ld_pair(s - 4u, yl, yh);
         }
         mc = (uint32_t)rc & 0xFFu;
+        lc = s_ltab[mc];
         rec_weights(im, rc, wn);
     };
     // One rune.  wc: this rune's weights (loaded a step ago); wn: gets the next rune's.
@@ -1186,11 +1197,12 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
         const uint64_t nx = P == 0 ? xl : (P == 1 ? yh : (P == 2 ? yl : xh));
         const uint64_t r1v = more ? nx : 0ull;  // the next rune's record (when it exists)
         const uint32_t mn = (uint32_t)r1v & 0xFFu;
+        const uint32_t ln = s_ltab[mn];
         rec_weights(im, r1v, wn);
         if (P == 0) ld_pair(s - 5u, xl, xh);
         if (P == 2) ld_pair(s - 5u, yl, yh);
         DpFold f;
-        rec_fold_s(mc, wc, f, c, ring);
+        rec_fold_s(lc, wc, f, c, ring);
         if (mc == 0u) dp_walk_rune(v, im, q, be, f, c, ring, longm, gbest, key0);  // overflowed record (rare)
         f.finish();
         ring[(c & (kZhRing - 1u)) * 64u] = f.bestP;
@@ -1202,6 +1214,7 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
             q -= 3u;
             s -= 1u;
             mc = mn;
+            lc = ln;
             ++c;
             return false;
         }
@@ -1577,6 +1590,8 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
     const uint32_t winw = (grp + (kZhWin - kZhGroupBytes)) / 32u + 1u;  // token words of a window (<= kZhWinWords)
     auto lmw = [&](uint32_t w) -> uint32_t { return w < nlw ? lanemask[w] : 0u; };
     Emitter em(sbits, ebits);
+    s_ltab[threadIdx.x] = ltab_entry(threadIdx.x);  // (256 threads)
+    __syncthreads();
     // diagnostic per-wave clocks (JB_ABLATE bit 8): [0] setup [1] DP [2] forward+Viterbi+flush [3] chunks
     // [4] sum of lane DP steps [5] sum of per-chunk max lane DP steps [6] blocks past the window [7] scratch
     uint64_t stv[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // [8] forward walk [9] Viterbi forward half
