@@ -1016,16 +1016,13 @@ __device__ __forceinline__ void dp_walk_rune(const V& v, const DevImage& im, uin
 
 // The weights of a record's edges (ascending L): four loads issued now, with
 // no branch (an absent edge loads wtab[0] and is ignored), so the compiler's
-// vmcnt bookkeeping stays exact and later waits do not drain other loads.
+// vmcnt bookkeeping stays exact and later waits do not drain other loads.  The
+// index fields of absent edges are 0 in every record k_mark_walk writes (its
+// shift register starts at 0), so no select is needed.
 __device__ __forceinline__ void rec_weights(const DevImage& im, uint64_t rc, double w[4]) {
-    uint32_t m = (uint32_t)rc & 0xFFu;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const bool has = m != 0u;
-        m &= m - 1u;
-        const uint32_t idx = (uint32_t)(rc >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u);
-        w[k] = im.wtab[has ? idx : 0u];
-    }
+    for (int k = 0; k < 4; k++)
+        w[k] = im.wtab[(uint32_t)(rc >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u)];
 }
 // Fold a record's edges (L <= kZhRing, so best(i+L) is in the ring or is the
 // sentinel), branch-free: every LDS read is issued and the items are selected.
