@@ -90,6 +90,13 @@ typedef struct {
  * parse the dictionary and emission table, build the device image and upload it
  * to every configured device. */
 int jb_open(const jb_config *cfg, jb_ctx **out);
+/* jb_open from an image built by jb_image_build, so the trie is placed once: what the
+ * Go binding calls after listing the image's log keys (jb_image_log_keys) and taking
+ * math.Log of each (NewTokenizer / NewJiebaTokenizer, tokenizer.go:61-75).  Only
+ * cfg->device, cfg->ndevices and the log table (log_keys, log_vals, nlog: the weights
+ * are recomputed from them, tokenizer.go:503,515-519) are read.  `img` is consumed on
+ * every path, success or not: do not jb_image_free it afterwards. */
+int jb_open_image(jb_image *img, const jb_config *cfg, jb_ctx **out);
 void jb_close(jb_ctx *ctx);
 /* Last error message of the calling thread (never NULL). */
 const char *jb_last_error(void);
@@ -117,12 +124,22 @@ int jb_cut_batch_into(jb_ctx *ctx, const uint8_t *text, const uint64_t *doc_off,
  * readable padding bytes; 16-byte aligned) and d_doc_off (ndocs+1 offsets, d_doc_off[0] == 0,
  * d_doc_off[ndocs] == nbytes) are device pointers on ctx's first device; the
  * work is queued on `stream` (a hipStream_t; NULL = default stream) and the
- * call returns without synchronising.  Results stay in ctx-owned device memory
- * until the next call: *d_start / *d_end (u32 token spans), *d_doc_tok
- * (u64[ndocs+1]) and *d_ntok (u64 token count). */
+ * call returns without synchronising.  Calls on one ctx may come from several
+ * threads and streams: each pipeline waits on the device for the previous one
+ * (the workspace is one per device).  Results stay in ctx-owned device memory
+ * only until the next call on this ctx, from any thread: *d_start / *d_end (u32
+ * token spans), *d_doc_tok (u64[ndocs+1]) and *d_ntok (u64 token count).
+ * Concurrent callers use jb_cut_device_into. */
 int jb_cut_device(jb_ctx *ctx, const uint8_t *d_text, uint64_t nbytes, const uint64_t *d_doc_off,
                   uint32_t ndocs, int hmm, void *stream, uint32_t **d_start, uint32_t **d_end,
                   uint64_t **d_doc_tok, uint64_t **d_ntok);
+/* jb_cut_device into caller-owned device arrays, which nothing else writes: d_start /
+ * d_end hold cap >= nbytes u32 entries (a batch of n bytes has at most n tokens),
+ * d_doc_tok ndocs+1 u64 and *d_ntok the u64 token count, all valid once `stream`
+ * reaches the end of this call's work.  Safe from several threads on one ctx. */
+int jb_cut_device_into(jb_ctx *ctx, const uint8_t *d_text, uint64_t nbytes, const uint64_t *d_doc_off,
+                       uint32_t ndocs, int hmm, void *stream, uint32_t *d_start, uint32_t *d_end, uint64_t cap,
+                       uint64_t *d_doc_tok, uint64_t *d_ntok);
 
 /* Contiguous byte-balanced document ranges, the multi-device partition of
  * jb_cut_batch (the reference's CutParallel deals blocks to
@@ -132,7 +149,9 @@ int jb_cut_device(jb_ctx *ctx, const uint8_t *d_text, uint64_t nbytes, const uin
 int jb_shard_bounds(const uint64_t *doc_off, uint32_t ndocs, uint32_t nparts, uint32_t *cut);
 
 /* Replaces Tokenizer.AddWord (tokenizer.go:372; the reference deadlocks there,
- * :376 + :581).  freq < 1 takes suggestFreq's value (tokenizer.go:589-614). */
+ * :376 + :581).  freq < 1 takes suggestFreq's value (tokenizer.go:589-614).
+ * Atomic: on any error (JB_ELIMIT for a word of more than 255 runes, JB_EDEVICE,
+ * JB_ENOMEM) the dictionary, pd.size and every device's image stay as they were. */
 int jb_add_word(jb_ctx *ctx, const char *word, size_t len, int64_t freq);
 
 /* suggestFreq (tokenizer.go:589-614): the frequency AddWord(word, freq < 1) would store. */

@@ -103,17 +103,21 @@ struct EventTimer final : KernelTimer {
     }
 };
 
-struct Device {
-    int ordinal = 0;
-    std::mutex mu;  // one pipeline at a time per device workspace
-    hipStream_t stream = nullptr;
-    // image
+// One device's copy of the image (jb_common.h layout).
+struct ImageBufs {
     uint16_t* pagemap = nullptr;
     double* emit = nullptr;
     uint64_t* cells = nullptr;
     uint32_t* code = nullptr;
     double* wtab = nullptr;
     uint64_t* l1row = nullptr;
+};
+
+struct Device {
+    int ordinal = 0;
+    std::mutex mu;  // one pipeline at a time per device workspace
+    hipStream_t stream = nullptr;
+    ImageBufs ib{};  // the device image
     DevImage dim{};
     // workspace
     Work w{};
@@ -142,16 +146,22 @@ struct Device {
     uint32_t ncu = 0;
     LaunchCfg lc{};  // launch shape, fixed at jb_open
     uint64_t last_nbytes = 0;  // batch size of the last pipeline run (jb_last_stats)
+    bool has_stats = false;    // this device took part in the last cut (jb_last_stats skips it otherwise)
+    // The workspace is shared by every stream a caller queues on (jb_cut_device): each
+    // pipeline is recorded here, and a pipeline on another stream waits for it first.
+    hipEvent_t ws_done = nullptr;
+    hipStream_t ws_stream = nullptr;
     EventTimer timer;
     bool profile = false;
     // replay cache: the whole pipeline captured as one HIP graph for the last
     // (buffers, sizes, grids) it ran with; any change re-captures
     struct GraphKey {
         const void* text; uint64_t nbytes; const void* doc_off; uint32_t ndocs; bool hmm;
-        uint64_t work_gen; hipStream_t stream;
+        uint64_t work_gen; hipStream_t stream; const void* out_s; const void* out_e; const void* out_d;
         bool operator==(const GraphKey& o) const {
             return text == o.text && nbytes == o.nbytes && doc_off == o.doc_off && ndocs == o.ndocs &&
-                   hmm == o.hmm && work_gen == o.work_gen && stream == o.stream;
+                   hmm == o.hmm && work_gen == o.work_gen && stream == o.stream && out_s == o.out_s &&
+                   out_e == o.out_e && out_d == o.out_d;
         }
     } gkey{};
     hipGraphExec_t gexec = nullptr;  // captured for gkey (null until the key repeats)
@@ -296,7 +306,8 @@ extern "C" int jb_image_build(const jb_config* cfg, jb_image** out) {
         for (size_t i = 0; i < cfg->nlog; i++) im->dict.log_of[cfg->log_keys[i]] = cfg->log_vals[i];
         if ((cfg->size_override > 0 && cfg->size_override != im->dict.size) || cfg->nlog) {  // reweigh
             if (cfg->size_override > 0) im->dict.size = cfg->size_override;
-            if ((rc = build_image(im->dict, im->emit, &im->img, &err))) return fail(rc, "%s", err.c_str());
+            if (!reweigh_image(im->dict, &im->img) && (rc = build_image(im->dict, im->emit, &im->img, &err)))
+                return fail(rc, "%s", err.c_str());
         }
         *out = im.release();
         return JB_OK;
@@ -411,33 +422,50 @@ extern "C" double jb_go_log(double x) { return go_log(x); }
 // ---------------------------------------------------------------------------
 template <class T>
 static int upload(T** dst, const std::vector<T>& src) {
-    dfree(*dst);
     *dst = nullptr;
     HIPCHK(hipMalloc(dst, std::max<size_t>(src.size(), 1) * sizeof(T)));
     if (!src.empty()) HIPCHK(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
     return JB_OK;
 }
 
-static int upload_image(Device* d, const Image& img) {
-    HIPCHK(hipSetDevice(d->ordinal));
-    int rc;
-    if ((rc = upload(&d->pagemap, img.pagemap)) || (rc = upload(&d->emit, img.emit)) ||
-        (rc = upload(&d->cells, img.cells)) || (rc = upload(&d->code, img.code)) || (rc = upload(&d->wtab, img.wtab)))
-        return rc;
-    {  // row-indexed level-1 table: code and level-1 cell of a rune in one 8-byte load
-        std::vector<uint64_t> l1(img.code.size());
-        for (size_t r = 0; r < l1.size(); r++) {
-            const uint32_t cd = img.code[r];
-            l1[r] = jb_l1row_make(cd, cd < img.cells.size() ? img.cells[cd] : 0ull);
-        }
-        if ((rc = upload(&d->l1row, l1))) return rc;
+static void free_image_bufs(ImageBufs* b) {
+    dfree(b->pagemap); dfree(b->emit); dfree(b->cells); dfree(b->code); dfree(b->wtab); dfree(b->l1row);
+    *b = ImageBufs{};
+}
+
+// Copy an image into fresh buffers on `ordinal` (nothing of the device's current image
+// changes; on failure nothing is left allocated).
+static int stage_image(int ordinal, const Image& img, ImageBufs* b) {
+    *b = ImageBufs{};
+    HIPCHK(hipSetDevice(ordinal));
+    // row-indexed level-1 table: code and level-1 cell of a rune in one 8-byte load
+    std::vector<uint64_t> l1(img.code.size());
+    for (size_t r = 0; r < l1.size(); r++) {
+        const uint32_t cd = img.code[r];
+        l1[r] = jb_l1row_make(cd, cd < img.cells.size() ? img.cells[cd] : 0ull);
     }
-    d->dim.l1row = d->l1row;
-    d->dim.pagemap = d->pagemap;
-    d->dim.emit = d->emit;
-    d->dim.cells = d->cells;
-    d->dim.code = d->code;
-    d->dim.wtab = d->wtab;
+    int rc;
+    if ((rc = upload(&b->pagemap, img.pagemap)) || (rc = upload(&b->emit, img.emit)) ||
+        (rc = upload(&b->cells, img.cells)) || (rc = upload(&b->code, img.code)) ||
+        (rc = upload(&b->wtab, img.wtab)) || (rc = upload(&b->l1row, l1))) {
+        free_image_bufs(b);
+        return rc;
+    }
+    return JB_OK;
+}
+
+// Make staged buffers the device's image (the old ones are freed).  The caller holds
+// d->mu and nothing is queued on the device that reads the old image.
+static int install_image(Device* d, ImageBufs* b, const Image& img) {
+    free_image_bufs(&d->ib);
+    d->ib = *b;
+    *b = ImageBufs{};
+    d->dim.l1row = d->ib.l1row;
+    d->dim.pagemap = d->ib.pagemap;
+    d->dim.emit = d->ib.emit;
+    d->dim.cells = d->ib.cells;
+    d->dim.code = d->ib.code;
+    d->dim.wtab = d->ib.wtab;
     d->dim.nrows = img.nrows;
     // a captured pipeline holds the old image pointers in its kernel arguments
     if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
@@ -577,8 +605,8 @@ static int init_launch_cfg(Device* d) {
     return JB_OK;
 }
 
-static int launch(Device* d, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off, uint32_t ndocs,
-                  bool hmm, hipStream_t s) {
+static int launch_pipeline(Device* d, const Work& w, const uint8_t* d_text, uint64_t nbytes,
+                           const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, hipStream_t s) {
     static const bool dbg = getenv("JB_DEBUG") != nullptr;
     const LaunchCfg& lc = d->lc;
     d->last_nbytes = nbytes;
@@ -588,14 +616,14 @@ static int launch(Device* d, const uint8_t* d_text, uint64_t nbytes, const uint6
                 ndocs, lc.grid_zh, lc.zh_group ? lc.zh_group : zh_group_for(nbytes));
     static const bool use_graph = env_int("JB_GRAPH", 1) != 0;
     if (use_graph && !d->profile && lc.diag == 0 && s != nullptr) {
-        const Device::GraphKey key{d_text, nbytes, d_doc_off, ndocs, hmm, d->work_gen, s};
+        const Device::GraphKey key{d_text, nbytes, d_doc_off, ndocs, hmm, d->work_gen, s, w.tok_start, w.tok_end, w.doc_tok};
         const bool repeat = d->gkey_gen != 0 && key == d->gkey;
         if (!repeat) {  // first call with this key: run directly, capture if it comes again
             if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
             d->gexec = nullptr;
             d->gkey = key;
             d->gkey_gen = 1;
-            const hipError_t e = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, lc, s, nullptr);
+            const hipError_t e = run_pipeline(d->dim, w, d_text, nbytes, d_doc_off, ndocs, hmm, lc, s, nullptr);
             if (e != hipSuccess) return fail(JB_EDEVICE, "pipeline launch: %s", hipGetErrorString(e));
             return JB_OK;
         }
@@ -604,7 +632,7 @@ static int launch(Device* d, const uint8_t* d_text, uint64_t nbytes, const uint6
             d->gexec = nullptr;
             hipGraph_t g = nullptr;
             HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-            const hipError_t ec = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, lc, s, nullptr);
+            const hipError_t ec = run_pipeline(d->dim, w, d_text, nbytes, d_doc_off, ndocs, hmm, lc, s, nullptr);
             const hipError_t ee = hipStreamEndCapture(s, &g);
             if (ec != hipSuccess) return fail(JB_EDEVICE, "pipeline capture: %s", hipGetErrorString(ec));
             if (ee != hipSuccess) return fail(JB_EDEVICE, "pipeline capture end: %s", hipGetErrorString(ee));
@@ -619,7 +647,7 @@ static int launch(Device* d, const uint8_t* d_text, uint64_t nbytes, const uint6
         if (el != hipSuccess) return fail(JB_EDEVICE, "pipeline graph launch: %s", hipGetErrorString(el));
         return JB_OK;
     }
-    const hipError_t e = run_pipeline(d->dim, d->w, d_text, nbytes, d_doc_off, ndocs, hmm, lc, s,
+    const hipError_t e = run_pipeline(d->dim, w, d_text, nbytes, d_doc_off, ndocs, hmm, lc, s,
                                       d->profile ? &d->timer : nullptr);
     if (e != hipSuccess) return fail(JB_EDEVICE, "pipeline launch: %s", hipGetErrorString(e));
     if ((lc.diag & 0x100u) && d->w.dbg) {  // diagnostic: per-wave clocks of k_zh (STAMPS builds)
@@ -670,43 +698,94 @@ static int launch(Device* d, const uint8_t* d_text, uint64_t nbytes, const uint6
     return JB_OK;
 }
 
+// Queue the pipeline on stream s.  The workspace is one per device: a pipeline waits
+// for the previous one (on whatever stream it ran) before it starts.  `w` is the
+// device's workspace, or a copy with caller-owned outputs (jb_cut_device_into).
+static int launch(Device* d, const Work& w, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off,
+                  uint32_t ndocs, bool hmm, hipStream_t s) {
+    if (!d->ws_done) HIPCHK(hipEventCreateWithFlags(&d->ws_done, hipEventDisableTiming));
+    else HIPCHK(hipStreamWaitEvent(s, d->ws_done, 0));  // (free on the stream that recorded it)
+    int rc = launch_pipeline(d, w, d_text, nbytes, d_doc_off, ndocs, hmm, s);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(d->ws_done, s));
+    d->ws_stream = s;
+    d->has_stats = true;
+    return JB_OK;
+}
+
+extern "C" void jb_close(jb_ctx* ctx);
+
+// Streams, image and launch shape of one device of a new ctx.
+static int open_device(Device* d, int ordinal, const Image& img) {
+    d->ordinal = ordinal;
+    int rc;
+    HIPCHK(hipSetDevice(d->ordinal));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, d->ordinal));
+    d->ncu = (uint32_t)prop.multiProcessorCount;
+    HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    {
+        // k_small runs one workgroup per call: pinned to one CU (JB_SMALL_CU, default 0) it
+        // finds its 21 KB of code in that CU's instruction cache (and the trie's hot lines
+        // in that XCD's L2) instead of fetching them cold on whichever CU the dispatcher picks
+        const int cu = env_int("JB_SMALL_CU", 0);
+        if (cu < 0 || cu >= (int)d->ncu) return fail(JB_EINVAL, "JB_SMALL_CU=%d: %u CUs", cu, d->ncu);
+        std::vector<uint32_t> mask((d->ncu + 31) / 32, 0u);
+        mask[cu / 32] = 1u << (cu % 32);
+        HIPCHK(hipExtStreamCreateWithCUMask(&d->sstream, (uint32_t)mask.size(), mask.data()));
+    }
+    ImageBufs b;
+    if ((rc = stage_image(d->ordinal, img, &b))) return rc;
+    if ((rc = install_image(d, &b, img))) return rc;
+    if ((rc = init_launch_cfg(d))) return rc;
+    return JB_OK;
+}
+
+extern "C" int jb_open_image(jb_image* img, const jb_config* cfg, jb_ctx** out) {
+    std::unique_ptr<jb_image> own(img);  // consumed on every path
+    if (!img || !cfg || !out) return fail(JB_EINVAL, "jb_open_image: null argument");
+    *out = nullptr;
+    if (cfg->nlog && (!cfg->log_keys || !cfg->log_vals)) return fail(JB_EINVAL, "nlog > 0 without log_keys/log_vals");
+    if (cfg->nlog) {  // the caller's logarithms: new weights, same trie
+        for (size_t i = 0; i < cfg->nlog; i++) img->dict.log_of[cfg->log_keys[i]] = cfg->log_vals[i];
+        if (!reweigh_image(img->dict, &img->img)) {
+            std::string err;
+            const int rc = build_image(img->dict, img->emit, &img->img, &err);
+            if (rc) return fail(rc, "%s", err.c_str());
+        }
+    }
+    auto ctx = std::make_unique<jb_ctx>();
+    ctx->im = std::move(own);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(JB_EDEVICE, "no HIP device available");
+    const int nuse = cfg->ndevices > 0 ? cfg->ndevices : 1;
+    // JB_DEVICE_WRAP=1 (tests): device ordinals wrap around the devices present, so the
+    // multi-device host path (one thread, stream and workspace per device) runs on one GPU
+    const bool wrap = env_int("JB_DEVICE_WRAP", 0) != 0;
+    if (cfg->device < 0 || (!wrap && cfg->device + nuse > ndev) || (wrap && cfg->device >= ndev))
+        return fail(JB_EINVAL, "devices %d..%d requested, %d present", cfg->device, cfg->device + nuse - 1, ndev);
+    int rc = JB_OK;
+    for (int k = 0; k < nuse && rc == JB_OK; k++) {
+        ctx->devs.push_back(std::make_unique<Device>());  // (jb_close releases a partial one)
+        rc = open_device(ctx->devs.back().get(), (cfg->device + k) % ndev, ctx->im->img);
+    }
+    if (rc) {
+        jb_close(ctx.release());
+        return rc;
+    }
+    *out = ctx.release();
+    return JB_OK;
+}
+
 extern "C" int jb_open(const jb_config* cfg, jb_ctx** out) {
     if (!cfg || !out) return fail(JB_EINVAL, "jb_open: null argument");
     *out = nullptr;
     jb_image* img = nullptr;
     int rc = jb_image_build(cfg, &img);
     if (rc) return rc;
-    auto ctx = std::make_unique<jb_ctx>();
-    ctx->im.reset(img);
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(JB_EDEVICE, "no HIP device available");
-    const int nuse = cfg->ndevices > 0 ? cfg->ndevices : 1;
-    if (cfg->device < 0 || cfg->device + nuse > ndev)
-        return fail(JB_EINVAL, "devices %d..%d requested, %d present", cfg->device, cfg->device + nuse - 1, ndev);
-    for (int k = 0; k < nuse; k++) {
-        auto d = std::make_unique<Device>();
-        d->ordinal = cfg->device + k;
-        HIPCHK(hipSetDevice(d->ordinal));
-        hipDeviceProp_t prop;
-        HIPCHK(hipGetDeviceProperties(&prop, d->ordinal));
-        d->ncu = (uint32_t)prop.multiProcessorCount;
-        HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
-        {
-            // k_small runs one workgroup per call: pinned to one CU (JB_SMALL_CU, default 0) it
-            // finds its 21 KB of code in that CU's instruction cache (and the trie's hot lines
-            // in that XCD's L2) instead of fetching them cold on whichever CU the dispatcher picks
-            const int cu = env_int("JB_SMALL_CU", 0);
-            if (cu < 0 || cu >= (int)d->ncu) return fail(JB_EINVAL, "JB_SMALL_CU=%d: %u CUs", cu, d->ncu);
-            std::vector<uint32_t> mask((d->ncu + 31) / 32, 0u);
-            mask[cu / 32] = 1u << (cu % 32);
-            HIPCHK(hipExtStreamCreateWithCUMask(&d->sstream, (uint32_t)mask.size(), mask.data()));
-        }
-        if ((rc = upload_image(d.get(), img->img))) return rc;
-        if ((rc = init_launch_cfg(d.get()))) return rc;
-        ctx->devs.push_back(std::move(d));
-    }
-    *out = ctx.release();
-    return JB_OK;
+    jb_config c = *cfg;
+    c.nlog = 0;  // (jb_image_build applied the log table)
+    return jb_open_image(img, &c, out);
 }
 
 extern "C" void jb_close(jb_ctx* ctx) {
@@ -719,8 +798,10 @@ extern "C" void jb_close(jb_ctx* ctx) {
         if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
         d->gexec = nullptr;
         free_work(&d->w);
-        dfree(d->text); dfree(d->doc_off); dfree(d->pagemap); dfree(d->emit); dfree(d->cells); dfree(d->code);
-        dfree(d->wtab); dfree(d->l1row);
+        if (d->ws_done) (void)hipEventSynchronize(d->ws_done);  // (a caller's stream may be gone by now)
+        dfree(d->text); dfree(d->doc_off);
+        free_image_bufs(&d->ib);
+        if (d->ws_done) (void)hipEventDestroy(d->ws_done);
         hfree(d->h_text); hfree(d->h_span); hfree(d->h_misc); hfree(d->h_cnt); hfree(d->h_sin); hfree(d->h_sout);
         for (hipEvent_t e : d->ev) (void)hipEventDestroy(e);
         (void)hipStreamDestroy(d->stream);
@@ -749,6 +830,7 @@ static int cut_small(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         HIPCHK(hipHostMalloc(&d->h_sout, kSmallOutBytes, fl));
         HIPCHK(hipHostGetDevicePointer((void**)&d->d_sin, d->h_sin, 0));
         HIPCHK(hipHostGetDevicePointer((void**)&d->d_sout, d->h_sout, 0));
+        d->h_sout[SM_DONE] = 0;  // (recycled pinned memory may hold any value; small_seq starts at 1)
     }
     const auto c0 = std::chrono::steady_clock::now();
     // a batch that fits the kernel arguments (96 bytes, 7 documents) travels in them (the kernel reads them from
@@ -788,6 +870,7 @@ static int cut_small(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
     const uint32_t* h = d->h_sout;
     memcpy(d->small_hdr, h, sizeof d->small_hdr);
     d->last_small = true;
+    d->has_stats = true;
     static const bool dbg = getenv("JB_DEBUG") != nullptr;
     if (dbg) {  // k_small's phase clocks (10 ns ticks from its start)
         auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
@@ -878,7 +961,7 @@ static int cut_range(jb_ctx* ctx, Device* d, const uint8_t* text, const uint64_t
             if (err) return fail(JB_EDEVICE, "H2D copy failed");
         }
         const auto c1 = now();
-        if ((rc = launch(d, d->text, nbytes, d->doc_off, nd, hmm, d->stream))) return rc;
+        if ((rc = launch(d, d->w, d->text, nbytes, d->doc_off, nd, hmm, d->stream))) return rc;
         HIPCHK(hipMemcpyAsync(d->h_cnt, d->w.counters, 8 * 4, hipMemcpyDeviceToHost, d->stream));
         HIPCHK(hipStreamSynchronize(d->stream));
         const auto c2 = now();
@@ -978,6 +1061,10 @@ static int cut_sharded(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off
     std::vector<uint32_t> cut(nd + 1, ndocs);
     int rc0 = jb_shard_bounds(doc_off, ndocs, (uint32_t)nd, cut.data());
     if (rc0) return rc0;
+    for (auto& d : ctx->devs) {  // jb_last_stats: only the devices this batch reaches
+        std::lock_guard<std::mutex> g(d->mu);
+        d->has_stats = false;
+    }
     std::vector<int> rcs(nd, JB_OK);
     std::vector<std::string> errs(nd);
     auto work = [&](size_t k) {
@@ -1126,25 +1213,57 @@ extern "C" void jb_spans_free(jb_spans* s) {
     memset(s, 0, sizeof *s);
 }
 
-extern "C" int jb_cut_device(jb_ctx* ctx, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off,
-                             uint32_t ndocs, int hmm, void* stream, uint32_t** d_start, uint32_t** d_end,
-                             uint64_t** d_doc_tok, uint64_t** d_ntok) {
+static int cut_device(jb_ctx* ctx, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off,
+                      uint32_t ndocs, int hmm, void* stream, uint32_t* o_start, uint32_t* o_end, uint64_t* o_doc_tok,
+                      uint64_t* o_ntok, uint32_t** d_start, uint32_t** d_end, uint64_t** d_doc_tok, uint64_t** d_ntok) {
     if (!ctx || (!d_text && nbytes) || !d_doc_off) return fail(JB_EINVAL, "jb_cut_device: null argument");
     if (nbytes >= (1ull << 31)) return fail(JB_ELIMIT, "device batch of %llu bytes (limit 2 GiB)",
                                             (unsigned long long)nbytes);
     if (((uintptr_t)d_text & 15u) != 0) return fail(JB_EINVAL, "d_text must be 16-byte aligned");
     std::shared_lock<std::shared_mutex> rl(ctx->lock);
+    for (size_t k = 1; k < ctx->devs.size(); k++) {
+        std::lock_guard<std::mutex> g(ctx->devs[k]->mu);
+        ctx->devs[k]->has_stats = false;
+    }
     Device* d = ctx->devs[0].get();
     std::lock_guard<std::mutex> g(d->mu);
     HIPCHK(hipSetDevice(d->ordinal));
     int rc;
     if ((rc = ensure_work(d, nbytes, ndocs))) return rc;
-    if ((rc = launch(d, d_text, nbytes, d_doc_off, ndocs, hmm != 0, (hipStream_t)stream))) return rc;
+    const hipStream_t s = (hipStream_t)stream;
+    if (o_start) {  // caller-owned outputs: the pipeline writes its spans and offsets there
+        Work w = d->w;
+        w.tok_start = o_start;
+        w.tok_end = o_end;
+        w.doc_tok = o_doc_tok;
+        if ((rc = launch(d, w, d_text, nbytes, d_doc_off, ndocs, hmm != 0, s))) return rc;
+        HIPCHK(hipMemcpyAsync(o_ntok, d->w.counters + CNT_NWORDS, 8, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipEventRecord(d->ws_done, s));  // (the counters are workspace too)
+        return JB_OK;
+    }
+    if ((rc = launch(d, d->w, d_text, nbytes, d_doc_off, ndocs, hmm != 0, s))) return rc;
     if (d_start) *d_start = d->w.tok_start;
     if (d_end) *d_end = d->w.tok_end;
     if (d_doc_tok) *d_doc_tok = d->w.doc_tok;
     if (d_ntok) *d_ntok = reinterpret_cast<uint64_t*>(d->w.counters + CNT_NWORDS);
     return JB_OK;
+}
+
+extern "C" int jb_cut_device(jb_ctx* ctx, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off,
+                             uint32_t ndocs, int hmm, void* stream, uint32_t** d_start, uint32_t** d_end,
+                             uint64_t** d_doc_tok, uint64_t** d_ntok) {
+    return cut_device(ctx, d_text, nbytes, d_doc_off, ndocs, hmm, stream, nullptr, nullptr, nullptr, nullptr, d_start,
+                      d_end, d_doc_tok, d_ntok);
+}
+
+extern "C" int jb_cut_device_into(jb_ctx* ctx, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off,
+                                  uint32_t ndocs, int hmm, void* stream, uint32_t* d_start, uint32_t* d_end,
+                                  uint64_t cap, uint64_t* d_doc_tok, uint64_t* d_ntok) {
+    if (!d_start || !d_end || !d_doc_tok || !d_ntok) return fail(JB_EINVAL, "jb_cut_device_into: null output");
+    if (cap < nbytes) return fail(JB_EINVAL, "jb_cut_device_into: cap %llu < nbytes %llu (a batch of n bytes "
+                                  "has up to n tokens)", (unsigned long long)cap, (unsigned long long)nbytes);
+    return cut_device(ctx, d_text, nbytes, d_doc_off, ndocs, hmm, stream, d_start, d_end, d_doc_tok, d_ntok, nullptr,
+                      nullptr, nullptr, nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -1212,18 +1331,39 @@ extern "C" int jb_add_word(jb_ctx* ctx, const char* word, size_t len, int64_t fr
     int rc;
     std::unique_lock<std::shared_mutex> wl(ctx->lock);  // (the reference deadlocks here: :376 + :581)
     if (freq < 1 && (rc = suggest_freq(ctx, word, len, &freq))) return rc;
-    // addTerm (tokenizer.go:580-585): no prefix entries are added
-    Dictionary& dict = ctx->im->dict;
-    dict.term_freq[std::string(word, len)] = freq;
-    dict.size += freq;
-    std::string err;
-    if ((rc = build_image(dict, ctx->im->emit, &ctx->im->img, &err))) return fail(rc, "%s", err.c_str());
-    if (ctx->im->img.maxlen > 255) return fail(JB_ELIMIT, "dictionary word of %u runes (max 255)", ctx->im->img.maxlen);
-    for (auto& d : ctx->devs) {
-        std::lock_guard<std::mutex> g(d->mu);
-        (void)hipSetDevice(d->ordinal);
-        (void)hipStreamSynchronize(d->stream);
-        if ((rc = upload_image(d.get(), ctx->im->img))) return rc;
+    // addTerm (tokenizer.go:580-585): no prefix entries are added.  The new dictionary and
+    // image are built aside and staged on every device; ctx changes only once all of that
+    // worked, so a failure (JB_ELIMIT, JB_EDEVICE, JB_ENOMEM) leaves it as it was.
+    try {
+        Dictionary nd = ctx->im->dict;
+        nd.term_freq[std::string(word, len)] = freq;
+        nd.size += freq;
+        Image ni;
+        std::string err;
+        if ((rc = build_image(nd, ctx->im->emit, &ni, &err))) return fail(rc, "%s", err.c_str());
+        if (ni.maxlen > 255) return fail(JB_ELIMIT, "dictionary word of %u runes (max 255)", ni.maxlen);
+        std::vector<ImageBufs> staged(ctx->devs.size());
+        for (size_t k = 0; k < ctx->devs.size() && rc == JB_OK; k++)
+            rc = stage_image(ctx->devs[k]->ordinal, ni, &staged[k]);
+        if (rc) {
+            for (auto& b : staged) {
+                (void)hipSetDevice(ctx->devs[&b - staged.data()]->ordinal);
+                free_image_bufs(&b);
+            }
+            return rc;
+        }
+        for (size_t k = 0; k < ctx->devs.size(); k++) {  // commit
+            Device* d = ctx->devs[k].get();
+            std::lock_guard<std::mutex> g(d->mu);
+            (void)hipSetDevice(d->ordinal);
+            (void)hipStreamSynchronize(d->stream);
+            if (d->ws_done) (void)hipEventSynchronize(d->ws_done);  // (a jb_cut_device pipeline)
+            (void)install_image(d, &staged[k], ni);
+        }
+        ctx->im->dict = std::move(nd);
+        ctx->im->img = std::move(ni);
+    } catch (const std::bad_alloc&) {
+        return fail(JB_ENOMEM, "out of host memory rebuilding the dictionary");
     }
     return JB_OK;
 }
@@ -1244,6 +1384,7 @@ extern "C" int jb_last_stats(jb_ctx* ctx, jb_stats* out) {
     std::shared_lock<std::shared_mutex> rl(ctx->lock);
     for (auto& d : ctx->devs) {
         std::lock_guard<std::mutex> g(d->mu);
+        if (!d->has_stats) continue;  // not reached by the last batch (its counters are older)
         if (d->last_small) {  // k_small's counters came back with its spans
             out->tokens += d->small_hdr[SM_NTOK];
             out->blocks += d->small_hdr[SM_BLOCKS];

@@ -697,6 +697,38 @@ int build_image(const Dictionary& d, const Emission& e, Image* img, std::string*
     return JB_OK;
 }
 
+bool reweigh_image(const Dictionary& d, Image* img) {
+    // weight index -> the frequency whose weight it holds (from the cells the keys reach)
+    std::vector<int64_t> freq_of(img->wtab.size(), 0);
+    std::vector<uint8_t> seen(img->wtab.size(), 0);
+    std::vector<uint32_t> runes;
+    const double total = dict_log(d, d.size);
+    auto weight = [&](int64_t f) { return dict_log(d, f) - total; };
+    for (const auto& kv : d.term_freq) {
+        if (!valid_runes(kv.first, &runes) || runes.empty()) continue;
+        bool han = true;
+        for (uint32_t r : runes) han = han && jb_is_han(r);
+        if (!han) continue;
+        const Lookup lk = image_lookup(*img, runes.data(), runes.size());
+        if (!lk.found) continue;  // unreachable (a txt-semantics key without its prefixes): no cell
+        if (lk.widx >= freq_of.size()) return false;  // not the image of these keys
+        if (!seen[lk.widx]) {
+            seen[lk.widx] = 1;
+            freq_of[lk.widx] = kv.second;
+        } else if (freq_of[lk.widx] != kv.second) {
+            const double a = weight(freq_of[lk.widx]), b = weight(kv.second);
+            if (memcmp(&a, &b, 8) != 0) return false;  // one index, two weights now
+        }
+    }
+    img->size = d.size;
+    img->total = total;
+    img->w_absent = dict_log(d, 1) - total;  // tf := 1.0 when the piece is absent (tokenizer.go:515)
+    img->wtab[0] = img->w_absent;
+    for (size_t i = 1; i < img->wtab.size(); i++)
+        if (seen[i]) img->wtab[i] = weight(freq_of[i]);
+    return true;
+}
+
 Lookup image_lookup(const Image& img, const uint32_t* runes, size_t n) {
     Lookup out;
     if (n == 0 || runes[0] >= 0x110000u) return out;

@@ -71,6 +71,11 @@ int parse_gob_dictionary(const char* buf, size_t len, Dictionary* out, std::stri
 int parse_emission(const char* buf, size_t len, Emission* out, std::string* err);
 // Returns 0 or JB_ELIMIT (too many trie nodes / distinct weights for the packed layout).
 int build_image(const Dictionary& d, const Emission& e, Image* img, std::string* err);
+// Recompute an image's weights (total, w_absent, wtab) from d's size and logarithms
+// (dict_log) without placing the trie again; img must have been built from d's keys
+// and frequencies.  Returns false when two frequencies that share a weight index get
+// different weights (the caller then runs build_image).
+bool reweigh_image(const Dictionary& d, Image* img);
 
 // Serialized image: dictionary + emission maps + device arrays (fast start).
 void save_image(const Dictionary& d, const Emission& e, const Image& img, std::string* out);

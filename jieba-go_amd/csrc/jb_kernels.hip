@@ -776,6 +776,14 @@ static_assert(kZhGroupBytes % 32u == 0u && kZhGroupSmall % 32u == 0u && kZhGroup
               "k_zh groups are whole token-bitmap words");
 static_assert(2u * kZhWinWords <= 2u * kZhRing * 64u, "token bitmaps fit over the ring");
 static_assert(kZhWin < 65536u, "window offsets are packed in 16 bits");
+// k_zh stages a group's lane-mask words plus two 64-word rounds after them (lm_collect reads
+// round rw and its lookahead rw + 64, with rw < the group's words) into the wave's ring area.
+// (A 12 KiB group once read 64 unstaged ring words here, built garbage block bounds from
+// them and faulted on global memory: the staged count now follows the group size.)
+constexpr uint32_t kZhStageWords = kZhGroupBytes / 16u + 128u;
+constexpr uint32_t kZhStagePer = (kZhStageWords + 63u) / 64u;  // words per lane
+static_assert(kZhStagePer * 64u <= 2u * kZhRing * 64u,
+              "k_zh: a group's lane-mask words and their lookahead must fit the wave's ring (JB_ZH_GROUP <= 14336)");
 
 // A3: every rune of the block is 3 bytes (no 4-byte Han), so rune steps are
 // plain arithmetic instead of dependent byte reads.
@@ -1616,15 +1624,15 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
         // words; a block ends at the next block start of any kind (bits 0-15).
         const uint32_t gw0 = wb >> 4;
         const uint32_t gnw = (uint32_t)((min((uint64_t)wb + grp, nbytes) - wb + 15u) >> 4);
-        // The group's lane-mask words and those after it (block ends, up to 8 KiB of text)
-        // are staged in the wave's ring area, which is free until the DP.
+        // The group's lane-mask words and the two rounds after them (block ends) are
+        // staged in the wave's ring area, which is free until the DP.
         uint32_t* const lmv = rb32;
         auto stage = [&]() {
-            uint32_t v[8];
+            uint32_t v[kZhStagePer];
 #pragma unroll
-            for (int k = 0; k < 8; k++) v[k] = lmw(gw0 + lane + 64u * (uint32_t)k);
+            for (uint32_t k = 0; k < kZhStagePer; k++) v[k] = lmw(gw0 + lane + 64u * k);
 #pragma unroll
-            for (int k = 0; k < 8; k++) lmv[lane + 64u * (uint32_t)k] = v[k];
+            for (uint32_t k = 0; k < kZhStagePer; k++) lmv[lane + 64u * k] = v[k];
             wave_sync();
         };
         stage();

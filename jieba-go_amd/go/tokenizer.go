@@ -40,6 +40,8 @@ func open(dictPath, emitPath string, kind C.int, size int64) *Tokenizer {
 	ce := C.CString(emitPath)
 	defer C.free(unsafe.Pointer(cd))
 	defer C.free(unsafe.Pointer(ce))
+	// cfg is Go memory passed to C by address, so every pointer it holds is C memory
+	// (cgo pointer rules: no Go pointer to memory that holds Go pointers).
 	var cfg C.jb_config
 	cfg.dict_path = cd
 	cfg.emit_path = ce
@@ -48,28 +50,37 @@ func open(dictPath, emitPath string, kind C.int, size int64) *Tokenizer {
 	cfg.device = 0
 	cfg.ndevices = 1
 	// calcDagProba's weights are math.Log(tf) - math.Log(pd.size) (tokenizer.go:503,
-	// 515-519): list the values the dictionary needs, take Go's own math.Log of
-	// each and hand the table to the library, so the weights are Go's bit for bit.
+	// 515-519): build the image once, list the values its weights need, take Go's own
+	// math.Log of each and open the device context from that image with the table
+	// (jb_open_image reweighs it; the trie is not placed again).
 	var img *C.jb_image
 	if rc := C.jb_image_build(&cfg, &img); rc != C.JB_OK {
 		log.Fatal("jiebahip: ", lastError())
 	}
 	var n C.size_t
-	C.jb_image_log_keys(img, nil, 0, &n)
-	keys := make([]int64, int(n)+1)
-	vals := make([]float64, int(n)+1)
-	if rc := C.jb_image_log_keys(img, (*C.int64_t)(unsafe.Pointer(&keys[0])), n, &n); rc != C.JB_OK {
+	if rc := C.jb_image_log_keys(img, nil, 0, &n); rc != C.JB_OK && rc != C.JB_ELIMIT {
+		C.jb_image_free(img)
 		log.Fatal("jiebahip: ", lastError())
 	}
-	C.jb_image_free(img)
-	for i := 0; i < int(n); i++ {
-		vals[i] = math.Log(float64(keys[i]))
+	cnt := int(n) + 1
+	ckeys := (*C.int64_t)(C.malloc(C.size_t(cnt) * C.size_t(unsafe.Sizeof(C.int64_t(0)))))
+	cvals := (*C.double)(C.malloc(C.size_t(cnt) * C.size_t(unsafe.Sizeof(C.double(0)))))
+	defer C.free(unsafe.Pointer(ckeys))
+	defer C.free(unsafe.Pointer(cvals))
+	if rc := C.jb_image_log_keys(img, ckeys, n, &n); rc != C.JB_OK {
+		C.jb_image_free(img)
+		log.Fatal("jiebahip: ", lastError())
 	}
-	cfg.log_keys = (*C.int64_t)(unsafe.Pointer(&keys[0]))
-	cfg.log_vals = (*C.double)(unsafe.Pointer(&vals[0]))
+	keys := unsafe.Slice(ckeys, cnt)
+	vals := unsafe.Slice(cvals, cnt)
+	for i := 0; i < int(n); i++ {
+		vals[i] = C.double(math.Log(float64(keys[i])))
+	}
+	cfg.log_keys = ckeys
+	cfg.log_vals = cvals
 	cfg.nlog = n
 	var ctx *C.jb_ctx
-	if rc := C.jb_open(&cfg, &ctx); rc != C.JB_OK {
+	if rc := C.jb_open_image(img, &cfg, &ctx); rc != C.JB_OK { // consumes img
 		// the reference stops the process on load errors (tokenizer.go:397,443,656)
 		log.Fatal("jiebahip: ", lastError())
 	}
@@ -212,9 +223,12 @@ func (t *Tokenizer) AddWord(word string, freq int) {
 	// Go's math.Log of the new frequency and of the new pd.size for the rebuild
 	// (addTerm adds freq to pd.size even when the word was present, tokenizer.go:580-585)
 	size := int64(C.jb_dict_size(t.ctx))
-	keys := []int64{int64(f), size + int64(f)}
+	keys := []int64{int64(f), size + int64(f)} // (Go memory without Go pointers: may be passed to C)
 	vals := []float64{math.Log(float64(keys[0])), math.Log(float64(keys[1]))}
-	C.jb_add_log(t.ctx, (*C.int64_t)(unsafe.Pointer(&keys[0])), (*C.double)(unsafe.Pointer(&vals[0])), 2)
+	if rc := C.jb_add_log(t.ctx, (*C.int64_t)(unsafe.Pointer(&keys[0])), (*C.double)(unsafe.Pointer(&vals[0])), 2); rc != C.JB_OK {
+		log.Fatal("jiebahip: ", lastError())
+	}
+	// atomic: on an error the dictionary and the device image are unchanged
 	if rc := C.jb_add_word(t.ctx, cw, C.size_t(len(word)), f); rc != C.JB_OK {
 		log.Fatal("jiebahip: ", lastError())
 	}

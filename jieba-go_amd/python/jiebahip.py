@@ -26,7 +26,7 @@ JIEBA_SIZE = 60_101_967  # tokenizer.go:454
 # Every symbol include/jiebahip.h declares.
 EXPORTS = [
     "jb_open", "jb_close", "jb_last_error", "jb_cut", "jb_cut_batch", "jb_cut_batch_into", "jb_spans_free",
-    "jb_cut_device",
+    "jb_cut_device", "jb_cut_device_into", "jb_open_image",
     "jb_add_word", "jb_dict_get", "jb_dict_size", "jb_save", "jb_profile_enable", "jb_profile_read",
     "jb_profile_reset", "jb_image_build", "jb_image_free", "jb_image_save", "jb_image_dict_info", "jb_image_lookup",
     "jb_image_stats", "jb_image_emit", "jb_go_log", "jb_shard_bounds", "jb_last_stats",
@@ -94,6 +94,9 @@ def lib():
         L.jb_spans_free.restype = None
         L.jb_cut_device.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_int, vp, C.POINTER(vp), C.POINTER(vp),
                                     C.POINTER(vp), C.POINTER(vp)]
+        L.jb_cut_device_into.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_int, vp, vp, vp, C.c_uint64, vp,
+                                         vp]
+        L.jb_open_image.argtypes = [vp, C.POINTER(jb_config), C.POINTER(vp)]
         L.jb_add_word.argtypes = [vp, cp, C.c_size_t, C.c_int64]
         L.jb_dict_get.argtypes = [vp, cp, C.c_size_t, C.POINTER(C.c_int64)]
         L.jb_dict_size.argtypes = [vp]
@@ -240,6 +243,18 @@ class Tokenizer:
         self.h = h
 
     @classmethod
+    def from_image(cls, image, device=0, ndevices=1, logs=None):
+        """jb_open_image: a ctx from an Image built by jb_image_build (the trie is placed
+        once), optionally reweighed with the caller's {x: math.Log(x)}.  Consumes `image`."""
+        cfg = make_config(dict_bytes=b"", device=device, ndevices=ndevices, logs=logs)
+        h, img = C.c_void_p(), image.h
+        image.h = None  # jb_open_image owns it from here, success or not
+        _check(lib().jb_open_image(img, C.byref(cfg), C.byref(h)))
+        self = cls.__new__(cls)
+        self.h = h
+        return self
+
+    @classmethod
     def NewTokenizer(cls, dictionaryFile, emit_path="prob_emit.json", device=0):
         """tokenizer.go:61 — dict.txt semantics."""
         return cls(make_config(dict_path=dictionaryFile, emit_path=emit_path, kind=JB_DICT_TXT, device=device))
@@ -340,6 +355,13 @@ class Tokenizer:
         _check(lib().jb_cut_device(self.h, C.c_void_p(d_text_ptr), nbytes, C.c_void_p(d_doc_off_ptr), ndocs,
                                    int(hmm), C.c_void_p(stream_ptr), C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
         return a.value, b.value, c.value, d.value
+
+    def cut_device_into(self, d_text_ptr, nbytes, d_doc_off_ptr, ndocs, hmm, d_start, d_end, cap, d_doc_tok, d_ntok,
+                        stream_ptr=0):
+        """jb_cut_device_into: caller-owned device outputs (raw pointers)."""
+        _check(lib().jb_cut_device_into(self.h, C.c_void_p(d_text_ptr), nbytes, C.c_void_p(d_doc_off_ptr), ndocs,
+                                        int(hmm), C.c_void_p(stream_ptr), C.c_void_p(d_start), C.c_void_p(d_end),
+                                        cap, C.c_void_p(d_doc_tok), C.c_void_p(d_ntok)))
 
     def last_stats(self):
         """Counters of the last pipeline run (jb_last_stats); synchronises."""

@@ -1,7 +1,9 @@
 /*
  * c_abi_smoke.c — a plain C99 consumer of include/jiebahip.h, the way a cgo
- * preamble binds it: open, Cut one text, cut a batch, cut a
- * batch into caller arrays, AddWord with suggestFreq, Cut again, close.
+ * preamble binds it: open as the Go binding does (build the
+ * image, list its log keys, hand malloc'd logarithms to jb_open_image), Cut one
+ * text, cut a batch, cut a batch into caller arrays, AddWord with suggestFreq,
+ * Cut again, close.
  * Spans go to stdout, one line per call, for tests/test_gpu_parity.py to check
  * against the oracle.
  *
@@ -69,7 +71,34 @@ int main(int argc, char **argv) {
     cfg.dict_path = argv[1];
     cfg.dict_kind = JB_DICT_TXT;
     cfg.emit_path = argv[2];
-    if ((rc = jb_open(&cfg, &ctx))) return die("jb_open", rc);
+    {
+        /* jieba-go_amd/go/tokenizer.go open(): the image is built once; the log table
+         * lives in C memory (cgo: no Go pointers inside a struct passed to C).  Go passes
+         * math.Log; this C caller passes the library's restatement of it. */
+        jb_image *img = NULL;
+        size_t nk = 0, i;
+        int64_t *keys;
+        double *vals;
+        if ((rc = jb_image_build(&cfg, &img))) return die("jb_image_build", rc);
+        rc = jb_image_log_keys(img, NULL, 0, &nk);
+        if (rc != JB_OK && rc != JB_ELIMIT) return die("jb_image_log_keys (count)", rc);
+        keys = (int64_t *)malloc((nk + 1) * sizeof *keys);
+        vals = (double *)malloc((nk + 1) * sizeof *vals);
+        if (!keys || !vals) return die("malloc", JB_ENOMEM);
+        if ((rc = jb_image_log_keys(img, keys, nk, &nk))) return die("jb_image_log_keys", rc);
+        for (i = 0; i < nk; i++) vals[i] = jb_go_log((double)keys[i]);
+        cfg.log_keys = keys;
+        cfg.log_vals = vals;
+        cfg.nlog = nk;
+        rc = jb_open_image(img, &cfg, &ctx); /* consumes img */
+        free(keys);
+        free(vals);
+        cfg.log_keys = NULL;
+        cfg.log_vals = NULL;
+        cfg.nlog = 0;
+        if (rc) return die("jb_open_image", rc);
+        printf("log keys %lu\n", (unsigned long)nk);
+    }
 
     /* Tokenizer.Cut(text, true) */
     if ((rc = jb_cut(ctx, (const uint8_t *)text, (size_t)len, 1, &sp))) return die("jb_cut", rc);

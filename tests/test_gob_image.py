@@ -162,3 +162,58 @@ def test_image_corruption_detected(syn_small, tmp_path):
             J.Image(J.make_config(dict_path=q, kind=J.JB_DICT_IMAGE))
         assert ei.value.code == J.JB_EPARSE, mutate
     assert not os.path.exists(p + ".tmp")
+
+
+def test_saved_image_reweighed_by_log_table(syn_small, tmp_path, monkeypatch, capfd):
+    """A saved image opened with a caller log table (and a new size) is reweighed in
+    place (reweigh_image: same trie, new wtab), and its weights equal those of a full
+    build from the dictionary with the same table."""
+    import math
+    dp, ep, _ = syn_small
+    a = J.Image(J.make_config(dict_path=dp, emit_path=ep))
+    p = str(tmp_path / "syn.jbimg")
+    a.save(p)
+    keys = [int(x) for x in a.log_keys()]
+    size = a.stats()["size"]
+    new_size = size + 12345
+    rng = random.Random(3)
+    # perturb a third of the logarithms by one ulp, either way, and the new size's
+    logs = {k: math.nextafter(J.go_log(k), rng.choice([math.inf, -math.inf])) if rng.random() < 0.33 else J.go_log(k)
+            for k in keys}
+    logs[new_size] = math.nextafter(J.go_log(new_size), math.inf)
+    monkeypatch.setenv("JB_DEBUG_BUILD", "1")  # build_image reports its trie placement
+    capfd.readouterr()
+    re = J.Image(J.make_config(dict_path=p, kind=J.JB_DICT_IMAGE, size_override=new_size, logs=logs))
+    assert "trie placement" not in capfd.readouterr().err  # reweighed, not rebuilt
+    full = J.Image(J.make_config(dict_path=dp, emit_path=ep, size_override=new_size, logs=logs))
+    assert re.stats()["cap"] == a.stats()["cap"]  # the saved trie, not a new placement
+    assert _bits(re.stats()["w_absent"]) == _bits(full.stats()["w_absent"])
+    o = O.Oracle.from_files(dp, ep, 0)
+    items = o.items()
+    n = 0
+    for k in sorted(items):
+        lk = re.lookup(k)
+        if lk is None:
+            continue
+        n += 1
+        assert _bits(lk[1]) == _bits(full.lookup(k)[1]), k
+        assert _bits(lk[1]) == _bits(logs.get(items[k], J.go_log(items[k])) - logs[new_size]), k
+    assert n > 5000
+
+
+def _bits(x):
+    import struct
+    return struct.pack("<d", x)
+
+
+def test_open_image_without_gpu_consumes_image(syn_small):
+    """jb_open_image (the Go binding's constructor path) fails loudly without a device
+    and takes ownership of the image either way."""
+    dp, ep, _ = syn_small
+    img = J.Image(J.make_config(dict_path=dp, emit_path=ep))
+    logs = {int(k): J.go_log(int(k)) for k in img.log_keys()}
+    with pytest.raises(J.JbError) as e:
+        J.Tokenizer.from_image(img, logs=logs)
+    assert e.value.code == J.JB_EDEVICE
+    assert img.h is None  # consumed: no double free at close
+    img.close()

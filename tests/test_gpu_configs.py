@@ -1,0 +1,155 @@
+"""GPU: BASELINE config 4 at its full size, the multi-device host path and
+concurrent device-resident callers — each against the oracle, bit-exact, through
+the C ABI.  Every test here needs the GPU."""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import jiebahip as J
+import oracle as O
+import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _threads():
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def _cmp(gs, ge, gd, os_, oe, od, label):
+    if not (len(gs) == len(os_) and np.array_equal(gs, os_) and np.array_equal(ge, oe)):
+        n = min(len(gs), len(os_))
+        bad = int(np.argmax((gs[:n] != os_[:n]) | (ge[:n] != oe[:n]))) if n else 0
+        raise AssertionError(f"{label}: {len(gs)} vs {len(os_)} tokens, first difference at token {bad}")
+    assert np.array_equal(gd, od), label
+
+
+def _device_cut(tk, buf, off, hmm):
+    """The bench's measured path (bench.GpuCutter): input resident in HBM,
+    jb_cut_device on the current stream, results copied back afterwards."""
+    import torch
+    nbytes, nd = int(off[-1]), len(off) - 1
+    d_text = torch.from_numpy(np.ascontiguousarray(buf[: nbytes + 64])).cuda()
+    d_off = torch.from_numpy(np.asarray(off, np.int64)).cuda()
+    stream = torch.cuda.current_stream().cuda_stream
+    ps, pe, pd, pn = tk.cut_device(d_text.data_ptr(), nbytes, d_off.data_ptr(), nd, hmm, stream)
+    torch.cuda.synchronize()
+    n = int(J.dev_to_host(pn, 8, np.uint64)[0])
+    out = (J.dev_to_host(ps, 4 * n, np.uint32).astype(np.uint64), J.dev_to_host(pe, 4 * n, np.uint32).astype(np.uint64),
+           J.dev_to_host(pd, 8 * (nd + 1), np.uint64))
+    del d_text, d_off
+    return out
+
+
+def test_config4_full_corpus(syn_full):
+    """BASELINE config 4 at the size its metric is quoted on: the 1 GiB C_syn corpus
+    (the bench's workload, 73k documents), cut on the device as bench.py times it,
+    every token against the oracle (tokenizer_test.go:16-26 cut big texts the same
+    way).  A 1M-rune unpunctuated document with 30 % OOV runes (config 5b) rides at
+    the end of the batch, so the long-block kernels run in the same pipeline."""
+    dp, ep, s = syn_full
+    tk = J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep))
+    o = O.Oracle.from_files(dp, ep, 0)
+    buf, off, _ = s.corpus_parallel(synth.KIND_DOCS, 0, target_bytes=1 << 30, threads=_threads())
+    lbuf, loff, _ = s.corpus(synth.KIND_LONG_OOV, 5, target_runes=1_000_000)
+    n0, nl = int(off[-1]), int(loff[-1])
+    big = np.zeros(n0 + nl + 64, np.uint8)
+    big[:n0] = buf[:n0]
+    big[n0:n0 + nl] = lbuf[:nl]
+    del buf
+    boff = np.concatenate([np.asarray(off, np.uint64), np.asarray(loff[1:], np.uint64) + np.uint64(n0)])
+    assert n0 >= (1 << 30) - (1 << 20) and len(boff) - 1 > 70_000
+    O.set_viterbi_backptr(True)  # same decisions as path copying (test_oracle_kats), O(m) on the long run
+    try:
+        for hmm in (True, False):
+            gs, ge, gd = _device_cut(tk, big, boff, hmm)
+            st = tk.last_stats()
+            if hmm:
+                assert st["long_blocks"] >= 1, st  # the 1M-rune document's Han runs
+            os_, oe, od = o.cut_batch(big, boff, hmm, nthreads=_threads())
+            _cmp(gs, ge, gd, os_, oe, od, f"config 4 (1 GiB) + 5b, hmm={hmm}")
+            assert st["tokens"] == len(os_)
+            del gs, ge, gd, os_, oe, od
+    finally:
+        O.set_viterbi_backptr(False)
+    tk.close()
+
+
+@pytest.mark.parametrize("ndev", [2, 3])
+def test_multi_device_host_path(syn_small, ndev, monkeypatch):
+    """jb_cut_batch over several devices: byte-balanced document ranges, one host
+    thread, stream and workspace per device, spans concatenated in document order
+    (SURVEY.md §8e).  JB_DEVICE_WRAP maps the devices onto the one GPU here."""
+    dp, ep, s = syn_small
+    monkeypatch.setenv("JB_DEVICE_WRAP", "1")
+    tk = J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep, ndevices=ndev))
+    monkeypatch.delenv("JB_DEVICE_WRAP")
+    o = O.Oracle.from_files(dp, ep, 0)
+    buf, off, _ = s.corpus(synth.KIND_DOCS, 40 + ndev, target_bytes=6 << 20)
+    for hmm in (False, True):
+        gs, ge, gd = tk.cut_batch(buf, off, hmm)
+        os_, oe, od = o.cut_batch(buf, off, hmm, nthreads=8)
+        _cmp(gs, ge, gd, os_, oe, od, f"{ndev} devices hmm={hmm}")
+        assert tk.last_stats()["tokens"] == len(os_)  # summed over the devices
+        s2, e2, d2, _ = tk.cut_batch_into(buf, off, hmm)
+        _cmp(s2, e2, d2, os_, oe, od, f"{ndev} devices into caller arrays hmm={hmm}")
+    # a batch smaller than the device count, and one tiny batch (k_small on one device)
+    few = off[:2]
+    gs, ge, gd = tk.cut_batch(buf, few, True)
+    os_, oe, od = o.cut_batch(buf, few, True)
+    _cmp(gs, ge, gd, os_, oe, od, "one document over several devices")
+    t = "我昨天去上海交通大學與老師討論量子力學"
+    assert tk.Cut(t, True) == o.cut(t, True)
+    st = tk.last_stats()
+    assert st["tokens"] == len(o.cut(t, True))  # no stale counts from the devices that got nothing
+    tk.close()
+
+
+def test_cut_device_into_concurrent_threads(syn_small):
+    """jb_cut_device_into from two threads on two streams at once, each with its
+    own output arrays: the shared workspace is ordered on the device, and neither
+    thread sees the other's tokens."""
+    import torch
+    dp, ep, s = syn_small
+    tk = J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep))
+    o = O.Oracle.from_files(dp, ep, 0)
+    batches = [s.corpus(synth.KIND_DOCS, 60 + k, target_bytes=(3 + k) << 20)[:2] for k in range(2)]
+    want = [o.cut_batch(b, f, True, nthreads=8) for b, f in batches]
+    errs = []
+
+    def run(k):
+        try:
+            buf, off = batches[k]
+            nbytes, nd = int(off[-1]), len(off) - 1
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                d_text = torch.from_numpy(np.ascontiguousarray(buf[: nbytes + 64])).cuda()
+                d_off = torch.from_numpy(np.asarray(off, np.int64)).cuda()
+                o_s = torch.empty(nbytes + 1, dtype=torch.int32, device="cuda")
+                o_e = torch.empty(nbytes + 1, dtype=torch.int32, device="cuda")
+                o_d = torch.empty(nd + 1, dtype=torch.int64, device="cuda")
+                o_n = torch.zeros(1, dtype=torch.int64, device="cuda")
+                for rep in range(6):
+                    o_s.fill_(-1)
+                    tk.cut_device_into(d_text.data_ptr(), nbytes, d_off.data_ptr(), nd, True, o_s.data_ptr(),
+                                       o_e.data_ptr(), nbytes + 1, o_d.data_ptr(), o_n.data_ptr(), st.cuda_stream)
+                    st.synchronize()
+                    n = int(o_n.item())
+                    got = (o_s[:n].cpu().numpy().view(np.uint32).astype(np.uint64),
+                           o_e[:n].cpu().numpy().view(np.uint32).astype(np.uint64), o_d.cpu().numpy().view(np.uint64))
+                    _cmp(*got, *want[k], f"thread {k} rep {rep}")
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    with pytest.raises(J.JbError) as e:  # outputs must hold a token per byte
+        tk.cut_device_into(0, 100, 0, 1, True, 1, 1, 99, 1, 1)
+    assert e.value.code == J.JB_EINVAL
+    tk.close()

@@ -153,7 +153,12 @@ def test_docs_corpus(full, hmm):
     _cmp_batch(tk, o, buf, off, hmm, f"docs hmm={hmm}")
 
 
-@pytest.mark.parametrize("group", [1024, 3072, 6144])
+# JB_TEST_ZH_GROUPS: the groups to force, e.g. "12288" with a library built by
+# `make ZH_GROUP=12288 OUT=../var/g12 OBJ=../var/g12o` and loaded through JB_LIB
+ZH_GROUPS = [int(x) for x in os.environ.get("JB_TEST_ZH_GROUPS", "1024,3072,6144").split(",")]
+
+
+@pytest.mark.parametrize("group", ZH_GROUPS)
 def test_docs_corpus_zh_groups(syn_full, group, monkeypatch):
     """k_zh picks its group size by batch size (1 KiB under 16 MiB, 6 KiB at the
     headline's size); JB_ZH_GROUP (read at jb_open) forces one, so the large-batch
@@ -279,6 +284,57 @@ def test_add_word(mini_paths):
     assert tk.dict_get("很好") == want
     assert tk.Cut(text, True) == o.cut(text, True)
     tk.close()
+
+
+def test_add_word_atomic(syn_small, tmp_path):
+    """AddWord that fails (a reachable word of 256 runes: JB_ELIMIT) changes nothing:
+    not the dictionary, not pd.size, not the device image (tokenizer.go:372-379,580-585)."""
+    dp, ep, s = syn_small
+    d2 = str(tmp_path / "dict255.txt")
+    with open(dp, encoding="utf-8") as f:
+        base = f.read()
+    with open(d2, "w", encoding="utf-8") as f:  # every prefix of the long word is a key, so it is reachable
+        f.write(base + "".join(f"{'丁' * k} 3\n" for k in range(1, 256)))
+    tk, o = _pair(d2, ep)
+    text = "丁" * 300 + "，" + "中文" * 20
+    buf, off, _ = s.corpus(synth.KIND_DOCS, 17, target_bytes=1 << 20)
+    before = tk.cut_batch(buf, off, True)
+    size0 = tk.size
+    with pytest.raises(J.JbError) as e:
+        tk.AddWord("丁" * 256, 5)
+    assert e.value.code == J.JB_ELIMIT
+    assert tk.dict_get("丁" * 256) is None and tk.size == size0 == o.size
+    assert tk.Cut(text, True) == o.cut(text, True)
+    after = tk.cut_batch(buf, off, True)
+    assert all(np.array_equal(a, b) for a, b in zip(before, after))
+    tk.AddWord("丁" * 255, 9)  # the limit itself still works
+    o.add_term("丁" * 255, 9)
+    assert tk.Cut(text, True) == o.cut(text, True)
+    tk.close()
+
+
+def test_open_image_with_log_table(syn_small):
+    """The Go binding's constructor path: jb_image_build, jb_image_log_keys, math.Log
+    of each key, jb_open_image (the trie placed once, the weights recomputed from the
+    table).  An identity table keeps bit parity; a perturbed table cuts exactly as
+    jb_open with the same table does."""
+    import math
+    dp, ep, s = syn_small
+    o = O.Oracle.from_files(dp, ep, 0)
+    buf, off, _ = s.corpus(synth.KIND_DOCS, 12, target_bytes=1 << 20)
+    img = J.Image(J.make_config(dict_path=dp, emit_path=ep))
+    keys = [int(x) for x in img.log_keys()]
+    tk = J.Tokenizer.from_image(img, logs={k: J.go_log(k) for k in keys})
+    for hmm in (False, True):
+        _cmp_batch(tk, o, buf, off, hmm, "jb_open_image, identity table")
+    tk.close()
+    bump = {k: math.nextafter(J.go_log(k), math.inf if i % 2 else -math.inf) for i, k in enumerate(keys)}
+    a = J.Tokenizer.from_image(J.Image(J.make_config(dict_path=dp, emit_path=ep)), logs=bump)
+    b = J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep, logs=bump))
+    ra, rb = a.cut_batch(buf, off, True), b.cut_batch(buf, off, True)
+    assert all(np.array_equal(x, y) for x, y in zip(ra, rb))
+    a.close()
+    b.close()
 
 
 def test_empty_batch_and_docs(small):
@@ -501,7 +557,8 @@ def _spans_line(line):
 
 
 def test_c_abi_smoke_program(syn_small, tmp_path):
-    """A C99 program bound to include/jiebahip.h (what cgo sees): open, Cut, a batch,
+    """A C99 program bound to include/jiebahip.h (what cgo sees): open as the Go binding
+    does (jb_image_build, jb_image_log_keys, jb_open_image), Cut, a batch,
     a batch into caller arrays, AddWord with suggestFreq, Cut again — every span
     against the oracle."""
     import subprocess
@@ -519,6 +576,7 @@ def test_c_abi_smoke_program(syn_small, tmp_path):
     r = subprocess.run([exe, dp, ep, str(tf), word], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     out = {ln.split()[0]: ln for ln in r.stdout.splitlines()}
+    assert int(out["log"].split()[2]) > 2  # opened through jb_image_build + jb_open_image with a log table
     o = O.Oracle.from_files(dp, ep, 0)
     s1, e1 = o.cut_spans(text, True)
     assert _spans_line(out["cut"]) == (s1.tolist(), e1.tolist())
