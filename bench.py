@@ -382,16 +382,45 @@ def run(args, world, rank, dist, agg_dev, make_cutter, open_oracle, log=print):
 
 
 def end_to_end(tk, buf, off, hmm, nrunes, reps=3):
-    """jb_cut_batch_into from host memory: pinned staging, H2D, all kernels, D2H
-    spans, u64 batch offsets into caller arrays (never `value`)."""
-    res = tk.cut_batch_into(buf, off, bool(hmm))  # warm the pinned staging and the output arrays
-    t = time.perf_counter()
-    for _ in range(reps):
-        res = tk.cut_batch_into(buf, off, bool(hmm), res[3])
-    s = (time.perf_counter() - t) / reps
-    return {"value": round(nrunes / s, 1), "unit": "chars/s", "ms": round(s * 1e3, 2),
-            "what": "jb_cut_batch_into from host memory: pinned staging, H2D text + offsets, all kernels, "
-                    "D2H spans, u64 batch offsets into caller arrays"}
+    """The host-memory paths a drop-in caller gets (never `value`): the batch in host
+    memory, text pieces copied up while earlier pieces are cut and their results come
+    back (three streams).  `value`: jb_cut_batch_into (u64 spans into caller arrays)
+    from pageable memory; `masks`: jb_cut_batch_mask (2 bits per byte); `masks_pinned`:
+    the same with the text in jb_host_alloc memory (no staging copy).  Each checked
+    against the spans of the device-resident run it follows."""
+    import jiebahip as J
+
+    def timed(fn):
+        r = fn(None)  # warm the pinned staging and the output arrays
+        t = time.perf_counter()
+        for _ in range(reps):
+            r = fn(r)
+        return r, (time.perf_counter() - t) / reps
+
+    res, s_sp = timed(lambda r: tk.cut_batch_into(buf, off, bool(hmm), r[3] if r else None))
+    ms, me, _ = tk.cut_batch_mask(buf, off, bool(hmm))
+    (ms, me, ntok), s_m = timed(lambda r: tk.cut_batch_mask(buf, off, bool(hmm), (r[0], r[1]) if r else None))
+    nb = int(off[-1] - off[0])
+    ms2, me2 = J.mask_to_spans(ms, me, nb, int(off[0]))
+    ok_mask = bool(np.array_equal(ms2, res[0]) and np.array_equal(me2, res[1]))
+    hb = J.HostBuffer(len(buf))
+    try:
+        hb.array[:] = buf
+        (pms, pme, _), s_p = timed(lambda r: tk.cut_batch_mask(hb.array, off, bool(hmm), (r[0], r[1]) if r else None))
+        ok_pin = bool(np.array_equal(pms, ms) and np.array_equal(pme, me))
+    finally:
+        hb.free()
+
+    def rate(sec):
+        return {"value": round(nrunes / sec, 1), "unit": "chars/s", "ms": round(sec * 1e3, 2)}
+    out = rate(s_sp)
+    out["what"] = ("jb_cut_batch_into from pageable host memory: pieces of 64 MiB staged into pinned memory and "
+                   "copied up while earlier pieces are cut, u32 spans back, u64 batch offsets into caller arrays")
+    out["masks"] = dict(rate(s_m), what="jb_cut_batch_mask from pageable host memory: 2 bits per input byte back",
+                        same_tokens_as_spans=ok_mask, tokens=int(ntok))
+    out["masks_pinned"] = dict(rate(s_p), what="jb_cut_batch_mask with the text in jb_host_alloc (pinned) memory: "
+                                               "no staging copy", same_as_pageable=ok_pin)
+    return out
 
 
 def sentence_latency(tk, o, n):

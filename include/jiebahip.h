@@ -120,6 +120,25 @@ void jb_spans_free(jb_spans *s);
 int jb_cut_batch_into(jb_ctx *ctx, const uint8_t *text, const uint64_t *doc_off, uint32_t ndocs, int hmm,
                       uint64_t *start, uint64_t *end, uint64_t cap, uint64_t *doc_tok, uint64_t *ntokens);
 
+/* Token boundaries as two bitmaps over the batch's bytes instead of spans (2 bits per
+ * input byte; 268 MB per GiB instead of 8 bytes per token): bit i of `starts` (word
+ * i / 64, bit i % 64) is set when a token begins at byte doc_off[0] + i, bit i of
+ * `ends` when a token's last byte is doc_off[0] + i.  Each array holds nwords >=
+ * (doc_off[ndocs] - doc_off[0] + 63) / 64 u64 words, and every one of them is written.
+ * Tokens never cross a document boundary and never overlap, so start bit k pairs
+ * with end bit k in order; a 1-byte token whose byte is >= 0x80 is "�" (as for spans).
+ * *ntokens receives the token count.  The host text moves to the device in pieces
+ * while earlier pieces are cut and their masks come back (three streams). */
+int jb_cut_batch_mask(jb_ctx *ctx, const uint8_t *text, const uint64_t *doc_off, uint32_t ndocs, int hmm,
+                      uint64_t *starts, uint64_t *ends, uint64_t nwords, uint64_t *ntokens);
+
+/* Pinned (page-locked) host memory for batch text: a batch that lies in one such
+ * allocation is copied to the device straight from it, without the staging copy
+ * that pageable memory needs.  A Go caller builds its CutBatch buffer here (C
+ * memory, so cgo's pointer rules allow it).  Free with jb_host_free. */
+int jb_host_alloc(size_t n, void **p);
+void jb_host_free(void *p);
+
 /* Device-resident form for pipelines and benchmarks: d_text (nbytes, plus 64
  * readable padding bytes; 16-byte aligned) and d_doc_off (ndocs+1 offsets, d_doc_off[0] == 0,
  * d_doc_off[ndocs] == nbytes) are device pointers on ctx's first device; the
@@ -141,12 +160,24 @@ int jb_cut_device_into(jb_ctx *ctx, const uint8_t *d_text, uint64_t nbytes, cons
                        uint32_t ndocs, int hmm, void *stream, uint32_t *d_start, uint32_t *d_end, uint64_t cap,
                        uint64_t *d_doc_tok, uint64_t *d_ntok);
 
-/* Contiguous byte-balanced document ranges, the multi-device partition of
- * jb_cut_batch (the reference's CutParallel deals blocks to
- * goroutines instead, tokenizer.go:81-148): part k owns documents
+/* Contiguous byte-balanced ranges of whole documents (the reference's
+ * CutParallel deals blocks to goroutines instead, tokenizer.go:81-148), the partition
+ * bench.py's one-process-per-GPU runs use (jb_cut_batch itself uses jb_split_points,
+ * which may cut inside a document): part k owns documents
  * [cut[k], cut[k+1]), cut has nparts + 1 entries, cut[0] = 0 and
  * cut[nparts] = ndocs.  Host only. */
 int jb_shard_bounds(const uint64_t *doc_off, uint32_t ndocs, uint32_t nparts, uint32_t *cut);
+
+/* Byte-balanced split points that may fall inside a document (one
+ * large document over several devices): cut has nparts + 1 entries, cut[0] =
+ * doc_off[0], cut[nparts] = doc_off[ndocs], and cut[k] is the first document start
+ * or Han-run start at or after doc_off[0] + total * k / nparts.  A Han-run start is
+ * a byte where a Han rune begins (Go's DecodeRune over the document) and the rune
+ * before it is not Han: cutting a document there leaves splitText's blocks
+ * (tokenizer.go:165-210) unchanged, and blocks are cut independently
+ * (tokenizer.go:158-160), so the parts' tokens are the whole's.  jb_cut_batch
+ * shards over its devices with these points.  Host only. */
+int jb_split_points(const uint8_t *text, const uint64_t *doc_off, uint32_t ndocs, uint32_t nparts, uint64_t *cut);
 
 /* Replaces Tokenizer.AddWord (tokenizer.go:372; the reference deadlocks there,
  * :376 + :581).  freq < 1 takes suggestFreq's value (tokenizer.go:589-614).
@@ -166,9 +197,8 @@ int jb_add_log(jb_ctx *ctx, const int64_t *keys, const double *vals, size_t n);
 int jb_dict_get(jb_ctx *ctx, const char *word, size_t len, int64_t *freq); /* 1 found, 0 absent */
 int64_t jb_dict_size(jb_ctx *ctx);
 
-/* Counters of the last pipeline run on each device of ctx, summed over the
- * devices (for a host batch larger than 1 GiB: of its last piece).
- * Synchronises the devices' streams. */
+/* Counters of the last cut on each device of ctx, summed over the devices (a host
+ * batch cut in pieces: summed over its pieces).  Synchronises the devices' streams. */
 typedef struct {
     uint64_t tokens;       /* tokens written */
     uint64_t blocks;       /* splitText blocks, zh and non-zh (tokenizer.go:165-210) */

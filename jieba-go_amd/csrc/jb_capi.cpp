@@ -124,15 +124,39 @@ struct Device {
     uint8_t* text = nullptr;   // staging for host batches (padded)
     uint64_t* doc_off = nullptr;
     uint64_t text_cap = 0;
-    uint32_t doc_cap = 0;
+    uint64_t doc_cap = 0;
     // pinned host staging for host batches (full-speed DMA both ways)
     uint8_t* h_text = nullptr;
     uint64_t h_text_cap = 0;
-    uint32_t* h_span = nullptr;  // starts then ends, u32
-    uint64_t h_span_cap = 0;     // tokens
-    uint64_t* h_misc = nullptr;  // doc offsets in / doc_tok out (u64)
+    uint64_t* h_misc = nullptr;  // piece-relative doc offsets (u64)
     uint64_t h_misc_cap = 0;
-    uint32_t* h_cnt = nullptr;   // counters (64 u32)
+    // host-batch pipeline (cut_pieces): a batch is cut in pieces of whole documents;
+    // piece k+1's text goes up on cstream while piece k runs on `stream` and the
+    // spans / masks of earlier pieces come back on dstream
+    hipStream_t cstream = nullptr, dstream = nullptr;
+    std::vector<hipEvent_t> ev_h2d, ev_comp, ev_d2h;  // per piece
+    static constexpr int kSets = 3;  // output sets in flight
+    struct OutSet {
+        uint32_t* ts = nullptr;  // device u32 spans and doc_tok of the piece
+        uint32_t* te = nullptr;
+        uint64_t* dt = nullptr;
+        uint64_t cap_tok = 0;
+        uint32_t cap_docs = 0;
+        uint32_t* hs = nullptr;  // pinned: starts then ends
+        uint64_t* hdt = nullptr; // pinned doc_tok
+        uint64_t hcap_tok = 0;
+        uint32_t hcap_docs = 0;
+    } outs[kSets];
+    uint32_t* h_pcnt = nullptr;  // pinned counters, kPieceCnt u32 per piece
+    uint64_t h_pcnt_cap = 0;
+    uint64_t* d_mask = nullptr;  // boundary masks of a range: starts then ends (u64 words)
+    uint64_t* h_mask = nullptr;  // pinned copy
+    uint64_t mask_cap = 0;       // u64 words of d_mask
+    uint64_t mask_cap_h = 0;     // u64 words of h_mask
+    uint2* h_ptile = nullptr;    // pinned per-tile (blocks, zh blocks) of every piece (jb_last_stats)
+    uint64_t h_ptile_cap = 0;
+    jb_stats acc{};              // counters summed over the pieces of the last host range
+    bool acc_valid = false;      // the last run was such a range
     // k_small's pinned, mapped host buffers (coherent: the kernel reads and writes them directly)
     uint8_t* h_sin = nullptr;    // text (kSmallBytes + 128), then u64 doc offsets (kSmallDocs + 1)
     uint32_t* h_sout = nullptr;  // header, spans, doc_tok (kSmallOutBytes)
@@ -142,8 +166,8 @@ struct Device {
     hipStream_t sstream = nullptr;  // k_small's stream, masked to one CU (its code stays in that I-cache)
     uint32_t small_seq = 0;         // k_small calls: the kernel writes this number last
     uint32_t small_hdr[kSmallHdr] = {0};
-    std::vector<hipEvent_t> ev;  // span pieces landed (host batches)
     uint32_t ncu = 0;
+    uint64_t piece_bytes = 64ull << 20;  // host-batch pipeline piece (JB_PIECE_KIB)
     LaunchCfg lc{};  // launch shape, fixed at jb_open
     uint64_t last_nbytes = 0;  // batch size of the last pipeline run (jb_last_stats)
     bool has_stats = false;    // this device took part in the last cut (jb_last_stats skips it otherwise)
@@ -529,47 +553,35 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     return JB_OK;
 }
 
-static int ensure_staging(Device* d, uint64_t nbytes, uint32_t ndocs) {
-    if (nbytes + 128 > d->text_cap) {
-        dfree(d->text);
-        d->text = nullptr;
-        const uint64_t cap = std::max<uint64_t>(nbytes + 128, d->text_cap * 3 / 2);
-        HIPCHK(hipMalloc(&d->text, cap));
-        d->text_cap = cap;
-    }
-    if (ndocs + 1 > d->doc_cap) {
-        dfree(d->doc_off);
-        d->doc_off = nullptr;
-        const uint32_t cap = std::max<uint32_t>(ndocs + 1, d->doc_cap * 3 / 2);
-        HIPCHK(hipMalloc(&d->doc_off, (uint64_t)cap * 8));
-        d->doc_cap = cap;
-    }
-    if (nbytes + 64 > d->h_text_cap) {
-        hfree(d->h_text);
-        d->h_text = nullptr;
-        const uint64_t cap = std::max<uint64_t>(nbytes + 64, d->h_text_cap * 3 / 2);
-        HIPCHK(hipHostMalloc(&d->h_text, cap, hipHostMallocDefault));
-        d->h_text_cap = cap;
-    }
-    if (ndocs + 2 > d->h_misc_cap) {
-        hfree(d->h_misc);
-        d->h_misc = nullptr;
-        const uint64_t cap = std::max<uint64_t>(ndocs + 2, d->h_misc_cap * 3 / 2);
-        HIPCHK(hipHostMalloc(&d->h_misc, cap * 8, hipHostMallocDefault));
-        d->h_misc_cap = cap;
-    }
-    if (!d->h_cnt) HIPCHK(hipHostMalloc(&d->h_cnt, 64 * 4, hipHostMallocDefault));
+// grow-only device / pinned buffers (a call never has work in flight on them when it grows them)
+template <class T>
+static int grow_dev(T** p, uint64_t* cap, uint64_t want) {
+    if (want <= *cap && *p) return JB_OK;
+    dfree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const uint64_t c = std::max<uint64_t>(want, 1);
+    HIPCHK(hipMalloc(p, c * sizeof(T)));
+    *cap = c;
+    return JB_OK;
+}
+template <class T>
+static int grow_pinned(T** p, uint64_t* cap, uint64_t want) {
+    if (want <= *cap && *p) return JB_OK;
+    const uint64_t c = std::max<uint64_t>(want, *cap * 3 / 2 + 1);
+    hfree(*p);
+    *p = nullptr;
+    *cap = 0;
+    HIPCHK(hipHostMalloc(p, c * sizeof(T), hipHostMallocDefault));
+    *cap = c;
     return JB_OK;
 }
 
-static int ensure_span_staging(Device* d, uint64_t ntok) {
-    if (ntok <= d->h_span_cap) return JB_OK;
-    hfree(d->h_span);
-    d->h_span = nullptr;
-    const uint64_t cap = std::max<uint64_t>(ntok, d->h_span_cap * 3 / 2);
-    HIPCHK(hipHostMalloc(&d->h_span, cap * 8, hipHostMallocDefault));
-    d->h_span_cap = cap;
-    return JB_OK;
+static void free_outs(Device* d) {
+    for (auto& o : d->outs) {
+        dfree(o.ts); dfree(o.te); dfree(o.dt); hfree(o.hs); hfree(o.hdt);
+        o = Device::OutSet{};
+    }
 }
 
 static int env_int(const char* name, int dflt) {
@@ -577,11 +589,16 @@ static int env_int(const char* name, int dflt) {
     return v && *v ? atoi(v) : dflt;
 }
 
+static const uint64_t kMaxPiece = 1ull << 30;  // (a piece of several documents; device offsets are u32)
+
 // The launch shape of a device, fixed at jb_open.  Tuning knobs come from the
 // environment once, here (results do not depend on them):
 //   JB_GRID_ZH   k_zh workgroups (default: resident workgroups per CU x CUs)
 //   JB_ZH_GROUP  k_zh group bytes, a multiple of 32 in [kZhGroupSmall, kZhGroupBytes]
 //                (default: by batch size, zh_group_for)
+//   JB_PIECE_KIB host batches are cut in pieces of whole documents of at most this many KiB
+//                (default 65536), pipelined over three streams (cut_range)
+//   JB_SMALL     host batches up to this many bytes take k_small (0: never)
 //   JB_STAMPS    (STAMPS=1 builds only) per-wave phase clocks to stderr
 static int init_launch_cfg(Device* d) {
     LaunchCfg& lc = d->lc;
@@ -598,6 +615,10 @@ static int init_launch_cfg(Device* d) {
 #if JB_STAMPS
     lc.diag = (uint32_t)env_int("JB_STAMPS", 0) ? 0x100u : 0u;
 #endif
+    const int pk = env_int("JB_PIECE_KIB", 64 << 10);  // host-batch pipeline piece (KiB of whole documents)
+    if (pk < 1 || (uint64_t)pk > kMaxPiece / 1024)
+        return fail(JB_EINVAL, "JB_PIECE_KIB=%d: want 1 .. %llu", pk, (unsigned long long)(kMaxPiece / 1024));
+    d->piece_bytes = (uint64_t)pk << 10;
     const int sm = env_int("JB_SMALL", (int)kSmallBytes);
     if (sm < 0 || sm > (int)kSmallBytes)
         return fail(JB_EINVAL, "JB_SMALL=%d: want 0 (off) .. %u bytes", sm, kSmallBytes);
@@ -606,7 +627,7 @@ static int init_launch_cfg(Device* d) {
 }
 
 static int launch_pipeline(Device* d, const Work& w, const uint8_t* d_text, uint64_t nbytes,
-                           const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, hipStream_t s) {
+                           const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, hipStream_t s, const MaskOut* mask) {
     static const bool dbg = getenv("JB_DEBUG") != nullptr;
     const LaunchCfg& lc = d->lc;
     d->last_nbytes = nbytes;
@@ -615,7 +636,7 @@ static int launch_pipeline(Device* d, const Work& w, const uint8_t* d_text, uint
         fprintf(stderr, "[jb] nbytes=%llu ndocs=%u grid_zh=%u zh_group=%u\n", (unsigned long long)nbytes,
                 ndocs, lc.grid_zh, lc.zh_group ? lc.zh_group : zh_group_for(nbytes));
     static const bool use_graph = env_int("JB_GRAPH", 1) != 0;
-    if (use_graph && !d->profile && lc.diag == 0 && s != nullptr) {
+    if (use_graph && !d->profile && lc.diag == 0 && s != nullptr && !mask) {
         const Device::GraphKey key{d_text, nbytes, d_doc_off, ndocs, hmm, d->work_gen, s, w.tok_start, w.tok_end, w.doc_tok};
         const bool repeat = d->gkey_gen != 0 && key == d->gkey;
         if (!repeat) {  // first call with this key: run directly, capture if it comes again
@@ -648,7 +669,7 @@ static int launch_pipeline(Device* d, const Work& w, const uint8_t* d_text, uint
         return JB_OK;
     }
     const hipError_t e = run_pipeline(d->dim, w, d_text, nbytes, d_doc_off, ndocs, hmm, lc, s,
-                                      d->profile ? &d->timer : nullptr);
+                                      d->profile ? &d->timer : nullptr, mask);
     if (e != hipSuccess) return fail(JB_EDEVICE, "pipeline launch: %s", hipGetErrorString(e));
     if ((lc.diag & 0x100u) && d->w.dbg) {  // diagnostic: per-wave clocks of k_zh (STAMPS builds)
         const uint32_t nwv = std::min<uint32_t>(lc.grid_zh * 4u, 65536u);
@@ -702,14 +723,15 @@ static int launch_pipeline(Device* d, const Work& w, const uint8_t* d_text, uint
 // for the previous one (on whatever stream it ran) before it starts.  `w` is the
 // device's workspace, or a copy with caller-owned outputs (jb_cut_device_into).
 static int launch(Device* d, const Work& w, const uint8_t* d_text, uint64_t nbytes, const uint64_t* d_doc_off,
-                  uint32_t ndocs, bool hmm, hipStream_t s) {
+                  uint32_t ndocs, bool hmm, hipStream_t s, const MaskOut* mask = nullptr) {
     if (!d->ws_done) HIPCHK(hipEventCreateWithFlags(&d->ws_done, hipEventDisableTiming));
     else HIPCHK(hipStreamWaitEvent(s, d->ws_done, 0));  // (free on the stream that recorded it)
-    int rc = launch_pipeline(d, w, d_text, nbytes, d_doc_off, ndocs, hmm, s);
+    int rc = launch_pipeline(d, w, d_text, nbytes, d_doc_off, ndocs, hmm, s, mask);
     if (rc) return rc;
     HIPCHK(hipEventRecord(d->ws_done, s));
     d->ws_stream = s;
     d->has_stats = true;
+    d->acc_valid = false;
     return JB_OK;
 }
 
@@ -724,6 +746,8 @@ static int open_device(Device* d, int ordinal, const Image& img) {
     HIPCHK(hipGetDeviceProperties(&prop, d->ordinal));
     d->ncu = (uint32_t)prop.multiProcessorCount;
     HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&d->cstream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&d->dstream, hipStreamNonBlocking));
     {
         // k_small runs one workgroup per call: pinned to one CU (JB_SMALL_CU, default 0) it
         // finds its 21 KB of code in that CU's instruction cache (and the trie's hot lines
@@ -802,8 +826,13 @@ extern "C" void jb_close(jb_ctx* ctx) {
         dfree(d->text); dfree(d->doc_off);
         free_image_bufs(&d->ib);
         if (d->ws_done) (void)hipEventDestroy(d->ws_done);
-        hfree(d->h_text); hfree(d->h_span); hfree(d->h_misc); hfree(d->h_cnt); hfree(d->h_sin); hfree(d->h_sout);
-        for (hipEvent_t e : d->ev) (void)hipEventDestroy(e);
+        hfree(d->h_text); hfree(d->h_misc); hfree(d->h_sin); hfree(d->h_sout);
+        free_outs(d.get());
+        hfree(d->h_pcnt); dfree(d->d_mask); hfree(d->h_mask); hfree(d->h_ptile);
+        for (auto* v : {&d->ev_h2d, &d->ev_comp, &d->ev_d2h})
+            for (hipEvent_t e : *v) (void)hipEventDestroy(e);
+        if (d->cstream) (void)hipStreamDestroy(d->cstream);
+        if (d->dstream) (void)hipStreamDestroy(d->dstream);
         (void)hipStreamDestroy(d->stream);
         if (d->sstream) (void)hipStreamDestroy(d->sstream);
     }
@@ -815,7 +844,6 @@ extern "C" const char* jb_last_error(void) { return g_err.c_str(); }
 // ---------------------------------------------------------------------------
 // cutting
 // ---------------------------------------------------------------------------
-static const uint64_t kChunkBytes = 1ull << 30;  // device offsets are u32 with a zh flag bit
 
 // A batch of at most lc.small_max bytes and kSmallDocs documents (a single Cut
 // call, BASELINE config 1): one k_small launch that reads the text and offsets
@@ -905,126 +933,315 @@ static int cut_small(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
     return JB_OK;
 }
 
-// Cut documents [d0, d1) of a host batch on one device; appends spans to `out`.
-// Host text goes through pinned staging (full-speed DMA), spans come back into
-// pinned memory and are widened to u64 batch offsets in place in `out`.
-static int cut_range(jb_ctx* ctx, Device* d, const uint8_t* text, const uint64_t* doc_off, uint32_t d0, uint32_t d1,
-                     bool hmm, SpanBuf* out) {
+// Caller-owned boundary masks (jb_cut_batch_mask): bit i of s / e is byte batch0 + i.
+struct MaskDst {
+    uint64_t* s;
+    uint64_t* e;
+    uint64_t batch0;
+};
+
+// Words [lo, hi) of a range's masks (range word j = caller word rw + j, nw words in all)
+// into the caller's arrays.  The range's first and last words may be shared with the
+// neighbouring ranges of other devices: those are ORed (atomically) into words the
+// caller zeroed first; the rest belong to this range alone and are stored.
+static void put_mask_words(const MaskDst* m, uint64_t rw, uint64_t nw, uint64_t lo, uint64_t hi, const uint64_t* ms,
+                           const uint64_t* me) {
+    auto one = [&](uint64_t j) {
+        if (j == 0 || j + 1 == nw) {
+            __atomic_fetch_or(m->s + rw + j, ms[j], __ATOMIC_RELAXED);
+            __atomic_fetch_or(m->e + rw + j, me[j], __ATOMIC_RELAXED);
+        } else {
+            m->s[rw + j] = ms[j];
+            m->e[rw + j] = me[j];
+        }
+    };
+    if (lo < hi && lo == 0) one(lo++);
+    if (lo < hi && hi == nw) one(--hi);
+    if (lo >= hi) return;
+    const uint64_t n = hi - lo;
+    const unsigned nth = n >= (1u << 18) ? kCopyThreads : 1u;
+    auto work = [&](unsigned t) {
+        const uint64_t a = lo + n * t / nth, b = lo + n * (t + 1) / nth;
+        memcpy(m->s + rw + a, ms + a, (b - a) * 8);
+        memcpy(m->e + rw + a, me + a, (b - a) * 8);
+    };
+    run_threads(nth, work);
+}
+
+// Text already in pinned memory (jb_host_alloc): the pieces are copied to the device
+// straight from it, without staging.
+struct HostAlloc { uintptr_t a; size_t n; };
+static std::mutex g_host_mu;
+static std::vector<HostAlloc> g_host;  // jb_host_alloc allocations
+static bool host_pinned(const void* p, uint64_t n) {
+    const uintptr_t x = (uintptr_t)p;
+    std::lock_guard<std::mutex> g(g_host_mu);
+    for (const HostAlloc& h : g_host)
+        if (x >= h.a && x + n <= h.a + h.n) return true;
+    return false;
+}
+
+constexpr uint32_t kPieceCnt = 16;  // counters copied back per piece (u32)
+
+// Cut documents [d0, d1) of a host batch on one device: appends spans to `out`, or
+// with `mask` writes the range's boundary bits into the caller's masks (out->n counts
+// the tokens).  A range that fits k_small is one launch.  A larger one is cut in
+// pieces of whole documents (JB_PIECE_MIB, default 64 MiB; a longer document is a
+// piece of its own) as a three-stage pipeline over three streams: piece k+1's text is
+// staged into pinned memory and copied up on cstream while piece k's kernels run on
+// `stream` and piece k-1's spans (or final mask words) come back on dstream, then are
+// widened to u64 batch offsets into `out` by kCopyThreads host threads.
+static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, uint32_t d0, uint32_t d1, bool hmm,
+                     SpanBuf* out, const MaskDst* mask) {
     std::lock_guard<std::mutex> g(d->mu);
     HIPCHK(hipSetDevice(d->ordinal));
-    uint32_t a = d0;
-    while (a < d1) {
-        // whole documents up to kChunkBytes (a single larger document is an error)
-        uint32_t b = a + 1;
-        if (doc_off[b] - doc_off[a] >= (1ull << 31))
-            return fail(JB_ELIMIT, "document %u is %llu bytes (limit 2 GiB)", a,
-                        (unsigned long long)(doc_off[b] - doc_off[a]));
-        while (b < d1 && doc_off[b + 1] - doc_off[a] <= kChunkBytes) b++;
-        const uint64_t base = doc_off[a], nbytes = doc_off[b] - base;
-        const uint32_t nd = b - a;
-        int rc;
-        if (d->lc.small_max && nbytes <= d->lc.small_max && nd <= kSmallDocs) {
-            if ((rc = cut_small(d, text, doc_off + a, nd, hmm, out))) return rc;
-            a = b;
-            continue;
+    if (d0 >= d1) return JB_OK;
+    for (uint32_t k = d0; k < d1; k++)
+        if (doc_off[k + 1] - doc_off[k] >= (1ull << 31))
+            return fail(JB_ELIMIT, "document %u is %llu bytes (limit 2 GiB)", k,
+                        (unsigned long long)(doc_off[k + 1] - doc_off[k]));
+    const uint64_t r0 = doc_off[d0], rbytes = doc_off[d1] - r0;
+    const uint32_t ndr = d1 - d0;
+    // mask geometry: range word j = caller word rw + j; the range's first bit is bit rsh of word 0
+    const uint64_t rrel = mask ? r0 - mask->batch0 : 0, rw = rrel >> 6, rsh = rrel & 63u;
+    const uint64_t nw = mask ? (rsh + rbytes + 63u) >> 6 : 0;
+    int rc;
+    if (d->lc.small_max && rbytes <= d->lc.small_max && ndr <= kSmallDocs) {
+        if (!mask) return cut_small(d, text, doc_off + d0, ndr, hmm, out);
+        SpanBuf tmp;
+        if ((rc = cut_small(d, text, doc_off + d0, ndr, hmm, &tmp))) {
+            tmp.release();
+            return rc;
         }
-        if ((rc = ensure_staging(d, nbytes, nd))) return rc;
-        if ((rc = ensure_work(d, nbytes, nd))) return rc;
-        static const bool tdbg = getenv("JB_DEBUG") != nullptr;
-        auto now = [] { return std::chrono::steady_clock::now(); };
-        auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
-            return std::chrono::duration<double, std::milli>(b - a).count();
-        };
-        const auto c0 = now();
-        // text into pinned staging in 32 MiB pieces, each sent while the next is copied
-        memset(d->h_text + nbytes, 0, 64);
-        for (uint32_t k = 0; k <= nd; k++) d->h_misc[k] = doc_off[a + k] - base;
-        HIPCHK(hipMemcpyAsync(d->doc_off, d->h_misc, (nd + 1) * 8, hipMemcpyHostToDevice, d->stream));
-        {
-            // kCopyThreads threads each copy their share of the text in 4 MiB pieces and queue
-            // each piece's H2D as soon as it is staged, so the DMA runs behind the copies
-            const uint64_t total = nbytes + 64, kPiece = 4ull << 20;
+        std::vector<uint64_t> ws(2 * nw, 0ull);
+        for (size_t k = 0; k < tmp.n; k++) {
+            const uint64_t a = tmp.s[k] - r0 + rsh, b = tmp.e[k] - 1 - r0 + rsh;
+            ws[a >> 6] |= 1ull << (a & 63u);
+            ws[nw + (b >> 6)] |= 1ull << (b & 63u);
+        }
+        put_mask_words(mask, rw, nw, 0, nw, ws.data(), ws.data() + nw);
+        out->n += tmp.n;
+        tmp.release();
+        return JB_OK;
+    }
+    const uint64_t kPiece = d->piece_bytes;
+    // documents, device text offset, offsets slot, tile-count slot
+    struct Piece { uint32_t d0, d1; uint64_t off, slot, tslot; };
+    std::vector<Piece> pcs;
+    uint64_t dev_bytes = 0, slots = 0, tslots = 0, maxb = 0;
+    uint32_t maxd = 0;
+    for (uint32_t a = d0; a < d1;) {
+        uint32_t b = a + 1;
+        while (b < d1 && doc_off[b + 1] - doc_off[a] <= kPiece) b++;
+        const uint64_t len = doc_off[b] - doc_off[a];
+        pcs.push_back(Piece{a, b, dev_bytes, slots, tslots});
+        dev_bytes += (len + 64 + 255) & ~255ull;  // 64 zero bytes after each piece, 256-byte aligned starts
+        slots += b - a + 1;
+        tslots += (len + kTileBytes - 1) / kTileBytes;
+        maxb = std::max(maxb, len);
+        maxd = std::max(maxd, b - a);
+        a = b;
+    }
+    const size_t np = pcs.size();
+    const bool pinned_in = host_pinned(text + r0, rbytes);
+    if ((rc = grow_dev(&d->text, &d->text_cap, dev_bytes)) || (rc = grow_dev(&d->doc_off, &d->doc_cap, slots)) ||
+        (rc = grow_pinned(&d->h_misc, &d->h_misc_cap, slots)) ||
+        (rc = grow_pinned(&d->h_pcnt, &d->h_pcnt_cap, (uint64_t)np * kPieceCnt)) ||
+        (rc = grow_pinned(&d->h_ptile, &d->h_ptile_cap, tslots + 1)) ||
+        (!pinned_in && (rc = grow_pinned(&d->h_text, &d->h_text_cap, dev_bytes))) ||
+        (rc = ensure_work(d, maxb, maxd)))
+        return rc;
+    for (auto* v : {&d->ev_h2d, &d->ev_comp, &d->ev_d2h})
+        while (v->size() < np) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            v->push_back(e);
+        }
+    if (!mask) {
+        for (auto& o : d->outs) {
+            uint64_t ct = o.cap_tok, cd = o.cap_docs;
+            if ((rc = grow_dev(&o.ts, &ct, maxb + 4)) || (rc = grow_dev(&o.te, &o.cap_tok, maxb + 4)) ||
+                (rc = grow_dev(&o.dt, &cd, (uint64_t)maxd + 2)))
+                return rc;
+            o.cap_docs = (uint32_t)cd;
+        }
+    } else {
+        if ((rc = grow_dev(&d->d_mask, &d->mask_cap, 2 * nw)) || (rc = grow_pinned(&d->h_mask, &d->mask_cap_h, 2 * nw)))
+            return rc;
+        HIPCHK(hipMemsetAsync(d->d_mask, 0, 2 * nw * 8, d->stream));
+    }
+    d->last_small = false;
+    jb_stats acc{};
+    auto drain = [&](int code) {  // an error with work in flight: let the streams finish first
+        (void)hipStreamSynchronize(d->cstream);
+        (void)hipStreamSynchronize(d->stream);
+        (void)hipStreamSynchronize(d->dstream);
+        return code;
+    };
+    std::vector<uint32_t> ntok(np, 0);
+    std::vector<std::pair<uint64_t, uint64_t>> words(np);  // mask words each piece copies back
+    uint64_t mask_done = 0;
+
+    auto stage = [&](size_t k) -> int {
+        const Piece& p = pcs[k];
+        const uint64_t pb = doc_off[p.d0], len = doc_off[p.d1] - pb;
+        for (uint32_t j = 0; j <= p.d1 - p.d0; j++) d->h_misc[p.slot + j] = doc_off[p.d0 + j] - pb;
+        HIPCHK(hipMemcpyAsync(d->doc_off + p.slot, d->h_misc + p.slot, (uint64_t)(p.d1 - p.d0 + 1) * 8,
+                              hipMemcpyHostToDevice, d->cstream));
+        if (pinned_in) {
+            if (len) HIPCHK(hipMemcpyAsync(d->text + p.off, text + pb, len, hipMemcpyHostToDevice, d->cstream));
+            HIPCHK(hipMemsetAsync(d->text + p.off + len, 0, 64, d->cstream));
+        } else {
+            // kCopyThreads threads stage their share in 4 MiB sub-pieces and queue each one's copy at once
+            const uint64_t total = len + 64, kSub = 4ull << 20;
+            memset(d->h_text + p.off + len, 0, 64);
             const unsigned nth = total >= (16ull << 20) ? kCopyThreads : 1u;
             const uint64_t share = ((total + nth - 1) / nth + 4095) & ~4095ull;
             std::atomic<int> err{0};
             auto work = [&](unsigned t) {
                 if (hipSetDevice(d->ordinal) != hipSuccess) err = 1;
                 const uint64_t lo = std::min(total, t * share), hi = std::min(total, lo + share);
-                for (uint64_t o = lo; o < hi; o += kPiece) {
-                    const uint64_t l = std::min(kPiece, hi - o);
-                    if (o < nbytes) memcpy(d->h_text + o, text + base + o, std::min(l, nbytes - o));
-                    if (hipMemcpyAsync(d->text + o, d->h_text + o, l, hipMemcpyHostToDevice, d->stream) != hipSuccess)
+                for (uint64_t o = lo; o < hi; o += kSub) {
+                    const uint64_t l = std::min(kSub, hi - o);
+                    if (o < len) memcpy(d->h_text + p.off + o, text + pb + o, std::min(l, len - o));
+                    if (hipMemcpyAsync(d->text + p.off + o, d->h_text + p.off + o, l, hipMemcpyHostToDevice,
+                                       d->cstream) != hipSuccess)
                         err = 1;
                 }
             };
             run_threads(nth, work);
             if (err) return fail(JB_EDEVICE, "H2D copy failed");
         }
-        const auto c1 = now();
-        if ((rc = launch(d, d->w, d->text, nbytes, d->doc_off, nd, hmm, d->stream))) return rc;
-        HIPCHK(hipMemcpyAsync(d->h_cnt, d->w.counters, 8 * 4, hipMemcpyDeviceToHost, d->stream));
-        HIPCHK(hipStreamSynchronize(d->stream));
-        const auto c2 = now();
-        if (d->h_cnt[CNT_ERR]) return fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)");
-        if (d->h_cnt[CNT_NTOK] != d->h_cnt[CNT_NTOKE])
-            return fail(JB_EDEVICE, "internal: %u token starts vs %u ends", d->h_cnt[CNT_NTOK], d->h_cnt[CNT_NTOKE]);
-        const uint32_t nt = d->h_cnt[CNT_NTOK];
-        if ((rc = ensure_span_staging(d, nt))) return rc;
+        HIPCHK(hipEventRecord(d->ev_h2d[k], d->cstream));
+        return JB_OK;
+    };
+    auto compute = [&](size_t k) -> int {
+        const Piece& p = pcs[k];
+        const uint64_t pb = doc_off[p.d0], len = doc_off[p.d1] - pb;
+        HIPCHK(hipStreamWaitEvent(d->stream, d->ev_h2d[k], 0));
+        Work w = d->w;
+        MaskOut mo{nullptr, nullptr, 0};
+        if (mask) {
+            mo = MaskOut{d->d_mask, d->d_mask + nw, rsh + (pb - r0)};
+        } else {
+            if (k >= (size_t)Device::kSets) HIPCHK(hipStreamWaitEvent(d->stream, d->ev_d2h[k - Device::kSets], 0));
+            const Device::OutSet& o = d->outs[k % Device::kSets];
+            w.tok_start = o.ts;
+            w.tok_end = o.te;
+            w.doc_tok = o.dt;
+        }
+        int r;
+        if ((r = launch(d, w, d->text + p.off, len, d->doc_off + p.slot, p.d1 - p.d0, hmm, d->stream,
+                        mask ? &mo : nullptr)))
+            return r;
+        d->last_nbytes = len;
+        HIPCHK(hipMemcpyAsync(d->h_pcnt + k * kPieceCnt, d->w.counters, kPieceCnt * 4, hipMemcpyDeviceToHost,
+                              d->stream));
+        const uint64_t nt_ = (len + kTileBytes - 1) / kTileBytes;  // (k_mark_walk's block counts, jb_last_stats)
+        if (nt_) HIPCHK(hipMemcpyAsync(d->h_ptile + p.tslot, d->w.tile_cnt, nt_ * sizeof(uint2), hipMemcpyDeviceToHost,
+                                       d->stream));
+        HIPCHK(hipEventRecord(d->ev_comp[k], d->stream));
+        return JB_OK;
+    };
+    auto collect = [&](size_t k) -> int {  // piece k's kernels are done: queue its results' copy back
+        const Piece& p = pcs[k];
+        HIPCHK(hipEventSynchronize(d->ev_comp[k]));
+        const uint32_t* c = d->h_pcnt + k * kPieceCnt;
+        if (c[CNT_ERR]) return fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)");
+        if (c[CNT_NTOK] != c[CNT_NTOKE])
+            return fail(JB_EDEVICE, "internal: %u token starts vs %u ends", c[CNT_NTOK], c[CNT_NTOKE]);
+        const uint32_t nt = ntok[k] = c[CNT_NTOK];
+        HIPCHK(hipStreamWaitEvent(d->dstream, d->ev_comp[k], 0));
+        if (!mask) {
+            Device::OutSet& o = d->outs[k % Device::kSets];
+            uint64_t hd = o.hcap_docs;
+            int r;
+            if ((r = grow_pinned(&o.hs, &o.hcap_tok, 2ull * nt + 2)) ||
+                (r = grow_pinned(&o.hdt, &hd, (uint64_t)(p.d1 - p.d0) + 2)))
+                return r;
+            o.hcap_docs = (uint32_t)hd;
+            if (nt) {
+                HIPCHK(hipMemcpyAsync(o.hs, o.ts, (uint64_t)nt * 4, hipMemcpyDeviceToHost, d->dstream));
+                HIPCHK(hipMemcpyAsync(o.hs + nt, o.te, (uint64_t)nt * 4, hipMemcpyDeviceToHost, d->dstream));
+            }
+            HIPCHK(hipMemcpyAsync(o.hdt, o.dt, (uint64_t)(p.d1 - p.d0 + 1) * 8, hipMemcpyDeviceToHost, d->dstream));
+        } else {
+            // final words: those before the word that holds the next piece's first bit
+            const uint64_t hi = k + 1 < np ? (rsh + (doc_off[pcs[k + 1].d0] - r0)) >> 6 : nw;
+            const uint64_t lo = mask_done;
+            if (hi > lo) {
+                HIPCHK(hipMemcpyAsync(d->h_mask + lo, d->d_mask + lo, (hi - lo) * 8, hipMemcpyDeviceToHost,
+                                      d->dstream));
+                HIPCHK(hipMemcpyAsync(d->h_mask + nw + lo, d->d_mask + nw + lo, (hi - lo) * 8,
+                                      hipMemcpyDeviceToHost, d->dstream));
+                mask_done = hi;
+            }
+            words[k] = {lo, std::max(lo, hi)};
+        }
+        HIPCHK(hipEventRecord(d->ev_d2h[k], d->dstream));
+        return JB_OK;
+    };
+    auto finish = [&](size_t k) -> int {  // piece k's results have landed: into the caller's arrays
+        const Piece& p = pcs[k];
+        HIPCHK(hipEventSynchronize(d->ev_d2h[k]));
+        const uint32_t nt = ntok[k];
+        {
+            const uint32_t* c = d->h_pcnt + k * kPieceCnt;
+            acc.tokens += nt;
+            acc.long_blocks += c[CNT_NLONG];
+            acc.viterbi_ties += c[CNT_TIES];
+            const uint64_t nt_ = (doc_off[p.d1] - doc_off[p.d0] + kTileBytes - 1) / kTileBytes;
+            for (uint64_t i = 0; i < nt_; i++) {
+                acc.blocks += d->h_ptile[p.tslot + i].x;
+                acc.zh_blocks += d->h_ptile[p.tslot + i].y;
+            }
+        }
+        if (mask) {
+            put_mask_words(mask, rw, nw, words[k].first, words[k].second, d->h_mask, d->h_mask + nw);
+            out->n += nt;
+            return JB_OK;
+        }
+        const Device::OutSet& o = d->outs[k % Device::kSets];
         const bool write = out->reserve(out->n + nt);
         if (!write && !out->external) return fail(JB_ENOMEM, "out of host memory for %u tokens", nt);
-        // spans back in pieces of 2M tokens; each piece is widened while the next ones are in flight
-        const uint32_t kTokPiece = 1u << 21;
-        const uint32_t np = (nt + kTokPiece - 1) / kTokPiece;
-        while (d->ev.size() < 2 * (size_t)np) {
-            hipEvent_t e;
-            HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            d->ev.push_back(e);
-        }
-        for (uint32_t q = 0; q < np; q++) {
-            const uint64_t t0 = (uint64_t)q * kTokPiece, l = std::min<uint64_t>(kTokPiece, nt - t0);
-            HIPCHK(hipMemcpyAsync(d->h_span + t0, d->w.tok_start + t0, l * 4, hipMemcpyDeviceToHost, d->stream));
-            HIPCHK(hipEventRecord(d->ev[2 * q], d->stream));
-            HIPCHK(hipMemcpyAsync(d->h_span + nt + t0, d->w.tok_end + t0, l * 4, hipMemcpyDeviceToHost, d->stream));
-            HIPCHK(hipEventRecord(d->ev[2 * q + 1], d->stream));
-        }
-        HIPCHK(hipMemcpyAsync(d->h_misc, d->w.doc_tok, (uint64_t)(nd + 1) * 8, hipMemcpyDeviceToHost, d->stream));
-        const auto c3 = now();
-        {
-            // kCopyThreads threads widen their share of each piece as soon as it has landed
-            const unsigned nth = nt >= (1u << 20) ? kCopyThreads : 1u;
+        if (write) {
+            const uint64_t base = doc_off[p.d0];
             uint64_t* const os = out->s + out->n;
             uint64_t* const oe = out->e + out->n;
-            const uint32_t* const hs = d->h_span;
+            const uint32_t* const hs = o.hs;
+            const unsigned nth = nt >= (1u << 20) ? kCopyThreads : 1u;
             auto work = [&](unsigned t) {
-                for (uint32_t q = 0; q < np; q++) {
-                    const uint64_t t0 = (uint64_t)q * kTokPiece, l = std::min<uint64_t>(kTokPiece, nt - t0);
-                    const uint64_t a0 = t0 + l * t / nth, a1 = t0 + l * (t + 1) / nth;
-                    (void)hipEventSynchronize(d->ev[2 * q]);
-                    if (write)
-                        for (uint64_t k = a0; k < a1; k++) os[k] = base + hs[k];
-                    (void)hipEventSynchronize(d->ev[2 * q + 1]);
-                    if (write)
-                        for (uint64_t k = a0; k < a1; k++) oe[k] = base + hs[nt + k];
-                }
+                const uint64_t a = (uint64_t)nt * t / nth, b = (uint64_t)nt * (t + 1) / nth;
+                for (uint64_t i = a; i < b; i++) os[i] = base + hs[i];
+                for (uint64_t i = a; i < b; i++) oe[i] = base + hs[nt + i];
             };
             run_threads(nth, work);
-        }
-        HIPCHK(hipStreamSynchronize(d->stream));
-        if (!write) {  // caller arrays too small: count the rest, write nothing more
+        } else {  // caller arrays too small: count the rest, write nothing more
             out->needed = out->n + nt;
-            out->n += nt;
             out->cap = 0;
-            for (uint32_t k = 0; k < nd; k++) out->per_doc.push_back(d->h_misc[k + 1] - d->h_misc[k]);
-            a = b;
-            continue;
         }
-        if (tdbg)
-            fprintf(stderr, "[jb] host batch %.1f MiB: copy in %.2f ms, H2D+kernels %.2f, D2H spans %.2f, widen %.2f\n",
-                    nbytes / 1048576.0, ms(c0, c1), ms(c1, c2), ms(c2, c3), ms(c3, now()));  // (D2H: the enqueue)
         out->n += nt;
-        for (uint32_t k = 0; k < nd; k++) out->per_doc.push_back(d->h_misc[k + 1] - d->h_misc[k]);
-        a = b;
+        for (uint32_t j = 0; j < p.d1 - p.d0; j++) out->per_doc.push_back(o.hdt[j + 1] - o.hdt[j]);
+        return JB_OK;
+    };
+    static const bool tdbg = getenv("JB_DEBUG") != nullptr;
+    const auto c0 = std::chrono::steady_clock::now();
+    if ((rc = stage(0))) return drain(rc);
+    for (size_t k = 0; k < np; k++) {
+        if ((rc = compute(k))) return drain(rc);
+        if (k + 1 < np && (rc = stage(k + 1))) return drain(rc);
+        if (k >= 1 && (rc = collect(k - 1))) return drain(rc);
+        if (k >= 2 && (rc = finish(k - 2))) return drain(rc);
     }
+    if ((rc = collect(np - 1))) return drain(rc);
+    for (size_t k = np >= 2 ? np - 2 : 0; k < np; k++)
+        if ((rc = finish(k))) return drain(rc);
+    d->acc = acc;
+    d->acc_valid = true;
+    if (tdbg)
+        fprintf(stderr, "[jb] host range %.1f MiB (%s) in %zu pieces: %.2f ms\n", rbytes / 1048576.0,
+                mask ? "masks" : "spans", np,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count());
     return JB_OK;
 }
 
@@ -1050,26 +1267,167 @@ extern "C" int jb_shard_bounds(const uint64_t* doc_off, uint32_t ndocs, uint32_t
     return JB_OK;
 }
 
-// Shard [0, ndocs) over the devices (jb_shard_bounds) and cut, one host
-// thread per device.  sb[k] receives device k's spans.  The caller holds
-// ctx->lock (shared for cuts, exclusive inside jb_add_word).
+// The first Han-run start of the document [lo, hi) at or after pos (and after lo):
+// a position q where a Han rune begins (Go's DecodeRune over the document) and the
+// rune before it is not Han; hi if there is none.  Cutting a document there is
+// exact: splitText's blocks (tokenizer.go:165-210) are the same in both parts, and
+// blocks are cut independently (tokenizer.go:158-160).  Decoding from lo lands on
+// every lead byte of a valid sequence (a continuation byte is never a lead byte), so
+// the rune before q is the valid 2-4 byte sequence that ends at q if there is one,
+// else the single byte q-1.
+static uint64_t han_run_start(const uint8_t* t, uint64_t lo, uint64_t hi, uint64_t pos) {
+    auto dec = [&](uint64_t q, uint32_t* r) -> uint32_t {
+        const uint64_t lim = std::min<uint64_t>(4, hi - q);
+        uint32_t x = 0;
+        for (uint64_t k = 0; k < lim; k++) x |= (uint32_t)t[q + k] << (8 * k);
+        return jb_decode(x, (uint32_t)lim, r);
+    };
+    for (uint64_t q = std::max(pos, lo + 1); q < hi; q++) {
+        if (t[q] < 0xE0u) continue;  // Han runes are 3 or 4 bytes long
+        uint32_t r;
+        if (dec(q, &r) < 3 || !jb_is_han(r)) continue;
+        bool prev_han = false;
+        if (t[q - 1] >= 0x80u)
+            for (uint32_t k = 2; k <= 4; k++) {
+                uint32_t pr;
+                if (q >= lo + k && dec(q - k, &pr) == k) {
+                    prev_han = jb_is_han(pr);
+                    break;
+                }
+            }
+        if (!prev_han) return q;
+    }
+    return hi;
+}
+
+extern "C" int jb_split_points(const uint8_t* text, const uint64_t* doc_off, uint32_t ndocs, uint32_t nparts,
+                               uint64_t* cut) {
+    if (!cut || nparts == 0 || (!doc_off && ndocs)) return fail(JB_EINVAL, "jb_split_points: bad argument");
+    for (uint32_t k = 0; k < ndocs; k++)
+        if (doc_off[k + 1] < doc_off[k]) return fail(JB_EINVAL, "doc_off not monotonic at %u", k);
+    const uint64_t b0 = ndocs ? doc_off[0] : 0, total = ndocs ? doc_off[ndocs] - b0 : 0;
+    if (total && !text) return fail(JB_EINVAL, "jb_split_points: null text");
+    cut[0] = b0;
+    cut[nparts] = b0 + total;
+    uint32_t j = 0;
+    uint64_t known = 0, known_q = 0;  // in document j: the first Han-run start at or after `known` is known_q
+    bool have = false;
+    for (uint32_t k = 1; k < nparts; k++) {
+        const uint64_t target = std::max(b0 + total * k / nparts, cut[k - 1]);
+        const uint32_t j0 = j;
+        while (j < ndocs && doc_off[j + 1] <= target) j++;
+        if (j != j0) have = false;
+        if (j >= ndocs) {
+            cut[k] = b0 + total;
+            continue;
+        }
+        if (doc_off[j] >= target) {
+            cut[k] = doc_off[j];
+            continue;
+        }
+        if (!have || target < known || target > known_q) {
+            known = target;
+            known_q = han_run_start(text, doc_off[j], doc_off[j + 1], target);
+            have = true;
+        }
+        cut[k] = known_q;  // (the next document's start when the rest of this one has none)
+    }
+    return JB_OK;
+}
+
+// Cut units: documents, or parts of documents cut at Han-run starts (han_run_start),
+// so that one large document spreads over several devices and over
+// several pipeline pieces within a device.  Unit u is bytes [off[u], off[u+1]) of
+// document doc[u]; device k owns units [dev[k], dev[k+1]).
+struct Units {
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> doc;
+    std::vector<uint32_t> dev;
+};
+
+// Shard the batch over the devices and cut, one host thread per device.  With one
+// device and no document longer than its pipeline piece the units are the
+// documents; otherwise the device ranges are byte-balanced (jb_split_points) and
+// documents longer than a piece are cut into units at Han-run starts.  sb[k]
+// receives device k's spans and tokens per unit; *unit_doc (left empty when units
+// are documents) maps units to documents.  The caller holds ctx->lock (shared for
+// cuts, exclusive inside jb_add_word).
 static int cut_sharded(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off, uint32_t ndocs, int hmm,
-                       std::vector<SpanBuf>* sbp) {
+                       std::vector<SpanBuf>* sbp, const MaskDst* mask = nullptr,
+                       std::vector<uint32_t>* unit_doc = nullptr) {
     if (ndocs && !text && doc_off[ndocs] > doc_off[0]) return fail(JB_EINVAL, "null text");
+    for (uint32_t k = 0; k < ndocs; k++)
+        if (doc_off[k + 1] < doc_off[k]) return fail(JB_EINVAL, "doc_off not monotonic at %u", k);
     std::vector<SpanBuf>& sb = *sbp;
     const size_t nd = ctx->devs.size();
-    std::vector<uint32_t> cut(nd + 1, ndocs);
-    int rc0 = jb_shard_bounds(doc_off, ndocs, (uint32_t)nd, cut.data());
-    if (rc0) return rc0;
+    const uint64_t b0 = ndocs ? doc_off[0] : 0, b1 = ndocs ? doc_off[ndocs] : 0;
+    bool split = nd > 1;
+    for (uint32_t j = 0; j < ndocs && !split; j++)
+        split = doc_off[j + 1] - doc_off[j] > ctx->devs[0]->piece_bytes;
+    Units un;
+    std::vector<uint64_t> cutb(nd + 1, b0);
+    cutb[nd] = b1;
+    if (split) {
+        int rc0 = jb_split_points(text, doc_off, ndocs, (uint32_t)nd, cutb.data());
+        if (rc0) return rc0;
+        un.off.reserve((size_t)ndocs + 2 * nd + 1);
+        un.doc.reserve((size_t)ndocs + 2 * nd);
+        un.dev.assign(nd + 1, 0);
+        size_t k = 0;
+        auto dev_of = [&](uint64_t pos) {  // the last device whose range starts at or before pos
+            while (k + 1 < nd && cutb[k + 1] <= pos && (cutb[k + 1] < b1 || pos >= b1)) {
+                k++;
+                un.dev[k] = (uint32_t)un.doc.size();
+            }
+        };
+        for (uint32_t j = 0; j < ndocs; j++) {
+            uint64_t pos = doc_off[j];
+            const uint64_t de = doc_off[j + 1];
+            for (;;) {
+                dev_of(pos);
+                const uint64_t end = std::min(de, k + 1 < nd && cutb[k + 1] > pos ? cutb[k + 1] : de);
+                const uint64_t pb = ctx->devs[k]->piece_bytes;
+                uint64_t u = pos;
+                while (end - u > pb) {  // a longer part: pipeline pieces at Han-run starts
+                    const uint64_t q = han_run_start(text, doc_off[j], de, u + pb);
+                    if (q >= end) break;
+                    un.off.push_back(u);
+                    un.doc.push_back(j);
+                    u = q;
+                }
+                un.off.push_back(u);
+                un.doc.push_back(j);
+                if (end >= de) break;
+                pos = end;
+            }
+        }
+        un.off.push_back(b1);
+        for (size_t q = k + 1; q <= nd; q++) un.dev[q] = (uint32_t)un.doc.size();
+        if (un.doc.size() > 0xFFFFFFFFull) return fail(JB_ELIMIT, "too many cut units");
+    }
+    const uint64_t* uoff = split ? un.off.data() : doc_off;
+    if (unit_doc) {
+        unit_doc->clear();
+        if (split) *unit_doc = un.doc;
+    }
     for (auto& d : ctx->devs) {  // jb_last_stats: only the devices this batch reaches
         std::lock_guard<std::mutex> g(d->mu);
         d->has_stats = false;
     }
+    if (mask)  // the words a device range shares with its neighbours are ORed into: clear them first
+        for (size_t k = 0; k < nd; k++)
+            if (cutb[k] < cutb[k + 1]) {
+                mask->s[(cutb[k] - mask->batch0) >> 6] = 0;
+                mask->e[(cutb[k] - mask->batch0) >> 6] = 0;
+                mask->s[(cutb[k + 1] - 1 - mask->batch0) >> 6] = 0;
+                mask->e[(cutb[k + 1] - 1 - mask->batch0) >> 6] = 0;
+            }
     std::vector<int> rcs(nd, JB_OK);
     std::vector<std::string> errs(nd);
     auto work = [&](size_t k) {
-        if (cut[k] < cut[k + 1]) {
-            rcs[k] = cut_range(ctx, ctx->devs[k].get(), text, doc_off, cut[k], cut[k + 1], hmm != 0, &sb[k]);
+        const uint32_t u0 = split ? un.dev[k] : (k == 0 ? 0u : ndocs), u1 = split ? un.dev[k + 1] : ndocs;
+        if (u0 < u1) {
+            rcs[k] = cut_range(ctx->devs[k].get(), text, uoff, u0, u1, hmm != 0, &sb[k], mask);
             if (rcs[k]) errs[k] = g_err;
         }
     };
@@ -1085,18 +1443,18 @@ static int cut_sharded(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off
     return JB_OK;
 }
 
-static void fill_doc_tok(const std::vector<SpanBuf>& sb, uint32_t ndocs, uint64_t* doc_tok) {
-    uint64_t w = 0, di = 0;
-    doc_tok[0] = 0;
-    for (const auto& b : sb) {
-        uint64_t acc = w;
+// doc_tok from the tokens per unit (in unit order over the devices' buffers)
+static void fill_doc_tok(const std::vector<SpanBuf>& sb, uint32_t ndocs, uint64_t* doc_tok,
+                         const std::vector<uint32_t>& unit_doc) {
+    for (uint32_t d = 0; d <= ndocs; d++) doc_tok[d] = 0;
+    size_t u = 0;
+    for (const auto& b : sb)
         for (uint64_t c : b.per_doc) {
-            acc += c;
-            doc_tok[++di] = acc;
+            const uint32_t d = unit_doc.empty() ? (uint32_t)u : unit_doc[u];
+            doc_tok[d + 1] += c;
+            u++;
         }
-        w += b.n;
-    }
-    while (di < ndocs) doc_tok[++di] = w;
+    for (uint32_t d = 0; d < ndocs; d++) doc_tok[d + 1] += doc_tok[d];
 }
 
 // jb_cut_batch with ctx->lock already held by the caller.
@@ -1107,7 +1465,8 @@ static int cut_batch_locked(jb_ctx* ctx, const uint8_t* text, const uint64_t* do
     auto release_all = [&] {
         for (auto& b : sb) b.release();
     };
-    int rc = cut_sharded(ctx, text, doc_off, ndocs, hmm, &sb);
+    std::vector<uint32_t> unit_doc;
+    int rc = cut_sharded(ctx, text, doc_off, ndocs, hmm, &sb, nullptr, &unit_doc);
     if (rc) {
         release_all();
         return rc;
@@ -1140,7 +1499,7 @@ static int cut_batch_locked(jb_ctx* ctx, const uint8_t* text, const uint64_t* do
         jb_spans_free(out);
         return fail(JB_ENOMEM, "out of host memory for %llu tokens", (unsigned long long)nt);
     }
-    fill_doc_tok(sb, ndocs, out->doc_tok);
+    fill_doc_tok(sb, ndocs, out->doc_tok, unit_doc);
     release_all();
     return JB_OK;
 }
@@ -1171,7 +1530,8 @@ extern "C" int jb_cut_batch_into(jb_ctx* ctx, const uint8_t* text, const uint64_
     auto release_all = [&] {
         for (auto& b : sb) b.release();
     };
-    int rc = cut_sharded(ctx, text, doc_off, ndocs, hmm, &sb);
+    std::vector<uint32_t> unit_doc;
+    int rc = cut_sharded(ctx, text, doc_off, ndocs, hmm, &sb, nullptr, &unit_doc);
     if (rc) {
         release_all();
         return rc;
@@ -1194,9 +1554,60 @@ extern "C" int jb_cut_batch_into(jb_ctx* ctx, const uint8_t* text, const uint64_
             w += sb[k].n;
         }
     }
-    fill_doc_tok(sb, ndocs, doc_tok);
+    fill_doc_tok(sb, ndocs, doc_tok, unit_doc);
     release_all();
     return JB_OK;
+}
+
+extern "C" int jb_cut_batch_mask(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off, uint32_t ndocs,
+                                 int hmm, uint64_t* starts, uint64_t* ends, uint64_t nwords, uint64_t* ntokens) {
+    if (!ctx || !ntokens || (!doc_off && ndocs)) return fail(JB_EINVAL, "jb_cut_batch_mask: null argument");
+    *ntokens = 0;
+    const uint64_t nbytes = ndocs ? doc_off[ndocs] - doc_off[0] : 0;
+    const uint64_t need = (nbytes + 63) / 64;
+    if (nwords < need) return fail(JB_EINVAL, "jb_cut_batch_mask: %llu words for %llu bytes (want %llu)",
+                                   (unsigned long long)nwords, (unsigned long long)nbytes, (unsigned long long)need);
+    if (need && (!starts || !ends)) return fail(JB_EINVAL, "jb_cut_batch_mask: null mask");
+    std::shared_lock<std::shared_mutex> rl(ctx->lock);
+    const size_t nd = ctx->devs.size();
+    std::vector<SpanBuf> sb(nd);
+    const MaskDst m{starts, ends, ndocs ? doc_off[0] : 0};
+    int rc = cut_sharded(ctx, text, doc_off, ndocs, hmm, &sb, &m);
+    uint64_t nt = 0;
+    for (auto& b : sb) {
+        nt += b.n;
+        b.release();
+    }
+    if (rc) return rc;
+    *ntokens = nt;
+    return JB_OK;
+}
+
+extern "C" int jb_host_alloc(size_t n, void** p) {
+    if (!p) return fail(JB_EINVAL, "jb_host_alloc: null argument");
+    *p = nullptr;
+    const hipError_t e = hipHostMalloc(p, std::max<size_t>(n, 1), hipHostMallocPortable);
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return fail(e == hipErrorOutOfMemory ? JB_ENOMEM : JB_EDEVICE, "hipHostMalloc(%zu): %s", n,
+                    hipGetErrorString(e));
+    }
+    std::lock_guard<std::mutex> g(g_host_mu);
+    g_host.push_back(HostAlloc{(uintptr_t)*p, n});
+    return JB_OK;
+}
+
+extern "C" void jb_host_free(void* p) {
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> g(g_host_mu);
+        for (size_t i = 0; i < g_host.size(); i++)
+            if (g_host[i].a == (uintptr_t)p) {
+                g_host.erase(g_host.begin() + (long)i);
+                break;
+            }
+    }
+    (void)hipHostFree(p);
 }
 
 extern "C" int jb_cut(jb_ctx* ctx, const uint8_t* text, size_t len, int hmm, jb_spans* out) {
@@ -1390,6 +1801,14 @@ extern "C" int jb_last_stats(jb_ctx* ctx, jb_stats* out) {
             out->blocks += d->small_hdr[SM_BLOCKS];
             out->zh_blocks += d->small_hdr[SM_ZHBLOCKS];
             out->viterbi_ties += d->small_hdr[SM_TIES];
+            continue;
+        }
+        if (d->acc_valid) {  // a host range cut in pieces: summed as they came back
+            out->tokens += d->acc.tokens;
+            out->blocks += d->acc.blocks;
+            out->zh_blocks += d->acc.zh_blocks;
+            out->long_blocks += d->acc.long_blocks;
+            out->viterbi_ties += d->acc.viterbi_ties;
             continue;
         }
         if (!d->w.counters) continue;

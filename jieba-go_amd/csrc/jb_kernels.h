@@ -85,7 +85,8 @@ struct Work {
 // Kernel ids for per-launch timing.
 enum KernelId {
     K_DOCBITS = 0, K_MARK_WALK, K_ZH, K_NONZH,
-    K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_LONG_DP, K_LONG_SEG, K_LONG_PATH, K_LONG_TAIL, K_NUM
+    K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_LONG_DP, K_LONG_SEG, K_LONG_PATH, K_LONG_TAIL, K_MASK_MERGE,
+    K_NUM
 };
 extern const char* const kKernelNames[K_NUM];
 
@@ -104,11 +105,21 @@ struct LaunchCfg {
     uint32_t small_max; // host batches up to this many bytes take k_small (0: never)
 };
 
+// Boundary-mask output of one pipeline run (jb_cut_batch_mask): the batch's token
+// start / end bits go into the u64 bitmaps s / e at bit offset rel (k_mask_merge)
+// instead of becoming spans; the counters still receive the token count.
+struct MaskOut {
+    uint64_t* s;
+    uint64_t* e;
+    uint64_t rel;
+};
+
 // Enqueue the whole Cut pipeline on `stream`.  Returns hipSuccess or the first
-// launch error.  d_text must be readable 64 bytes past nbytes.
+// launch error.  d_text must be readable 64 bytes past nbytes.  mask != nullptr:
+// boundary masks instead of spans (tok_start / tok_end / doc_tok are not written).
 hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text, uint64_t nbytes,
                         const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, const LaunchCfg& lc,
-                        hipStream_t stream, KernelTimer* timer);
+                        hipStream_t stream, KernelTimer* timer, const MaskOut* mask = nullptr);
 
 // One-workgroup path for small batches (k_small): the text and document offsets
 // are read from `text`/`doc_off` (device or mapped pinned host memory; text

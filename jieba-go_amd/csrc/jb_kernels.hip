@@ -39,7 +39,7 @@ namespace jb {
 
 const char* const kKernelNames[K_NUM] = {"k_docbits", "k_mark_walk", "k_zh", "k_nonzh", "k_tok_count", "k_scan_tok",
                                          "k_tok_write", "k_doc_tok", "k_long_dp", "k_long_seg", "k_long_path",
-                                         "k_long_tail"};
+                                         "k_long_tail", "k_mask_merge"};
 
 // newJiebaHMM literals (tokenizer.go:629-652)
 #define START_B (-0.26268660809250016)
@@ -2622,6 +2622,54 @@ __global__ void k_doc_tok(const uint64_t* __restrict__ doc_off, uint32_t ndocs, 
     doc_tok[d] = lo;
 }
 
+// Boundary-mask output (jb_cut_batch_mask): a piece's token bitmaps (bit j = byte j
+// of the piece, u32 words) into the range's u64 bitmaps at bit offset `rel`, bits
+// of other pieces untouched: a word the piece shares with its neighbours (its first
+// and last) is ORed in, the others stored.  Pieces of one range run in order on one
+// stream over bitmaps cleared at the start.  Counts the piece's token starts and
+// ends into the counters (the spans kernels do not run in this mode).
+__global__ __launch_bounds__(256) void k_mask_merge(const uint32_t* __restrict__ sbits,
+                                                    const uint32_t* __restrict__ ebits, uint64_t n, uint64_t rel,
+                                                    uint64_t* __restrict__ ms, uint64_t* __restrict__ me,
+                                                    uint32_t* __restrict__ counters) {
+    const uint32_t sh = (uint32_t)(rel & 63u);
+    const uint64_t nout = (sh + n + 63u) >> 6, nw32 = (n + 31u) >> 5;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t cs = 0, ce = 0;
+    if (t < nout) {
+        auto piece64 = [&](const uint32_t* b, int64_t i) -> uint64_t {  // piece bits [64i, 64i + 64)
+            if (i < 0) return 0ull;
+            const uint64_t lo = 2u * (uint64_t)i, hi = lo + 1u;
+            return (lo < nw32 ? (uint64_t)b[lo] : 0ull) | ((hi < nw32 ? (uint64_t)b[hi] : 0ull) << 32);
+        };
+        uint64_t os = piece64(sbits, (int64_t)t), oe = piece64(ebits, (int64_t)t);
+        if (sh) {
+            os = (os << sh) | (piece64(sbits, (int64_t)t - 1) >> (64u - sh));
+            oe = (oe << sh) | (piece64(ebits, (int64_t)t - 1) >> (64u - sh));
+        }
+        const uint64_t w = (rel >> 6) + t;
+        if (t == 0 || t == nout - 1u) {
+            if (os) atomicOr(reinterpret_cast<unsigned long long*>(ms + w), (unsigned long long)os);
+            if (oe) atomicOr(reinterpret_cast<unsigned long long*>(me + w), (unsigned long long)oe);
+        } else {
+            ms[w] = os;
+            me[w] = oe;
+        }
+        cs = (uint32_t)__popcll(os);
+        ce = (uint32_t)__popcll(oe);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        cs += (uint32_t)__shfl_xor((int)cs, d, 64);
+        ce += (uint32_t)__shfl_xor((int)ce, d, 64);
+    }
+    if ((threadIdx.x & 63u) == 0 && (cs | ce)) {
+        atomicAdd(counters + CNT_NTOK, cs);
+        atomicAdd(counters + CNT_NTOKE, ce);
+        atomicAdd(reinterpret_cast<unsigned long long*>(counters + CNT_NWORDS), (unsigned long long)cs);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // k_small: a whole small batch (<= kSmallBytes of text) in one workgroup, for
 // single Cut calls (tokenizer.go:151-162; BASELINE config 1).  The eleven-kernel
@@ -3161,7 +3209,7 @@ uint32_t zh_blocks_per_cu(bool hmm) { return hmm ? occ_zh<true>() : occ_zh<false
 
 hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text, uint64_t nbytes,
                         const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, const LaunchCfg& lc,
-                        hipStream_t stream, KernelTimer* timer) {
+                        hipStream_t stream, KernelTimer* timer, const MaskOut* mask) {
     const uint32_t diag = lc.diag;
     const uint64_t nwords = (nbytes + 31) / 32;
     const uint32_t ntiles = (uint32_t)((nbytes + kTileBytes - 1) / kTileBytes);
@@ -3225,6 +3273,13 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3((nw + 255u) / 256u), dim3(256), 0, stream, d_text,
                                              (uint32_t)nbytes, w.lanemask, w.tile_cnt, ntiles, w.alnum16, w.sbits,
                                              w.ebits));
+    }
+    if (mask) {  // boundary masks instead of spans
+        const uint64_t nout = ((mask->rel & 63u) + nbytes + 63u) >> 6;
+        JB_TIMED(K_MASK_MERGE, hipLaunchKernelGGL(k_mask_merge, dim3((uint32_t)((nout + 255u) / 256u)), dim3(256), 0,
+                                                  stream, w.sbits, w.ebits, nbytes, mask->rel, mask->s, mask->e,
+                                                  w.counters));
+        return hipGetLastError();
     }
     JB_TIMED(K_TOK_COUNT, hipLaunchKernelGGL((k_tok<false>), dim3(nttiles), dim3(256), 0, stream, w.sbits, w.ebits,
                                              nwords, w.ttile_cnt, w.supt, w.counters, nullptr, nullptr));

@@ -26,7 +26,8 @@ JIEBA_SIZE = 60_101_967  # tokenizer.go:454
 # Every symbol include/jiebahip.h declares.
 EXPORTS = [
     "jb_open", "jb_close", "jb_last_error", "jb_cut", "jb_cut_batch", "jb_cut_batch_into", "jb_spans_free",
-    "jb_cut_device", "jb_cut_device_into", "jb_open_image",
+    "jb_cut_device", "jb_cut_device_into", "jb_open_image", "jb_cut_batch_mask", "jb_host_alloc", "jb_host_free",
+    "jb_split_points",
     "jb_add_word", "jb_dict_get", "jb_dict_size", "jb_save", "jb_profile_enable", "jb_profile_read",
     "jb_profile_reset", "jb_image_build", "jb_image_free", "jb_image_save", "jb_image_dict_info", "jb_image_lookup",
     "jb_image_stats", "jb_image_emit", "jb_go_log", "jb_shard_bounds", "jb_last_stats",
@@ -97,6 +98,10 @@ def lib():
         L.jb_cut_device_into.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_int, vp, vp, vp, C.c_uint64, vp,
                                          vp]
         L.jb_open_image.argtypes = [vp, C.POINTER(jb_config), C.POINTER(vp)]
+        L.jb_cut_batch_mask.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, vp, vp, C.c_uint64, C.POINTER(C.c_uint64)]
+        L.jb_host_alloc.argtypes = [C.c_size_t, C.POINTER(vp)]
+        L.jb_host_free.argtypes = [vp]
+        L.jb_host_free.restype = None
         L.jb_add_word.argtypes = [vp, cp, C.c_size_t, C.c_int64]
         L.jb_dict_get.argtypes = [vp, cp, C.c_size_t, C.POINTER(C.c_int64)]
         L.jb_dict_size.argtypes = [vp]
@@ -118,6 +123,7 @@ def lib():
         L.jb_go_log.argtypes = [C.c_double]
         L.jb_go_log.restype = C.c_double
         L.jb_shard_bounds.argtypes = [vp, C.c_uint32, C.c_uint32, vp]
+        L.jb_split_points.argtypes = [vp, vp, C.c_uint32, C.c_uint32, vp]
         L.jb_image_log_keys.argtypes = [vp, vp, C.c_size_t, C.POINTER(C.c_size_t)]
         L.jb_suggest_freq.argtypes = [vp, cp, C.c_size_t, C.POINTER(C.c_int64)]
         L.jb_add_log.argtypes = [vp, vp, vp, C.c_size_t]
@@ -349,6 +355,20 @@ class Tokenizer:
         k = n.value
         return out[0][:k], out[1][:k], out[2], out
 
+    def cut_batch_mask(self, buf, doc_off, hmm, out=None):
+        """jb_cut_batch_mask: (starts u64 words, ends u64 words, ntokens); `out` = the
+        two arrays to reuse."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)  # (a HostBuffer's .array stays where it is)
+        doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
+        nd = len(doc_off) - 1
+        nw = (int(doc_off[-1] - doc_off[0]) + 63) // 64 if nd else 0
+        if out is None or len(out[0]) < nw:
+            out = (np.empty(max(nw, 1), np.uint64), np.empty(max(nw, 1), np.uint64))
+        n = C.c_uint64()
+        _check(lib().jb_cut_batch_mask(self.h, buf.ctypes.data, doc_off.ctypes.data, nd, int(hmm), out[0].ctypes.data,
+                                       out[1].ctypes.data, len(out[0]), C.byref(n)))
+        return out[0], out[1], n.value
+
     def cut_device(self, d_text_ptr, nbytes, d_doc_off_ptr, ndocs, hmm, stream_ptr=0):
         """Device-resident cut; returns device pointers (start, end, doc_tok, ntok)."""
         a, b, c, d = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
@@ -415,6 +435,32 @@ class Tokenizer:
         return {names[i].decode(): (ms[i], n[i]) for i in range(k)}
 
 
+class HostBuffer:
+    """jb_host_alloc'd pinned memory as a numpy uint8 array (`.array`); batches cut
+    from that array skip the library's staging copy."""
+
+    def __init__(self, n):
+        p = C.c_void_p()
+        _check(lib().jb_host_alloc(n, C.byref(p)))
+        self.p = p
+        self.array = np.ctypeslib.as_array((C.c_uint8 * max(n, 1)).from_address(p.value))[:n]
+
+    def free(self):
+        if self.p:
+            self.array = None
+            lib().jb_host_free(self.p)
+            self.p = None
+
+
+def mask_to_spans(ms, me, nbytes, base=0):
+    """Boundary masks -> (starts, ends) byte spans (start bit k pairs with end bit k)."""
+    nw = (nbytes + 63) // 64
+    sb = np.unpackbits(np.asarray(ms[:nw]).view(np.uint8), bitorder="little")[:nbytes]
+    eb = np.unpackbits(np.asarray(me[:nw]).view(np.uint8), bitorder="little")[:nbytes]
+    return (np.flatnonzero(sb).astype(np.uint64) + np.uint64(base),
+            np.flatnonzero(eb).astype(np.uint64) + np.uint64(base + 1))
+
+
 _hip = None
 
 
@@ -451,6 +497,15 @@ def shard_bounds(doc_off, nparts):
     doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
     cut = np.zeros(nparts + 1, np.uint32)
     _check(lib().jb_shard_bounds(doc_off.ctypes.data, len(doc_off) - 1, nparts, cut.ctypes.data))
+    return [int(x) for x in cut]
+
+
+def split_points(buf, doc_off, nparts):
+    """jb_split_points: byte cuts at document starts or Han-run starts."""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
+    cut = np.zeros(nparts + 1, np.uint64)
+    _check(lib().jb_split_points(buf.ctypes.data, doc_off.ctypes.data, len(doc_off) - 1, nparts, cut.ctypes.data))
     return [int(x) for x in cut]
 
 

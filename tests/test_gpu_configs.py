@@ -153,3 +153,123 @@ def test_cut_device_into_concurrent_threads(syn_small):
         tk.cut_device_into(0, 100, 0, 1, True, 1, 1, 99, 1, 1)
     assert e.value.code == J.JB_EINVAL
     tk.close()
+
+
+def _mask_spans(tk, buf, off, hmm):
+    ms, me, n = tk.cut_batch_mask(buf, off, hmm)
+    base = int(off[0])
+    s, e = J.mask_to_spans(ms, me, int(off[-1]) - base, base)
+    assert len(s) == len(e) == n
+    return s, e
+
+
+@pytest.mark.parametrize("piece_kib", [256, 65536])
+def test_host_pipeline_pieces_and_masks(syn_small, piece_kib, monkeypatch):
+    """Host batches cut in pieces of whole documents, pipelined over three streams
+    (JB_PIECE_KIB; 256 KiB makes dozens of pieces here, and the 1M-rune document one
+    piece of its own): spans, caller arrays, boundary masks (jb_cut_batch_mask),
+    pinned input (jb_host_alloc) and the summed counters all equal the oracle's."""
+    dp, ep, s = syn_small
+    monkeypatch.setenv("JB_PIECE_KIB", str(piece_kib))
+    tk = J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep))
+    monkeypatch.delenv("JB_PIECE_KIB")
+    ref = J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep))
+    o = O.Oracle.from_files(dp, ep, 0)
+    buf, off, _ = s.corpus(synth.KIND_DOCS, 70, target_bytes=5 << 20)
+    lbuf, loff, _ = s.corpus(synth.KIND_LONG_PUNCT, 71, target_runes=1_000_000)
+    n0, nl = int(off[-1]), int(loff[-1])
+    big = np.zeros(n0 + nl + 64, np.uint8)
+    big[:n0], big[n0:n0 + nl] = buf[:n0], lbuf[:nl]
+    boff = np.concatenate([np.asarray(off, np.uint64), np.asarray(loff[1:], np.uint64) + np.uint64(n0)])
+    for hmm in (False, True):
+        os_, oe, od = o.cut_batch(big, boff, hmm, nthreads=8)
+        gs, ge, gd = tk.cut_batch(big, boff, hmm)
+        _cmp(gs, ge, gd, os_, oe, od, f"pieces of {piece_kib} KiB, hmm={hmm}")
+        st = tk.last_stats()
+        ref.cut_batch(big, boff, hmm)
+        rst = ref.last_stats()
+        assert st["tokens"] == len(os_) and st["blocks"] == rst["blocks"] and st["zh_blocks"] == rst["zh_blocks"], \
+            (st, rst)
+        s2, e2, d2, _ = tk.cut_batch_into(big, boff, hmm)
+        _cmp(s2, e2, d2, os_, oe, od, f"into, pieces of {piece_kib} KiB")
+        ms, me = _mask_spans(tk, big, boff, hmm)
+        _cmp(ms, me, od, os_, oe, od, f"masks, pieces of {piece_kib} KiB, hmm={hmm}")
+        assert tk.last_stats()["tokens"] == len(os_)
+    # a batch that starts inside the buffer (mask bit 0 = byte doc_off[0]), and documents
+    # of it from pinned memory
+    sub = boff[5:400]
+    os_, oe, od = o.cut_batch(big, sub, True)
+    ms, me = _mask_spans(tk, big, sub, True)
+    _cmp(ms, me, od, os_, oe, od, "masks of a batch at an offset")
+    hb = J.HostBuffer(len(big))
+    try:
+        hb.array[:] = big
+        gs, ge, gd = tk.cut_batch(hb.array, boff, True)
+        os_, oe, od = o.cut_batch(big, boff, True, nthreads=8)
+        _cmp(gs, ge, gd, os_, oe, od, "pinned input")
+        ms, me = _mask_spans(tk, hb.array, boff, True)
+        _cmp(ms, me, od, os_, oe, od, "masks from pinned input")
+    finally:
+        hb.free()
+    # tiny batches (k_small) and empty ones
+    for t in ("", "中文", "我昨天去上海交通大學與老師討論量子力學", "abc 中文 x"):
+        b = np.frombuffer(t.encode() + b"\0" * 16, np.uint8)
+        f = np.array([0, len(t.encode())], np.uint64)
+        ms, me = _mask_spans(tk, b, f, True)
+        os_, oe = o.cut_spans(t.encode(), True)
+        assert ms.tolist() == os_.tolist() and me.tolist() == oe.tolist(), t
+    rc = J.lib().jb_cut_batch_mask(tk.h, big.ctypes.data, boff.ctypes.data, len(boff) - 1, 1, None, None, 3,
+                                   J.C.byref(J.C.c_uint64()))
+    assert rc == J.JB_EINVAL  # 3 words cannot hold the batch
+    tk.close()
+    ref.close()
+
+
+@pytest.mark.parametrize("ndev", [2, 3])
+def test_multi_device_masks(syn_small, ndev, monkeypatch):
+    """Boundary masks over several devices: the words two device ranges share are
+    ORed together, the others written once."""
+    dp, ep, s = syn_small
+    monkeypatch.setenv("JB_DEVICE_WRAP", "1")
+    monkeypatch.setenv("JB_PIECE_KIB", "512")
+    tk = J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep, ndevices=ndev))
+    monkeypatch.delenv("JB_DEVICE_WRAP")
+    monkeypatch.delenv("JB_PIECE_KIB")
+    o = O.Oracle.from_files(dp, ep, 0)
+    buf, off, _ = s.corpus(synth.KIND_DOCS, 80 + ndev, target_bytes=4 << 20)
+    for hmm in (False, True):
+        os_, oe, od = o.cut_batch(buf, off, hmm, nthreads=8)
+        ms, me = _mask_spans(tk, buf, off, hmm)
+        _cmp(ms, me, od, os_, oe, od, f"masks over {ndev} devices, hmm={hmm}")
+    tk.close()
+
+
+@pytest.mark.parametrize("ndev,piece_kib", [(1, 1024), (2, 65536), (4, 512)])
+def test_one_large_document_split(syn_small, ndev, piece_kib, monkeypatch):
+    """One 1M-rune document (config 5a, ~3 MB) cut as several units at Han-run starts
+    (jb_split_points): over devices (JB_DEVICE_WRAP) and over pipeline pieces within a
+    device (JB_PIECE_KIB smaller than the document).  Spans, doc_tok, masks and the
+    counters equal the oracle's on the whole document."""
+    dp, ep, s = syn_small
+    monkeypatch.setenv("JB_DEVICE_WRAP", "1")
+    monkeypatch.setenv("JB_PIECE_KIB", str(piece_kib))
+    tk = J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep, ndevices=ndev))
+    monkeypatch.delenv("JB_DEVICE_WRAP")
+    monkeypatch.delenv("JB_PIECE_KIB")
+    o = O.Oracle.from_files(dp, ep, 0)
+    buf, off, _ = s.corpus(synth.KIND_LONG_PUNCT, 90 + ndev, target_runes=1_000_000)
+    # the document alone, and between two short ones
+    pre = "短句。".encode()
+    b2 = np.frombuffer(pre + bytes(buf[: int(off[-1])]) + pre + b"\0" * 64, np.uint8)
+    off2 = np.array([0, len(pre), len(pre) + int(off[-1]), 2 * len(pre) + int(off[-1])], np.uint64)
+    for bb, ff in ((buf, off), (b2, off2)):
+        for hmm in (False, True):
+            os_, oe, od = o.cut_batch(bb, ff, hmm)
+            gs, ge, gd = tk.cut_batch(bb, ff, hmm)
+            _cmp(gs, ge, gd, os_, oe, od, f"1M runes over {ndev} devices / {piece_kib} KiB pieces, hmm={hmm}")
+            assert tk.last_stats()["tokens"] == len(os_)
+            s2, e2, d2, _ = tk.cut_batch_into(bb, ff, hmm)
+            _cmp(s2, e2, d2, os_, oe, od, "into")
+            ms, me = _mask_spans(tk, bb, ff, hmm)
+            _cmp(ms, me, od, os_, oe, od, "masks")
+    tk.close()

@@ -1,0 +1,42 @@
+// PCIe copy rates from/to pinned host memory, one direction and both at once
+// (diagnostic).  build: hipcc --offload-arch=gfx950 -O2 tools/diag/pcie.hip -o tools/diag/pcie
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <chrono>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
+
+int main() {
+    const size_t n = 256u << 20, piece = 16u << 20;
+    const int reps = 4;
+    void *h1, *h2, *d1, *d2;
+    CK(hipHostMalloc(&h1, n, hipHostMallocDefault));
+    CK(hipHostMalloc(&h2, n, hipHostMallocDefault));
+    CK(hipMalloc(&d1, n));
+    CK(hipMalloc(&d2, n));
+    hipStream_t s1, s2;
+    CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto gbs = [&](std::chrono::steady_clock::time_point a, size_t bytes) {
+        return bytes / std::chrono::duration<double>(now() - a).count() / 1e9;
+    };
+    for (int mode = 0; mode < 4; mode++) {
+        // 0: H2D alone, 1: D2H alone, 2: both at once (whole buffers), 3: both at once in 16 MiB pieces
+        CK(hipDeviceSynchronize());
+        auto t = now();
+        for (int r = 0; r < reps; r++) {
+            if (mode == 0 || mode == 2) CK(hipMemcpyAsync(d1, h1, n, hipMemcpyHostToDevice, s1));
+            if (mode == 1 || mode == 2) CK(hipMemcpyAsync(h2, d2, n, hipMemcpyDeviceToHost, s2));
+            if (mode == 3)
+                for (size_t o = 0; o < n; o += piece) {
+                    CK(hipMemcpyAsync((char*)d1 + o, (char*)h1 + o, piece, hipMemcpyHostToDevice, s1));
+                    CK(hipMemcpyAsync((char*)h2 + o, (char*)d2 + o, piece, hipMemcpyDeviceToHost, s2));
+                }
+        }
+        CK(hipDeviceSynchronize());
+        const char* name[] = {"h2d alone", "d2h alone", "both, whole", "both, 16 MiB pieces"};
+        printf("%-20s %.1f GB/s per direction\n", name[mode], gbs(t, n * reps));
+    }
+    return 0;
+}
