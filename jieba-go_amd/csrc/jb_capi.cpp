@@ -19,6 +19,7 @@
 #include <string>
 #include <thread>
 #include <chrono>
+#include <condition_variable>
 #include <vector>
 
 #include "../../include/jiebahip.h"
@@ -1225,23 +1226,90 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         return JB_OK;
     };
     static const bool tdbg = getenv("JB_DEBUG") != nullptr;
-    const auto c0 = std::chrono::steady_clock::now();
-    if ((rc = stage(0))) return drain(rc);
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto c0 = now();
+    // Staging runs ahead on a thread of its own (every piece has its own pinned and device
+    // text region): it stages piece after piece and publishes how many are queued; piece k's
+    // kernels are queued once its copy is.  This thread meanwhile hands results back.
+    std::mutex smu;
+    std::condition_variable scv;
+    size_t staged = 0;
+    int src = JB_OK;
+    std::string serr;
+    bool stop = false;
+    double t_stage = 0;
+    std::thread stager([&] {
+        const auto a = now();
+        if (hipSetDevice(d->ordinal) != hipSuccess) {
+            std::lock_guard<std::mutex> l(smu);
+            src = fail(JB_EDEVICE, "hipSetDevice(%d) failed", d->ordinal);
+            serr = g_err;
+            scv.notify_all();
+            return;
+        }
+        for (size_t k = 0; k < np; k++) {
+            {
+                std::lock_guard<std::mutex> l(smu);
+                if (stop) break;
+            }
+            const int r = stage(k);
+            std::lock_guard<std::mutex> l(smu);
+            if (r) {
+                src = r;
+                serr = g_err;
+                scv.notify_all();
+                break;
+            }
+            staged = k + 1;
+            scv.notify_all();
+        }
+        t_stage = ms(a, now());
+    });
+    auto stop_stager = [&] {
+        {
+            std::lock_guard<std::mutex> l(smu);
+            stop = true;
+        }
+        stager.join();
+    };
+    auto wait_staged = [&](size_t k) -> int {
+        std::unique_lock<std::mutex> l(smu);
+        scv.wait(l, [&] { return staged > k || src != JB_OK; });
+        return staged > k ? JB_OK : fail(src, "%s", serr.c_str());
+    };
+    auto bail = [&](int code) {  // (after stop_stager: drain keeps g_err)
+        const std::string e = g_err;
+        stop_stager();
+        drain(code);
+        g_err = e;
+        return code;
+    };
+    double t_wait = 0, t_collect = 0, t_finish = 0;
+    auto timed = [&](double& acc, auto&& fn) {
+        const auto a = now();
+        const int r = fn();
+        acc += ms(a, now());
+        return r;
+    };
     for (size_t k = 0; k < np; k++) {
-        if ((rc = compute(k))) return drain(rc);
-        if (k + 1 < np && (rc = stage(k + 1))) return drain(rc);
-        if (k >= 1 && (rc = collect(k - 1))) return drain(rc);
-        if (k >= 2 && (rc = finish(k - 2))) return drain(rc);
+        if ((rc = timed(t_wait, [&] { return wait_staged(k); }))) return bail(rc);
+        if ((rc = compute(k))) return bail(rc);
+        if (k >= 1 && (rc = timed(t_collect, [&] { return collect(k - 1); }))) return bail(rc);
+        if (k >= 2 && (rc = timed(t_finish, [&] { return finish(k - 2); }))) return bail(rc);
     }
+    stop_stager();
     if ((rc = collect(np - 1))) return drain(rc);
     for (size_t k = np >= 2 ? np - 2 : 0; k < np; k++)
         if ((rc = finish(k))) return drain(rc);
     d->acc = acc;
     d->acc_valid = true;
     if (tdbg)
-        fprintf(stderr, "[jb] host range %.1f MiB (%s) in %zu pieces: %.2f ms\n", rbytes / 1048576.0,
-                mask ? "masks" : "spans", np,
-                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count());
+        fprintf(stderr, "[jb] host range %.1f MiB (%s%s) in %zu pieces: %.2f ms (staging thread %.2f; waits: staged %.2f, "
+                        "kernels %.2f, results %.2f)\n", rbytes / 1048576.0, mask ? "masks" : "spans",
+                pinned_in ? ", pinned input" : "", np, ms(c0, now()), t_stage, t_wait, t_collect, t_finish);
     return JB_OK;
 }
 

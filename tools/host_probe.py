@@ -70,6 +70,15 @@ def main():
             m = tk.cut_batch_mask(buf, off, True, m)
             dt = time.perf_counter() - t
             print(f"cut_batch_mask rep {r}: {dt * 1e3:.2f} ms, {nchars / dt / 1e9:.2f} G chars/s", flush=True)
+        hb = J.HostBuffer(len(buf))
+        hb.array[:] = buf
+        m = tk.cut_batch_mask(hb.array, off, True, m)
+        for r in range(3):
+            t = time.perf_counter()
+            m = tk.cut_batch_mask(hb.array, off, True, m)
+            dt = time.perf_counter() - t
+            print(f"cut_batch_mask pinned rep {r}: {dt * 1e3:.2f} ms, {nchars / dt / 1e9:.2f} G chars/s", flush=True)
+        hb.free()
     tk.close()
 
 
