@@ -154,6 +154,7 @@ struct Device {
     uint64_t* h_mask = nullptr;  // pinned copy
     uint64_t mask_cap = 0;       // u64 words of d_mask
     uint64_t mask_cap_h = 0;     // u64 words of h_mask
+    uint8_t* h_zero = nullptr;   // 64 pinned zero bytes
     uint2* h_ptile = nullptr;    // pinned per-tile (blocks, zh blocks) of every piece (jb_last_stats)
     uint64_t h_ptile_cap = 0;
     jb_stats acc{};              // counters summed over the pieces of the last host range
@@ -748,6 +749,8 @@ static int open_device(Device* d, int ordinal, const Image& img) {
     d->ncu = (uint32_t)prop.multiProcessorCount;
     HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&d->cstream, hipStreamNonBlocking));
+    HIPCHK(hipHostMalloc(&d->h_zero, 64, hipHostMallocDefault));
+    memset(d->h_zero, 0, 64);
     HIPCHK(hipStreamCreateWithFlags(&d->dstream, hipStreamNonBlocking));
     {
         // k_small runs one workgroup per call: pinned to one CU (JB_SMALL_CU, default 0) it
@@ -829,7 +832,7 @@ extern "C" void jb_close(jb_ctx* ctx) {
         if (d->ws_done) (void)hipEventDestroy(d->ws_done);
         hfree(d->h_text); hfree(d->h_misc); hfree(d->h_sin); hfree(d->h_sout);
         free_outs(d.get());
-        hfree(d->h_pcnt); dfree(d->d_mask); hfree(d->h_mask); hfree(d->h_ptile);
+        hfree(d->h_pcnt); dfree(d->d_mask); hfree(d->h_mask); hfree(d->h_ptile); hfree(d->h_zero);
         for (auto* v : {&d->ev_h2d, &d->ev_comp, &d->ev_d2h})
             for (hipEvent_t e : *v) (void)hipEventDestroy(e);
         if (d->cstream) (void)hipStreamDestroy(d->cstream);
@@ -1081,6 +1084,16 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
     };
     std::vector<uint32_t> ntok(np, 0);
     std::vector<std::pair<uint64_t, uint64_t>> words(np);  // mask words each piece copies back
+    static const bool tdbg2 = env_int("JB_DEBUG", 0) >= 2;  // per-piece event clocks
+    std::vector<hipEvent_t> tev;  // t0, then per piece: H2D done, kernels done, results back
+    auto tmark = [&](size_t i, hipStream_t st) {
+        if (tdbg2 && i < tev.size()) (void)hipEventRecord(tev[i], st);
+    };
+    if (tdbg2) {
+        tev.resize(1 + 3 * np);
+        for (auto& e : tev) (void)hipEventCreate(&e);
+        (void)hipEventRecord(tev[0], d->stream);
+    }
     uint64_t mask_done = 0;
 
     auto stage = [&](size_t k) -> int {
@@ -1090,8 +1103,10 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         HIPCHK(hipMemcpyAsync(d->doc_off + p.slot, d->h_misc + p.slot, (uint64_t)(p.d1 - p.d0 + 1) * 8,
                               hipMemcpyHostToDevice, d->cstream));
         if (pinned_in) {
+            // (the 64 zero bytes after the piece come from pinned zeros: a memset would be a
+            // kernel, queued behind the persistent k_zh for CUs, and the copies behind it)
             if (len) HIPCHK(hipMemcpyAsync(d->text + p.off, text + pb, len, hipMemcpyHostToDevice, d->cstream));
-            HIPCHK(hipMemsetAsync(d->text + p.off + len, 0, 64, d->cstream));
+            HIPCHK(hipMemcpyAsync(d->text + p.off + len, d->h_zero, 64, hipMemcpyHostToDevice, d->cstream));
         } else {
             // kCopyThreads threads stage their share in 4 MiB sub-pieces and queue each one's copy at once
             const uint64_t total = len + 64, kSub = 4ull << 20;
@@ -1114,6 +1129,7 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
             if (err) return fail(JB_EDEVICE, "H2D copy failed");
         }
         HIPCHK(hipEventRecord(d->ev_h2d[k], d->cstream));
+        tmark(1 + 3 * k, d->cstream);
         return JB_OK;
     };
     auto compute = [&](size_t k) -> int {
@@ -1142,6 +1158,7 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         if (nt_) HIPCHK(hipMemcpyAsync(d->h_ptile + p.tslot, d->w.tile_cnt, nt_ * sizeof(uint2), hipMemcpyDeviceToHost,
                                        d->stream));
         HIPCHK(hipEventRecord(d->ev_comp[k], d->stream));
+        tmark(2 + 3 * k, d->stream);
         return JB_OK;
     };
     auto collect = [&](size_t k) -> int {  // piece k's kernels are done: queue its results' copy back
@@ -1180,6 +1197,7 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
             words[k] = {lo, std::max(lo, hi)};
         }
         HIPCHK(hipEventRecord(d->ev_d2h[k], d->dstream));
+        tmark(3 + 3 * k, d->dstream);
         return JB_OK;
     };
     auto finish = [&](size_t k) -> int {  // piece k's results have landed: into the caller's arrays
@@ -1231,85 +1249,126 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         return std::chrono::duration<double, std::milli>(b - a).count();
     };
     const auto c0 = now();
-    // Staging runs ahead on a thread of its own (every piece has its own pinned and device
-    // text region): it stages piece after piece and publishes how many are queued; piece k's
-    // kernels are queued once its copy is.  This thread meanwhile hands results back.
-    std::mutex smu;
-    std::condition_variable scv;
-    size_t staged = 0;
-    int src = JB_OK;
-    std::string serr;
+    // Three threads: the stager stages piece after piece (every piece has its own pinned
+    // and device text region); the launcher queues piece k's kernels once its copy is
+    // queued (and, for spans, once the output set it reuses has been copied back); this
+    // thread hands results back in order.  Each publishes its progress under `pm`.
+    std::mutex pm;
+    std::condition_variable pcv;
+    size_t staged = 0, launched = 0, collected = 0;
+    int prc = JB_OK;
+    std::string perr;
     bool stop = false;
-    double t_stage = 0;
+    double t_stage = 0, t_launch = 0;
+    auto publish = [&](size_t* ctr, size_t v, int r) {
+        std::lock_guard<std::mutex> l(pm);
+        if (r && prc == JB_OK) {
+            prc = r;
+            perr = g_err;
+        }
+        if (!r) *ctr = v;
+        pcv.notify_all();
+    };
+    auto wait_for = [&](const size_t* ctr, size_t v) -> bool {  // false: an error or stop
+        std::unique_lock<std::mutex> l(pm);
+        pcv.wait(l, [&] { return *ctr >= v || prc != JB_OK || stop; });
+        return *ctr >= v;
+    };
     std::thread stager([&] {
         const auto a = now();
         if (hipSetDevice(d->ordinal) != hipSuccess) {
-            std::lock_guard<std::mutex> l(smu);
-            src = fail(JB_EDEVICE, "hipSetDevice(%d) failed", d->ordinal);
-            serr = g_err;
-            scv.notify_all();
+            publish(&staged, 0, fail(JB_EDEVICE, "hipSetDevice(%d) failed", d->ordinal));
             return;
         }
         for (size_t k = 0; k < np; k++) {
             {
-                std::lock_guard<std::mutex> l(smu);
-                if (stop) break;
+                std::lock_guard<std::mutex> l(pm);
+                if (stop || prc) break;
             }
             const int r = stage(k);
-            std::lock_guard<std::mutex> l(smu);
-            if (r) {
-                src = r;
-                serr = g_err;
-                scv.notify_all();
-                break;
-            }
-            staged = k + 1;
-            scv.notify_all();
+            publish(&staged, k + 1, r);
+            if (r) break;
         }
         t_stage = ms(a, now());
     });
-    auto stop_stager = [&] {
+    std::thread launcher([&] {
+        const auto a = now();
+        if (hipSetDevice(d->ordinal) != hipSuccess) {
+            publish(&launched, 0, fail(JB_EDEVICE, "hipSetDevice(%d) failed", d->ordinal));
+            return;
+        }
+        for (size_t k = 0; k < np; k++) {
+            if (!wait_for(&staged, k + 1)) break;
+            if (!mask && k >= (size_t)Device::kSets && !wait_for(&collected, k - Device::kSets + 1)) break;
+            const int r = compute(k);
+            publish(&launched, k + 1, r);
+            if (r) break;
+        }
+        t_launch = ms(a, now());
+    });
+    auto stop_threads = [&] {
         {
-            std::lock_guard<std::mutex> l(smu);
+            std::lock_guard<std::mutex> l(pm);
             stop = true;
         }
+        pcv.notify_all();
         stager.join();
+        launcher.join();
     };
-    auto wait_staged = [&](size_t k) -> int {
-        std::unique_lock<std::mutex> l(smu);
-        scv.wait(l, [&] { return staged > k || src != JB_OK; });
-        return staged > k ? JB_OK : fail(src, "%s", serr.c_str());
-    };
-    auto bail = [&](int code) {  // (after stop_stager: drain keeps g_err)
-        const std::string e = g_err;
-        stop_stager();
+    auto bail = [&](int code, const std::string& msg) {  // stop the other threads, drain, keep the message
+        stop_threads();
         drain(code);
-        g_err = e;
+        g_err = msg;
         return code;
     };
     double t_wait = 0, t_collect = 0, t_finish = 0;
-    auto timed = [&](double& acc, auto&& fn) {
+    auto timed = [&](double& accm, auto&& fn) {
         const auto a = now();
         const int r = fn();
-        acc += ms(a, now());
+        accm += ms(a, now());
         return r;
     };
     for (size_t k = 0; k < np; k++) {
-        if ((rc = timed(t_wait, [&] { return wait_staged(k); }))) return bail(rc);
-        if ((rc = compute(k))) return bail(rc);
-        if (k >= 1 && (rc = timed(t_collect, [&] { return collect(k - 1); }))) return bail(rc);
-        if (k >= 2 && (rc = timed(t_finish, [&] { return finish(k - 2); }))) return bail(rc);
+        {
+            const auto a = now();
+            const bool ok = wait_for(&launched, k + 1);
+            t_wait += ms(a, now());
+            if (!ok) {
+                int code;
+                std::string msg;
+                {
+                    std::lock_guard<std::mutex> l(pm);
+                    code = prc ? prc : JB_EDEVICE;
+                    msg = prc ? perr : "host pipeline stopped";
+                }
+                return bail(code, msg);
+            }
+        }
+        if ((rc = timed(t_collect, [&] { return collect(k); }))) return bail(rc, g_err);
+        publish(&collected, k + 1, JB_OK);
+        if (k >= 1 && (rc = timed(t_finish, [&] { return finish(k - 1); }))) return bail(rc, g_err);
     }
-    stop_stager();
-    if ((rc = collect(np - 1))) return drain(rc);
-    for (size_t k = np >= 2 ? np - 2 : 0; k < np; k++)
-        if ((rc = finish(k))) return drain(rc);
+    stop_threads();
+    if ((rc = finish(np - 1))) return drain(rc);
     d->acc = acc;
     d->acc_valid = true;
+    if (tdbg2) {
+        (void)hipDeviceSynchronize();
+        fprintf(stderr, "[jb] piece: H2D done / kernels done / results back (ms from the start)\n");
+        for (size_t k = 0; k < np; k++) {
+            float a = 0, b = 0, c = 0;
+            (void)hipEventElapsedTime(&a, tev[0], tev[1 + 3 * k]);
+            (void)hipEventElapsedTime(&b, tev[0], tev[2 + 3 * k]);
+            (void)hipEventElapsedTime(&c, tev[0], tev[3 + 3 * k]);
+            fprintf(stderr, "[jb]   %2zu: %7.2f %7.2f %7.2f\n", k, a, b, c);
+        }
+        for (auto& e : tev) (void)hipEventDestroy(e);
+    }
     if (tdbg)
-        fprintf(stderr, "[jb] host range %.1f MiB (%s%s) in %zu pieces: %.2f ms (staging thread %.2f; waits: staged %.2f, "
-                        "kernels %.2f, results %.2f)\n", rbytes / 1048576.0, mask ? "masks" : "spans",
-                pinned_in ? ", pinned input" : "", np, ms(c0, now()), t_stage, t_wait, t_collect, t_finish);
+        fprintf(stderr, "[jb] host range %.1f MiB (%s%s) in %zu pieces: %.2f ms (stager %.2f, launcher %.2f; here: "
+                        "waits for launches %.2f, kernels %.2f, results %.2f)\n", rbytes / 1048576.0,
+                mask ? "masks" : "spans", pinned_in ? ", pinned input" : "", np, ms(c0, now()), t_stage, t_launch,
+                t_wait, t_collect, t_finish);
     return JB_OK;
 }
 

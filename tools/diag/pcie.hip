@@ -4,6 +4,14 @@
 #include <stdio.h>
 #include <chrono>
 
+// a kernel that keeps every CU busy for about `cycles` clocks
+__global__ void spin(unsigned long long cycles, int* sink) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    int x = threadIdx.x;
+    while (__builtin_amdgcn_s_memtime() - t0 < cycles) x = x * 1664525 + 1013904223;
+    if (x == 0x7fffffff) sink[0] = x;
+}
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
 int main() {
@@ -37,6 +45,21 @@ int main() {
         CK(hipDeviceSynchronize());
         const char* name[] = {"h2d alone", "d2h alone", "both, whole", "both, 16 MiB pieces"};
         printf("%-20s %.1f GB/s per direction\n", name[mode], gbs(t, n * reps));
+    }
+    // H2D while a kernel holds every CU (the pipeline's persistent k_zh does): is the copy an SDMA
+    // transfer that runs beside it, or a blit kernel that waits for CUs?
+    int* sink;
+    CK(hipMalloc(&sink, 4));
+    hipStream_t s3;
+    CK(hipStreamCreateWithFlags(&s3, hipStreamNonBlocking));
+    for (int withk = 0; withk < 2; withk++) {
+        CK(hipDeviceSynchronize());
+        if (withk) hipLaunchKernelGGL(spin, dim3(256 * 8), dim3(256), 0, s3, 100000000ull, sink);  // ~45 ms
+        auto t = now();
+        for (int r = 0; r < reps; r++) CK(hipMemcpyAsync(d1, h1, n, hipMemcpyHostToDevice, s1));
+        CK(hipStreamSynchronize(s1));
+        printf("h2d %s: %.1f GB/s\n", withk ? "beside a kernel on every CU" : "alone", gbs(t, n * reps));
+        CK(hipDeviceSynchronize());
     }
     return 0;
 }

@@ -8,7 +8,7 @@ import sys
 import tempfile
 import time
 
-os.environ["JB_DEBUG"] = "1"
+os.environ.setdefault("JB_DEBUG", "1")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for sub in ("oracle", "gen", os.path.join("jieba-go_amd", "python")):
     sys.path.insert(0, os.path.join(ROOT, sub))
