@@ -1028,9 +1028,19 @@ __device__ __forceinline__ void dp_walk_rune(const V& v, const DevImage& im, uin
 // index fields of absent edges are 0 in every record k_mark_walk writes (its
 // shift register starts at 0), so no select is needed.
 __device__ __forceinline__ void rec_weights(const DevImage& im, uint64_t rc, double w[4]) {
+#if JB_X_BUFW
+    // buffer loads: a 32-bit byte offset per lane against a descriptor of wtab (no 64-bit address math)
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)im.wtab, 0, 0x7FFFFFF0, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t off = ((uint32_t)(rc >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u)) << 3;
+        w[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, 0, 0));
+    }
+#else
 #pragma unroll
     for (int k = 0; k < 4; k++)
         w[k] = im.wtab[(uint32_t)(rc >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u)];
+#endif
 }
 // Fold a record's edges (L <= kZhRing, so best(i+L) is in the ring or is the
 // sentinel), branch-free: every LDS read is issued and the items are selected.

@@ -166,9 +166,11 @@ func (t *Tokenizer) Cut(text string, useHmm bool) []string {
 	return spansToTokens(text, &s, 0)
 }
 
-// CutParallel (tokenizer.go:81) returns the tokens of Cut in document order;
-// the device splits the work itself, numWorkers is accepted for API parity.
-// ordered=false allows any block order in the reference; this order is one of them.
+// CutParallel (tokenizer.go:81) returns the tokens of Cut in document order.
+// The library splits the work itself: the text goes to the device in pieces cut
+// at Han-run starts (jb_split_points), and over every device of a multi-device
+// context; numWorkers is accepted for API parity.  ordered=false allows any block
+// order in the reference; this order is one of them.
 func (t *Tokenizer) CutParallel(text string, hmm bool, numWorkers int, ordered bool) []string {
 	return t.Cut(text, hmm)
 }
