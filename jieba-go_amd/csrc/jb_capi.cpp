@@ -148,15 +148,14 @@ struct Device {
         uint64_t hcap_tok = 0;
         uint32_t hcap_docs = 0;
     } outs[kSets];
-    uint32_t* h_pcnt = nullptr;  // pinned counters, kPieceCnt u32 per piece
+    uint32_t* h_pcnt = nullptr;  // mapped pinned: kSnapWords u32 per piece (k_snap writes them)
+    uint32_t* d_pcnt = nullptr;  // its device address
     uint64_t h_pcnt_cap = 0;
     uint64_t* d_mask = nullptr;  // boundary masks of a range: starts then ends (u64 words)
     uint64_t* h_mask = nullptr;  // pinned copy
     uint64_t mask_cap = 0;       // u64 words of d_mask
     uint64_t mask_cap_h = 0;     // u64 words of h_mask
     uint8_t* h_zero = nullptr;   // 64 pinned zero bytes
-    uint2* h_ptile = nullptr;    // pinned per-tile (blocks, zh blocks) of every piece (jb_last_stats)
-    uint64_t h_ptile_cap = 0;
     jb_stats acc{};              // counters summed over the pieces of the last host range
     bool acc_valid = false;      // the last run was such a range
     // k_small's pinned, mapped host buffers (coherent: the kernel reads and writes them directly)
@@ -579,6 +578,20 @@ static int grow_pinned(T** p, uint64_t* cap, uint64_t want) {
     return JB_OK;
 }
 
+// grow-only mapped (device-visible), coherent pinned memory: kernels write it directly
+template <class T>
+static int grow_mapped(T** p, T** dp, uint64_t* cap, uint64_t want) {
+    if (want <= *cap && *p) return JB_OK;
+    const uint64_t c = std::max<uint64_t>(want, *cap * 3 / 2 + 1);
+    hfree(*p);
+    *p = *dp = nullptr;
+    *cap = 0;
+    HIPCHK(hipHostMalloc(p, c * sizeof(T), hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void**)dp, *p, 0));
+    *cap = c;
+    return JB_OK;
+}
+
 static void free_outs(Device* d) {
     for (auto& o : d->outs) {
         dfree(o.ts); dfree(o.te); dfree(o.dt); hfree(o.hs); hfree(o.hdt);
@@ -832,7 +845,7 @@ extern "C" void jb_close(jb_ctx* ctx) {
         if (d->ws_done) (void)hipEventDestroy(d->ws_done);
         hfree(d->h_text); hfree(d->h_misc); hfree(d->h_sin); hfree(d->h_sout);
         free_outs(d.get());
-        hfree(d->h_pcnt); dfree(d->d_mask); hfree(d->h_mask); hfree(d->h_ptile); hfree(d->h_zero);
+        hfree(d->h_pcnt); dfree(d->d_mask); hfree(d->h_mask); hfree(d->h_zero);
         for (auto* v : {&d->ev_h2d, &d->ev_comp, &d->ev_d2h})
             for (hipEvent_t e : *v) (void)hipEventDestroy(e);
         if (d->cstream) (void)hipStreamDestroy(d->cstream);
@@ -985,7 +998,6 @@ static bool host_pinned(const void* p, uint64_t n) {
     return false;
 }
 
-constexpr uint32_t kPieceCnt = 16;  // counters copied back per piece (u32)
 
 // Cut documents [d0, d1) of a host batch on one device: appends spans to `out`, or
 // with `mask` writes the range's boundary bits into the caller's masks (out->n counts
@@ -1029,19 +1041,17 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         return JB_OK;
     }
     const uint64_t kPiece = d->piece_bytes;
-    // documents, device text offset, offsets slot, tile-count slot
-    struct Piece { uint32_t d0, d1; uint64_t off, slot, tslot; };
+    struct Piece { uint32_t d0, d1; uint64_t off, slot; };  // documents, device text offset, offsets slot
     std::vector<Piece> pcs;
-    uint64_t dev_bytes = 0, slots = 0, tslots = 0, maxb = 0;
+    uint64_t dev_bytes = 0, slots = 0, maxb = 0;
     uint32_t maxd = 0;
     for (uint32_t a = d0; a < d1;) {
         uint32_t b = a + 1;
         while (b < d1 && doc_off[b + 1] - doc_off[a] <= kPiece) b++;
         const uint64_t len = doc_off[b] - doc_off[a];
-        pcs.push_back(Piece{a, b, dev_bytes, slots, tslots});
+        pcs.push_back(Piece{a, b, dev_bytes, slots});
         dev_bytes += (len + 64 + 255) & ~255ull;  // 64 zero bytes after each piece, 256-byte aligned starts
         slots += b - a + 1;
-        tslots += (len + kTileBytes - 1) / kTileBytes;
         maxb = std::max(maxb, len);
         maxd = std::max(maxd, b - a);
         a = b;
@@ -1050,8 +1060,7 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
     const bool pinned_in = host_pinned(text + r0, rbytes);
     if ((rc = grow_dev(&d->text, &d->text_cap, dev_bytes)) || (rc = grow_dev(&d->doc_off, &d->doc_cap, slots)) ||
         (rc = grow_pinned(&d->h_misc, &d->h_misc_cap, slots)) ||
-        (rc = grow_pinned(&d->h_pcnt, &d->h_pcnt_cap, (uint64_t)np * kPieceCnt)) ||
-        (rc = grow_pinned(&d->h_ptile, &d->h_ptile_cap, tslots + 1)) ||
+        (rc = grow_mapped(&d->h_pcnt, &d->d_pcnt, &d->h_pcnt_cap, (uint64_t)np * kSnapWords)) ||
         (!pinned_in && (rc = grow_pinned(&d->h_text, &d->h_text_cap, dev_bytes))) ||
         (rc = ensure_work(d, maxb, maxd)))
         return rc;
@@ -1072,7 +1081,7 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
     } else {
         if ((rc = grow_dev(&d->d_mask, &d->mask_cap, 2 * nw)) || (rc = grow_pinned(&d->h_mask, &d->mask_cap_h, 2 * nw)))
             return rc;
-        HIPCHK(hipMemsetAsync(d->d_mask, 0, 2 * nw * 8, d->stream));
+        HIPCHK(run_zero(d->d_mask, 2 * nw * 8, d->stream));
     }
     d->last_small = false;
     jb_stats acc{};
@@ -1152,11 +1161,10 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
                         mask ? &mo : nullptr)))
             return r;
         d->last_nbytes = len;
-        HIPCHK(hipMemcpyAsync(d->h_pcnt + k * kPieceCnt, d->w.counters, kPieceCnt * 4, hipMemcpyDeviceToHost,
-                              d->stream));
-        const uint64_t nt_ = (len + kTileBytes - 1) / kTileBytes;  // (k_mark_walk's block counts, jb_last_stats)
-        if (nt_) HIPCHK(hipMemcpyAsync(d->h_ptile + p.tslot, d->w.tile_cnt, nt_ * sizeof(uint2), hipMemcpyDeviceToHost,
-                                       d->stream));
+        // counters and block counts by a kernel into mapped memory: a copy-engine transfer here
+        // would queue behind the bulk copies of later pieces and hold up this stream
+        const hipError_t es = run_snap(d->w, len, d->d_pcnt + k * kSnapWords, d->stream);
+        if (es != hipSuccess) return fail(JB_EDEVICE, "k_snap: %s", hipGetErrorString(es));
         HIPCHK(hipEventRecord(d->ev_comp[k], d->stream));
         tmark(2 + 3 * k, d->stream);
         return JB_OK;
@@ -1164,7 +1172,7 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
     auto collect = [&](size_t k) -> int {  // piece k's kernels are done: queue its results' copy back
         const Piece& p = pcs[k];
         HIPCHK(hipEventSynchronize(d->ev_comp[k]));
-        const uint32_t* c = d->h_pcnt + k * kPieceCnt;
+        const volatile uint32_t* c = d->h_pcnt + k * kSnapWords;
         if (c[CNT_ERR]) return fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)");
         if (c[CNT_NTOK] != c[CNT_NTOKE])
             return fail(JB_EDEVICE, "internal: %u token starts vs %u ends", c[CNT_NTOK], c[CNT_NTOKE]);
@@ -1205,15 +1213,12 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         HIPCHK(hipEventSynchronize(d->ev_d2h[k]));
         const uint32_t nt = ntok[k];
         {
-            const uint32_t* c = d->h_pcnt + k * kPieceCnt;
+            const volatile uint32_t* c = d->h_pcnt + k * kSnapWords;
             acc.tokens += nt;
             acc.long_blocks += c[CNT_NLONG];
             acc.viterbi_ties += c[CNT_TIES];
-            const uint64_t nt_ = (doc_off[p.d1] - doc_off[p.d0] + kTileBytes - 1) / kTileBytes;
-            for (uint64_t i = 0; i < nt_; i++) {
-                acc.blocks += d->h_ptile[p.tslot + i].x;
-                acc.zh_blocks += d->h_ptile[p.tslot + i].y;
-            }
+            acc.blocks += (uint64_t)c[CNT_CLEAR] | (uint64_t)c[CNT_CLEAR + 1] << 32;
+            acc.zh_blocks += (uint64_t)c[CNT_CLEAR + 2] | (uint64_t)c[CNT_CLEAR + 3] << 32;
         }
         if (mask) {
             put_mask_words(mask, rw, nw, words[k].first, words[k].second, d->h_mask, d->h_mask + nw);
@@ -1274,6 +1279,7 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         pcv.wait(l, [&] { return *ctr >= v || prc != JB_OK || stop; });
         return *ctr >= v;
     };
+    constexpr size_t kAhead = 3;
     std::thread stager([&] {
         const auto a = now();
         if (hipSetDevice(d->ordinal) != hipSuccess) {
@@ -1285,6 +1291,10 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
                 std::lock_guard<std::mutex> l(pm);
                 if (stop || prc) break;
             }
+            // at most kAhead pieces' copies queued beyond the last piece whose kernels are done: a
+            // deeper queue of bulk copies (pinned input queues all of them at once) delayed the
+            // first pieces' kernels by 13 ms, everything on the device waiting behind the copies
+            if (k >= kAhead && !wait_for(&collected, k - kAhead + 1)) break;
             const int r = stage(k);
             publish(&staged, k + 1, r);
             if (r) break;

@@ -145,6 +145,14 @@ hipError_t run_small(const DevImage& im, const uint8_t* text, uint32_t nbytes, c
                      uint32_t ndocs, bool hmm, uint32_t* out, uint32_t seq, const SmallInline& in,
                      hipStream_t stream);
 
+// After a pipeline run on `stream`: its counters (u32[CNT_CLEAR]) and the summed
+// (blocks, zh blocks) of its tiles (two u64 after them) into `out`, mapped pinned
+// host memory of kSnapWords u32, by a one-workgroup kernel.
+constexpr uint32_t kSnapWords = CNT_CLEAR + 4;
+// Zero `bytes` (a multiple of 4) at p with a kernel on `stream`.
+hipError_t run_zero(void* p, uint64_t bytes, hipStream_t stream);
+hipError_t run_snap(const Work& w, uint64_t nbytes, uint32_t* out, hipStream_t stream);
+
 // Resident k_zh workgroups per CU (occupancy API).
 uint32_t zh_blocks_per_cu(bool hmm);
 

@@ -31,6 +31,8 @@
 
 #include "jb_kernels.h"
 
+#include <algorithm>
+
 #ifndef JB_STAMPS
 #define JB_STAMPS 0
 #endif
@@ -1028,19 +1030,9 @@ __device__ __forceinline__ void dp_walk_rune(const V& v, const DevImage& im, uin
 // index fields of absent edges are 0 in every record k_mark_walk writes (its
 // shift register starts at 0), so no select is needed.
 __device__ __forceinline__ void rec_weights(const DevImage& im, uint64_t rc, double w[4]) {
-#if JB_X_BUFW
-    // buffer loads: a 32-bit byte offset per lane against a descriptor of wtab (no 64-bit address math)
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)im.wtab, 0, 0x7FFFFFF0, 0x00020000);
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t off = ((uint32_t)(rc >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u)) << 3;
-        w[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, 0, 0));
-    }
-#else
 #pragma unroll
     for (int k = 0; k < 4; k++)
         w[k] = im.wtab[(uint32_t)(rc >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u)];
-#endif
 }
 // Fold a record's edges (L <= kZhRing, so best(i+L) is in the ring or is the
 // sentinel), branch-free: every LDS read is issued and the items are selected.
@@ -2638,20 +2630,84 @@ __global__ void k_doc_tok(const uint64_t* __restrict__ doc_off, uint32_t ndocs, 
 // and last) is ORed in, the others stored.  Pieces of one range run in order on one
 // stream over bitmaps cleared at the start.  Counts the piece's token starts and
 // ends into the counters (the spans kernels do not run in this mode).
+// A pipeline run's counters and summed tile block counts, written straight into
+// mapped pinned host memory (cut_range: no copy-engine transfer on the kernels'
+// stream, where it would queue behind the bulk copies of later pieces).
+// out: u32[kSnapWords]: counters[0..CNT_CLEAR), then u64 blocks, u64 zh blocks.
+__global__ __launch_bounds__(256) void k_snap(const uint32_t* __restrict__ counters, const uint2* __restrict__ tile_cnt,
+                                              uint32_t ntiles, uint32_t* __restrict__ out) {
+    __shared__ unsigned long long red[8];
+    unsigned long long b = 0, z = 0;
+    for (uint32_t t = threadIdx.x; t < ntiles; t += 256u) {
+        const uint2 c = tile_cnt[t];
+        b += c.x;
+        z += c.y;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        b += (unsigned long long)__shfl_xor((long long)b, d, 64);
+        z += (unsigned long long)__shfl_xor((long long)z, d, 64);
+    }
+    if ((threadIdx.x & 63u) == 0) {
+        red[threadIdx.x >> 6] = b;
+        red[4 + (threadIdx.x >> 6)] = z;
+    }
+    __syncthreads();
+    if (threadIdx.x < CNT_CLEAR) out[threadIdx.x] = counters[threadIdx.x];
+    if (threadIdx.x == 0) {
+        const unsigned long long bs = red[0] + red[1] + red[2] + red[3], zs = red[4] + red[5] + red[6] + red[7];
+        out[CNT_CLEAR] = (uint32_t)bs;
+        out[CNT_CLEAR + 1] = (uint32_t)(bs >> 32);
+        out[CNT_CLEAR + 2] = (uint32_t)zs;
+        out[CNT_CLEAR + 3] = (uint32_t)(zs >> 32);
+    }
+    __threadfence_system();
+}
+
+// Zero n u32 words (instead of hipMemsetAsync, which may go to the copy engine and
+// queue there behind the host pipeline's bulk transfers).
+__global__ __launch_bounds__(256) void k_zero(uint32_t* __restrict__ p, uint64_t n, bool v4) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256u, t0 = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint64_t n4 = v4 ? n / 4u : 0u;
+    uint4* p4 = reinterpret_cast<uint4*>(p);
+    for (uint64_t i = t0; i < n4; i += stride) p4[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (uint64_t i = 4u * n4 + t0; i < n; i += stride) p[i] = 0u;
+}
+
+hipError_t run_zero(void* p, uint64_t bytes, hipStream_t stream) {
+    const uint64_t n = bytes / 4u;  // (callers pass whole words)
+    if (!n) return hipSuccess;
+    const bool v4 = ((uintptr_t)p & 15u) == 0;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(2048u, (n / 4u + 255u) / 256u + 1u);
+    hipLaunchKernelGGL(k_zero, dim3(grid), dim3(256), 0, stream, reinterpret_cast<uint32_t*>(p), n, v4);
+    return hipGetLastError();
+}
+
+hipError_t run_snap(const Work& w, uint64_t nbytes, uint32_t* out, hipStream_t stream) {
+    const uint32_t ntiles = (uint32_t)((nbytes + kTileBytes - 1) / kTileBytes);
+    hipLaunchKernelGGL(k_snap, dim3(1), dim3(256), 0, stream, w.counters, w.tile_cnt, ntiles, out);
+    return hipGetLastError();
+}
+
+constexpr uint32_t kMergeWords = 16;  // k_mask_merge: output words per thread
 __global__ __launch_bounds__(256) void k_mask_merge(const uint32_t* __restrict__ sbits,
                                                     const uint32_t* __restrict__ ebits, uint64_t n, uint64_t rel,
                                                     uint64_t* __restrict__ ms, uint64_t* __restrict__ me,
                                                     uint32_t* __restrict__ counters) {
+    __shared__ uint32_t red[8];
     const uint32_t sh = (uint32_t)(rel & 63u);
     const uint64_t nout = (sh + n + 63u) >> 6, nw32 = (n + 31u) >> 5;
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    auto piece64 = [&](const uint32_t* b, int64_t i) -> uint64_t {  // piece bits [64i, 64i + 64)
+        if (i < 0) return 0ull;
+        const uint64_t lo = 2u * (uint64_t)i, hi = lo + 1u;
+        return (lo < nw32 ? (uint64_t)b[lo] : 0ull) | ((hi < nw32 ? (uint64_t)b[hi] : 0ull) << 32);
+    };
     uint32_t cs = 0, ce = 0;
-    if (t < nout) {
-        auto piece64 = [&](const uint32_t* b, int64_t i) -> uint64_t {  // piece bits [64i, 64i + 64)
-            if (i < 0) return 0ull;
-            const uint64_t lo = 2u * (uint64_t)i, hi = lo + 1u;
-            return (lo < nw32 ? (uint64_t)b[lo] : 0ull) | ((hi < nw32 ? (uint64_t)b[hi] : 0ull) << 32);
-        };
+    const uint64_t t0 = (uint64_t)blockIdx.x * (256u * kMergeWords) + threadIdx.x;
+#pragma unroll 4
+    for (uint32_t j = 0; j < kMergeWords; j++) {
+        const uint64_t t = t0 + 256u * j;  // (consecutive threads: consecutive words)
+        if (t >= nout) break;
         uint64_t os = piece64(sbits, (int64_t)t), oe = piece64(ebits, (int64_t)t);
         if (sh) {
             os = (os << sh) | (piece64(sbits, (int64_t)t - 1) >> (64u - sh));
@@ -2665,18 +2721,29 @@ __global__ __launch_bounds__(256) void k_mask_merge(const uint32_t* __restrict__
             ms[w] = os;
             me[w] = oe;
         }
-        cs = (uint32_t)__popcll(os);
-        ce = (uint32_t)__popcll(oe);
+        cs += (uint32_t)__popcll(os);
+        ce += (uint32_t)__popcll(oe);
     }
+    // one set of counter atomics per workgroup (one per wave serialised on three addresses)
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         cs += (uint32_t)__shfl_xor((int)cs, d, 64);
         ce += (uint32_t)__shfl_xor((int)ce, d, 64);
     }
-    if ((threadIdx.x & 63u) == 0 && (cs | ce)) {
-        atomicAdd(counters + CNT_NTOK, cs);
-        atomicAdd(counters + CNT_NTOKE, ce);
-        atomicAdd(reinterpret_cast<unsigned long long*>(counters + CNT_NWORDS), (unsigned long long)cs);
+    const uint32_t wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 0) {
+        red[wv] = cs;
+        red[4 + wv] = ce;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        cs = red[0] + red[1] + red[2] + red[3];
+        ce = red[4] + red[5] + red[6] + red[7];
+        if (cs | ce) {
+            atomicAdd(counters + CNT_NTOK, cs);
+            atomicAdd(counters + CNT_NTOKE, ce);
+            atomicAdd(reinterpret_cast<unsigned long long*>(counters + CNT_NWORDS), (unsigned long long)cs);
+        }
     }
 }
 
@@ -3230,11 +3297,11 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     const uint64_t ngroups = (nbytes + grp - 1) / grp;
     const uint32_t grid_zh = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(lc.grid_zh, (ngroups + 3) / 4));
     hipError_t e;
-    if ((e = hipMemsetAsync(w.counters, 0, CNT_CLEAR * sizeof(uint32_t), stream))) return e;
-    // (k_mark_walk clears the token bitmaps tile by tile)
-    if ((e = hipMemsetAsync(w.docbits, 0, (nwords + 2) * 4, stream))) return e;
+    // (kernels, not hipMemsetAsync: see k_zero; k_mark_walk clears the token bitmaps tile by tile)
+    if ((e = run_zero(w.counters, CNT_CLEAR * sizeof(uint32_t), stream))) return e;
+    if ((e = run_zero(w.docbits, (nwords + 2) * 4, stream))) return e;
     if (nbytes == 0) {
-        if ((e = hipMemsetAsync(w.doc_tok, 0, (ndocs + 1) * sizeof(uint64_t), stream))) return e;
+        if ((e = run_zero(w.doc_tok, (ndocs + 1) * sizeof(uint64_t), stream))) return e;
         return hipSuccess;
     }
     if (ndocs)
@@ -3286,7 +3353,9 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     }
     if (mask) {  // boundary masks instead of spans
         const uint64_t nout = ((mask->rel & 63u) + nbytes + 63u) >> 6;
-        JB_TIMED(K_MASK_MERGE, hipLaunchKernelGGL(k_mask_merge, dim3((uint32_t)((nout + 255u) / 256u)), dim3(256), 0,
+        JB_TIMED(K_MASK_MERGE, hipLaunchKernelGGL(k_mask_merge,
+                                                  dim3((uint32_t)((nout + 256u * kMergeWords - 1u) / (256u * kMergeWords))),
+                                                  dim3(256), 0,
                                                   stream, w.sbits, w.ebits, nbytes, mask->rel, mask->s, mask->e,
                                                   w.counters));
         return hipGetLastError();

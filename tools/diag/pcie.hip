@@ -12,6 +12,12 @@ __global__ void spin(unsigned long long cycles, int* sink) {
     if (x == 0x7fffffff) sink[0] = x;
 }
 
+// copy device -> mapped pinned host memory with vector stores (a D2H that is not a copy-engine transfer)
+__global__ void kcopy(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
 int main() {
@@ -60,6 +66,24 @@ int main() {
         CK(hipStreamSynchronize(s1));
         printf("h2d %s: %.1f GB/s\n", withk ? "beside a kernel on every CU" : "alone", gbs(t, n * reps));
         CK(hipDeviceSynchronize());
+    }
+    // D2H by a kernel's stores into mapped pinned memory, alone and beside an SDMA H2D
+    void* hm;
+    uint4* dm;
+    CK(hipHostMalloc(&hm, n, hipHostMallocMapped | hipHostMallocCoherent));
+    CK(hipHostGetDevicePointer((void**)&dm, hm, 0));
+    for (int both = 0; both < 2; both++) {
+        for (int grid : {64, 256, 1024}) {
+            CK(hipDeviceSynchronize());
+            auto t = now();
+            for (int r = 0; r < reps; r++) {
+                if (both) CK(hipMemcpyAsync(d1, h1, n, hipMemcpyHostToDevice, s1));
+                hipLaunchKernelGGL(kcopy, dim3(grid), dim3(256), 0, s2, (const uint4*)d2, dm, n / 16);
+            }
+            CK(hipDeviceSynchronize());
+            printf("kernel-store d2h, grid %d%s: %.1f GB/s per direction\n", grid, both ? ", beside SDMA h2d" : "",
+                   gbs(t, n * reps));
+        }
     }
     return 0;
 }

@@ -79,6 +79,24 @@ def main():
             dt = time.perf_counter() - t
             print(f"cut_batch_mask pinned rep {r}: {dt * 1e3:.2f} ms, {nchars / dt / 1e9:.2f} G chars/s", flush=True)
         hb.free()
+    # per-kernel times: the host path (one call, masks) against the device-resident path on the same batch
+    import torch
+    nb = int(off[-1])
+    tk.profile(True)
+    tk.profile_reset()
+    tk.cut_batch_mask(buf, off, True, m)
+    host_k = tk.profile_read()
+    tk.profile_reset()
+    d_text = torch.from_numpy(np.asarray(buf[: nb + 64])).cuda()
+    d_off = torch.from_numpy(np.asarray(off, np.int64)).cuda()
+    for _ in range(2):
+        tk.cut_device(d_text.data_ptr(), nb, d_off.data_ptr(), len(off) - 1, True, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    dev_k = tk.profile_read()
+    for k in host_k:
+        if host_k[k][1] or dev_k[k][1]:
+            print(f"  {k:14s} host path {host_k[k][0]:8.3f} ms / {host_k[k][1]} launches   device path "
+                  f"{dev_k[k][0] / max(1, dev_k[k][1]) * (host_k[k][1] and 1):8.3f} ms per launch", flush=True)
     tk.close()
 
 
