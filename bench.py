@@ -382,12 +382,12 @@ def run(args, world, rank, dist, agg_dev, make_cutter, open_oracle, log=print):
 
 
 def end_to_end(tk, buf, off, hmm, nrunes, reps=3):
-    """The host-memory paths a drop-in caller gets (never `value`): the batch in host
-    memory, text pieces copied up while earlier pieces are cut and their results come
-    back (three streams).  `value`: jb_cut_batch_into (u64 spans into caller arrays)
-    from pageable memory; `masks`: jb_cut_batch_mask (2 bits per byte); `masks_pinned`:
-    the same with the text in jb_host_alloc memory (no staging copy).  Each checked
-    against the spans of the device-resident run it follows."""
+    """The host-memory paths a drop-in caller gets (never the line's `value`): the batch
+    in host memory, text pieces copied up while earlier pieces are cut and their
+    results come back (three streams).  `value`: jb_cut_batch_mask (2 bits per byte)
+    from pageable memory; `spans`: jb_cut_batch_into (u64 spans into caller arrays);
+    `masks_pinned`: masks with the text in jb_host_alloc memory (no staging copy).
+    The masks are checked against the spans."""
     import jiebahip as J
 
     def timed(fn):
@@ -413,11 +413,14 @@ def end_to_end(tk, buf, off, hmm, nrunes, reps=3):
 
     def rate(sec):
         return {"value": round(nrunes / sec, 1), "unit": "chars/s", "ms": round(sec * 1e3, 2)}
-    out = rate(s_sp)
-    out["what"] = ("jb_cut_batch_into from pageable host memory: pieces of 64 MiB staged into pinned memory and "
-                   "copied up while earlier pieces are cut, u32 spans back, u64 batch offsets into caller arrays")
-    out["masks"] = dict(rate(s_m), what="jb_cut_batch_mask from pageable host memory: 2 bits per input byte back",
-                        same_tokens_as_spans=ok_mask, tokens=int(ntok))
+    out = rate(s_m)
+    out["what"] = ("jb_cut_batch_mask from pageable host memory: pieces of 64 MiB staged into pinned memory and "
+                   "copied up while earlier pieces are cut, token boundaries back as 2 bits per input byte "
+                   "(SURVEY.md §8d's output format); checked against the spans below")
+    out["tokens"] = int(ntok)
+    out["same_tokens_as_spans"] = ok_mask
+    out["spans"] = dict(rate(s_sp), what="jb_cut_batch_into from pageable host memory: the same pipeline with u32 "
+                                         "spans back (8 B per token), widened to u64 batch offsets in caller arrays")
     out["masks_pinned"] = dict(rate(s_p), what="jb_cut_batch_mask with the text in jb_host_alloc (pinned) memory: "
                                                "no staging copy", same_as_pageable=ok_pin)
     return out
