@@ -469,10 +469,14 @@ static int stage_image(int ordinal, const Image& img, ImageBufs* b) {
         const uint32_t cd = img.code[r];
         l1[r] = jb_l1row_make(cd, cd < img.cells.size() ? img.cells[cd] : 0ull);
     }
+    // the weights behind one leading -Inf (DevImage::wtab1: record slots hold index + 1)
+    std::vector<double> wt1(img.wtab.size() + 1);
+    wt1[0] = -HUGE_VAL;
+    std::copy(img.wtab.begin(), img.wtab.end(), wt1.begin() + 1);
     int rc;
     if ((rc = upload(&b->pagemap, img.pagemap)) || (rc = upload(&b->emit, img.emit)) ||
         (rc = upload(&b->cells, img.cells)) || (rc = upload(&b->code, img.code)) ||
-        (rc = upload(&b->wtab, img.wtab)) || (rc = upload(&b->l1row, l1))) {
+        (rc = upload(&b->wtab, wt1)) || (rc = upload(&b->l1row, l1))) {
         free_image_bufs(b);
         return rc;
     }
@@ -490,8 +494,12 @@ static int install_image(Device* d, ImageBufs* b, const Image& img) {
     d->dim.emit = d->ib.emit;
     d->dim.cells = d->ib.cells;
     d->dim.code = d->ib.code;
-    d->dim.wtab = d->ib.wtab;
+    d->dim.wtab1 = d->ib.wtab;
+    d->dim.wtab = d->ib.wtab + 1;
     d->dim.nrows = img.nrows;
+    d->dim.plainw = 1u;
+    for (double w : img.wtab)
+        if (std::isnan(w) || w == HUGE_VAL) d->dim.plainw = 0u;  // (a dictionary size <= 0)
     // a captured pipeline holds the old image pointers in its kernel arguments
     if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
     d->gexec = nullptr;

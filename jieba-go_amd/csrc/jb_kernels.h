@@ -14,11 +14,18 @@ struct DevImage {
     const uint32_t* code;   // dense rune code per row (0: in no key)
     const uint64_t* cells;  // double-array trie over codes; level-1 nodes at their codes
     const double* wtab;
+    // wtab shifted by one: wtab1[0] = -Inf, wtab1[i + 1] = wtab[i].  DAG records hold
+    // weight index + 1 per slot, so an unused slot gathers -Inf (k_mark_walk, k_zh)
+    const double* wtab1;
     // per row: the rune's level-1 cell cells[code] with its check field
     // replaced by the code (bits 0-16) and bit 21 = "that check was the root",
     // so k_mark_walk gets code and level-1 cell in one load (jb_l1row_make)
     const uint64_t* l1row;
     uint32_t nrows;
+    // 1: every weight is finite or -Inf (a dictionary whose size is > 0).  k_zh's
+    // record fold relies on it; otherwise k_mark_walk writes only overflow records
+    // and k_zh folds every rune with maxIndexProba's literal rule.
+    uint32_t plainw;
 };
 
 // Device counters (u32 slots unless noted)

@@ -244,7 +244,9 @@ __device__ __forceinline__ bool han_cp(uint32_t r) {
 }
 
 constexpr uint32_t kEdgeMaxL = 8;     // edge lengths a record holds
-constexpr uint32_t kEdgeIdxBits = 14;
+constexpr uint32_t kEdgeIdxBits = 14;  // a record field: weight index + 1 (0: phantom edge)
+constexpr uint32_t kRecIdxMax = (1u << kEdgeIdxBits) - 2u;  // the largest weight index a record holds
+constexpr uint32_t kRecTop = 8u + 3u * kEdgeIdxBits;         // bit of the last field (a new edge enters there)
 constexpr uint32_t kTileE = kTileBytes / 3 + 2;  // Han rune entries of a tile (>= 3 bytes each)
 constexpr uint32_t kLA = 8;                      // lookahead entries: runes of the last run past the tile end
 constexpr uint32_t kLABytes = 40;                // ... starting in the first 40 bytes after it
@@ -349,11 +351,14 @@ __device__ __forceinline__ bool dat_hit(uint64_t child, uint32_t id) { return jb
 // Output per rune, slot = byte offset / 3 (Han runes are >= 3 bytes, so slots
 // never collide), one u64 record erec[slot]:
 //   bits 0-7    bit L-1 set for an edge of L runes (:479-481)
-//   bits 8-63   weight indices of the edges in ascending L, 14 bits each
+//   bits 8-63   four 14-bit fields, field k at bit 8 + 14k: weight index + 1.
+//               The n edges fill the LAST n fields in ascending L; the first
+//               4 - n fields are 0, a "phantom" edge whose weight is -Inf
+//               (DevImage::wtab1[0]), which k_zh's fold passes over (rec_fold_a3).
 // A rune with more than 4 edges, an edge longer than 8 runes or a weight index
-// >= 2^14 gets the record 0 (a Han rune always has at least one edge); k_zh
-// then walks that rune itself.  A rune that is absent or has count 0 gets the
-// single edge L = 1 (:468-471) with weight index 0 (Log(1) - Log(size)) or
+// past kRecIdxMax gets the record 0 (a Han rune always has at least one edge);
+// k_zh then walks that rune itself.  A rune that is absent or has count 0 gets
+// the single edge L = 1 (:468-471) with weight index 0 (Log(1) - Log(size)) or
 // that of Log(0) - Log(size) = -Inf.
 // At most 80 SGPRs (the rest spill to VGPR lanes) and 20.2 KB of LDS: 8
 // workgroups per CU instead of 6 (k_mark_walk is latency-bound: 0.695 -> 0.618 ms).
@@ -621,14 +626,18 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         uint64_t r1 = 0;
         bool go = false;
         if (jb_cell_check(c1) != JB_CHECK_ROOT) {
-            r1 = 1ull | ((uint64_t)JB_WIDX_ABSENT << 8);  // absent: the single edge only, Log(1) (:468-471)
-        } else if (wi >= (1u << kEdgeIdxBits) && fc != JB_FC_NEG) {
+            r1 = 1ull | ((uint64_t)(JB_WIDX_ABSENT + 1u) << kRecTop);  // absent: the single edge only, Log(1) (:468-471)
+        } else if (wi > kRecIdxMax && fc != JB_FC_NEG) {
             r1 = 0ull;  // the weight index does not fit a record: k_zh walks this rune
         } else if (fc == JB_FC_ZERO) {
-            r1 = 1ull | ((uint64_t)wi << 8);  // count 0: the single edge only, Log(0) = -Inf
+            r1 = 1ull | ((uint64_t)(wi + 1u) << kRecTop);  // count 0: the single edge only, Log(0) = -Inf
         } else {
-            if (fc == JB_FC_POS) r1 = 1ull | ((uint64_t)wi << 8);  // (a negative count has no edge)
+            if (fc == JB_FC_POS) r1 = 1ull | ((uint64_t)(wi + 1u) << kRecTop);  // (a negative count has no edge)
             go = jb_cell_hc(c1) != 0u && f != 0u;
+        }
+        if (!im.plainw) {  // weights that are +Inf or NaN: k_zh folds every rune literally
+            r1 = 0ull;
+            go = false;
         }
         if (!go) s_c[i] = r1;
         else s_wl[atomicAdd(&s_nwl, 1u)] = (uint16_t)i;
@@ -644,10 +653,11 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     const uint32_t hi = (nwl * (wv + 1u)) >> 2;
     // Walk state per lane: entry j of the current node's rune, start entry js,
     // the current node's cell index id and base.  The record builds as an edge
-    // mask m and a shift register rw of weight indices (each new one enters at
-    // bit 50, so after k edges the first is at bit 50 - 14(k-1); shifting right
-    // by 14(4-k) puts it at bit 8, the record's layout).  One trip = one probe,
-    // with selects instead of branches (k_mark_walk is issue-bound).
+    // mask m and a shift register rw of weight indices + 1 (each new one enters
+    // at the last field, kRecTop, pushing the earlier ones a field down: after n
+    // edges they fill the last n fields, the record's layout, and the first
+    // 4 - n fields are still 0).  One trip = one probe, with selects instead of
+    // branches (k_mark_walk is issue-bound).
     bool act = false, ovf = false;
     uint32_t j = 0, js = 0, id = 0, base = 0, len = 0, nedge = 0, m = 0;
     uint64_t rw = 0;
@@ -667,7 +677,7 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
             const bool pos = jb_cell_fc(c) == JB_FC_POS;  // (weight index < 2^14: checked by the run links)
             m = pos ? 1u : 0u;
             nedge = m;
-            rw = pos ? (uint64_t)jb_cell_widx(c) << 50 : 0ull;
+            rw = pos ? (uint64_t)(jb_cell_widx(c) + 1u) << kRecTop : 0ull;
             len = 1u;
             ovf = false;
             act = true;
@@ -680,11 +690,11 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
             ++len;
             const uint32_t wi = jb_cell_widx(child);
             const bool pos = hit && jb_cell_fc(child) == JB_FC_POS;
-            const bool bad = pos && (len > kEdgeMaxL || nedge >= 4u || wi >= (1u << kEdgeIdxBits));
+            const bool bad = pos && (len > kEdgeMaxL || nedge >= 4u || wi > kRecIdxMax);
             const bool add = pos && !bad;
             ovf |= bad;
             m |= add ? 1u << ((len - 1u) & 7u) : 0u;
-            rw = add ? (rw >> kEdgeIdxBits) | ((uint64_t)wi << 50) : rw;
+            rw = add ? (rw >> kEdgeIdxBits) | ((uint64_t)(wi + 1u) << kRecTop) : rw;
             nedge += add ? 1u : 0u;
             const bool more = hit && jb_cell_hc(child) && !ovf;
             const bool go = more && (en & kEntCont);
@@ -693,7 +703,7 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
             id = t;
             base = jb_cell_base(child);
             if (!go) {  // the record goes to the start entry's LDS cell (read when the walk began)
-                s_c[js] = (ovf || dfr) ? 0ull : ((uint64_t)m | (rw >> (kEdgeIdxBits * (4u - nedge))));
+                s_c[js] = (ovf || dfr) ? 0ull : ((uint64_t)m | rw);
                 act = false;
             }
         }
@@ -773,6 +783,9 @@ __device__ uint32_t block_end_at(const uint32_t* __restrict__ lanemask, const ui
 constexpr uint32_t kZhRing = 8;                            // LDS best ring per lane (runes)
 constexpr uint32_t kZhWin = kZhGroupBytes + 1024u;         // window: group span + slack for the last blocks
 constexpr uint32_t kZhChunk = 192;                         // blocks ranked together (3 per lane)
+// (a block whose end lm_collect did not find spans its round and the lookahead round
+// after it, so it is over 1 KiB long: a group has at most one per KiB, plus one)
+static_assert(kZhGroupBytes / 1024u + 1u <= 64u, "k_zh: a chunk's unresolved blocks fit the wave's 64 hist words");
 constexpr uint32_t kZhWinWords = kZhWin / 32u + 1u;        // token bitmap words of a window
 static_assert(kZhGroupBytes % 32u == 0u && kZhGroupSmall % 32u == 0u && kZhGroupSmall <= kZhGroupBytes,
               "k_zh groups are whole token-bitmap words");
@@ -1024,66 +1037,121 @@ __device__ __forceinline__ void dp_walk_rune(const V& v, const DevImage& im, uin
     }
 }
 
-// The weights of a record's edges (ascending L): four loads issued now, with
-// no branch (an absent edge loads wtab[0] and is ignored), so the compiler's
-// vmcnt bookkeeping stays exact and later waits do not drain other loads.  The
-// index fields of absent edges are 0 in every record k_mark_walk writes (its
-// shift register starts at 0), so no select is needed.
+// The weights of a record's four fields: four loads issued now, with no branch
+// (a phantom field, index + 1 = 0, loads wtab1[0] = -Inf), so the compiler's
+// vmcnt bookkeeping stays exact and later waits do not drain other loads.  Each
+// address is the image's wtab1 plus a 32-bit byte offset (the saddr form of the
+// load: no 64-bit address arithmetic).
+typedef const __attribute__((address_space(1))) char gchar;  // global memory, whatever inference concludes
 __device__ __forceinline__ void rec_weights(const DevImage& im, uint64_t rc, double w[4]) {
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-        w[k] = im.wtab[(uint32_t)(rc >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u)];
-}
-// Fold a record's edges (L <= kZhRing, so best(i+L) is in the ring or is the
-// sentinel), branch-free: every LDS read is issued and the items are selected.
-__device__ __forceinline__ void rec_fold(uint32_t m, const double w[4], DpFold& f, uint32_t c, const double* ring) {
+    gchar* const wb = (gchar*)im.wtab1;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const bool has = m != 0u;
-        const uint32_t L = has ? (uint32_t)__builtin_ctz(m) + 1u : 1u;
-        m &= m - 1u;
-        const double rv = ring[((c - L) & (kZhRing - 1u)) * 64u];
-        const double pp = w[k] + ((L == c) ? 0.0 : rv);
-        const bool take = has && pp >= f.prevP;
-        f.bestL = take ? L : f.bestL;
-        f.bestP = take ? pp : f.bestP;
-        f.prevP = has ? pp : f.prevP;
-        f.lastL = has ? L : f.lastL;
+        const uint32_t off = (uint32_t)(rc >> (8 + kEdgeIdxBits * k - 3)) & (((1u << kEdgeIdxBits) - 1u) << 3);
+        w[k] = *(const __attribute__((address_space(1))) double*)(wb + off);
     }
 }
 
-// A record's edge lengths (its 8-bit mask's set bits + 1, ascending, a byte each,
-// 0 = no edge), from a 256-entry LDS table that k_zh fills at its start.
-__shared__ uint32_t s_ltab[256];
-__device__ __forceinline__ uint32_t ltab_entry(uint32_t m) {
-    uint32_t v = 0, k = 0;
-    for (uint32_t b = 0; b < 8u && k < 4u; b++)
-        if ((m >> b) & 1u) v |= (b + 1u) << (8u * k++);
-    return v;
+// A record's edge lengths by its 8-bit mask, a 16-bit field per record field k
+// holding L << 9 (the byte stride of a ring slot): the mask's n set bits + 1 in
+// the last n fields, ascending, and L = 1 in the phantom fields before them.
+// A 256-entry LDS table that k_zh (and k_long_dp) fill at their start.
+__shared__ uint64_t s_ltab[256];
+__device__ __forceinline__ uint64_t ltab_entry(uint32_t m) {
+    uint32_t L[4] = {1u, 1u, 1u, 1u}, n = 0;
+    for (uint32_t b = 0; b < 8u; b++)
+        if ((m >> b) & 1u) {
+            L[0] = L[1];
+            L[1] = L[2];
+            L[2] = L[3];
+            L[3] = b + 1u;
+            n++;
+        }
+    (void)n;
+    uint64_t v = 0;
+    for (int k = 0; k < 4; k++) v |= (uint64_t)(L[k] << 9) << (16 * k);
+    return m ? v : (v | 0x8000u);  // record 0 (mask 0): overflowed (zh_dp_a3's kLtabOvf)
 }
 
-// The same with the {n, 0.0} sentinel kept in the ring: the caller writes 0.0
-// to slot 0 when a block (re)starts at c = 1, so the edge with L == c reads
-// best(n) = 0.0 from slot (c - L) & 7 = 0, which step 8 is the first to
-// overwrite (after its reads).  No per-edge select for the sentinel.  lp: the
-// record's lengths (s_ltab), looked up a step ahead.
-__device__ __forceinline__ void rec_fold_s(uint32_t lp, const double w[4], DpFold& f, uint32_t c, const double* ring) {
+// maxIndexProba (:565-578) over a record's four fields, phantoms first.
+//
+// The reference keeps the last item whose proba is >= its predecessor's, with
+// {-1, minFloat} before the first, and falls back to the last item when none
+// qualified.  Every proba here is finite (> minFloat) or -Inf (count 0 gives
+// Log(0); plainw excludes +Inf and NaN weights), and that rule gives the same
+// item when the first item is compared with -Inf instead of minFloat: the
+// first item then always qualifies, and when it is -Inf (where the reference
+// skips it) with a second item behind it, the second qualifies in both forms;
+// with none behind it, the fallback returns it anyway.  A phantom field's
+// proba is -Inf + best(i + 1) = -Inf, so it qualifies against -Inf and leaves
+// the state as it was before any item: the phantoms pass over, the real items
+// fold as the reference folds them, and the last field is always real, so the
+// chosen length is never a phantom's.  No per-field presence test, no
+// fallback step: the first field is taken outright, each later one by one
+// compare and three selects.
+//
+// Ring addresses: best(i + L) of this lane is in ring slot (c - L) & 7 at byte
+// ((c - L) << 9 & 0xE00) | lb, where lb = wave ring offset + lane * 8 (bits 3-8
+// and 12-13: disjoint from 0xE00, so the OR is an add) and rb0 is the ring
+// array's LDS base (folded into the instruction offset).  cs = c << 9, lp the
+// record's s_ltab entry.  Returns the chosen L << 9 and its proba.
+__device__ __forceinline__ uint32_t ring_off(uint32_t x, uint32_t lb) {  // (x & 0xE00) | lb in one VALU
+    uint32_t r;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(0xE00u), "v"(lb));
+    return r;
+}
+__device__ __forceinline__ double rec_fold_a3(uint64_t lp, const double w[4], uint32_t cs, const char* rb0, uint32_t lb,
+                                              uint32_t& bls) {
+    double pp[4], rv[4];
+    uint32_t Ls[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const uint32_t L = (lp >> (8 * k)) & 0xFFu;
-        const bool has = L != 0u;
-        const double pp = w[k] + ring[((c - L) & (kZhRing - 1u)) * 64u];
-        const bool take = has && pp >= f.prevP;
-        f.bestL = take ? L : f.bestL;
-        f.bestP = take ? pp : f.bestP;
-        f.prevP = has ? pp : f.prevP;
-        f.lastL = has ? L : f.lastL;
+        Ls[k] = (uint32_t)(lp >> (16 * k));  // (bits past the field: no effect on & 0xE00, nor on (uint8_t)(Ls >> 9))
+        rv[k] = *reinterpret_cast<const double*>(rb0 + ring_off(cs - Ls[k], lb));
     }
+    __builtin_amdgcn_sched_barrier(0);  // the four ring reads issue back to back
+#pragma unroll
+    for (int k = 0; k < 4; k++) pp[k] = w[k] + rv[k];
+    uint32_t bL = Ls[0];
+    double bP = pp[0];
+#pragma unroll
+    for (int k = 1; k < 4; k++) {
+        const bool take = pp[k] >= pp[k - 1];
+        bL = take ? Ls[k] : bL;
+        bP = take ? pp[k] : bP;
+    }
+    bls = bL;
+    return bP;
+}
+
+// The same fold on a per-lane ring pointer (slot stride 64 doubles).  Returns L.
+__device__ __forceinline__ double rec_fold_g(uint64_t lp, const double w[4], uint32_t c, const double* ring,
+                                             uint32_t& bl) {
+    double pp[4];
+    uint32_t L[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        L[k] = (uint32_t)(lp >> (16 * k + 9)) & 0x7Fu;
+        pp[k] = w[k] + ring[((c - L[k]) & (kZhRing - 1u)) * 64u];
+    }
+    uint32_t bL = L[0];
+    double bP = pp[0];
+#pragma unroll
+    for (int k = 1; k < 4; k++) {
+        const bool take = pp[k] >= pp[k - 1];
+        bL = take ? L[k] : bL;
+        bP = take ? pp[k] : bP;
+    }
+    bl = bL;
+    return bP;
 }
 
 // General form (any rune widths): the next rune's record is loaded one step ahead.
+// best(n) = 0.0 (the {n, 0.0} sentinel) sits in ring slot 0 from each (re)start:
+// the edge with L == c reads slot (c - L) & 7 = 0, which step 8 is the first to
+// overwrite (after its reads).
 template <class V, class Src>
-__device__ uint32_t zh_dp(const V& v, const DevImage& im, const uint64_t* __restrict__ erec,
+__device__ __forceinline__ uint32_t zh_dp(const V& v, const DevImage& im, const uint64_t* __restrict__ erec,
                           double* __restrict__ gbest, double* ring, const Src& src) {
     uint32_t j = 0, bs = 0, be = 0;
     if (!src.next(j, bs, be)) return 0;
@@ -1091,36 +1159,43 @@ __device__ uint32_t zh_dp(const V& v, const DevImage& im, const uint64_t* __rest
     bool longm = false;
     uint32_t q = z_prev(v, be, bs), c = 1;
     uint64_t rc = erec[q / 3u];
+    ring[0] = 0.0;
     for (;;) {
         const bool more = q > bs;
-        DpFold f;
-        uint32_t qn = 0;
+        uint32_t qn = 0, bL = 0;
         uint64_t rn = 0;
-        if ((uint32_t)rc & 0xFFu) {
+        double bP;
+        bool redo = false;
+        if (rc) {
             double w4[4];
             rec_weights(im, rc, w4);
             if (more) {  // next rune's record, in flight while this rune folds
                 qn = z_prev(v, q, bs);
                 rn = erec[qn / 3u];
             }
-            rec_fold((uint32_t)rc & 0xFFu, w4, f, c, ring);
+            bP = rec_fold_g(s_ltab[(uint32_t)rc & 0xFFu], w4, c, ring, bL);
         } else {
             if (more) {
                 qn = z_prev(v, q, bs);
                 rn = erec[qn / 3u];
             }
+            DpFold f;
             dp_walk_rune(v, im, q, be, f, c, ring, longm, gbest, key0);
+            f.finish();
+            bL = f.bestL;
+            bP = f.bestP;
+            redo = f.redo;
         }
-        f.finish();
-        ring[(c & (kZhRing - 1u)) * 64u] = f.bestP;
-        if (longm) gbest[key0 - c] = f.bestP;
-        v.bl(q) = (uint8_t)f.bestL;
+        ring[(c & (kZhRing - 1u)) * 64u] = bP;
+        if (longm) gbest[key0 - c] = bP;
+        v.bl(q) = (uint8_t)bL;
         steps++;
-        if (f.redo) {  // an edge past the ring: this block again, every best value kept in gbest
+        if (redo) {  // an edge past the ring: this block again, every best value kept in gbest
             longm = true;
             q = z_prev(v, be, bs);
             c = 1;
             rc = erec[q / 3u];
+            ring[0] = 0.0;
             continue;
         }
         if (more) {
@@ -1135,6 +1210,7 @@ __device__ uint32_t zh_dp(const V& v, const DevImage& im, const uint64_t* __rest
         q = z_prev(v, be, bs);
         c = 1;
         rc = erec[q / 3u];
+        ring[0] = 0.0;
     }
     return steps;
 }
@@ -1153,31 +1229,41 @@ __device__ uint32_t zh_dp(const V& v, const DevImage& im, const uint64_t* __rest
 //   1: B_Y  uses Y.hi = E(s-1)
 //   2: A_Y  uses Y.lo = E(s-1), reloads Y = (E(s-5), E(s-4))
 //   3: B_X  uses X.hi = E(s-1)
+// The ring is addressed as rec_fold_a3 describes (rb0 + lb: this lane's slot 0),
+// the chosen length goes to the window slot bi = (q - wb) / 3, counted down
+// with q.  Length-table entries carry kLtabOvf for record 0 (an overflowed
+// record: dp_walk_rune folds that rune).
+constexpr uint64_t kLtabOvf = 0x8000u;  // (bit 15 of field 0: no effect on a ring offset)
 template <class Src>
 __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const uint64_t* __restrict__ erec,
-                             double* __restrict__ gbest, double* ring, const Src& src) {
+                             double* __restrict__ gbest, double* ring, const char* rb0, uint32_t lb, const Src& src) {
     uint32_t j = 0, bs = 0, be = 0;
     if (!src.next(j, bs, be)) return 0;
-    uint32_t key0 = 0, steps = 0, q = 0, c = 1, s = 0, mc = 0, lc = 0;
+    uint32_t key0 = 0, steps = 0, q = 0, c = 1, s = 0, bi = 0;
+    uint64_t lc = 0;
     bool longm = false;
     // Slots before a block (or before the text: erec has kErecPad slots of padding in
     // front) are garbage that `more` masks at the use.
     uint64_t xl = 0, xh = 0, yl = 0, yh = 0;
-    auto ld_pair = [&](uint32_t k, uint64_t& lo, uint64_t& hi) {  // slots k, k+1 in one 16-byte load
+    auto ld_pair = [&](uint32_t k, uint64_t& lo, uint64_t& hi) __attribute__((always_inline)) {  // slots k, k+1
         typedef uint64_t u64x2 __attribute__((ext_vector_type(2), aligned(8)));
         const u64x2 x = *reinterpret_cast<const u64x2*>(erec + (int32_t)k);
         lo = x.x;
         hi = x.y;
     };
-    auto setup = [&]() {  // (re)start at the last rune of [bs, be)
+    auto ring_at = [&](uint32_t cs) -> double& {
+        return *reinterpret_cast<double*>(const_cast<char*>(rb0) + ring_off(cs, lb));
+    };
+    auto setup = [&]() __attribute__((always_inline)) {  // (re)start at the last rune of [bs, be)
         key0 = be / 3u;
         q = be - 3u;
         c = 1;
         s = q / 3u;
-        ring[0] = 0.0;  // best(n), the {n, 0.0} sentinel (rec_fold_s)
+        bi = (q - v.wb) / 3u;
+        ring_at(0u) = 0.0;  // best(n), the {n, 0.0} sentinel
     };
     // The pairs a step of kind P at slot s (the block's last rune) and the steps after it read.
-    auto prime = [&](const int P, double (&wn)[4]) {
+    auto prime = [&](const int P, double (&wn)[4]) __attribute__((always_inline)) {
         const uint64_t rc = erec[s];
         if (P == 0) {
             ld_pair(s - 1u, xl, xh);
@@ -1192,40 +1278,46 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
             ld_pair(s - 2u, xl, xh);
             ld_pair(s - 4u, yl, yh);
         }
-        mc = (uint32_t)rc & 0xFFu;
-        lc = s_ltab[mc];
+        lc = s_ltab[(uint32_t)rc & 0xFFu];
         rec_weights(im, rc, wn);
     };
     // One rune.  wc: this rune's weights (loaded a step ago); wn: gets the next rune's.
     // Weight registers alternate between steps, so nothing is copied out of a
     // load's destination (a copy would wait for the load).
-    auto step = [&](const int P, double (&wc)[4], double (&wn)[4]) -> bool {
+    auto step = [&](const int P, double (&wc)[4], double (&wn)[4]) __attribute__((always_inline)) -> bool {
         const bool more = q > bs;
         const uint64_t nx = P == 0 ? xl : (P == 1 ? yh : (P == 2 ? yl : xh));
         const uint64_t r1v = more ? nx : 0ull;  // the next rune's record (when it exists)
-        const uint32_t mn = (uint32_t)r1v & 0xFFu;
-        const uint32_t ln = s_ltab[mn];
+        const uint64_t ln = s_ltab[(uint32_t)r1v & 0xFFu];
         rec_weights(im, r1v, wn);
         if (P == 0) ld_pair(s - 5u, xl, xh);
         if (P == 2) ld_pair(s - 5u, yl, yh);
-        DpFold f;
-        rec_fold_s(lc, wc, f, c, ring);
-        if (mc == 0u) dp_walk_rune(v, im, q, be, f, c, ring, longm, gbest, key0);  // overflowed record (rare)
-        f.finish();
-        ring[(c & (kZhRing - 1u)) * 64u] = f.bestP;
-        if (longm) gbest[key0 - c] = f.bestP;
-        v.bl(q) = (uint8_t)f.bestL;
+        const uint32_t cs = c << 9;
+        uint32_t bLs;
+        double bP = rec_fold_a3(lc, wc, cs, rb0, lb, bLs);
+        bool redo = false;
+        if (lc & kLtabOvf) {  // overflowed record (rare)
+            DpFold f;
+            dp_walk_rune(v, im, q, be, f, c, ring, longm, gbest, key0);
+            f.finish();
+            bLs = f.bestL << 9;
+            bP = f.bestP;
+            redo = f.redo;
+        }
+        ring_at(cs) = bP;
+        if (longm) gbest[key0 - c] = bP;
+        v.bls[bi] = (uint8_t)(bLs >> 9);
         steps++;
-        const bool restart = f.redo || !more;
+        const bool restart = redo || !more;
         if (!restart) {
             q -= 3u;
             s -= 1u;
-            mc = mn;
+            bi -= 1u;
             lc = ln;
             ++c;
             return false;
         }
-        if (f.redo) longm = true;  // an edge past the ring: this block again, every best value kept in gbest
+        if (redo) longm = true;  // an edge past the ring: this block again, every best value kept in gbest
         else {
             if (!src.next(j, bs, be)) return true;
             longm = false;
@@ -1342,7 +1434,7 @@ __device__ uint32_t viterbi_fwd_runs(const GrpZvT<true>& v, const DevImage& im, 
 // reference panics (a rune on the chosen path with no DAG edge: cutDAG slices
 // with tail index -1).
 template <bool HMM, class V, class E>
-__device__ bool zh_fwd(const V& v, const DevImage& im, uint32_t bs, uint32_t be, E& em, RunList* rl) {
+__device__ __forceinline__ bool zh_fwd(const V& v, const DevImage& im, uint32_t bs, uint32_t be, E& em, RunList* rl) {
     auto run_end = [&](uint32_t rs, uint32_t re, uint32_t m) {
         if (m == 1u) em.token(rs, re);  // a single rune is always "S" (:672-674)
         else if (rl && rl->n < kZhRuns) {
@@ -1447,14 +1539,14 @@ __device__ __forceinline__ bool text_has4(const uint8_t* __restrict__ text, uint
 }
 
 template <bool HMM, bool A3>
-__device__ void zh_chunk_main(const uint8_t* __restrict__ text, const DevImage& im,
+__device__ __forceinline__ void zh_chunk_main(const uint8_t* __restrict__ text, const DevImage& im,
                               const uint64_t* __restrict__ erec, double* __restrict__ gbest, uint8_t* bls,
-                              double* ring, uint32_t* rb32, uint32_t* runs, const TblSrc& src, uint32_t wb,
-                              uint32_t lane,
+                              double* ring, const char* rb0, uint32_t lb, uint32_t* rb32, uint32_t* runs,
+                              const TblSrc& src, uint32_t wb, uint32_t lane,
                               uint32_t* __restrict__ counters, uint32_t winw, uint32_t& nties, uint64_t* st) {
     const GrpZvT<A3> v{text, bls, wb};
     uint32_t steps;
-    if constexpr (A3) steps = zh_dp_a3(v, im, erec, gbest, ring, src);
+    if constexpr (A3) steps = zh_dp_a3(v, im, erec, gbest, ring, rb0, lb, src);
     else steps = zh_dp(v, im, erec, gbest, ring, src);
     wave_sync();  // ring dead: its space takes the window's token bitmaps
     if (st) {
@@ -1588,6 +1680,9 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
     __shared__ uint32_t s_runs[4][kZhRuns * 64];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     double* ring = s_rb[wv] + lane;
+    const char* const rb0 = reinterpret_cast<const char*>(&s_rb[0][0]);  // (rec_fold_a3's ring addressing)
+    const uint32_t lb = wv * (uint32_t)sizeof(s_rb[0]) + lane * 8u;
+    static_assert(sizeof(s_rb[0]) == 4096u, "a wave's ring is 8 slots x 64 lanes x 8 bytes (offsets 0xE00 | lb)");
     uint32_t* rb32 = reinterpret_cast<uint32_t*>(s_rb[wv]);
     uint32_t* tbl = s_tbl[wv];
     uint32_t* hist = s_hist[wv];
@@ -1596,7 +1691,6 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
     const uint32_t nlw = ntiles * 256u;                                  // lane-mask words (16 bytes each)
     const uint32_t winw = (grp + (kZhWin - kZhGroupBytes)) / 32u + 1u;  // token words of a window (<= kZhWinWords)
     auto lmw = [&](uint32_t w) -> uint32_t { return w < nlw ? lanemask[w] : 0u; };
-    Emitter em(sbits, ebits);
     s_ltab[threadIdx.x] = ltab_entry(threadIdx.x);  // (256 threads)
     __syncthreads();
     // diagnostic per-wave clocks (JB_ABLATE bit 8): [0] setup [1] DP [2] forward+Viterbi+flush [3] chunks
@@ -1608,7 +1702,7 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
     uint64_t* const st = nullptr;  // built without the diagnostic clocks (make STAMPS=1)
 #endif
     const uint64_t tk0 = st ? __builtin_amdgcn_s_memtime() : 0;
-    uint32_t nties = 0;  // Viterbi route ties of the in-window blocks (em.ties: the others)
+    uint32_t nties = 0;  // Viterbi route ties
     // Wave w takes group w first, then the next unclaimed one from the counter: only
     // waves that finished a group touch the counter (4096 waves all claiming their
     // first group on one address cost ~80 us on a one-sentence batch).
@@ -1672,26 +1766,20 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
                 used = ru.y;
             }
             wave_sync();
-            // this lane's items k = lane + 64 i of the chunk
+            // this lane's items k = lane + 64 i of the chunk.  Blocks whose end lm_collect did
+            // not find in its two rounds (at least 1 KiB long; they may still end inside the
+            // window) are cut one by one after the chunk: their starts wait in the wave's
+            // hist words meanwhile, so nothing of them stays in registers across the DP.
             uint32_t bsi[3], bei[3];
             bool in[3], out[3];
 #pragma unroll
             for (int i = 0; i < 3; i++) {
                 const uint32_t k = lane + 64u * (uint32_t)i;
-                bsi[i] = bei[i] = 0;
-                in[i] = out[i] = false;
-                if (k < m) {
-                    const uint32_t x = tbl[k];
-                    if (x & 0x80000000u) {  // ends past the window (rare)
-                        bsi[i] = wb + (x & 0xFFFFu);
-                        bei[i] = block_end_at(lanemask, tile_cnt, ntiles, (uint32_t)nbytes, bsi[i]);
-                        out[i] = true;
-                    } else {
-                        bsi[i] = wb + (x & 0xFFFFu);
-                        bei[i] = wb + (x >> 16);
-                        in[i] = true;
-                    }
-                }
+                const uint32_t x = k < m ? tbl[k] : 0x80000000u;
+                in[i] = !(x & 0x80000000u);
+                out[i] = k < m && !in[i];
+                bsi[i] = wb + (x & 0xFFFFu);
+                bei[i] = in[i] ? wb + (x >> 16) : bsi[i];
             }
             // rank in-window blocks by length (descending; counting sort on len/4)
             hist[lane] = 0u;
@@ -1728,6 +1816,14 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
                 }
             }
             wave_sync();
+            uint32_t nout = 0;  // (hist is free once the blocks are dealt)
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                const uint64_t ob = __ballot(out[i]);
+                if (out[i]) hist[nout + __builtin_amdgcn_mbcnt_hi((uint32_t)(ob >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ob, 0u))] = bsi[i];
+                nout += (uint32_t)__popcll(ob);
+            }
+            wave_sync();
             const TblSrc src{tbl + lane, (nin + 63u) >> 6, wb};
             if (st) {
                 const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -1736,10 +1832,10 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
                 stv[3]++;
             }
             if (all3)
-                zh_chunk_main<HMM, true>(text, im, erec, gbest, s_bl[wv], ring, rb32, s_runs[wv] + lane, src, wb, lane,
+                zh_chunk_main<HMM, true>(text, im, erec, gbest, s_bl[wv], ring, rb0, lb, rb32, s_runs[wv] + lane, src, wb, lane,
                                          counters, winw, nties, st);
             else
-                zh_chunk_main<HMM, false>(text, im, erec, gbest, s_bl[wv], ring, rb32, s_runs[wv] + lane, src, wb,
+                zh_chunk_main<HMM, false>(text, im, erec, gbest, s_bl[wv], ring, rb0, lb, rb32, s_runs[wv] + lane, src, wb,
                                           lane, counters, winw, nties, st);
             // the window's token words: consecutive words per lane, one OR each (edge
             // words are shared with neighbouring groups and with k_nonzh)
@@ -1754,22 +1850,26 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
                 }
             }
             wave_sync();  // bitmaps read: the ring is free again
-            // blocks that end past the window (rare): each on its own, in HBM
-#pragma unroll
-            for (int i = 0; i < 3; i++) {
-                if (st) stv[6] += __popcll(__ballot(out[i]));
-                if (out[i] && bei[i] - bsi[i] >= kZhLongMin) {  // the k_long_* kernels cut it
+            // blocks whose end was not found in the staged rounds (rare): one per lane, each
+            // on its own in HBM (or, from 8 KiB, by the k_long_* kernels)
+            if (st) stv[6] += nout;
+            if (lane < nout) {
+                const uint32_t obs = hist[lane];
+                const uint32_t obe = block_end_at(lanemask, tile_cnt, ntiles, (uint32_t)nbytes, obs);
+                if (obe - obs >= kZhLongMin) {  // the k_long_* kernels cut it
                     // block index and first segment from one atomic, so lsegb ascends with the index
-                    const uint32_t nsg = ((bei[i] - bsi[i]) / 3u + kSeg - 1u) / kSeg;
+                    const uint32_t nsg = ((obe - obs) / 3u + kSeg - 1u) / kSeg;
                     const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long*>(counters + CNT_NLONG),
                                                              ((unsigned long long)nsg << 32) | 1ull);
-                    longblk[(uint32_t)old] = make_uint2(bsi[i], bei[i]);
+                    longblk[(uint32_t)old] = make_uint2(obs, obe);
                     lsegb[(uint32_t)old] = (uint32_t)(old >> 32);
-                } else if (out[i]) {
+                } else {
+                    Emitter em(sbits, ebits);
                     const GlbZv gv{text, gbl};
-                    zh_dp(gv, im, erec, gbest, ring, OneSrc{bsi[i], bei[i]});
-                    if (!zh_fwd<HMM>(gv, im, bsi[i], bei[i], em, nullptr))
-                        atomicOr(counters + CNT_ERR, 1u);
+                    zh_dp(gv, im, erec, gbest, ring, OneSrc{obs, obe});
+                    if (!zh_fwd<HMM>(gv, im, obs, obe, em, nullptr)) atomicOr(counters + CNT_ERR, 1u);
+                    em.flush();
+                    nties += em.ties;
                 }
             }
             wave_sync();
@@ -1781,9 +1881,8 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
         }
         g = next_group();
     }
-    em.flush();
     {
-        uint32_t t = nties + em.ties;
+        uint32_t t = nties;
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) t += (uint32_t)__shfl_xor((int)t, d, 64);
         if (lane == 0 && t) atomicAdd(counters + CNT_TIES, t);
@@ -1878,11 +1977,11 @@ __device__ __forceinline__ void long_items(const uint8_t* __restrict__ text, con
     const uint32_t q = bs + 3u * i;
     const uint64_t rc = erec[q / 3u];
     uint32_t mk = (uint32_t)rc & 0xFFu;
-    if (mk) {
-        for (int k = 0; k < 4 && mk; k++) {
+    if (mk) {  // the edges are in the last popc(mk) fields (the first ones are phantoms)
+        for (int k = 4 - __popc(mk); k < 4; k++) {
             const uint32_t L = (uint32_t)__builtin_ctz(mk) + 1u;
             mk &= mk - 1u;
-            f(L, im.wtab[(uint32_t)(rc >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u)]);
+            f(L, im.wtab1[(uint32_t)(rc >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u)]);
         }
         return;
     }
@@ -1959,6 +2058,7 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const uint32_t nlong = counters[CNT_NLONG];
     const char* const rb = reinterpret_cast<const char*>(S.ring);
+    s_ltab[tid] = ltab_entry(tid);  // (zh_dp's record lengths; 256 threads, read after the barriers below)
     for (uint32_t bi = blockIdx.x; bi < nlong; bi += gridDim.x) {
         const uint2 bb = longblk[bi];
         const uint32_t bs = bb.x, be = bb.y;
@@ -2016,7 +2116,7 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                     }
                     m++;
                 });
-                if (m >= 1u && m <= 4u && L[0] == 1u) {
+                if (im.plainw && m >= 1u && m <= 4u && L[0] == 1u) {  // (the classes assume no +Inf/NaN weight)
 #pragma unroll
                     for (int k = 0; k < 4; k++) d.w[k] = w[k];
 #pragma unroll
