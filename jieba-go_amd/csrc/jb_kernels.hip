@@ -958,6 +958,24 @@ struct TblSrc {
         return false;
     }
 };
+struct TblPeek {  // (the lane's block after the current one, TblSrc::peek)
+    uint32_t bs, be;
+    bool ok;
+};
+__device__ __forceinline__ TblPeek tbl_peek(const TblSrc& src, uint32_t j) {
+    TblPeek p{0u, 0u, false};
+    while (j < src.nseg) {
+        const uint32_t x = src.t[j * 64u];
+        j++;
+        if (x != ~0u) {
+            p.bs = src.wb + (x & 0xFFFFu);
+            p.be = src.wb + (x >> 16);
+            p.ok = true;
+            break;
+        }
+    }
+    return p;
+}
 struct OneSrc {  // a single block
     uint32_t bs0, be0;
     __device__ __forceinline__ bool next(uint32_t& j, uint32_t& bs, uint32_t& be) const {
@@ -1262,25 +1280,42 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
         bi = (q - v.wb) / 3u;
         ring_at(0u) = 0.0;  // best(n), the {n, 0.0} sentinel
     };
-    // The pairs a step of kind P at slot s (the block's last rune) and the steps after it read.
-    auto prime = [&](const int P, double (&wn)[4]) __attribute__((always_inline)) {
-        const uint64_t rc = erec[s];
+    // The records of the lane's NEXT block's last two runes, E(s'-1) and E(s'), in one
+    // 16-byte load issued when this block starts (after everything else of its prime),
+    // so a block change finds them landed instead of waiting for HBM twice (its last
+    // rune's record, then the record the first step reads).
+    typedef uint64_t u64x2v __attribute__((ext_vector_type(2), aligned(8)));
+    u64x2v pre = {0ull, 0ull};
+    auto load_pre = [&]() __attribute__((always_inline)) {
+        const TblPeek nb = tbl_peek(src, j);
+        if (nb.ok) pre = *reinterpret_cast<const u64x2v*>(erec + (int32_t)((nb.be - 3u) / 3u - 1u));
+    };
+    // The pairs a step of kind P at slot s (the block's last rune) and the steps after it
+    // read.  e: (E(s-1), E(s)), from pre or (a redo) loaded here.
+    auto prime = [&](const int P, double (&wn)[4], const u64x2v e) __attribute__((always_inline)) {
+        const uint64_t rc = e.y;
         if (P == 0) {
-            ld_pair(s - 1u, xl, xh);
+            xl = e.x;
+            xh = e.y;
             ld_pair(s - 3u, yl, yh);
         } else if (P == 1) {
-            ld_pair(s - 2u, yl, yh);
+            yl = erec[s - 2u];
+            yh = e.x;
             ld_pair(s - 4u, xl, xh);
         } else if (P == 2) {
-            ld_pair(s - 1u, yl, yh);
+            yl = e.x;
+            yh = e.y;
             ld_pair(s - 3u, xl, xh);
         } else {
-            ld_pair(s - 2u, xl, xh);
+            xl = erec[s - 2u];
+            xh = e.x;
             ld_pair(s - 4u, yl, yh);
         }
         lc = s_ltab[(uint32_t)rc & 0xFFu];
         rec_weights(im, rc, wn);
+        load_pre();
     };
+    auto ld_e = [&]() -> u64x2v { return *reinterpret_cast<const u64x2v*>(erec + (int32_t)(s - 1u)); };
     // One rune.  wc: this rune's weights (loaded a step ago); wn: gets the next rune's.
     // Weight registers alternate between steps, so nothing is copied out of a
     // load's destination (a copy would wait for the load).
@@ -1317,18 +1352,21 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
             ++c;
             return false;
         }
-        if (redo) longm = true;  // an edge past the ring: this block again, every best value kept in gbest
-        else {
-            if (!src.next(j, bs, be)) return true;
-            longm = false;
+        if (redo) {  // an edge past the ring: this block again, every best value kept in gbest
+            longm = true;
+            setup();
+            prime((P + 1) & 3, wn, ld_e());  // (pre keeps the next block's records)
+            return false;
         }
+        if (!src.next(j, bs, be)) return true;
+        longm = false;
         setup();
-        prime((P + 1) & 3, wn);  // the next step is the next kind
+        prime((P + 1) & 3, wn, pre);  // the next step is the next kind
         return false;
     };
     double wa[4], wb[4];
     setup();
-    prime(0, wa);
+    prime(0, wa, ld_e());
     for (;;) {
         if (step(0, wa, wb)) break;
         if (step(1, wb, wa)) break;
