@@ -456,6 +456,85 @@ def sentence_latency(tk, o, n):
     return lat, olat
 
 
+STAMPS_LIB = os.path.join(ROOT, "jieba-go_amd", "lib_st", "libjiebahip.so")
+
+
+def parse_zh_clocks(err):
+    """The last "[jb] k_zh clocks/wave" line a STAMPS build printed: (DP cycles per
+    wave, DP loop trips per wave, k_zh cycles per wave, DP lane use)."""
+    import re
+    last = None
+    for ln in err.splitlines():
+        m = re.search(r"k_zh clocks/wave: setup (\S+) dp (\S+) .* total (\S+); chunks/wave \S+; "
+                      r"lane DP steps (\S+) vs 64\*max (\S+) \(DP lane use (\S+)\)", ln)
+        if m:
+            last = m
+    if not last:
+        return None
+    dp, total, max64, use = float(last.group(2)), float(last.group(3)), float(last.group(5)), float(last.group(6))
+    return dp, max64 / 64.0, total, use
+
+
+def latency_probe(args):
+    """Child process (JB_LIB = the STAMPS build, JB_STAMPS=1): k_zh's per-wave phase
+    clocks on a loaded chip (the first 128 MiB of the headline corpus: every wave has
+    ~11 groups) and on one wave alone (a 1 KiB batch: one group), printed by the
+    library to stderr and parsed by the parent."""
+    import torch
+    import jiebahip as J
+    import synth
+    s = synth.Synth(nwords=args.nwords)
+    tmp = tempfile.mkdtemp(prefix="jb_lat_")
+    dpath, epath = s.write_files(tmp)
+    tk = J.Tokenizer(J.make_config(dict_path=dpath, emit_path=epath, kind=J.JB_DICT_PREFIX,
+                                   size_override=J.JIEBA_SIZE, device=0))
+    buf, off, _ = s.corpus_parallel(synth.KIND_DOCS, 0, target_bytes=128 << 20,
+                                    threads=max(1, min(16, effective_cpus()[0])))
+    one = int(np.searchsorted(off, 1024, side="right")) - 1  # whole documents in the first KiB
+    small = (np.concatenate([np.asarray(buf[: int(off[max(one, 1)])]), np.zeros(64, np.uint8)]),
+             np.asarray(off[: max(one, 1) + 1], np.uint64))
+    for tag, (b, o) in (("loaded", (buf, off)), ("one_wave", small)):
+        c = GpuCutter(tk, b, o, True, 0)
+        for _ in range(2):
+            c.step()
+            c.sync()
+        print(f"[probe] {tag} done", file=sys.stderr, flush=True)
+    tk.close()
+
+
+def roofline_latency(timeout=240):
+    """k_zh's DP against its latency floor: cycles per DP step
+    per wave with every wave busy, beside the same for one wave alone on an idle
+    chip (the step's own dependent chain: record and weight loads, ring reads,
+    float64 adds and compares).  frac = floor / loaded: 1.0 would mean the 4 waves
+    per SIMD only share the SIMD, none slows another.  From the STAMPS build in a
+    child process; None when it is absent or fails."""
+    import subprocess
+    if not os.path.exists(STAMPS_LIB):
+        return None
+    env = dict(os.environ, JB_LIB=STAMPS_LIB, JB_STAMPS="1", JB_GRAPH="0")
+    try:
+        p = subprocess.run([sys.executable, os.path.abspath(__file__), "--latency-probe"], env=env,
+                           capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return None
+    err = p.stderr
+    parts = err.split("[probe] loaded done")
+    if p.returncode != 0 or len(parts) != 2:
+        return {"error": err[-400:]}
+    loaded, alone = parse_zh_clocks(parts[0]), parse_zh_clocks(parts[1])
+    if not loaded or not alone:
+        return {"error": "no k_zh clocks in the probe's output"}
+    cl, ca = loaded[0] / loaded[1], alone[0] / alone[1]
+    return {"bound": "latency", "unit": "cycles per DP step per wave",
+            "achieved": round(cl, 1), "floor": round(ca, 1), "frac": round(ca / cl, 4),
+            "dp_share_of_k_zh": round(loaded[0] / loaded[2], 4), "dp_lane_use": loaded[3],
+            "waves_per_simd": 4,
+            "what": "k_zh's backward DP (calcDagProba + maxIndexProba): s_memtime cycles per step of a wave's "
+                    "DP loop, every wave busy (first 128 MiB of the corpus) vs one wave alone (a 1 KiB batch); "
+                    "STAMPS build of the same source, per-wave clocks cost a few %"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -475,7 +554,12 @@ def main():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--sentence-iters", type=int, default=5000)
+    ap.add_argument("--no-latency", action="store_true", help="skip the roofline_latency probe")
+    ap.add_argument("--latency-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.latency_probe:
+        latency_probe(args)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -534,6 +618,8 @@ def main():
         line, (sbuf, soff, _) = out
         if world == 1 and not args.no_e2e:
             line["end_to_end_host"] = end_to_end(tk, sbuf, soff, args.hmm, line["config"]["corpus_chars"])
+        if world == 1 and args.workload == "docs" and not args.no_latency:
+            line["roofline_latency"] = roofline_latency()
         line["loaded"] = J.loaded_runtime()
         print(json.dumps(line), flush=True)
     tk.close()

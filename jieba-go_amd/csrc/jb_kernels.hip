@@ -1285,37 +1285,43 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
     // so a block change finds them landed instead of waiting for HBM twice (its last
     // rune's record, then the record the first step reads).
     typedef uint64_t u64x2v __attribute__((ext_vector_type(2), aligned(8)));
-    u64x2v pre = {0ull, 0ull};
+    u64x2v pre = {0ull, 0ull}, pre0 = {0ull, 0ull};  // E(s'-1), E(s') and E(s'-3), E(s'-2)
     auto load_pre = [&]() __attribute__((always_inline)) {
         const TblPeek nb = tbl_peek(src, j);
-        if (nb.ok) pre = *reinterpret_cast<const u64x2v*>(erec + (int32_t)((nb.be - 3u) / 3u - 1u));
+        if (nb.ok) {
+            const u64x2v* p = reinterpret_cast<const u64x2v*>(erec + (int32_t)((nb.be - 3u) / 3u - 3u));
+            pre0 = p[0];
+            pre = p[1];
+        }
     };
     // The pairs a step of kind P at slot s (the block's last rune) and the steps after it
-    // read.  e: (E(s-1), E(s)), from pre or (a redo) loaded here.
-    auto prime = [&](const int P, double (&wn)[4], const u64x2v e) __attribute__((always_inline)) {
-        const uint64_t rc = e.y;
+    // read.  e1: (E(s-1), E(s)), e0: (E(s-3), E(s-2)), from pre or (a redo) loaded here.
+    auto prime = [&](const int P, double (&wn)[4], const u64x2v e1, const u64x2v e0) __attribute__((always_inline)) {
+        const uint64_t rc = e1.y;
         if (P == 0) {
-            xl = e.x;
-            xh = e.y;
-            ld_pair(s - 3u, yl, yh);
+            xl = e1.x;
+            xh = e1.y;
+            yl = e0.x;
+            yh = e0.y;
         } else if (P == 1) {
-            yl = erec[s - 2u];
-            yh = e.x;
+            yl = e0.y;
+            yh = e1.x;
             ld_pair(s - 4u, xl, xh);
         } else if (P == 2) {
-            yl = e.x;
-            yh = e.y;
-            ld_pair(s - 3u, xl, xh);
+            yl = e1.x;
+            yh = e1.y;
+            xl = e0.x;
+            xh = e0.y;
         } else {
-            xl = erec[s - 2u];
-            xh = e.x;
+            xl = e0.y;
+            xh = e1.x;
             ld_pair(s - 4u, yl, yh);
         }
         lc = s_ltab[(uint32_t)rc & 0xFFu];
         rec_weights(im, rc, wn);
         load_pre();
     };
-    auto ld_e = [&]() -> u64x2v { return *reinterpret_cast<const u64x2v*>(erec + (int32_t)(s - 1u)); };
+    auto ld_e = [&](int d) -> u64x2v { return *reinterpret_cast<const u64x2v*>(erec + (int32_t)(s - 1u - d)); };
     // One rune.  wc: this rune's weights (loaded a step ago); wn: gets the next rune's.
     // Weight registers alternate between steps, so nothing is copied out of a
     // load's destination (a copy would wait for the load).
@@ -1355,18 +1361,18 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
         if (redo) {  // an edge past the ring: this block again, every best value kept in gbest
             longm = true;
             setup();
-            prime((P + 1) & 3, wn, ld_e());  // (pre keeps the next block's records)
+            prime((P + 1) & 3, wn, ld_e(0), ld_e(2));  // (pre keeps the next block's records)
             return false;
         }
         if (!src.next(j, bs, be)) return true;
         longm = false;
         setup();
-        prime((P + 1) & 3, wn, pre);  // the next step is the next kind
+        prime((P + 1) & 3, wn, pre, pre0);  // the next step is the next kind
         return false;
     };
     double wa[4], wb[4];
     setup();
-    prime(0, wa, ld_e());
+    prime(0, wa, ld_e(0), ld_e(2));
     for (;;) {
         if (step(0, wa, wb)) break;
         if (step(1, wb, wa)) break;

@@ -808,3 +808,40 @@ def test_small_batches_one_workgroup(syn_small, monkeypatch):
     assert tk.Cut(SENTENCE, True) == o.cut(SENTENCE, True) == tp.Cut(SENTENCE, True)
     tk.close()
     tp.close()
+
+
+@pytest.mark.parametrize("entries", [
+    [("中", 0), ("文", 0), ("中文", 0), ("上海", 0)],          # size 0: Log(0) - Log(0) = NaN, Log(1) - Log(0) = +Inf
+    [("中", 5), ("文", 1), ("中文", -20), ("天氣", 2)],         # size < 0: every weight NaN
+    [("中", 5), ("文", -9), ("中文", 1), ("天氣", 2)],          # ... and a lone 文 has no DAG edge: panic
+])
+def test_degenerate_dictionary_weights(tmp_path, mini_paths, entries, monkeypatch):
+    """A dictionary whose size is <= 0 makes pieceFreq +Inf or NaN (tokenizer.go:503,515-519).
+    k_zh's record fold assumes finite or -Inf weights (DevImage::plainw); here k_mark_walk
+    writes only overflow records and every rune is folded by maxIndexProba's literal rule.
+    Both the pipeline (JB_SMALL=0) and k_small, against the oracle's IEEE arithmetic."""
+    dp = str(tmp_path / "dict.txt")
+    with open(dp, "w", encoding="utf-8") as f:
+        for w, c in entries:
+            f.write(f"{w} {c}\n")
+    texts = ["中文", "中文上海天氣很好", "我昨天去上海交通大學與老師討論量子力學", "中" * 40 + "，" + "文中" * 30,
+             "abc 中文 def", "一丁㐀中文" * 20]
+    buf, off = _batch_of(texts * 3)
+    for small in ("0", None):
+        if small is None:
+            monkeypatch.delenv("JB_SMALL", raising=False)
+        else:
+            monkeypatch.setenv("JB_SMALL", small)
+        tk, o = _pair(dp, mini_paths[1])
+
+        def outcome(fn, t, hmm):  # the tokens, or "panic" where the reference panics (cutDAG, JB_EPANIC)
+            try:
+                return fn(t, hmm)
+            except (J.JbError, RuntimeError, ValueError):
+                return "panic"
+        for hmm in (False, True):
+            for t in texts:
+                assert outcome(tk.Cut, t, hmm) == outcome(o.cut, t, hmm), (small, hmm, t)
+            if all(outcome(o.cut, t, hmm) != "panic" for t in texts):
+                _cmp_batch(tk, o, buf, off, hmm, f"degenerate dict JB_SMALL={small}")
+        tk.close()
