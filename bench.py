@@ -526,10 +526,12 @@ def roofline_latency(timeout=240):
     if not loaded or not alone:
         return {"error": "no k_zh clocks in the probe's output"}
     cl, ca = loaded[0] / loaded[1], alone[0] / alone[1]
+    lines = [ln.split("] ", 1)[1] for ln in parts[0].splitlines()
+             if ln.startswith("[jb] k_zh clocks") or ln.startswith("[jb] k_mark_walk clocks")]
     return {"bound": "latency", "unit": "cycles per DP step per wave",
             "achieved": round(cl, 1), "floor": round(ca, 1), "frac": round(ca / cl, 4),
             "dp_share_of_k_zh": round(loaded[0] / loaded[2], 4), "dp_lane_use": loaded[3],
-            "waves_per_simd": 4,
+            "waves_per_simd": 4, "phase_clocks_loaded": lines[-2:],
             "what": "k_zh's backward DP (calcDagProba + maxIndexProba): s_memtime cycles per step of a wave's "
                     "DP loop, every wave busy (first 128 MiB of the corpus) vs one wave alone (a 1 KiB batch); "
                     "STAMPS build of the same source, per-wave clocks cost a few %"}

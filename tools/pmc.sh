@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 OUT=gpurun_out/${TAG:-pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:---steps 3 --warmup 1 --no-parity --no-profile --no-e2e}
+ARGS=${BENCH_ARGS:---steps 3 --warmup 1 --no-parity --no-profile --no-e2e --no-latency}
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" \
            "SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
