@@ -1563,6 +1563,63 @@ __device__ bool zh_fwd_lane(const V& v, const DevImage& im, const Src& src, E& e
     return ok;
 }
 
+// The same for an all-3-byte window (the common case), leaner: a piece's length is
+// read by slot ((q - wb) / 3 kept beside q, no division), and each token ORs its two bits
+// straight into the wave's LDS bitmaps (two LDS atomics, no register state to flush
+// when the word changes).  Runs of single-rune pieces go to the run list as before
+// (a run of one rune is "S", its own token).
+template <bool HMM, class Src>
+__device__ __forceinline__ bool zh_fwd_a3(const GrpZvT<true>& v, const DevImage& im, const Src& src,
+                                          uint32_t* sb, uint32_t* eb, LdsEmitter& le, RunList* rl) {
+    const uint32_t w0 = v.wb >> 5;
+    auto token = [&](uint32_t a, uint32_t b) __attribute__((always_inline)) {
+        atomicOr(sb + ((a >> 5) - w0), 1u << (a & 31u));
+        atomicOr(eb + (((b - 1u) >> 5) - w0), 1u << ((b - 1u) & 31u));
+    };
+    auto run_end = [&](uint32_t rs, uint32_t re, uint32_t m) __attribute__((always_inline)) {
+        if (m == 1u) token(rs, re);  // a single rune is always "S" (:672-674)
+        else if (rl->n < kZhRuns) {
+            rl->t[rl->n * 64u] = (rs - rl->wb) | ((re - rl->wb) << 16);
+            rl->n++;
+        } else viterbi_run(v, im, rs, re, m, le);
+    };
+    uint32_t j = 0, bs = 0, be = 0;
+    bool ok = true;
+    if (!src.next(j, bs, be)) return ok;
+    uint32_t p = bs, sp = (bs - v.wb) / 3u, run_s = 0, run_n = 0;  // sp: GrpZvT::bl's slot of p
+    for (;;) {
+        if (p >= be) {  // the block is done: its last run, then the lane's next block
+            if (HMM && run_n) run_end(run_s, be, run_n);
+            run_n = 0;
+            if (!src.next(j, bs, be)) break;
+            p = bs;
+            sp = (bs - v.wb) / 3u;
+            continue;
+        }
+        const uint32_t L = v.bls[sp];
+        if (L == 0) {  // tail index -1: cutDAG's slice panics in the reference
+            ok = false;
+            p = be;
+            run_n = 0;
+            continue;
+        }
+        const uint32_t pe = p + 3u * L;
+        if (HMM && L == 1u) {
+            run_s = run_n ? run_s : p;
+            run_n++;
+        } else {
+            if (HMM && run_n) {
+                run_end(run_s, p, run_n);
+                run_n = 0;
+            }
+            token(p, pe);
+        }
+        p = pe;
+        sp += L;
+    }
+    return ok;
+}
+
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1615,7 +1672,8 @@ __device__ __forceinline__ void zh_chunk_main(const uint8_t* __restrict__ text, 
         bool ok;
         RunList rl{runs, wb, 0u};
         RunList* const rlp = (HMM && A3) ? &rl : nullptr;
-        ok = zh_fwd_lane<HMM>(v, im, src, le, rlp);
+        if constexpr (A3) ok = zh_fwd_a3<HMM>(v, im, src, sb, eb, le, &rl);
+        else ok = zh_fwd_lane<HMM>(v, im, src, le, rlp);
         if (st) {
             const uint64_t t = __builtin_amdgcn_s_memtime();
             st[8] += t - st[7];
