@@ -157,7 +157,8 @@ hipError_t run_small(const DevImage& im, const uint8_t* text, uint32_t nbytes, c
 // host memory of kSnapWords u32, by a one-workgroup kernel.
 constexpr uint32_t kSnapWords = CNT_CLEAR + 4;
 // Zero `bytes` (a multiple of 4) at p with a kernel on `stream`.
-hipError_t run_zero(void* p, uint64_t bytes, hipStream_t stream);
+// (and, in the same launch, bytes2 <= 1024 at p2)
+hipError_t run_zero(void* p, uint64_t bytes, hipStream_t stream, void* p2 = nullptr, uint32_t bytes2 = 0);
 hipError_t run_snap(const Work& w, uint64_t nbytes, uint32_t* out, hipStream_t stream);
 
 // Resident k_zh workgroups per CU (occupancy API).

@@ -2868,20 +2868,23 @@ __global__ __launch_bounds__(256) void k_snap(const uint32_t* __restrict__ count
 
 // Zero n u32 words (instead of hipMemsetAsync, which may go to the copy engine and
 // queue there behind the host pipeline's bulk transfers).
-__global__ __launch_bounds__(256) void k_zero(uint32_t* __restrict__ p, uint64_t n, bool v4) {
+__global__ __launch_bounds__(256) void k_zero(uint32_t* __restrict__ p, uint64_t n, bool v4,
+                                             uint32_t* __restrict__ p2, uint32_t n2) {
     const uint64_t stride = (uint64_t)gridDim.x * 256u, t0 = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (t0 < n2) p2[t0] = 0u;  // a second, small range (n2 <= 256) in the same launch
     const uint64_t n4 = v4 ? n / 4u : 0u;
     uint4* p4 = reinterpret_cast<uint4*>(p);
     for (uint64_t i = t0; i < n4; i += stride) p4[i] = make_uint4(0u, 0u, 0u, 0u);
     for (uint64_t i = 4u * n4 + t0; i < n; i += stride) p[i] = 0u;
 }
 
-hipError_t run_zero(void* p, uint64_t bytes, hipStream_t stream) {
+hipError_t run_zero(void* p, uint64_t bytes, hipStream_t stream, void* p2, uint32_t bytes2) {
     const uint64_t n = bytes / 4u;  // (callers pass whole words)
-    if (!n) return hipSuccess;
+    if (!n && !bytes2) return hipSuccess;
     const bool v4 = ((uintptr_t)p & 15u) == 0;
     const uint32_t grid = (uint32_t)std::min<uint64_t>(2048u, (n / 4u + 255u) / 256u + 1u);
-    hipLaunchKernelGGL(k_zero, dim3(grid), dim3(256), 0, stream, reinterpret_cast<uint32_t*>(p), n, v4);
+    hipLaunchKernelGGL(k_zero, dim3(grid), dim3(256), 0, stream, reinterpret_cast<uint32_t*>(p), n, v4,
+                       reinterpret_cast<uint32_t*>(p2), bytes2 / 4u);
     return hipGetLastError();
 }
 
@@ -3500,8 +3503,8 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     const uint32_t grid_zh = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(lc.grid_zh, (ngroups + 3) / 4));
     hipError_t e;
     // (kernels, not hipMemsetAsync: see k_zero; k_mark_walk clears the token bitmaps tile by tile)
-    if ((e = run_zero(w.counters, CNT_CLEAR * sizeof(uint32_t), stream))) return e;
-    if ((e = run_zero(w.docbits, (nwords + 2) * 4, stream))) return e;
+    // (one launch: the document bitmap and, beside it, the counters)
+    if ((e = run_zero(w.docbits, (nwords + 2) * 4, stream, w.counters, CNT_CLEAR * sizeof(uint32_t)))) return e;
     if (nbytes == 0) {
         if ((e = run_zero(w.doc_tok, (ndocs + 1) * sizeof(uint64_t), stream))) return e;
         return hipSuccess;
