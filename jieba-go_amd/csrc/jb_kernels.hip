@@ -1394,6 +1394,8 @@ struct RunList {
     uint32_t* t;
     uint32_t wb;
     uint32_t n;
+    uint32_t* pool = nullptr;  // zh_fwd_a3: the wave's run list (kZhRuns * 64 entries) and its count
+    uint32_t* cnt = nullptr;
 };
 
 // The forward half of viterbi for all of a lane's deferred runs (all-3-byte
@@ -1576,12 +1578,17 @@ __device__ __forceinline__ bool zh_fwd_a3(const GrpZvT<true>& v, const DevImage&
         atomicOr(sb + ((a >> 5) - w0), 1u << (a & 31u));
         atomicOr(eb + (((b - 1u) >> 5) - w0), 1u << ((b - 1u) & 31u));
     };
+    // A run of more than one rune goes to the wave's run list (one LDS atomic), whose
+    // entries are then dealt to the lanes round-robin: runs are short (2-4 runes,
+    // about one per two blocks), and a lane's own runs would leave most lanes idle
+    // while a few work through several.  A full list (rare) cuts the run here.
     auto run_end = [&](uint32_t rs, uint32_t re, uint32_t m) __attribute__((always_inline)) {
         if (m == 1u) token(rs, re);  // a single rune is always "S" (:672-674)
-        else if (rl->n < kZhRuns) {
-            rl->t[rl->n * 64u] = (rs - rl->wb) | ((re - rl->wb) << 16);
-            rl->n++;
-        } else viterbi_run(v, im, rs, re, m, le);
+        else {
+            const uint32_t k = atomicAdd(rl->cnt, 1u);
+            if (k < kZhRuns * 64u) rl->pool[k] = (rs - rl->wb) | ((re - rl->wb) << 16);
+            else viterbi_run(v, im, rs, re, m, le);
+        }
     };
     uint32_t j = 0, bs = 0, be = 0;
     bool ok = true;
@@ -1643,6 +1650,7 @@ template <bool HMM, bool A3>
 __device__ __forceinline__ void zh_chunk_main(const uint8_t* __restrict__ text, const DevImage& im,
                               const uint64_t* __restrict__ erec, double* __restrict__ gbest, uint8_t* bls,
                               double* ring, const char* rb0, uint32_t lb, uint32_t* rb32, uint32_t* runs,
+                              uint32_t* nrun,
                               const TblSrc& src, uint32_t wb, uint32_t lane,
                               uint32_t* __restrict__ counters, uint32_t winw, uint32_t& nties, uint64_t* st) {
     const GrpZvT<A3> v{text, bls, wb};
@@ -1670,10 +1678,18 @@ __device__ __forceinline__ void zh_chunk_main(const uint8_t* __restrict__ text, 
     {
         LdsEmitter le(sb, eb, wb >> 5);
         bool ok;
-        RunList rl{runs, wb, 0u};
+        RunList rl{runs, wb, 0u, runs - lane, nrun};
         RunList* const rlp = (HMM && A3) ? &rl : nullptr;
-        if constexpr (A3) ok = zh_fwd_a3<HMM>(v, im, src, sb, eb, le, &rl);
-        else ok = zh_fwd_lane<HMM>(v, im, src, le, rlp);
+        if constexpr (A3) {
+            if (lane == 0u) *nrun = 0u;
+            wave_sync();
+            ok = zh_fwd_a3<HMM>(v, im, src, sb, eb, le, &rl);
+            wave_sync();
+            const uint32_t nr = min(*nrun, kZhRuns * 64u);  // the pool's entries k = lane + 64 r are this lane's
+            rl.n = nr > lane ? (nr - lane + 63u) / 64u : 0u;
+        } else {
+            ok = zh_fwd_lane<HMM>(v, im, src, le, rlp);
+        }
         if (st) {
             const uint64_t t = __builtin_amdgcn_s_memtime();
             st[8] += t - st[7];
@@ -1780,6 +1796,7 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
     __shared__ uint32_t s_tbl[4][kZhChunk];   // the chunk's blocks as found, then as dealt to the lanes
     __shared__ uint32_t s_hist[4][64];
     __shared__ uint32_t s_runs[4][kZhRuns * 64];
+    __shared__ uint32_t s_nrun[4];  // entries in a wave's run list (zh_fwd_a3)
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     double* ring = s_rb[wv] + lane;
     const char* const rb0 = reinterpret_cast<const char*>(&s_rb[0][0]);  // (rec_fold_a3's ring addressing)
@@ -1934,10 +1951,10 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
                 stv[3]++;
             }
             if (all3)
-                zh_chunk_main<HMM, true>(text, im, erec, gbest, s_bl[wv], ring, rb0, lb, rb32, s_runs[wv] + lane, src, wb, lane,
+                zh_chunk_main<HMM, true>(text, im, erec, gbest, s_bl[wv], ring, rb0, lb, rb32, s_runs[wv] + lane, &s_nrun[wv], src, wb, lane,
                                          counters, winw, nties, st);
             else
-                zh_chunk_main<HMM, false>(text, im, erec, gbest, s_bl[wv], ring, rb0, lb, rb32, s_runs[wv] + lane, src, wb,
+                zh_chunk_main<HMM, false>(text, im, erec, gbest, s_bl[wv], ring, rb0, lb, rb32, s_runs[wv] + lane, &s_nrun[wv], src, wb,
                                           lane, counters, winw, nties, st);
             // the window's token words: consecutive words per lane, one OR each (edge
             // words are shared with neighbouring groups and with k_nonzh)
