@@ -709,9 +709,9 @@ static int launch_pipeline(Device* d, const Work& w, const uint8_t* d_text, uint
         if (n == 0) n = 1;
         fprintf(stderr, "[jb] k_zh clocks/wave: setup %.0f dp %.0f fwd walk %.0f viterbi fwd %.0f back+flush+rest %.0f "
                         "total %.0f; chunks/wave %.1f; lane DP steps %.0f vs 64*max %.0f (DP lane use %.2f); blocks past "
-                        "the window per chunk %.3f\n",
+                        "the window per chunk %.3f; Viterbi lane use %.2f (longest lane %.1f runes per chunk)\n",
                 a[0] / n, a[1] / n, a[8] / n, a[9] / n, a[2] / n, a[6] / n, a[3] / n, a[4] / n, 64.0 * a[5] / n,
-                a[4] / (64.0 * a[5] + 1e-9), a[7] / (a[3] + 1e-9));
+                a[4] / (64.0 * a[5] + 1e-9), a[7] / (a[3] + 1e-9), a[10] / (64.0 * a[11] + 1e-9), a[11] / (a[3] + 1e-9));
         HIPCHK(hipMemsetAsync(d->w.dbg, 0, (size_t)nwv * 128, s));
         const uint64_t nww = (nbytes + kTileBytes - 1) / kTileBytes * 4;
         std::vector<uint64_t> sw(nww * 8);

@@ -88,6 +88,19 @@ int main(int argc, char** argv) {
     Lru l2(4u << 20 >> 7), l2r(4u << 20 >> 7);
     std::vector<uint64_t> line_hits((img.cells.size() * 8 >> 7) + 1, 0);
     uint64_t probes = 0, runes = 0, walks = 0;
+    // Child-code filters: per node with children, bit h(code) of each child's code for
+    // B-bit filters (h = code mod B); a probe the filter rejects need not be made.
+    constexpr int kFB[] = {1, 2, 3, 4, 5, 6, 8, 12, 16};
+    constexpr int kNF = sizeof(kFB) / sizeof(kFB[0]);
+    std::vector<uint32_t> filt(img.cells.size() * kNF, 0);
+    for (size_t t = 0; t < img.cells.size(); t++) {
+        const uint32_t ck = jb_cell_check(img.cells[t]);
+        if (ck == 0 || ck == JB_CHECK_ROOT) continue;
+        const uint32_t par = ck - 1u;
+        const uint32_t code = (uint32_t)t - jb_cell_base(img.cells[par]);
+        for (int f = 0; f < kNF; f++) filt[(size_t)par * kNF + f] |= 1u << (code % kFB[f]);
+    }
+    uint64_t miss_probes = 0, rejected[kNF] = {0};
     auto flush = [&]() {
         for (size_t i = 0; i < run.size(); i++) {
             runes++;
@@ -103,6 +116,12 @@ int main(int argc, char** argv) {
                 l2.touch(t * 8 >> 7);
                 line_hits[t * 8 >> 7]++;
                 const uint64_t ch = img.cells[t];
+                if (jb_cell_check(ch) != id + 1u) {
+                    miss_probes++;
+                    const uint32_t code = img.code[jb_row(pm, run[j])];
+                    for (int f = 0; f < kNF; f++)
+                        if (!((filt[(size_t)id * kNF + f] >> (code % kFB[f])) & 1u)) rejected[f]++;
+                }
                 if (jb_cell_check(ch) != id + 1u || !jb_cell_hc(ch)) break;
                 id = (uint32_t)t;
                 c = ch;
@@ -138,5 +157,9 @@ int main(int argc, char** argv) {
     printf("cell probes: LRU-4MB hit %.4f; hottest lines for 90/95/99%% of probes: %.2f / %.2f / %.2f MB\n",
            (double)l2.hit / (double)(l2.hit + l2.miss), at90 * 128 / 1e6, at95 * 128 / 1e6, at99 * 128 / 1e6);
     printf("l1row loads: LRU-4MB hit %.4f\n", (double)l2r.hit / (double)(l2r.hit + l2r.miss));
+    printf("walk-ending misses %llu (%.3f of probes); rejected by a B-bit child-code filter:",
+           (unsigned long long)miss_probes, (double)miss_probes / (double)probes);
+    for (int f = 0; f < kNF; f++) printf(" B=%d %.3f", kFB[f], (double)rejected[f] / (double)probes);
+    printf(" (of all probes)\n");
     return 0;
 }
