@@ -191,6 +191,9 @@ struct Device {
     } gkey{};
     hipGraphExec_t gexec = nullptr;  // captured for gkey (null until the key repeats)
     uint64_t work_gen = 0;           // bumped whenever the workspace is reallocated
+    // The workspace's document bitmap may hold set bits: a new workspace, or a pipeline
+    // launch that failed part way.  Pipelines leave it all zeros (k_docbits, k_nonzh).
+    bool docbits_dirty = true;
     uint64_t gkey_gen = 0;
 };
 
@@ -559,6 +562,7 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     }
     w.cap_bytes = nb;
     w.cap_docs = ndc;
+    d->docbits_dirty = true;
     return JB_OK;
 }
 
@@ -649,8 +653,20 @@ static int init_launch_cfg(Device* d) {
     return JB_OK;
 }
 
+static int launch_pipeline_(Device* d, const Work& w, const uint8_t* d_text, uint64_t nbytes,
+                            const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, hipStream_t s, const MaskOut* mask);
 static int launch_pipeline(Device* d, const Work& w, const uint8_t* d_text, uint64_t nbytes,
                            const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, hipStream_t s, const MaskOut* mask) {
+    if (d->docbits_dirty) {  // the whole bitmap, once (see Device::docbits_dirty)
+        HIPCHK(run_zero(w.docbits, w.bits_stride * 4, s));
+        d->docbits_dirty = false;
+    }
+    const int rc = launch_pipeline_(d, w, d_text, nbytes, d_doc_off, ndocs, hmm, s, mask);
+    if (rc) d->docbits_dirty = true;
+    return rc;
+}
+static int launch_pipeline_(Device* d, const Work& w, const uint8_t* d_text, uint64_t nbytes,
+                            const uint64_t* d_doc_off, uint32_t ndocs, bool hmm, hipStream_t s, const MaskOut* mask) {
     static const bool dbg = getenv("JB_DEBUG") != nullptr;
     const LaunchCfg& lc = d->lc;
     d->last_nbytes = nbytes;

@@ -136,9 +136,13 @@ struct LdsEmitter {
 // ---------------------------------------------------------------------------
 // k_docbits
 // ---------------------------------------------------------------------------
+// The bitmap is all zeros between pipeline runs: k_nonzh clears the words a run
+// set (one per document), after k_mark_walk (their only reader) is done with them.  The first
+// launch also clears the run's counters (no kernel before it uses them).
 __global__ void k_docbits(const uint64_t* __restrict__ doc_off, uint32_t ndocs, uint64_t nbytes,
-                          uint32_t* __restrict__ bits) {
+                          uint32_t* __restrict__ bits, uint32_t* __restrict__ counters) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d < CNT_CLEAR) counters[d] = 0u;
     if (d >= ndocs) return;
     const uint64_t o = doc_off[d];
     if (o < nbytes) atomicOr(bits + (o >> 5), 1u << (o & 31u));
@@ -2720,9 +2724,16 @@ __global__ __launch_bounds__(256) void k_nonzh(const uint8_t* __restrict__ text,
                                                const uint32_t* __restrict__ lanemask,
                                                const uint2* __restrict__ tile_cnt, uint32_t ntiles,
                                                const uint64_t* __restrict__ alnum16, uint32_t* __restrict__ sbits,
-                                               uint32_t* __restrict__ ebits) {
+                                               uint32_t* __restrict__ ebits, uint32_t* __restrict__ docbits,
+                                               const uint64_t* __restrict__ doc_off, uint32_t ndocs) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[256][80];
     const uint32_t nch = (nbytes + 15u) >> 4, nw = (nch + 63u) >> 6;
+    // the words k_docbits set back to zero for the next run (k_mark_walk, their only
+    // reader, is done): one store per document
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < ndocs; d += gridDim.x * blockDim.x) {
+        const uint64_t o = doc_off[d];
+        if (o < nbytes) docbits[o >> 5] = 0u;
+    }
     Emitter em(sbits, ebits);
     for (uint32_t wi = blockIdx.x * blockDim.x + threadIdx.x; wi < nw; wi += gridDim.x * blockDim.x) {
         uint64_t a = alnum16[wi];
@@ -2845,20 +2856,34 @@ __global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits,
     }
 }
 
-// tokens of document d: [doc_tok[d], doc_tok[d+1]) = lower_bound over starts
-__global__ void k_doc_tok(const uint64_t* __restrict__ doc_off, uint32_t ndocs, const uint32_t* __restrict__ tok_start,
-                          const uint32_t* __restrict__ counters, uint64_t* __restrict__ doc_tok) {
-    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-    if (d > ndocs) return;
+// tokens of document d: [doc_tok[d], doc_tok[d+1]) = lower_bound over starts.
+// Sixteen lanes per document search 16-ary: each trip, lane k probes the last start
+// of the k-th sixteenth of the range and a ballot counts the sixteenths wholly before
+// the target (log16 dependent loads per document instead of log2: this kernel is
+// load latency, and for a small batch its whole time).
+__global__ __launch_bounds__(256) void k_doc_tok(const uint64_t* __restrict__ doc_off, uint32_t ndocs,
+                                                 const uint32_t* __restrict__ tok_start,
+                                                 const uint32_t* __restrict__ counters, uint64_t* __restrict__ doc_tok) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t d = g >> 4, k = threadIdx.x & 15u, gsh = threadIdx.x & 48u;  // (16-lane group of the wave)
+    if (d > ndocs) return;  // (whole groups: a group is one document)
     const uint32_t n = counters[CNT_NTOK];
     const uint64_t target = doc_off[d];
-    uint32_t lo = 0, hi = n;
+    uint32_t lo = 0, hi = n;  // the answer is in [lo, hi]
     while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if ((uint64_t)tok_start[mid] < target) lo = mid + 1;
-        else hi = mid;
+        const uint32_t s = (hi - lo + 15u) >> 4;  // a sixteenth, rounded up
+        const uint32_t i = lo + (k + 1u) * s - 1u;
+        const bool before = i < hi && (uint64_t)tok_start[i] < target;
+        const uint32_t c = (uint32_t)__popcll((__ballot(before) >> gsh) & 0xFFFFull);
+        const uint32_t nlo = lo + c * s;
+        if (s == 1u || nlo >= hi) {
+            lo = min(nlo, hi);
+            break;
+        }
+        hi = min(hi, nlo + s - 1u);  // (the probe ending the c-th sixteenth is >= target)
+        lo = nlo;
     }
-    doc_tok[d] = lo;
+    if (k == 0u) doc_tok[d] = lo;
 }
 
 // Boundary-mask output (jb_cut_batch_mask): a piece's token bitmaps (bit j = byte j
@@ -3536,17 +3561,13 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     // k_zh: a persistent grid, but no more 4-wave workgroups than the batch has groups
     const uint64_t ngroups = (nbytes + grp - 1) / grp;
     const uint32_t grid_zh = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(lc.grid_zh, (ngroups + 3) / 4));
-    hipError_t e;
-    // (kernels, not hipMemsetAsync: see k_zero; k_mark_walk clears the token bitmaps tile by tile)
-    // (one launch: the document bitmap and, beside it, the counters)
-    if ((e = run_zero(w.docbits, (nwords + 2) * 4, stream, w.counters, CNT_CLEAR * sizeof(uint32_t)))) return e;
-    if (nbytes == 0) {
-        if ((e = run_zero(w.doc_tok, (ndocs + 1) * sizeof(uint64_t), stream))) return e;
-        return hipSuccess;
-    }
-    if (ndocs)
-        JB_TIMED(K_DOCBITS, hipLaunchKernelGGL(k_docbits, dim3((ndocs + 255) / 256), dim3(256), 0, stream,
-                                               d_doc_off, ndocs, nbytes, w.docbits));
+    // No clearing pass: the document bitmap is all zeros between runs (k_nonzh clears
+    // what k_docbits set; a fresh or dirty workspace is cleared by the caller), k_docbits
+    // clears the counters and k_mark_walk the token bitmaps, tile by tile.
+    if (nbytes == 0)  // (kernels, not hipMemsetAsync: see k_zero)
+        return run_zero(w.doc_tok, (ndocs + 1) * sizeof(uint64_t), stream, w.counters, CNT_CLEAR * sizeof(uint32_t));
+    JB_TIMED(K_DOCBITS, hipLaunchKernelGGL(k_docbits, dim3(std::max(1u, (ndocs + 255) / 256)), dim3(256), 0, stream,
+                                           d_doc_off, ndocs, nbytes, w.docbits, w.counters));
     JB_TIMED(K_MARK_WALK, hipLaunchKernelGGL(k_mark_walk, dim3(ntiles), dim3(256), 0, stream, d_text, nbytes,
                                              w.docbits, im, w.lanemask, w.tile_cnt, w.erec + kErecPad,
                                              w.tile4, w.alnum16, w.sbits, w.ebits, diag, w.dbg_walk));
@@ -3589,7 +3610,7 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         const uint32_t nw = (uint32_t)((nbytes + 1023u) / 1024u);  // alnum16 words
         JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3((nw + 255u) / 256u), dim3(256), 0, stream, d_text,
                                              (uint32_t)nbytes, w.lanemask, w.tile_cnt, ntiles, w.alnum16, w.sbits,
-                                             w.ebits));
+                                             w.ebits, w.docbits, d_doc_off, ndocs));
     }
     if (mask) {  // boundary masks instead of spans
         const uint64_t nout = ((mask->rel & 63u) + nbytes + 63u) >> 6;
@@ -3602,11 +3623,12 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     }
     JB_TIMED(K_TOK_COUNT, hipLaunchKernelGGL((k_tok<false>), dim3(nttiles), dim3(256), 0, stream, w.sbits, w.ebits,
                                              nwords, w.ttile_cnt, w.supt, w.counters, nullptr, nullptr));
-    JB_TIMED(K_SCAN_TOK, hipLaunchKernelGGL(k_sup, dim3((nttiles + 255) / 256), dim3(256), 0, stream, w.ttile_cnt,
-                                            nttiles, w.supt));
+    if (nttiles > 256u)  // (k_tok's write pass reads the sums of whole groups of 256 tiles only)
+        JB_TIMED(K_SCAN_TOK, hipLaunchKernelGGL(k_sup, dim3((nttiles + 255) / 256), dim3(256), 0, stream,
+                                                w.ttile_cnt, nttiles, w.supt));
     JB_TIMED(K_TOK_WRITE, hipLaunchKernelGGL((k_tok<true>), dim3(nttiles), dim3(256), 0, stream, w.sbits, w.ebits,
                                              nwords, w.ttile_cnt, w.supt, w.counters, w.tok_start, w.tok_end));
-    JB_TIMED(K_DOC_TOK, hipLaunchKernelGGL(k_doc_tok, dim3((ndocs + 1 + 255) / 256), dim3(256), 0, stream,
+    JB_TIMED(K_DOC_TOK, hipLaunchKernelGGL(k_doc_tok, dim3((uint32_t)((16ull * (ndocs + 1) + 255) / 256)), dim3(256), 0, stream,
                                            d_doc_off, ndocs, w.tok_start, w.counters, w.doc_tok));
     return hipGetLastError();
 }
