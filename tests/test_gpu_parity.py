@@ -845,3 +845,24 @@ def test_degenerate_dictionary_weights(tmp_path, mini_paths, entries, monkeypatc
             if all(outcome(o.cut, t, hmm) != "panic" for t in texts):
                 _cmp_batch(tk, o, buf, off, hmm, f"degenerate dict JB_SMALL={small}")
         tk.close()
+
+
+def test_document_bitmap_between_runs(small):
+    """The document-start bitmap is not cleared by a pass of its own: k_nonzh clears
+    the words a run set.  The same bytes cut under different document layouts, one
+    after another on one context (pipeline sizes, past k_small), must each match the
+    oracle: a start left over from an earlier run would split a Han run."""
+    tk, o, s = small
+    rng = random.Random(7)
+    text = "".join(rng.choice(["中文", "文字", "测试", "丁", "，", "abc", " ", "𠀀"]) for _ in range(40000)).encode()
+    n = len(text)
+    buf = np.frombuffer(text + b"\0" * 16, np.uint8)
+    layouts = []
+    for k in range(3):  # random cut points (a cut may fall inside a rune: invalid bytes, as Go strings)
+        cuts = sorted(set(rng.randrange(1, n) for _ in range(200 * (k + 1))))
+        layouts.append(np.array([0] + cuts + [n], np.uint64))
+    layouts.append(np.array([0, n], np.uint64))
+    for hmm in (0, 1):
+        for rep in range(2):
+            for i, off in enumerate(layouts):
+                _cmp_batch(tk, o, buf, off, hmm, f"layout {i} rep {rep}")
