@@ -2857,34 +2857,46 @@ __global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits,
 }
 
 // tokens of document d: [doc_tok[d], doc_tok[d+1]) = lower_bound over starts.
-// Sixteen lanes per document search 16-ary: each trip, lane k probes the last start
-// of the k-th sixteenth of the range and a ballot counts the sixteenths wholly before
-// the target (log16 dependent loads per document instead of log2: this kernel is
-// load latency, and for a small batch its whole time).
+// G lanes per document.  G = 16 (a small batch: few documents, so the kernel's time
+// is one search's dependent loads): each trip, lane k probes the last start of the
+// k-th sixteenth of the range and a ballot counts the sixteenths wholly before the
+// target, log16 loads instead of log2.  G = 1 (many documents: their searches hide
+// each other's latency, and 16 lanes each would cost more loads in all): binary.
+template <uint32_t G>
 __global__ __launch_bounds__(256) void k_doc_tok(const uint64_t* __restrict__ doc_off, uint32_t ndocs,
                                                  const uint32_t* __restrict__ tok_start,
                                                  const uint32_t* __restrict__ counters, uint64_t* __restrict__ doc_tok) {
+    static_assert(G == 1u || G == 16u, "binary or 16-ary");
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t d = g >> 4, k = threadIdx.x & 15u, gsh = threadIdx.x & 48u;  // (16-lane group of the wave)
+    const uint32_t d = g / G, k = threadIdx.x & (G - 1u), gsh = threadIdx.x & (63u & ~(G - 1u));
     if (d > ndocs) return;  // (whole groups: a group is one document)
     const uint32_t n = counters[CNT_NTOK];
     const uint64_t target = doc_off[d];
     uint32_t lo = 0, hi = n;  // the answer is in [lo, hi]
-    while (lo < hi) {
-        const uint32_t s = (hi - lo + 15u) >> 4;  // a sixteenth, rounded up
-        const uint32_t i = lo + (k + 1u) * s - 1u;
-        const bool before = i < hi && (uint64_t)tok_start[i] < target;
-        const uint32_t c = (uint32_t)__popcll((__ballot(before) >> gsh) & 0xFFFFull);
-        const uint32_t nlo = lo + c * s;
-        if (s == 1u || nlo >= hi) {
-            lo = min(nlo, hi);
-            break;
+    if constexpr (G == 1u) {
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((uint64_t)tok_start[mid] < target) lo = mid + 1;
+            else hi = mid;
         }
-        hi = min(hi, nlo + s - 1u);  // (the probe ending the c-th sixteenth is >= target)
-        lo = nlo;
+    } else {
+        while (lo < hi) {
+            const uint32_t s = (hi - lo + 15u) >> 4;  // a sixteenth, rounded up
+            const uint32_t i = lo + (k + 1u) * s - 1u;
+            const bool before = i < hi && (uint64_t)tok_start[i] < target;
+            const uint32_t c = (uint32_t)__popcll((__ballot(before) >> gsh) & 0xFFFFull);
+            const uint32_t nlo = lo + c * s;
+            if (s == 1u || nlo >= hi) {
+                lo = min(nlo, hi);
+                break;
+            }
+            hi = min(hi, nlo + s - 1u);  // (the probe ending the c-th sixteenth is >= target)
+            lo = nlo;
+        }
     }
     if (k == 0u) doc_tok[d] = lo;
 }
+constexpr uint32_t kDocTokWide = 16384;  // documents from which k_doc_tok searches one lane each
 
 // Boundary-mask output (jb_cut_batch_mask): a piece's token bitmaps (bit j = byte j
 // of the piece, u32 words) into the range's u64 bitmaps at bit offset `rel`, bits
@@ -3628,8 +3640,12 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                                 w.ttile_cnt, nttiles, w.supt));
     JB_TIMED(K_TOK_WRITE, hipLaunchKernelGGL((k_tok<true>), dim3(nttiles), dim3(256), 0, stream, w.sbits, w.ebits,
                                              nwords, w.ttile_cnt, w.supt, w.counters, w.tok_start, w.tok_end));
-    JB_TIMED(K_DOC_TOK, hipLaunchKernelGGL(k_doc_tok, dim3((uint32_t)((16ull * (ndocs + 1) + 255) / 256)), dim3(256), 0, stream,
-                                           d_doc_off, ndocs, w.tok_start, w.counters, w.doc_tok));
+    if (ndocs >= kDocTokWide)
+        JB_TIMED(K_DOC_TOK, hipLaunchKernelGGL(k_doc_tok<1>, dim3((ndocs + 1 + 255) / 256), dim3(256), 0, stream,
+                                               d_doc_off, ndocs, w.tok_start, w.counters, w.doc_tok));
+    else
+        JB_TIMED(K_DOC_TOK, hipLaunchKernelGGL(k_doc_tok<16>, dim3((16u * (ndocs + 1) + 255) / 256), dim3(256), 0,
+                                               stream, d_doc_off, ndocs, w.tok_start, w.counters, w.doc_tok));
     return hipGetLastError();
 }
 
