@@ -2793,7 +2793,7 @@ __global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits,
     constexpr uint32_t W = kTokTileWords / 256;  // bitmap words per lane
     constexpr uint32_t kCap = 3072;              // tokens per tile staged in LDS
     __shared__ uint32_t lds[8];
-    __shared__ uint32_t s_s[WRITE ? kCap : 1], s_e[WRITE ? kCap : 1];
+    __shared__ __attribute__((aligned(16))) uint32_t s_s[WRITE ? kCap + 4 : 1], s_e[WRITE ? kCap + 4 : 1];
     const uint64_t w0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * W;
     PrefixLoads pl{0u, 0u};
     if (WRITE) pl = pf_load(tile_cnt, supt, blockIdx.x);
@@ -2832,8 +2832,13 @@ __global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits,
     // spans go to LDS in tile order, then out in one coalesced pass (a lane's own
     // tokens are ~60 bytes apart in the output: direct stores touch a line each)
     const bool staged = ts <= kCap && te <= kCap;
-    uint32_t* os = staged ? s_s : tok_start + to.x;
-    uint32_t* oe = staged ? s_e : tok_end + to.y;
+    // staged at LDS index (output index mod 4) + k, so that LDS and output share their
+    // 16-byte alignment and the copy-out moves four spans per lane and store
+    // (k_tok_write 0.298 -> 0.288 ms at 1 GiB; caller arrays not 16-byte aligned: one each)
+    const bool v4 = (((uintptr_t)tok_start | (uintptr_t)tok_end) & 15u) == 0u;
+    const uint32_t shs = v4 ? (to.x & 3u) : 0u, she = v4 ? (to.y & 3u) : 0u;
+    uint32_t* os = staged ? s_s + shs : tok_start + to.x;
+    uint32_t* oe = staged ? s_e + she : tok_end + to.y;
     uint32_t gs = xs, ge = xe;
 #pragma unroll
     for (uint32_t k = 0; k < W; k++) {
@@ -2851,6 +2856,23 @@ __global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits,
     }
     if (staged) {
         __syncthreads();
+        if (v4) {
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            auto out = [&](const uint32_t* a, uint32_t sh, uint32_t n, uint32_t* g) {  // g: output at LDS index 0
+                const uint32_t lo = (sh + 3u) & ~3u, hi = (sh + n) & ~3u;  // whole vectors: [lo, hi)
+                if (lo < hi) {
+                    for (uint32_t p = lo + 4u * threadIdx.x; p < hi; p += 1024u)
+                        __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(a + p), reinterpret_cast<u32x4*>(g + p));
+                    if (threadIdx.x < lo - sh) __builtin_nontemporal_store(a[sh + threadIdx.x], g + sh + threadIdx.x);
+                    if (threadIdx.x < sh + n - hi) __builtin_nontemporal_store(a[hi + threadIdx.x], g + hi + threadIdx.x);
+                } else if (threadIdx.x < n) {
+                    __builtin_nontemporal_store(a[sh + threadIdx.x], g + sh + threadIdx.x);
+                }
+            };
+            out(s_s, shs, ts, tok_start + to.x - shs);
+            out(s_e, she, te, tok_end + to.y - she);
+            return;
+        }
         for (uint32_t k = threadIdx.x; k < ts; k += 256u) __builtin_nontemporal_store(s_s[k], tok_start + to.x + k);
         for (uint32_t k = threadIdx.x; k < te; k += 256u) __builtin_nontemporal_store(s_e[k], tok_end + to.y + k);
     }
