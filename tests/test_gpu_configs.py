@@ -273,3 +273,34 @@ def test_one_large_document_split(syn_small, ndev, piece_kib, monkeypatch):
             ms, me = _mask_spans(tk, bb, ff, hmm)
             _cmp(ms, me, od, os_, oe, od, "masks")
     tk.close()
+
+
+def test_cut_device_into_unaligned_outputs(syn_small):
+    """Caller span arrays that are not 16-byte aligned: k_tok's write pass then stores
+    one span per lane instead of four (its 16-byte stores need aligned outputs)."""
+    import torch
+    dp, ep, s = syn_small
+    tk = J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep))
+    o = O.Oracle.from_files(dp, ep, 0)
+    buf, off = s.corpus(synth.KIND_DOCS, 65, target_bytes=2 << 20)[:2]
+    want = o.cut_batch(buf, off, True, nthreads=8)
+    nbytes, nd = int(off[-1]), len(off) - 1
+    d_text = torch.from_numpy(np.ascontiguousarray(buf[: nbytes + 64])).cuda()
+    d_off = torch.from_numpy(np.asarray(off, np.int64)).cuda()
+    o_s = torch.full((nbytes + 8,), -1, dtype=torch.int32, device="cuda")
+    o_e = torch.full((nbytes + 8,), -1, dtype=torch.int32, device="cuda")
+    o_d = torch.empty(nd + 1, dtype=torch.int64, device="cuda")
+    o_n = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for sh in (1, 2, 3):  # 4, 8, 12 bytes past a 16-byte boundary
+        o_s.fill_(-1)
+        o_e.fill_(-1)
+        tk.cut_device_into(d_text.data_ptr(), nbytes, d_off.data_ptr(), nd, True, o_s.data_ptr() + 4 * sh,
+                           o_e.data_ptr() + 4 * sh, nbytes + 1, o_d.data_ptr(), o_n.data_ptr(),
+                           torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        n = int(o_n.item())
+        got = (o_s[sh:sh + n].cpu().numpy().view(np.uint32).astype(np.uint64),
+               o_e[sh:sh + n].cpu().numpy().view(np.uint32).astype(np.uint64), o_d.cpu().numpy().view(np.uint64))
+        _cmp(*got, *want, f"outputs {4 * sh} bytes past alignment")
+        assert int(o_s[sh - 1].item()) == -1 and int(o_s[sh + n].item()) == -1  # nothing written outside
+    tk.close()
