@@ -2790,8 +2790,10 @@ __global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits,
                                              uint64_t nwords, uint2* __restrict__ tile_cnt,
                                              const uint2* __restrict__ supt, uint32_t* __restrict__ counters,
                                              uint32_t* __restrict__ tok_start, uint32_t* __restrict__ tok_end) {
-    constexpr uint32_t W = kTokTileWords / 256;  // bitmap words per lane
-    constexpr uint32_t kCap = 3072;              // tokens per tile staged in LDS
+    // bitmap words per lane: the write pass takes a token tile per workgroup, the count
+    // pass two (16-byte loads, half the workgroups; a tile's count is the half's sum)
+    constexpr uint32_t W = (WRITE ? 1u : 2u) * (kTokTileWords / 256);
+    constexpr uint32_t kCap = 3072;              // tokens per tile staged in LDS (write pass)
     __shared__ uint32_t lds[8];
     __shared__ __attribute__((aligned(16))) uint32_t s_s[WRITE ? kCap + 4 : 1], s_e[WRITE ? kCap + 4 : 1];
     const uint64_t w0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * W;
@@ -2799,10 +2801,17 @@ __global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits,
     if (WRITE) pl = pf_load(tile_cnt, supt, blockIdx.x);
     uint32_t s[W], e[W];
     if (w0 + W <= nwords) {
-        const uint2 a = *reinterpret_cast<const uint2*>(sbits + w0);
-        const uint2 b = *reinterpret_cast<const uint2*>(ebits + w0);
-        s[0] = a.x; s[1] = a.y;
-        e[0] = b.x; e[1] = b.y;
+        if constexpr (W == 4u) {
+            const uint4 a = *reinterpret_cast<const uint4*>(sbits + w0);
+            const uint4 b = *reinterpret_cast<const uint4*>(ebits + w0);
+            s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w;
+            e[0] = b.x; e[1] = b.y; e[2] = b.z; e[3] = b.w;
+        } else {
+            const uint2 a = *reinterpret_cast<const uint2*>(sbits + w0);
+            const uint2 b = *reinterpret_cast<const uint2*>(ebits + w0);
+            s[0] = a.x; s[1] = a.y;
+            e[0] = b.x; e[1] = b.y;
+        }
     } else {
 #pragma unroll
         for (uint32_t k = 0; k < W; k++) {
@@ -2819,8 +2828,11 @@ __global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits,
     uint32_t ts, te;
     const uint32_t xs = block_scan_u32(cs, lds, &ts);
     const uint32_t xe = block_scan_u32(ce, lds, &te);
-    if (!WRITE) {
-        if (threadIdx.x == 0) tile_cnt[blockIdx.x] = make_uint2(ts, te);
+    if (!WRITE) {  // lanes 0-127 hold the first tile: its count is lane 128's exclusive prefix
+        if (threadIdx.x == 128u) {
+            tile_cnt[2u * blockIdx.x] = make_uint2(xs, xe);
+            tile_cnt[2u * blockIdx.x + 1u] = make_uint2(ts - xs, te - xe);
+        }
         return;
     }
     const uint2 to = pf_sum(pl, lds);
@@ -3655,7 +3667,7 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                                   w.counters));
         return hipGetLastError();
     }
-    JB_TIMED(K_TOK_COUNT, hipLaunchKernelGGL((k_tok<false>), dim3(nttiles), dim3(256), 0, stream, w.sbits, w.ebits,
+    JB_TIMED(K_TOK_COUNT, hipLaunchKernelGGL((k_tok<false>), dim3((nttiles + 1u) / 2u), dim3(256), 0, stream, w.sbits, w.ebits,
                                              nwords, w.ttile_cnt, w.supt, w.counters, nullptr, nullptr));
     if (nttiles > 256u)  // (k_tok's write pass reads the sums of whole groups of 256 tiles only)
         JB_TIMED(K_SCAN_TOK, hipLaunchKernelGGL(k_sup, dim3((nttiles + 255) / 256), dim3(256), 0, stream,
