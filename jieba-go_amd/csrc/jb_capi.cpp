@@ -639,6 +639,12 @@ static int init_launch_cfg(Device* d) {
                         kZhGroupBytes);
         lc.zh_group = (uint32_t)grp;
     }
+    const int zt = env_int("JB_ZH_TAIL_KIB", 0), ztg = env_int("JB_ZH_TAIL_GROUP", 1024);
+    if (zt < 0 || zt > (1 << 20) || ztg < (int)kZhGroupSmall || ztg > (int)kZhGroupBytes || ztg % 32 != 0)
+        return fail(JB_EINVAL, "JB_ZH_TAIL_KIB=%d / JB_ZH_TAIL_GROUP=%d: want 0 .. 1048576 KiB, a multiple of 32 "
+                    "in [%u, %u] bytes", zt, ztg, kZhGroupSmall, kZhGroupBytes);
+    lc.zh_tail = (uint32_t)zt << 10;
+    lc.zh_tail_group = (uint32_t)ztg;
 #if JB_STAMPS
     lc.diag = (uint32_t)env_int("JB_STAMPS", 0) ? 0x100u : 0u;
 #endif
@@ -723,6 +729,17 @@ static int launch_pipeline_(Device* d, const Work& w, const uint8_t* d_text, uin
                 n++;
             }
         if (n == 0) n = 1;
+        {  // the grid's tail: every wave starts with the kernel, so the spread of their totals is idle time
+            std::vector<uint64_t> tot;
+            for (uint32_t i = 0; i < nwv; i++)
+                if (st[i * 16 + 3]) tot.push_back(st[i * 16 + 6]);
+            if (!tot.empty()) {
+                std::sort(tot.begin(), tot.end());
+                fprintf(stderr, "[jb] k_zh wave totals: min %llu p10 %llu median %llu max %llu (waves %zu)\n",
+                        (unsigned long long)tot.front(), (unsigned long long)tot[tot.size() / 10],
+                        (unsigned long long)tot[tot.size() / 2], (unsigned long long)tot.back(), tot.size());
+            }
+        }
         fprintf(stderr, "[jb] k_zh clocks/wave: setup %.0f dp %.0f fwd walk %.0f viterbi fwd %.0f back+flush+rest %.0f "
                         "total %.0f; chunks/wave %.1f; lane DP steps %.0f vs 64*max %.0f (DP lane use %.2f); blocks past "
                         "the window per chunk %.3f; Viterbi lane use %.2f (longest lane %.1f runes per chunk)\n",

@@ -110,7 +110,22 @@ struct LaunchCfg {
     uint32_t zh_group;  // k_zh group bytes (0: zh_group_for(nbytes))
     uint32_t diag;      // diagnostic clocks (STAMPS builds only; 0 otherwise)
     uint32_t small_max; // host batches up to this many bytes take k_small (0: never)
+    uint32_t zh_tail;        // k_zh: about this many bytes at the batch end go in smaller groups (0: none)
+    uint32_t zh_tail_group;  // ... of this many bytes (a multiple of 32, at most the group size)
 };
+
+// k_zh's group split: g1 groups of grp bytes, then groups of *sgrp bytes to the end.
+// Returns the number of groups.
+inline uint64_t zh_tail_groups(uint64_t nbytes, uint32_t grp, const LaunchCfg& lc, uint32_t* g1, uint32_t* sgrp) {
+    *sgrp = grp;
+    *g1 = (uint32_t)((nbytes + grp - 1) / grp);
+    if (lc.zh_tail && lc.zh_tail_group && lc.zh_tail_group < grp && nbytes > lc.zh_tail) {
+        *g1 = (uint32_t)((nbytes - lc.zh_tail) / grp);
+        *sgrp = lc.zh_tail_group;
+    }
+    const uint64_t tail0 = (uint64_t)*g1 * grp;
+    return *g1 + (tail0 < nbytes ? (nbytes - tail0 + *sgrp - 1) / *sgrp : 0);
+}
 
 // Boundary-mask output of one pipeline run (jb_cut_batch_mask): the batch's token
 // start / end bits go into the u64 bitmaps s / e at bit offset rel (k_mask_merge)

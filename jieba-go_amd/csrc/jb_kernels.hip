@@ -1809,7 +1809,7 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
                                             double* __restrict__ gbest,
                                             uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
                                             uint2* __restrict__ longblk, uint32_t* __restrict__ lsegb, uint32_t grp,
-                                            uint32_t diag, uint64_t* __restrict__ dbg) {
+                                            uint32_t g1, uint32_t sgrp, uint32_t diag, uint64_t* __restrict__ dbg) {
     __shared__ uint8_t s_bl[4][kZhWin / 3u + 4u];
     __shared__ double s_rb[4][kZhRing * 64];  // DP ring, then the window's token bitmaps
     __shared__ uint32_t s_tbl[4][kZhChunk];   // the chunk's blocks as found, then as dealt to the lanes
@@ -1824,7 +1824,10 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
     uint32_t* rb32 = reinterpret_cast<uint32_t*>(s_rb[wv]);
     uint32_t* tbl = s_tbl[wv];
     uint32_t* hist = s_hist[wv];
-    const uint32_t ngroups = (uint32_t)((nbytes + grp - 1u) / grp);  // (grp <= kZhGroupBytes)
+    // groups 0..g1-1 are grp bytes, the rest (the batch's tail) sgrp <= grp bytes: the
+    // persistent grid's last claims are short, so its waves finish closer together
+    const uint32_t tail0 = g1 * grp;
+    const uint32_t ngroups = g1 + (tail0 < nbytes ? (uint32_t)((nbytes - tail0 + sgrp - 1u) / sgrp) : 0u);
     const uint32_t ntiles = (uint32_t)((nbytes + kTileBytes - 1u) / kTileBytes);
     const uint32_t nlw = ntiles * 256u;                                  // lane-mask words (16 bytes each)
     const uint32_t winw = (grp + (kZhWin - kZhGroupBytes)) / 32u + 1u;  // token words of a window (<= kZhWinWords)
@@ -1854,11 +1857,12 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
     };
     for (;; ) {
         if (g >= ngroups) break;
-        const uint32_t wb = g * grp, wend = wb + grp + (kZhWin - kZhGroupBytes);
+        const uint32_t gl = g < g1 ? grp : sgrp;
+        const uint32_t wb = g < g1 ? g * grp : tail0 + (g - g1) * sgrp, wend = wb + gl + (kZhWin - kZhGroupBytes);
         // The group's zh blocks are the Han block starts (lane-mask bits 16-31) in its
         // words; a block ends at the next block start of any kind (bits 0-15).
         const uint32_t gw0 = wb >> 4;
-        const uint32_t gnw = (uint32_t)((min((uint64_t)wb + grp, nbytes) - wb + 15u) >> 4);
+        const uint32_t gnw = (uint32_t)((min((uint64_t)wb + gl, nbytes) - wb + 15u) >> 4);
         // The group's lane-mask words and the two rounds after them (block ends) are
         // staged in the wave's ring area, which is free until the DP.
         uint32_t* const lmv = rb32;
@@ -3605,7 +3609,9 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     const uint32_t grp = lc.zh_group ? lc.zh_group : zh_group_for(nbytes);
     const uint32_t nttiles = (uint32_t)((nwords + kTokTileWords - 1) / kTokTileWords);
     // k_zh: a persistent grid, but no more 4-wave workgroups than the batch has groups
-    const uint64_t ngroups = (nbytes + grp - 1) / grp;
+    // the last zh_tail bytes (at most) in groups of zh_tail_group (tail_groups)
+    uint32_t g1, sgrp;
+    const uint64_t ngroups = zh_tail_groups(nbytes, grp, lc, &g1, &sgrp);
     const uint32_t grid_zh = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(lc.grid_zh, (ngroups + 3) / 4));
     // No clearing pass: the document bitmap is all zeros between runs (k_nonzh clears
     // what k_docbits set; a fresh or dirty workspace is cleared by the caller), k_docbits
@@ -3620,11 +3626,11 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     if (hmm)
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes,
                                           w.lanemask, w.tile_cnt, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
-                                          w.longblk, w.lsegb, grp, diag, w.dbg));
+                                          w.longblk, w.lsegb, grp, g1, sgrp, diag, w.dbg));
     else
         JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes,
                                           w.lanemask, w.tile_cnt, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
-                                          w.longblk, w.lsegb, grp, diag, w.dbg));
+                                          w.longblk, w.lsegb, grp, g1, sgrp, diag, w.dbg));
     {
         // long blocks: the chain, then one lane per 64-rune segment (at most
         // nbytes / 192 + nbytes / kZhLongMin segments), one wave per block
