@@ -395,20 +395,22 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     uint64_t c0 = stamps ? __builtin_amdgcn_s_memtime() : 0, c1 = 0, c2 = 0, c3 = 0, c0b = 0, c1b = 0;
     uint32_t trips = 0;
     const uint64_t t0 = (uint64_t)blockIdx.x * kTileBytes;
-    for (uint32_t k = threadIdx.x; k < kMwStage / 16; k += 256) {
-        const int64_t g = (int64_t)t0 - 16 + 16 * (int64_t)k;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (g >= 0 && (uint64_t)g + 16 <= nbytes + 64) v = *reinterpret_cast<const uint4*>(text + g);
-        reinterpret_cast<uint4*>(s_t)[k] = v;
+    // The prologue's global loads (the staged text, the tile's document words and the
+    // lane's window words for M below) are all issued before any is waited on: as a
+    // staging loop and separate stores they were four round trips in a row.
+    static_assert(kMwStage / 16 > 256u && kMwStage / 16 <= 512u, "the staged text is two loads per thread at most");
+    uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
+    {
+        const int64_t g = (int64_t)t0 - 16 + 16 * (int64_t)threadIdx.x, g2 = g + 16 * 256;
+        if (g >= 0 && (uint64_t)g + 16 <= nbytes + 64) va = *reinterpret_cast<const uint4*>(text + g);
+        if (threadIdx.x < kMwStage / 16 - 256u && (uint64_t)g2 + 16 <= nbytes + 64)
+            vb = *reinterpret_cast<const uint4*>(text + g2);
     }
     const uint64_t lastw = (nbytes + 31) >> 5;
-    {  // clear the tile's words of the token bitmaps (k_zh and k_nonzh OR into them): no memset pass
-        const uint64_t wz = (t0 >> 5) + (threadIdx.x & 127u);
-        if (wz < lastw + 2u) __builtin_nontemporal_store(0u, (threadIdx.x < 128u ? sbits : ebits) + wz);
-    }
+    uint32_t dbw = 0;
     if (threadIdx.x < kTileBytes / 32 + 3) {
         const uint64_t wi = (t0 >> 5) + threadIdx.x;
-        s_db[threadIdx.x] = wi < lastw ? docbits[wi] : 0u;
+        dbw = wi < lastw ? docbits[wi] : 0u;
     }
     if (threadIdx.x == 0) {
         s_nla = 0;
@@ -433,6 +435,13 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
             if (endk <= 0) M = ~0ull;
             else M |= ~0ull << endk;
         }
+    }
+    reinterpret_cast<uint4*>(s_t)[threadIdx.x] = va;
+    if (threadIdx.x < kMwStage / 16 - 256u) reinterpret_cast<uint4*>(s_t)[threadIdx.x + 256u] = vb;
+    if (threadIdx.x < kTileBytes / 32 + 3) s_db[threadIdx.x] = dbw;
+    {  // clear the tile's words of the token bitmaps (k_zh and k_nonzh OR into them): no memset pass
+        const uint64_t wz = (t0 >> 5) + (threadIdx.x & 127u);
+        if (wz < lastw + 2u) __builtin_nontemporal_store(0u, (threadIdx.x < 128u ? sbits : ebits) + wz);
     }
     __syncthreads();
     if (stamps) c0b = __builtin_amdgcn_s_memtime();  // (text staged)
@@ -556,6 +565,22 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         const uint32_t top = hsm ? 31u - (uint32_t)__builtin_clz(hsm) : 0u;
         const uint32_t lastend =  // window index past the lane's last Han rune
             hsm ? ((kp >> (4u * top)) & 15u) + 4u + 3u + ((w4m >> top) & 1u) : 0u;
+        // (the lookahead's decode and code loads, issued before the level-1 loads are
+        // waited on, so that the last wave does not add a round trip before the barrier)
+        const uint32_t le255 = __builtin_amdgcn_readlane(lastend, 63);  // (meaningful in the last wave)
+        const bool la = threadIdx.x >= 192u && le255 >= 20u;
+        uint32_t law = 0, lar = 0, lacd = 0;
+        if (la) {
+            const uint32_t j = threadIdx.x & 63u, q = kTileBytes + j;
+            if (j < kLABytes) {
+                const uint64_t db = ((((uint64_t)s_db[(q >> 5) + 1u]) << 32) | s_db[q >> 5]) >> (q & 31u);
+                uint32_t lim = 1u + (uint32_t)__builtin_ctzll(((db >> 1) & 7ull) | 8ull);
+                const uint64_t gq = t0 + q;
+                if (gq + lim > nbytes) lim = gq < nbytes ? (uint32_t)(nbytes - gq) : 0u;
+                lar = (db & 1ull) ? 0u : han_rune(lds4(s_t, q + 16u), lim, &law);
+            }
+            lacd = lar ? rune_code(im, lar) : 0u;
+        }
 #pragma unroll
         for (int i = 0; i < 7; i++) {  // (s_e is not under the staged text)
             if ((hsm >> i) & 1u)
@@ -574,18 +599,9 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         // the chain from the rune after lane 255's last one is then walked on the
         // ballot masks (scalar), and each lane on it writes its entry.  (One lane
         // stepping rune by rune took a long serial chain and a large code body.)
-        const uint32_t le255 = __builtin_amdgcn_readlane(lastend, 63);  // (meaningful in the last wave)
-        if (threadIdx.x >= 192u && le255 >= 20u) {
-            const uint32_t j = threadIdx.x & 63u, q = kTileBytes + j;
-            uint32_t w = 0, r = 0;
-            if (j < kLABytes) {
-                const uint64_t db = ((((uint64_t)s_db[(q >> 5) + 1u]) << 32) | s_db[q >> 5]) >> (q & 31u);
-                uint32_t lim = 1u + (uint32_t)__builtin_ctzll(((db >> 1) & 7ull) | 8ull);
-                const uint64_t gq = t0 + q;
-                if (gq + lim > nbytes) lim = gq < nbytes ? (uint32_t)(nbytes - gq) : 0u;
-                r = (db & 1ull) ? 0u : han_rune(lds4(s_t, q + 16u), lim, &w);
-            }
-            const uint32_t cdj = r ? rune_code(im, r) : 0u;
+        if (la) {
+            const uint32_t j = threadIdx.x & 63u;
+            const uint32_t w = law, r = lar, cdj = lacd;
             const uint64_t hm = __ballot(r != 0u), w4b = __ballot(w == 4u);
             // the chain (wave-uniform): runes at jj, jj + w, ... while Han, at most kLA
             uint64_t chain = 0;
@@ -665,6 +681,7 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     bool act = false, ovf = false;
     uint32_t j = 0, js = 0, id = 0, base = 0, len = 0, nedge = 0, m = 0;
     uint64_t rw = 0;
+    uint32_t en = 0;  // entry j + 1 (the next rune of the walk), read a trip ahead
     for (;;) {
         const uint64_t need = __ballot(!act);
         const uint32_t rank =
@@ -685,11 +702,12 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
             len = 1u;
             ovf = false;
             act = true;
+            en = ent[j + 1u];
         }
         if (act) {  // one round trip: the next rune's cell
-            const uint32_t en = ent[j + 1u];
             const uint32_t t = base + ent_code(en);
             const uint64_t child = im.cells[t];
+            const uint32_t en2 = ent[j + 2u];  // (used only when the walk goes on: then entry j + 2 exists)
             const bool hit = dat_hit(child, id);
             ++len;
             const uint32_t wi = jb_cell_widx(child);
@@ -704,6 +722,7 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
             const bool go = more && (en & kEntCont);
             const bool dfr = more && !(en & kEntCont) && (en & kEntEdge);  // past the lookahead: k_zh walks it
             ++j;
+            en = en2;
             id = t;
             base = jb_cell_base(child);
             if (!go) {  // the record goes to the start entry's LDS cell (read when the walk began)
@@ -2741,14 +2760,31 @@ __global__ __launch_bounds__(256) void k_nonzh(const uint8_t* __restrict__ text,
     Emitter em(sbits, ebits);
     for (uint32_t wi = blockIdx.x * blockDim.x + threadIdx.x; wi < nw; wi += gridDim.x * blockDim.x) {
         uint64_t a = alnum16[wi];
+        // the next alnum chunk's text and lane mask load while this one is cut
+        uint32_t cn = a ? wi * 64u + (uint32_t)__builtin_ctzll(a) : 0u;
+        uint4 txn = make_uint4(0, 0, 0, 0);
+        uint32_t lmn = 0;
+        if (a && cn < nch) {
+            txn = *reinterpret_cast<const uint4*>(text + cn * 16u);
+            lmn = lanemask[cn];
+        }
         while (a) {
-            const uint32_t c = wi * 64u + (uint32_t)__builtin_ctzll(a);
+            const uint32_t c = cn;
+            const uint4 tx = txn;
+            const uint32_t lm = lmn;
             a &= a - 1ull;
             if (c >= nch) break;  // (padding past the batch)
+            if (a) {
+                cn = wi * 64u + (uint32_t)__builtin_ctzll(a);
+                if (cn < nch) {
+                    txn = *reinterpret_cast<const uint4*>(text + cn * 16u);
+                    lmn = lanemask[cn];
+                }
+            }
             const uint32_t c0 = c * 16u;
-            uint32_t A = alnum_mask16(*reinterpret_cast<const uint4*>(text + c0));
+            uint32_t A = alnum_mask16(tx);
             if (c0 + 16u > nbytes) A &= (1u << (nbytes - c0)) - 1u;
-            const uint32_t bm = lanemask[c] & 0xFFFFu;
+            const uint32_t bm = lm & 0xFFFFu;
             while (A) {  // a block with an alnum byte in this chunk
                 const uint32_t i = (uint32_t)__builtin_ctz(A);
                 const uint32_t le = bm & ((2u << i) - 1u), after = bm & ~((2u << i) - 1u);
