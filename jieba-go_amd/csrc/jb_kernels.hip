@@ -154,15 +154,23 @@ __global__ void k_docbits(const uint64_t* __restrict__ doc_off, uint32_t ndocs, 
 // utf8.DecodeRune, bounded by the document end) covers it, else it starts a
 // rune of its own.  Block starts: document starts and changes of Han-ness.
 // ---------------------------------------------------------------------------
+// Inclusive prefix sum over a wave's 64 lanes with DPP moves (VALU, no LDS round
+// trips): row_shr 1/2/4/8 scans each row of 16 lanes, row_bcast15/31 carry the row
+// totals into the rows above.  Lanes a move cannot source keep 0 (old = 0, bound_ctrl off).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
 __device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t* lds, uint32_t* total) {
     // exclusive scan over a 256-thread workgroup
     const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= (uint32_t)d) x += y;
-    }
+    const uint32_t x = wave_incl_scan(v);
     if (lane == 63) lds[wid] = x;
     __syncthreads();
     uint32_t base = 0, tot = 0;
@@ -202,12 +210,9 @@ __device__ __forceinline__ PrefixLoads pf_load(const uint2* __restrict__ cnt, co
     return p;
 }
 __device__ uint2 pf_sum(PrefixLoads p, uint32_t* lds) {
-    uint32_t x = p.x, y = p.y;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        x += (uint32_t)__shfl_xor((int)x, d, 64);
-        y += (uint32_t)__shfl_xor((int)y, d, 64);
-    }
+    // wave sums by DPP scans (a shuffle reduction was twelve LDS round trips)
+    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(p.x), 63);
+    const uint32_t y = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(p.y), 63);
     const uint32_t wid = threadIdx.x >> 6;
     if ((threadIdx.x & 63u) == 0) {
         lds[wid] = x;
@@ -1770,13 +1775,8 @@ __device__ __noinline__ uint2 lm_collect(const uint32_t* lmv, uint32_t* tbl, uin
         const uint32_t bm = xa & 0xFFFFu;
         const uint32_t zm = (rw + lane < gnw) ? (xa >> 16) : 0u;
         const uint32_t cz = (uint32_t)__popc(zm);
-        uint32_t incl = cz;  // inclusive prefix over the lanes
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t t = (uint32_t)__shfl_up((int)incl, d, 64);
-            if (lane >= (uint32_t)d) incl += t;
-        }
-        const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
+        const uint32_t incl = wave_incl_scan(cz);  // inclusive prefix over the lanes
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         // the first block start after this lane's word: in a later lane of this round, else
         // in the lookahead round, else past it (0xFFFFFFFF: found later) or the batch end
         const uint64_t la = __ballot(bm != 0u), lb = __ballot((xb & 0xFFFFu) != 0u);
@@ -1885,22 +1885,24 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
         // The group's lane-mask words and the two rounds after them (block ends) are
         // staged in the wave's ring area, which is free until the DP.
         uint32_t* const lmv = rb32;
-        auto stage = [&]() {
+        // (returns the lane's count of Han block starts in the group's words, from the
+        // registers: read back from LDS it was a round trip per word)
+        auto stage = [&]() -> uint32_t {
             uint32_t v[kZhStagePer];
 #pragma unroll
             for (uint32_t k = 0; k < kZhStagePer; k++) v[k] = lmw(gw0 + lane + 64u * k);
+            uint32_t c = 0;
 #pragma unroll
-            for (uint32_t k = 0; k < kZhStagePer; k++) lmv[lane + 64u * k] = v[k];
+            for (uint32_t k = 0; k < kZhStagePer; k++) {
+                lmv[lane + 64u * k] = v[k];
+                c += lane + 64u * k < gnw ? (uint32_t)__popc(v[k] >> 16) : 0u;
+            }
             wave_sync();
+            return c;
         };
-        stage();
         uint32_t n = 0;
         {
-            uint32_t c = 0;
-            for (uint32_t w = lane; w < gnw; w += 64u) c += (uint32_t)__popc(lmv[w] >> 16);
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) c += (uint32_t)__shfl_xor((int)c, d, 64);
-            n = __builtin_amdgcn_readfirstlane(c);
+            n = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(stage()), 63);
         }
         if (n == 0u) {  // no Han block starts here
             g = next_group();
@@ -1955,15 +1957,10 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
             }
             wave_sync();
             {  // start of each bucket in descending order: sum of the counts of longer buckets
-                const uint32_t h = hist[lane];
-                uint32_t incl = h;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t t = __shfl_down(incl, d, 64);
-                    if (lane + (uint32_t)d < 64u) incl += t;
-                }
+                const uint32_t incl = wave_incl_scan(hist[lane]);  // (buckets 0..lane)
+                const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
                 wave_sync();
-                hist[lane] = incl - h;
+                hist[lane] = total - incl;  // (buckets lane+1..63)
             }
             wave_sync();
             uint32_t nin = 0;
