@@ -10,7 +10,13 @@ byte-balanced document range shard.shard_bounds(...)[r] (jb_shard_bounds, the
 rule jb_cut_batch uses across the devices of one context), so N = 1 cuts the
 whole GiB on one GPU.  Documents are independent (tokenizer.go:158-160): no
 data-path collective, ranks only meet at the timing barriers and for the
-job-level sums.
+job-level sums, over gloo (CPU tensors; no RCCL).
+
+Ranks: `python bench.py --gpus N` starts N child processes of itself, one per
+GPU (RANK = LOCAL_RANK = r), before any GPU call, and exits non-zero when
+fewer than N GPUs are visible or a rank fails; under torch.distributed.run
+(WORLD_SIZE set) the ranks come from the environment and --gpus must match.
+Rank 0 generates the fixed corpus once and the other ranks map it.
 
 A step is one full Cut pass (every kernel, token spans out) over the rank's
 shard, inputs already resident in HBM.  `value` = all ranks' runes x K / the
@@ -122,16 +128,38 @@ def load_pmc_traffic(kernel, workload_key):
 # ---------------------------------------------------------------------------
 # workload
 # ---------------------------------------------------------------------------
-def make_workload(args, s, rank):
-    """(buf, doc_off, description) of the WHOLE job's input (every rank builds the
+def shared_corpus_dir():
+    """Where rank 0 leaves the generated corpus for the other ranks of a job (one
+    directory per rendezvous port, under the temp dir)."""
+    return os.path.join(tempfile.gettempdir(), f"jb_bench_corpus_{os.environ.get('MASTER_PORT', 'local')}")
+
+
+def make_workload(args, s, rank, world=1, dist=None):
+    """(buf, doc_off, description) of the WHOLE job's input (every rank sees the
     same one and takes its shard) — or of this rank's own input for the
-    single-document / per-GPU workloads."""
+    single-document / per-GPU workloads.  With several ranks, rank 0 generates the
+    fixed corpus on all the job's CPUs and writes it to a temp directory; the other
+    ranks map it read-only after a barrier (one generation per job, not per rank)."""
     import synth
     if args.workload == "docs":
         mib = args.corpus_mib
-        buf, off, _ = s.corpus_parallel(synth.KIND_DOCS, 0, target_bytes=int(mib * (1 << 20)),
-                                        threads=max(1, min(16, effective_cpus()[0])))
-        return buf, off, f"C_syn corpus, {mib:g} MiB fixed ({'1 GiB = config 4' if mib == 1024 else 'reduced'})"
+        desc = f"C_syn corpus, {mib:g} MiB fixed ({'1 GiB = config 4' if mib == 1024 else 'reduced'})"
+        if dist is None or world == 1:
+            buf, off, _ = s.corpus_parallel(synth.KIND_DOCS, 0, target_bytes=int(mib * (1 << 20)),
+                                            threads=max(1, min(16, effective_cpus()[0])))
+            return buf, off, desc
+        d = shared_corpus_dir()
+        if rank == 0:
+            buf, off, _ = s.corpus_parallel(synth.KIND_DOCS, 0, target_bytes=int(mib * (1 << 20)),
+                                            threads=max(1, min(16, effective_cpus()[0])))
+            os.makedirs(d, exist_ok=True)
+            np.save(os.path.join(d, "buf.npy"), buf)
+            np.save(os.path.join(d, "off.npy"), off)
+        dist.barrier()
+        if rank != 0:
+            buf = np.load(os.path.join(d, "buf.npy"), mmap_mode="r")
+            off = np.load(os.path.join(d, "off.npy"))
+        return buf, off, desc
     if args.workload == "s10k":
         buf, off, _ = s.corpus(synth.KIND_SENTENCES, 0, max_docs=10_000, target_bytes=64 << 20)
         return buf, off, "S10k: 10,000 synthetic sentences (configs 2/3)"
@@ -265,10 +293,14 @@ def run(args, world, rank, dist, agg_dev, make_cutter, open_oracle, log=print):
     t0 = time.time()
     s = synth.Synth(nwords=args.nwords)
     sharded = args.workload == "docs"
-    buf, off, wdesc = make_workload(args, s, rank)
+    buf, off, wdesc = make_workload(args, s, rank, world, dist)
     sbuf, soff, d0, base = shard_for(buf, off, world, rank, sharded)
     if sharded and world > 1:
         del buf
+        dist.barrier()  # every rank holds its own copy of its shard: the shared corpus file can go
+        if rank == 0:
+            import shutil
+            shutil.rmtree(shared_corpus_dir(), ignore_errors=True)
     nbytes = int(soff[-1])
     nrunes = count_runes(sbuf, nbytes)
     hbytes = han_bytes(sbuf, nbytes)
@@ -537,9 +569,94 @@ def roofline_latency(timeout=240):
                     "STAMPS build of the same source, per-wave clocks cost a few %"}
 
 
-def main():
+class GpuBackend:
+    """The measured path: one jb context on the rank's GPU, GpuCutter over it."""
+    name = "gpu"
+
+    def device_count(self):
+        import torch
+        return torch.cuda.device_count()  # (counts devices without initialising one)
+
+    def open(self, cfg_kw, local):
+        import torch
+        import jiebahip as J
+        torch.cuda.set_device(local)
+        self.tk = J.Tokenizer(J.make_config(device=local, **cfg_kw))
+        return self.tk
+
+    def make_cutter(self, buf, off, hmm, local):
+        return GpuCutter(self.tk, buf, off, hmm, local)
+
+    def close(self):
+        self.tk.close()
+
+
+def load_backend():
+    """GpuBackend, or — for the CPU test of the N-rank launcher only — the class
+    JB_BENCH_TEST_BACKEND names ("module:Class", e.g. an oracle stand-in).  A
+    test backend's line says so in `data`; the driver never sets the variable."""
+    spec = os.environ.get("JB_BENCH_TEST_BACKEND")
+    if not spec:
+        return GpuBackend()
+    import importlib
+    mod, cls = spec.split(":")
+    return getattr(importlib.import_module(mod), cls)()
+
+
+def _free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch(n, argv, backend):
+    """`--gpus N` without an inherited WORLD_SIZE: start N fresh child processes of
+    this script, one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on
+    127.0.0.1), before this process makes any GPU call.  The children meet over
+    gloo (barriers and job sums on CPU tensors; no RCCL); rank 0 prints the line on
+    the inherited stdout.  If a child fails, the others are stopped (they would
+    wait at a barrier forever) and the launcher exits non-zero."""
+    import signal
+    import subprocess
+    have = backend.device_count()
+    if have < n:
+        print(f"bench.py: --gpus {n} but only {have} GPU(s) visible; not running a smaller job in its place",
+              file=sys.stderr)
+        return 2
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port, JB_BENCH_LAUNCHER="bench.py")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env,
+                                      start_new_session=True))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        time.sleep(0.2)
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                      file=sys.stderr)
+                for q in alive:
+                    try:
+                        os.killpg(q.pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+    return rc
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one process each). Without WORLD_SIZE in the environment bench.py starts the "
+                         "N ranks itself; under torch.distributed.run it must equal WORLD_SIZE. Default 1")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["docs", "sentence", "s10k", "long-punct", "long-oov"], default="docs")
@@ -558,14 +675,32 @@ def main():
     ap.add_argument("--sentence-iters", type=int, default=5000)
     ap.add_argument("--no-latency", action="store_true", help="skip the roofline_latency probe")
     ap.add_argument("--latency-probe", action="store_true", help=argparse.SUPPRESS)
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
     if args.latency_probe:
         latency_probe(args)
-        return
+        return 0
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = load_backend()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if (args.gpus or 1) > 1:
+            return launch(args.gpus, argv, backend)
+        world, rank, local = 1, 0, 0
+    else:
+        world = int(env_world)
+        rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if args.gpus is not None and args.gpus != world:
+            print(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world}", file=sys.stderr)
+            return 2
+    if local >= backend.device_count():
+        print(f"bench.py: rank {rank} wants GPU {local}, only {backend.device_count()} visible", file=sys.stderr)
+        return 2
 
     import torch
     import jiebahip as J
@@ -574,16 +709,14 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
-    agg_dev = torch.device("cuda", local)
+        dist.init_process_group("gloo", init_method="env://")  # barriers + scalar sums only: no RCCL
+    agg_dev = torch.device("cpu")
 
     tmp = tempfile.mkdtemp(prefix=f"jb_bench_r{rank}_")
     dpath, epath = synth.Synth(nwords=args.nwords).write_files(tmp)
     kind = J.JB_DICT_PREFIX if args.dict_kind == "prefix" else J.JB_DICT_TXT
     size_override = J.JIEBA_SIZE if args.dict_kind == "prefix" else 0
-    tk = J.Tokenizer(J.make_config(dict_path=dpath, emit_path=epath, kind=kind, size_override=size_override,
-                                   device=local))
+    tk = backend.open(dict(dict_path=dpath, emit_path=epath, kind=kind, size_override=size_override), local)
 
     def open_oracle():
         import oracle as O
@@ -611,23 +744,30 @@ def main():
                                            "same sentence, ctypes call overhead included", "cpu_model": cpu_model()},
                 "roofline": None}
         print(json.dumps(line), flush=True)
-        tk.close()
-        return
+        backend.close()
+        return 0
 
     out = run(args, world, rank, dist, agg_dev,
-              lambda b, o_, h: GpuCutter(tk, b, o_, h, local), open_oracle)
+              lambda b, o_, h: backend.make_cutter(b, o_, h, local), open_oracle)
     if rank == 0:
         line, (sbuf, soff, _) = out
+        launcher = os.environ.get("JB_BENCH_LAUNCHER") or ("torch.distributed.run" if world > 1 else "single process")
+        line["config"]["ranks"] = {"launcher": launcher, "processes": world, "rank_to_gpu": "rank r -> GPU r",
+                                   "host_group": "gloo (timing barriers + job sums; no RCCL)" if world > 1 else None}
+        if backend.name != "gpu":
+            line["data"] = f"TEST BACKEND {backend.name}: not a measurement"
         if world == 1 and not args.no_e2e:
             line["end_to_end_host"] = end_to_end(tk, sbuf, soff, args.hmm, line["config"]["corpus_chars"])
         if world == 1 and args.workload == "docs" and not args.no_latency:
             line["roofline_latency"] = roofline_latency()
-        line["loaded"] = J.loaded_runtime()
+        line["loaded"] = J.loaded_runtime() if backend.name == "gpu" else None
         print(json.dumps(line), flush=True)
-    tk.close()
+    backend.close()
     if dist:
+        dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -181,8 +181,10 @@ int jb_split_points(const uint8_t *text, const uint64_t *doc_off, uint32_t ndocs
 
 /* Replaces Tokenizer.AddWord (tokenizer.go:372; the reference deadlocks there,
  * :376 + :581).  freq < 1 takes suggestFreq's value (tokenizer.go:589-614).
- * Atomic: on any error (JB_ELIMIT for a word of more than 255 runes, JB_EDEVICE,
- * JB_ENOMEM) the dictionary, pd.size and every device's image stay as they were. */
+ * Atomic: on any error (JB_ELIMIT for an all-Han word of more than 255 runes -- the
+ * trie holds only all-Han keys, so a longer word with a non-Han rune is stored in
+ * the dictionary and never walked; JB_EDEVICE, JB_ENOMEM) the dictionary, pd.size
+ * and every device's image stay as they were. */
 int jb_add_word(jb_ctx *ctx, const char *word, size_t len, int64_t freq);
 
 /* suggestFreq (tokenizer.go:589-614): the frequency AddWord(word, freq < 1) would store. */

@@ -877,10 +877,13 @@ extern "C" void jb_close(jb_ctx* ctx) {
         (void)hipStreamSynchronize(d->stream);
         if (d->sstream) (void)hipStreamSynchronize(d->sstream);
         d->timer.reset();
+        // a jb_cut_device pipeline queued on a caller's stream may still use the workspace:
+        // wait for its completion event before freeing anything (the caller's stream may be
+        // gone by now, the event is ours)
+        if (d->ws_done) (void)hipEventSynchronize(d->ws_done);
         if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
         d->gexec = nullptr;
         free_work(&d->w);
-        if (d->ws_done) (void)hipEventSynchronize(d->ws_done);  // (a caller's stream may be gone by now)
         dfree(d->text); dfree(d->doc_off);
         free_image_bufs(&d->ib);
         if (d->ws_done) (void)hipEventDestroy(d->ws_done);
@@ -1757,6 +1760,10 @@ extern "C" int jb_cut_batch_mask(jb_ctx* ctx, const uint8_t* text, const uint64_
         b.release();
     }
     if (rc) return rc;
+    if (nwords > need) {  // the header promises every word: clear the caller's tail past the batch
+        memset(starts + need, 0, (nwords - need) * 8);
+        memset(ends + need, 0, (nwords - need) * 8);
+    }
     *ntokens = nt;
     return JB_OK;
 }

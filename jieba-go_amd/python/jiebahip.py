@@ -367,7 +367,7 @@ class Tokenizer:
         n = C.c_uint64()
         _check(lib().jb_cut_batch_mask(self.h, buf.ctypes.data, doc_off.ctypes.data, nd, int(hmm), out[0].ctypes.data,
                                        out[1].ctypes.data, len(out[0]), C.byref(n)))
-        return out[0], out[1], n.value
+        return out[0][:nw], out[1][:nw], n.value
 
     def cut_device(self, d_text_ptr, nbytes, d_doc_off_ptr, ndocs, hmm, stream_ptr=0):
         """Device-resident cut; returns device pointers (start, end, doc_tok, ntok)."""

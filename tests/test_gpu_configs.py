@@ -221,6 +221,22 @@ def test_host_pipeline_pieces_and_masks(syn_small, piece_kib, monkeypatch):
     rc = J.lib().jb_cut_batch_mask(tk.h, big.ctypes.data, boff.ctypes.data, len(boff) - 1, 1, None, None, 3,
                                    J.C.byref(J.C.c_uint64()))
     assert rc == J.JB_EINVAL  # 3 words cannot hold the batch
+    # caller arrays longer than the batch (reused after a larger one): every word is
+    # written, the tail past the batch as zeros, so a popcount counts the batch's tokens
+    nw = (int(boff[-1]) + 63) // 64
+    ws = np.full(nw, ~np.uint64(0), np.uint64)
+    we = np.full(nw, ~np.uint64(0), np.uint64)
+    small_off = boff[:40]
+    os_, oe, od = o.cut_batch(big, small_off, True)
+    n = J.C.c_uint64()
+    J._check(J.lib().jb_cut_batch_mask(tk.h, big.ctypes.data, small_off.ctypes.data, len(small_off) - 1, 1,
+                                       ws.ctypes.data, we.ctypes.data, nw, J.C.byref(n)))
+    need = (int(small_off[-1]) + 63) // 64
+    assert n.value == len(os_) and not ws[need:].any() and not we[need:].any()
+    pop = lambda a: int(np.unpackbits(a.view(np.uint8)).sum())  # noqa: E731
+    assert pop(ws) == pop(we) == len(os_)
+    ms, me, nt = tk.cut_batch_mask(big, small_off, True, (ws, we))
+    assert len(ms) == need and nt == len(os_)
     tk.close()
     ref.close()
 

@@ -175,6 +175,25 @@ def test_docs_corpus_zh_groups(syn_full, group, monkeypatch):
     tk.close()
 
 
+@pytest.mark.parametrize("tail_group", [1024, 2048])
+def test_docs_corpus_zh_tail_groups(syn_full, tail_group, monkeypatch):
+    """JB_ZH_TAIL_KIB / JB_ZH_TAIL_GROUP (off by default): the last KiB of a batch in
+    smaller k_zh groups (groups start at tail0 + (g - g1) * sgrp).  With the 6 KiB
+    body group forced and a 1 MiB tail, a 6 MiB batch has both geometries; bit-exact
+    with HMM on and off."""
+    dp, ep, s = syn_full
+    monkeypatch.setenv("JB_ZH_GROUP", "6144")
+    monkeypatch.setenv("JB_ZH_TAIL_KIB", "1024")
+    monkeypatch.setenv("JB_ZH_TAIL_GROUP", str(tail_group))
+    tk, o = _pair(dp, ep)
+    for k in ("JB_ZH_GROUP", "JB_ZH_TAIL_KIB", "JB_ZH_TAIL_GROUP"):
+        monkeypatch.delenv(k)
+    buf, off, nr = s.corpus(synth.KIND_DOCS, 2100 + tail_group, target_bytes=6 << 20)
+    for hmm in (False, True):
+        _cmp_batch(tk, o, buf, off, hmm, f"docs tail group={tail_group} hmm={hmm}")
+    tk.close()
+
+
 def test_graph_replay_after_add_word(syn_small):
     """A batch cut twice is replayed from a captured HIP graph; AddWord re-uploads
     the image (new device buffers), so the next cut must not replay the old graph."""

@@ -3,6 +3,8 @@ aggregation (bench.py's max-over-ranks time, summed work), with the oracle
 standing in for each rank's device."""
 import os
 import socket
+import subprocess
+import sys
 import tempfile
 
 import numpy as np
@@ -11,40 +13,15 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import shard
+from bench_backend import OracleCutter
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
-
-
-class OracleCutter:
-    """Stands in for bench.GpuCutter on CPU (test only): the rank's "device"
-    output is the oracle's, optionally with one token corrupted."""
-
-    def __init__(self, o, buf, off, hmm, corrupt=False):
-        self.o, self.buf, self.off, self.hmm, self.corrupt = o, buf, off, hmm, corrupt
-        self.steps = 0
-
-    def step(self):
-        self.steps += 1
-
-    def sync(self):
-        pass
-
-    def profile(self, steps):
-        return {}, None
-
-    def results(self):
-        s, e, d = self.o.cut_batch(self.buf, self.off, bool(self.hmm), nthreads=2)
-        s = s.copy()
-        if self.corrupt and len(s):
-            s[len(s) // 2] += 1
-        return s, e, d
-
-    def ties(self):
-        return 0
 
 
 def _worker(rank, world, port, dict_path, emit_path, corpus_mib, corrupt_rank, out_dir):
@@ -147,3 +124,58 @@ def test_bench_two_ranks_gloo(syn_small, corrupt_rank):
     assert line["parity"]["mismatches"] == (0 if corrupt_rank < 0 else 1)
     assert line["cpu_baseline"] is None  # (rank 0 at N = 1 only)
     assert abs(line["value"] - nr * 3 / (line["ms_per_step"] * 3e-3)) / line["value"] < 0.05  # (ms rounded)
+
+
+def _bench_cmd(*extra):
+    return [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "docs", "--corpus-mib", "0.75",
+            "--nwords", "20000", "--steps", "3", "--warmup", "1", "--no-profile", "--no-e2e", "--no-latency",
+            "--cpu1-sample-mib", "0", "--dict-kind", "txt", *extra]
+
+
+def _bench_env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    tests = os.path.dirname(os.path.abspath(__file__))
+    env.update(JB_BENCH_TEST_BACKEND="bench_backend:OracleBackend",
+               PYTHONPATH=os.pathsep.join([tests, ROOT] + ([env["PYTHONPATH"]] if env.get("PYTHONPATH") else [])),
+               **kw)
+    return env
+
+
+@pytest.mark.parametrize("corrupt_rank", [-1, 1])
+def test_bench_launcher_two_ranks(corrupt_rank):
+    """`python bench.py --gpus 2` with no WORLD_SIZE: bench.py starts the two ranks
+    itself (child processes, gloo), each cuts its shard of the fixed corpus and
+    checks it; one JSON line comes out, from rank 0, with n_gpus 2 and both
+    ranks' parity in it.  The measured path is the oracle stand-in
+    (tests/bench_backend.py), so this checks the launcher, not a GPU."""
+    import json
+    p = subprocess.run(_bench_cmd("--gpus", "2"), env=_bench_env(JB_TEST_CORRUPT_RANK=str(corrupt_rank)),
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["parity"]["ranks_checked"] == 2
+    assert line["config"]["ranks"]["launcher"] == "bench.py" and line["config"]["ranks"]["processes"] == 2
+    assert line["parity"]["bit_exact"] == (corrupt_rank < 0)
+    assert line["parity"]["mismatches"] == (0 if corrupt_rank < 0 else 1)
+    assert line["data"].startswith("TEST BACKEND")
+    assert line["value"] > 0 and line["cpu_baseline"] is None
+
+
+def test_bench_launcher_refuses_missing_devices():
+    """`--gpus 2` on a box with one GPU fails loudly instead of printing a 1-GPU line."""
+    p = subprocess.run(_bench_cmd("--gpus", "2"), env=_bench_env(JB_TEST_DEVICES="1"),
+                       capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert p.returncode != 0 and "only 1 GPU" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_gpus_must_match_world_size():
+    """Under torch.distributed.run (WORLD_SIZE set), a different --gpus is an error."""
+    p = subprocess.run(_bench_cmd("--gpus", "4"),
+                       env=_bench_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                                      MASTER_PORT=str(_free_port())),
+                       capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert p.returncode != 0 and "disagrees with WORLD_SIZE=2" in p.stderr
