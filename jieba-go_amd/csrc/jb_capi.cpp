@@ -500,6 +500,7 @@ static int install_image(Device* d, ImageBufs* b, const Image& img) {
     d->dim.wtab1 = d->ib.wtab;
     d->dim.wtab = d->ib.wtab + 1;
     d->dim.nrows = img.nrows;
+    d->dim.nw1 = (uint32_t)std::min<size_t>(img.wtab.size() + 1, 0xFFFFFFFFu);
     d->dim.plainw = 1u;
     for (double w : img.wtab)
         if (std::isnan(w) || w == HUGE_VAL) d->dim.plainw = 0u;  // (a dictionary size <= 0)
@@ -629,9 +630,13 @@ static const uint64_t kMaxPiece = 1ull << 30;  // (a piece of several documents;
 //   JB_STAMPS    (STAMPS=1 builds only) per-wave phase clocks to stderr
 static int init_launch_cfg(Device* d) {
     LaunchCfg& lc = d->lc;
-    lc.grid_zh = d->ncu * std::max(zh_blocks_per_cu(true), zh_blocks_per_cu(false));
-    const int gz = env_int("JB_GRID_ZH", 0);
-    if (gz > 0) lc.grid_zh = (uint32_t)gz;
+    lc.zh_waves = d->ncu * std::max(zh_waves_per_cu(true, false), zh_waves_per_cu(false, false));
+    lc.zh_waves_wide = d->ncu * std::max(zh_waves_per_cu(true, true), zh_waves_per_cu(false, true));
+    const int gz = env_int("JB_GRID_ZH", 0);  // (in 4-wave workgroups)
+    if (gz > 0) lc.zh_waves = lc.zh_waves_wide = 4u * (uint32_t)gz;
+    const int wide = env_int("JB_ZH_WIDE", -1);
+    if (wide < -1 || wide > 1) return fail(JB_EINVAL, "JB_ZH_WIDE=%d: want -1 (by batch size), 0 or 1", wide);
+    lc.zh_wide = wide;
     const int grp = env_int("JB_ZH_GROUP", 0);
     if (grp != 0) {
         if (grp < (int)kZhGroupSmall || grp > (int)kZhGroupBytes || grp % 32 != 0)
@@ -678,8 +683,8 @@ static int launch_pipeline_(Device* d, const Work& w, const uint8_t* d_text, uin
     d->last_nbytes = nbytes;
     d->last_small = false;
     if (dbg)
-        fprintf(stderr, "[jb] nbytes=%llu ndocs=%u grid_zh=%u zh_group=%u\n", (unsigned long long)nbytes,
-                ndocs, lc.grid_zh, lc.zh_group ? lc.zh_group : zh_group_for(nbytes));
+        fprintf(stderr, "[jb] nbytes=%llu ndocs=%u zh_waves=%u/%u wide=%d zh_group=%u\n", (unsigned long long)nbytes,
+                ndocs, lc.zh_waves, lc.zh_waves_wide, lc.zh_wide, lc.zh_group ? lc.zh_group : zh_group_for(nbytes));
     static const bool use_graph = env_int("JB_GRAPH", 1) != 0;
     if (use_graph && !d->profile && lc.diag == 0 && s != nullptr && !mask) {
         const Device::GraphKey key{d_text, nbytes, d_doc_off, ndocs, hmm, d->work_gen, s, w.tok_start, w.tok_end, w.doc_tok};
@@ -717,7 +722,7 @@ static int launch_pipeline_(Device* d, const Work& w, const uint8_t* d_text, uin
                                       d->profile ? &d->timer : nullptr, mask);
     if (e != hipSuccess) return fail(JB_EDEVICE, "pipeline launch: %s", hipGetErrorString(e));
     if ((lc.diag & 0x100u) && d->w.dbg) {  // diagnostic: per-wave clocks of k_zh (STAMPS builds)
-        const uint32_t nwv = std::min<uint32_t>(lc.grid_zh * 4u, 65536u);
+        const uint32_t nwv = std::min<uint32_t>(std::max(lc.zh_waves, lc.zh_waves_wide), 16384u);
         std::vector<uint64_t> st((size_t)nwv * 16);
         HIPCHK(hipMemcpyAsync(st.data(), d->w.dbg, st.size() * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));

@@ -22,6 +22,7 @@ struct DevImage {
     // so k_mark_walk gets code and level-1 cell in one load (jb_l1row_make)
     const uint64_t* l1row;
     uint32_t nrows;
+    uint32_t nw1;  // entries in wtab1 (distinct weights + 1)
     // 1: every weight is finite or -Inf (a dictionary whose size is > 0).  k_zh's
     // record fold relies on it; otherwise k_mark_walk writes only overflow records
     // and k_zh folds every rune with maxIndexProba's literal rule.
@@ -56,6 +57,10 @@ constexpr uint64_t kZhSmallBatch = 16ull << 20;
 constexpr uint32_t kZhLongMin = 8192;  // zh blocks of at least this many bytes go to k_long_*
 constexpr uint32_t kSeg = 64;          // runes per segment of a long block (k_long_seg/path/tail)
 inline uint32_t zh_group_for(uint64_t nbytes) { return nbytes < kZhSmallBatch ? kZhGroupSmall : kZhGroupBytes; }
+// k_zh's wide form: 16-wave workgroups, one per CU, sharing one LDS copy of the weight
+// table (up to kZhWtab entries of wtab1) for the DP's weight reads
+constexpr uint32_t kZhWgWide = 16;
+constexpr uint32_t kZhWtab = 5120;
 
 // Per-call device workspace, sized for `nbytes` of text.
 struct Work {
@@ -106,7 +111,9 @@ struct KernelTimer {
 
 // Launch shape of one pipeline run (fixed per device at jb_open).
 struct LaunchCfg {
-    uint32_t grid_zh;   // persistent grid of k_zh
+    uint32_t zh_waves;       // persistent grid of k_zh, in waves (4-wave workgroups)
+    uint32_t zh_waves_wide;  // ... of its wide form (kZhWgWide-wave workgroups)
+    int32_t zh_wide;         // k_zh's wide form: -1 by batch size, 0 never, 1 whenever the weights fit
     uint32_t zh_group;  // k_zh group bytes (0: zh_group_for(nbytes))
     uint32_t diag;      // diagnostic clocks (STAMPS builds only; 0 otherwise)
     uint32_t small_max; // host batches up to this many bytes take k_small (0: never)
@@ -176,7 +183,7 @@ constexpr uint32_t kSnapWords = CNT_CLEAR + 4;
 hipError_t run_zero(void* p, uint64_t bytes, hipStream_t stream, void* p2 = nullptr, uint32_t bytes2 = 0);
 hipError_t run_snap(const Work& w, uint64_t nbytes, uint32_t* out, hipStream_t stream);
 
-// Resident k_zh workgroups per CU (occupancy API).
-uint32_t zh_blocks_per_cu(bool hmm);
+// Resident k_zh waves per CU (occupancy API), 4-wave or wide workgroups.
+uint32_t zh_waves_per_cu(bool hmm, bool wide);
 
 }  // namespace jb

@@ -818,6 +818,14 @@ constexpr uint32_t kZhWinWords = kZhWin / 32u + 1u;        // token bitmap words
 static_assert(kZhGroupBytes % 32u == 0u && kZhGroupSmall % 32u == 0u && kZhGroupSmall <= kZhGroupBytes,
               "k_zh groups are whole token-bitmap words");
 static_assert(2u * kZhWinWords <= 2u * kZhRing * 64u, "token bitmaps fit over the ring");
+// the wave's run list (zh_fwd_a3 -> viterbi_fwd_runs) sits in the ring area too, past the bitmaps
+constexpr uint32_t kZhPool = 512u;  // (u32 word offset in the wave's ring)
+constexpr uint32_t kZhBlBytes = kZhWin / 3u + 4u;
+// LDS of the wide form: per wave the slots, ring, block table and histogram, plus the
+// length table and the weight table; all of it within one CU's 160 KiB
+static_assert(kZhWgWide * (((kZhBlBytes + 15u) & ~15u) + 8u * kZhRing * 64u + 4u * kZhChunk + 256u + 4u) + 2048u +
+                      8u * kZhWtab <= 163840u,
+              "k_zh wide form: LDS");
 static_assert(kZhWin < 65536u, "window offsets are packed in 16 bits");
 // k_zh stages a group's lane-mask words plus two 64-word rounds after them (lm_collect reads
 // round rw and its lookahead rw + 64, with rw < the group's words) into the wave's ring area.
@@ -1088,13 +1096,23 @@ __device__ __forceinline__ void dp_walk_rune(const V& v, const DevImage& im, uin
 // vmcnt bookkeeping stays exact and later waits do not drain other loads.  Each
 // address is the image's wtab1 plus a 32-bit byte offset (the saddr form of the
 // load: no 64-bit address arithmetic).
+//
+// WL: the whole table sits in LDS (s_wt, k_zh's wide workgroups), so the four
+// reads are ds_read_b64 instead of global gathers.  A global gather whose 64
+// lanes hit different cache lines costs the CU's vector L1 one cycle per lane
+// (64 cycles per wave instruction; tools/diag/gather.hip), and the DP's four per
+// step kept that unit saturated; LDS reads take the LDS pipe instead.
 typedef const __attribute__((address_space(1))) char gchar;  // global memory, whatever inference concludes
+typedef const __attribute__((address_space(3))) char lchar;  // LDS
+__shared__ double s_wt[kZhWtab];  // wtab1 in LDS (k_zh<.., kZhWgWide>: one copy per CU)
+template <bool WL = false>
 __device__ __forceinline__ void rec_weights(const DevImage& im, uint64_t rc, double w[4]) {
     gchar* const wb = (gchar*)im.wtab1;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const uint32_t off = (uint32_t)(rc >> (8 + kEdgeIdxBits * k - 3)) & (((1u << kEdgeIdxBits) - 1u) << 3);
-        w[k] = *(const __attribute__((address_space(1))) double*)(wb + off);
+        if constexpr (WL) w[k] = *(const __attribute__((address_space(3))) double*)((lchar*)s_wt + off);
+        else w[k] = *(const __attribute__((address_space(1))) double*)(wb + off);
     }
 }
 
@@ -1280,7 +1298,7 @@ __device__ __forceinline__ uint32_t zh_dp(const V& v, const DevImage& im, const 
 // with q.  Length-table entries carry kLtabOvf for record 0 (an overflowed
 // record: dp_walk_rune folds that rune).
 constexpr uint64_t kLtabOvf = 0x8000u;  // (bit 15 of field 0: no effect on a ring offset)
-template <class Src>
+template <bool WL, class Src>
 __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const uint64_t* __restrict__ erec,
                              double* __restrict__ gbest, double* ring, const char* rb0, uint32_t lb, const Src& src) {
     uint32_t j = 0, bs = 0, be = 0;
@@ -1346,7 +1364,7 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
             ld_pair(s - 4u, yl, yh);
         }
         lc = s_ltab[(uint32_t)rc & 0xFFu];
-        rec_weights(im, rc, wn);
+        rec_weights<WL>(im, rc, wn);
         load_pre();
     };
     auto ld_e = [&](int d) -> u64x2v { return *reinterpret_cast<const u64x2v*>(erec + (int32_t)(s - 1u - d)); };
@@ -1358,7 +1376,7 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
         const uint64_t nx = P == 0 ? xl : (P == 1 ? yh : (P == 2 ? yl : xh));
         const uint64_t r1v = more ? nx : 0ull;  // the next rune's record (when it exists)
         const uint64_t ln = s_ltab[(uint32_t)r1v & 0xFFu];
-        rec_weights(im, r1v, wn);
+        rec_weights<WL>(im, r1v, wn);
         if (P == 0) ld_pair(s - 5u, xl, xh);
         if (P == 2) ld_pair(s - 5u, yl, yh);
         const uint32_t cs = c << 9;
@@ -1418,6 +1436,8 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
 #define JB_ZH_RUNS 4
 #endif
 constexpr uint32_t kZhRuns = JB_ZH_RUNS;
+static_assert(2u * kZhWinWords <= kZhPool && kZhPool + kZhRuns * 64u <= 2u * kZhRing * 64u,
+              "k_zh: token bitmaps, then the run list, within the wave's ring");
 struct RunList {
     uint32_t* t;
     uint32_t wb;
@@ -1674,7 +1694,7 @@ __device__ __forceinline__ bool text_has4(const uint8_t* __restrict__ text, uint
     return (acc & 0x80808080u) != 0u;
 }
 
-template <bool HMM, bool A3>
+template <bool HMM, bool A3, bool WL>
 __device__ __forceinline__ void zh_chunk_main(const uint8_t* __restrict__ text, const DevImage& im,
                               const uint64_t* __restrict__ erec, double* __restrict__ gbest, uint8_t* bls,
                               double* ring, const char* rb0, uint32_t lb, uint32_t* rb32, uint32_t* runs,
@@ -1683,7 +1703,7 @@ __device__ __forceinline__ void zh_chunk_main(const uint8_t* __restrict__ text, 
                               uint32_t* __restrict__ counters, uint32_t winw, uint32_t& nties, uint64_t* st) {
     const GrpZvT<A3> v{text, bls, wb};
     uint32_t steps;
-    if constexpr (A3) steps = zh_dp_a3(v, im, erec, gbest, ring, rb0, lb, src);
+    if constexpr (A3) steps = zh_dp_a3<WL>(v, im, erec, gbest, ring, rb0, lb, src);
     else steps = zh_dp(v, im, erec, gbest, ring, src);
     wave_sync();  // ring dead: its space takes the window's token bitmaps
     if (st) {
@@ -1819,8 +1839,10 @@ __device__ __noinline__ uint2 lm_collect(const uint32_t* lmv, uint32_t* tbl, uin
 #define JB_ZH_WAVES 4
 #endif
 #define JB_ZH_ATTR __attribute__((amdgpu_waves_per_eu(JB_ZH_WAVES)))
-template <bool HMM>
-__global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict__ text, uint64_t nbytes,
+// NW waves per workgroup: 4, or kZhWgWide = 16 (one workgroup per CU) with the
+// weight table in LDS for the DP (rec_weights<true>), when it fits (kZhWtab).
+template <bool HMM, uint32_t NW>
+__global__ __launch_bounds__(NW * 64) JB_ZH_ATTR void k_zh(const uint8_t* __restrict__ text, uint64_t nbytes,
                                             const uint32_t* __restrict__ lanemask, const uint2* __restrict__ tile_cnt,
                                             const uint32_t* __restrict__ tile4,
                                             uint32_t* __restrict__ counters, DevImage im,
@@ -1829,12 +1851,12 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
                                             uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
                                             uint2* __restrict__ longblk, uint32_t* __restrict__ lsegb, uint32_t grp,
                                             uint32_t g1, uint32_t sgrp, uint32_t diag, uint64_t* __restrict__ dbg) {
-    __shared__ uint8_t s_bl[4][kZhWin / 3u + 4u];
-    __shared__ double s_rb[4][kZhRing * 64];  // DP ring, then the window's token bitmaps
-    __shared__ uint32_t s_tbl[4][kZhChunk];   // the chunk's blocks as found, then as dealt to the lanes
-    __shared__ uint32_t s_hist[4][64];
-    __shared__ uint32_t s_runs[4][kZhRuns * 64];
-    __shared__ uint32_t s_nrun[4];  // entries in a wave's run list (zh_fwd_a3)
+    constexpr bool WL = NW == kZhWgWide;
+    __shared__ uint8_t s_bl[NW][kZhBlBytes];
+    __shared__ double s_rb[NW][kZhRing * 64];  // DP ring, then the window's token bitmaps and run list
+    __shared__ uint32_t s_tbl[NW][kZhChunk];   // the chunk's blocks as found, then as dealt to the lanes
+    __shared__ uint32_t s_hist[NW][64];
+    __shared__ uint32_t s_nrun[NW];  // entries in a wave's run list (zh_fwd_a3)
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     double* ring = s_rb[wv] + lane;
     const char* const rb0 = reinterpret_cast<const char*>(&s_rb[0][0]);  // (rec_fold_a3's ring addressing)
@@ -1851,7 +1873,9 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
     const uint32_t nlw = ntiles * 256u;                                  // lane-mask words (16 bytes each)
     const uint32_t winw = (grp + (kZhWin - kZhGroupBytes)) / 32u + 1u;  // token words of a window (<= kZhWinWords)
     auto lmw = [&](uint32_t w) -> uint32_t { return w < nlw ? lanemask[w] : 0u; };
-    s_ltab[threadIdx.x] = ltab_entry(threadIdx.x);  // (256 threads)
+    if (threadIdx.x < 256u) s_ltab[threadIdx.x] = ltab_entry(threadIdx.x);
+    if constexpr (WL)  // the weights, once per CU (the host launches this form only when they fit)
+        for (uint32_t i = threadIdx.x; i < im.nw1; i += NW * 64u) s_wt[i] = im.wtab1[i];
     __syncthreads();
     // diagnostic per-wave clocks (JB_ABLATE bit 8): [0] setup [1] DP [2] forward+Viterbi+flush [3] chunks
     // [4] sum of lane DP steps [5] sum of per-chunk max lane DP steps [6] blocks past the window [7] scratch
@@ -1991,11 +2015,11 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
                 stv[3]++;
             }
             if (all3)
-                zh_chunk_main<HMM, true>(text, im, erec, gbest, s_bl[wv], ring, rb0, lb, rb32, s_runs[wv] + lane, &s_nrun[wv], src, wb, lane,
-                                         counters, winw, nties, st);
+                zh_chunk_main<HMM, true, WL>(text, im, erec, gbest, s_bl[wv], ring, rb0, lb, rb32, rb32 + kZhPool + lane,
+                                             &s_nrun[wv], src, wb, lane, counters, winw, nties, st);
             else
-                zh_chunk_main<HMM, false>(text, im, erec, gbest, s_bl[wv], ring, rb0, lb, rb32, s_runs[wv] + lane, &s_nrun[wv], src, wb,
-                                          lane, counters, winw, nties, st);
+                zh_chunk_main<HMM, false, WL>(text, im, erec, gbest, s_bl[wv], ring, rb0, lb, rb32, rb32 + kZhPool + lane,
+                                              &s_nrun[wv], src, wb, lane, counters, winw, nties, st);
             // the window's token words: consecutive words per lane, one OR each (edge
             // words are shared with neighbouring groups and with k_nonzh)
             {
@@ -2056,7 +2080,7 @@ __global__ __launch_bounds__(256) JB_ZH_ATTR void k_zh(const uint8_t* __restrict
             sum += ((uint64_t)hi << 32) | lo;
         }
         if (lane == 0) {
-            uint64_t* o = dbg + (blockIdx.x * 4u + wv) * 16u;
+            uint64_t* o = dbg + (blockIdx.x * NW + wv) * 16u;
             o[8] = stv[8];
             o[9] = stv[9];
             o[10] = stv[10];
@@ -3614,14 +3638,17 @@ hipError_t run_small(const DevImage& im, const uint8_t* text, uint32_t nbytes, c
     return hipGetLastError();
 }
 
-template <bool HMM>
+template <bool HMM, uint32_t NW>
 static uint32_t occ_zh() {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_zh<HMM>, 256, 0) != hipSuccess || n <= 0) return 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_zh<HMM, NW>, NW * 64, 0) != hipSuccess || n <= 0) return 1;
     return (uint32_t)n;
 }
 
-uint32_t zh_blocks_per_cu(bool hmm) { return hmm ? occ_zh<true>() : occ_zh<false>(); }
+uint32_t zh_waves_per_cu(bool hmm, bool wide) {
+    if (wide) return kZhWgWide * (hmm ? occ_zh<true, kZhWgWide>() : occ_zh<false, kZhWgWide>());
+    return 4u * (hmm ? occ_zh<true, 4>() : occ_zh<false, 4>());
+}
 
 
 #define JB_TIMED_ON(id, st, ...)                  \
@@ -3645,7 +3672,12 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     // the last zh_tail bytes (at most) in groups of zh_tail_group (tail_groups)
     uint32_t g1, sgrp;
     const uint64_t ngroups = zh_tail_groups(nbytes, grp, lc, &g1, &sgrp);
-    const uint32_t grid_zh = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(lc.grid_zh, (ngroups + 3) / 4));
+    // the wide form (16 waves per workgroup, weights in LDS) for batches in 6 KiB groups whose
+    // weight table fits; JB_ZH_WIDE (lc.zh_wide) forces either form
+    const bool wide = im.nw1 <= kZhWtab && (lc.zh_wide > 0 || (lc.zh_wide < 0 && grp == kZhGroupBytes));
+    const uint32_t nw = wide ? kZhWgWide : 4u;
+    const uint32_t grid_zh = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>((wide ? lc.zh_waves_wide : lc.zh_waves) / nw, (ngroups + nw - 1) / nw));
     // No clearing pass: the document bitmap is all zeros between runs (k_nonzh clears
     // what k_docbits set; a fresh or dirty workspace is cleared by the caller), k_docbits
     // clears the counters and k_mark_walk the token bitmaps, tile by tile.
@@ -3656,14 +3688,18 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     JB_TIMED(K_MARK_WALK, hipLaunchKernelGGL(k_mark_walk, dim3(ntiles), dim3(256), 0, stream, d_text, nbytes,
                                              w.docbits, im, w.lanemask, w.tile_cnt, w.erec + kErecPad,
                                              w.tile4, w.alnum16, w.sbits, w.ebits, diag, w.dbg_walk));
-    if (hmm)
-        JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<true>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes,
-                                          w.lanemask, w.tile_cnt, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
-                                          w.longblk, w.lsegb, grp, g1, sgrp, diag, w.dbg));
-    else
-        JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<false>), dim3(grid_zh), dim3(256), 0, stream, d_text, nbytes,
-                                          w.lanemask, w.tile_cnt, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl, w.gbest, w.sbits, w.ebits,
-                                          w.longblk, w.lsegb, grp, g1, sgrp, diag, w.dbg));
+#define JB_ZH_LAUNCH(H, N)                                                                                      \
+    JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<H, N>), dim3(grid_zh), dim3((N) * 64), 0, stream, d_text, nbytes,       \
+                                      w.lanemask, w.tile_cnt, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl,     \
+                                      w.gbest, w.sbits, w.ebits, w.longblk, w.lsegb, grp, g1, sgrp, diag, w.dbg))
+    if (hmm) {
+        if (wide) JB_ZH_LAUNCH(true, kZhWgWide);
+        else JB_ZH_LAUNCH(true, 4u);
+    } else {
+        if (wide) JB_ZH_LAUNCH(false, kZhWgWide);
+        else JB_ZH_LAUNCH(false, 4u);
+    }
+#undef JB_ZH_LAUNCH
     {
         // long blocks: the chain, then one lane per 64-rune segment (at most
         // nbytes / 192 + nbytes / kZhLongMin segments), one wave per block

@@ -19,18 +19,31 @@ def _pair(dp, ep, kind=J.JB_DICT_TXT, size_override=0):
     return tk, o
 
 
-@pytest.fixture(scope="module")
-def small(syn_small):
+def _pair_env(dp, ep, env, **kw):
+    with pytest.MonkeyPatch.context() as mp:
+        for k, v in env.items():
+            mp.setenv(k, v)
+        return _pair(dp, ep, **kw)
+
+
+# k_zh's two forms: 4-wave workgroups with the weights gathered from HBM (what batches
+# under 16 MiB get), and 16-wave workgroups with the weight table in LDS (the headline
+# batches' form), forced with JB_ZH_WIDE=1 on these small ones
+ZH_FORMS = {"auto": {}, "wide": {"JB_ZH_WIDE": "1"}}
+
+
+@pytest.fixture(scope="module", params=list(ZH_FORMS))
+def small(syn_small, request):
     dp, ep, s = syn_small
-    tk, o = _pair(dp, ep)
+    tk, o = _pair_env(dp, ep, ZH_FORMS[request.param])
     yield tk, o, s
     tk.close()
 
 
-@pytest.fixture(scope="module")
-def full(syn_full):
+@pytest.fixture(scope="module", params=list(ZH_FORMS))
+def full(syn_full, request):
     dp, ep, s = syn_full
-    tk, o = _pair(dp, ep)
+    tk, o = _pair_env(dp, ep, ZH_FORMS[request.param])
     yield tk, o, s
     tk.close()
 
@@ -392,11 +405,14 @@ def test_device_api_and_profile(small):
     assert np.array_equal(gs, hs) and np.array_equal(ge, he) and np.array_equal(gd, hd)
 
 
+@pytest.mark.parametrize("nfill", [20000, 3000])
 @pytest.mark.parametrize("kind", [J.JB_DICT_TXT, J.JB_DICT_PREFIX])
-def test_record_overflow_paths(tmp_path, syn_small, kind):
+def test_record_overflow_paths(tmp_path, syn_small, kind, nfill):
     """Dictionaries that push k_walk's packed records past their limits: runes
     with more than 4 edges, edges longer than 8 runes (k_zh's redo with the
-    global best array) and more than 2^14 distinct weights (14-bit indices)."""
+    global best array) and more than 2^14 distinct weights (14-bit indices;
+    nfill 20000).  With 3000 fill words the weight table fits k_zh's LDS copy, and
+    JB_ZH_WIDE=1 runs the wide form on the same overflow records."""
     _, ep, _ = syn_small
     rng = random.Random(11)
     pool = [chr(c) for c in range(0x4E00, 0x4E00 + 600)]
@@ -410,13 +426,14 @@ def test_record_overflow_paths(tmp_path, syn_small, kind):
                 f += rng.randint(1, 5)
                 lines.append(f"{s[:k]} {f}")
     fill = []
-    for i in range(20000):  # distinct frequencies -> > 2^14 weights
+    for i in range(nfill):  # distinct frequencies (20000: > 2^14 weights)
         w = rng.choice(pool) + rng.choice(pool) + (rng.choice(pool) if i % 3 == 0 else "")
         fill.append(w)
         lines.append(f"{w} {1000 + 3 * i}")
     dp = tmp_path / "dict.txt"
     dp.write_text("\n".join(lines) + "\n", encoding="utf-8")
-    tk, o = _pair(str(dp), ep, kind=kind, size_override=60101967 if kind == J.JB_DICT_PREFIX else 0)
+    tk, o = _pair_env(str(dp), ep, ZH_FORMS["wide"], kind=kind,
+                      size_override=60101967 if kind == J.JB_DICT_PREFIX else 0)
     try:
         texts = []
         for _ in range(400):

@@ -65,12 +65,14 @@ struct Vec<16> {
 template <int W>
 __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ table, uint32_t line_mask, uint32_t D,
                                                uint32_t iters, uint32_t* __restrict__ sink,
-                                               unsigned long long* __restrict__ clk) {
+                                               unsigned long long* __restrict__ clk, uint32_t active, uint32_t bcast) {
     typedef typename Vec<W>::T T;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
     const uint32_t lpart = (lane % D) * 97u;
-    const uint32_t off = ((lane / D) * (uint32_t)W) & 127u;
+    const uint32_t off = bcast ? 0u : ((lane / D) * (uint32_t)W) & 127u;
+    // only lanes (lane * 64 / active) hold an active load: "active" lanes spread over the wave
+    if (active < 64u && (lane % (64u / active)) != 0u) return;
     uint32_t acc = 0;
     uint64_t t0 = 0, r0 = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -116,6 +118,38 @@ int main(int argc, char** argv) {
     const int widths[] = {8, 4, 16};
     const uint32_t Ds[] = {1, 4, 16, 32, 64};
     const uint32_t occs[] = {8, 4, 2, 1};
+    const bool extra = argc > 2 && argv[2][0] == 'x';  // masked and broadcast loads only
+    uint32_t A = 64, B = 0;
+    if (extra) {
+        // (active lanes, broadcast) at D = 64 / D = 1, W = 8, 8 waves per SIMD, L1- and L2-sized tables
+        const uint32_t As[] = {64, 16, 8, 4, 1};
+        for (size_t T : {(size_t)16 << 10, (size_t)2 << 20})
+            for (int bc = 0; bc < 2; bc++)
+                for (uint32_t a : As) {
+                    A = a;
+                    B = (uint32_t)bc;
+                    const uint32_t D = bc ? 1u : 64u, O = 8, nwg = ncu * O, lines = (uint32_t)(T >> 7);
+                    auto launch = [&]() { k_gather<8><<<nwg, 256>>>(table, lines - 1u, D, iters, sink, clk, A, B); };
+                    launch();
+                    CHK(hipDeviceSynchronize());
+                    CHK(hipEventRecord(e0));
+                    for (int r = 0; r < 5; r++) launch();
+                    CHK(hipEventRecord(e1));
+                    CHK(hipEventSynchronize(e1));
+                    float ms = 0;
+                    CHK(hipEventElapsedTime(&ms, e0, e1));
+                    unsigned long long c[2];
+                    CHK(hipMemcpy(c, clk, 16, hipMemcpyDeviceToHost));
+                    const double ghz = c[1] ? (double)c[0] / (double)c[1] * 0.1 : 0.0;
+                    const double sec = ms * 1e-3 / 5;
+                    const double winst = (double)nwg * 4.0 * iters * K;
+                    printf("{\"W\": 8, \"T_bytes\": %zu, \"D\": %u, \"active_lanes\": %u, \"broadcast\": %d, "
+                           "\"ms\": %.4f, \"cyc_per_winst_per_cu\": %.2f}\n",
+                           T, D, a, bc, sec * 1e3, ncu * sec * ghz * 1e9 / winst);
+                    fflush(stdout);
+                }
+        return 0;
+    }
     for (int W : widths)
         for (size_t T : tables)
             for (uint32_t D : Ds)
@@ -126,11 +160,11 @@ int main(int argc, char** argv) {
                     const uint32_t lines = (uint32_t)(T >> 7);
                     auto launch = [&]() {
                         if (W == 4)
-                            k_gather<4><<<nwg, 256>>>(table, lines - 1u, D, iters, sink, clk);
+                            k_gather<4><<<nwg, 256>>>(table, lines - 1u, D, iters, sink, clk, A, B);
                         else if (W == 8)
-                            k_gather<8><<<nwg, 256>>>(table, lines - 1u, D, iters, sink, clk);
+                            k_gather<8><<<nwg, 256>>>(table, lines - 1u, D, iters, sink, clk, A, B);
                         else
-                            k_gather<16><<<nwg, 256>>>(table, lines - 1u, D, iters, sink, clk);
+                            k_gather<16><<<nwg, 256>>>(table, lines - 1u, D, iters, sink, clk, A, B);
                     };
                     launch();
                     launch();
