@@ -20,6 +20,7 @@
 #include <thread>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <vector>
 
 #include "../../include/jiebahip.h"
@@ -114,6 +115,8 @@ struct ImageBufs {
     uint64_t* l1row = nullptr;
 };
 
+struct SmallReq;  // (cut_small)
+
 struct Device {
     int ordinal = 0;
     std::mutex mu;  // one pipeline at a time per device workspace
@@ -166,6 +169,11 @@ struct Device {
     bool last_small = false;     // the last batch took k_small (jb_last_stats reads small_hdr)
     hipStream_t sstream = nullptr;  // k_small's stream, masked to one CU (its code stays in that I-cache)
     uint32_t small_seq = 0;         // k_small calls: the kernel writes this number last
+    // concurrent small calls, coalesced into shared k_small launches (cut_small)
+    std::mutex small_mu;
+    std::condition_variable small_cv;
+    std::deque<SmallReq*> small_q;
+    bool small_leader = false;
     uint32_t small_hdr[kSmallHdr] = {0};
     uint32_t ncu = 0;
     uint64_t piece_bytes = 64ull << 20;  // host-batch pipeline piece (JB_PIECE_KIB)
@@ -912,19 +920,59 @@ extern "C" const char* jb_last_error(void) { return g_err.c_str(); }
 // ---------------------------------------------------------------------------
 
 // A batch of at most lc.small_max bytes and kSmallDocs documents (a single Cut
-// call, BASELINE config 1): one k_small launch that reads the text and offsets
-// from mapped pinned host memory and writes the spans there, then one sync.
-// text/doc_off are the batch's (doc_off[0..nd] absolute, base = doc_off[0]).
-static int cut_small(Device* d, const uint8_t* text, const uint64_t* doc_off, uint32_t nd, bool hmm,
-                     SpanBuf* out) {
-    const uint64_t base = doc_off[0], nbytes = doc_off[nd] - base;
+// call, BASELINE config 1) is one k_small launch that reads the text and offsets
+// from mapped pinned host memory (or its kernel arguments) and writes the spans
+// there.  Concurrent calls on a device are coalesced (the reference runs Cut calls
+// side by side under RLock, tokenizer.go:151-153): each call queues a SmallReq;
+// whichever caller finds no leader becomes it, and launches the queue's head
+// requests (same hmm, up to the k_small limits together) as ONE k_small batch,
+// their documents back to back, then hands each caller its own spans by its
+// documents' doc_tok ranges.  A leader leads until its own request is done and then
+// passes the role on, so no caller serves others for long.  One caller alone: a
+// batch of one, as before.
+namespace {
+struct SmallReq {
+    const uint8_t* text;
+    const uint64_t* doc_off;  // doc_off[0..nd] absolute in text
+    uint32_t nd;
+    bool hmm;
+    SpanBuf* out;
+    int rc = JB_OK;
+    std::string err;
+    bool done = false;
+};
+}  // namespace
+
+// One k_small launch over requests rq[0..n) (together within the limits): stage, launch,
+// wait for the completion word, split the spans.  Sets each request's rc / err.
+static void small_batch(Device* d, SmallReq* const* rq, uint32_t n) {
+    auto fail_all = [&](int rc) {
+        for (uint32_t i = 0; i < n; i++) {
+            rq[i]->rc = rc;
+            rq[i]->err = g_err;
+        }
+    };
+    auto chk = [&](hipError_t e, const char* what) {
+        if (e == hipSuccess) return true;
+        fail_all(fail(e == hipErrorOutOfMemory ? JB_ENOMEM : JB_EDEVICE, "%s: %s", what, hipGetErrorString(e)));
+        return false;
+    };
+    if (!chk(hipSetDevice(d->ordinal), "hipSetDevice")) return;
     if (!d->h_sin) {
         const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
-        HIPCHK(hipHostMalloc(&d->h_sin, kSmallBytes + 128 + 8 * (kSmallDocs + 1), fl));
-        HIPCHK(hipHostMalloc(&d->h_sout, kSmallOutBytes, fl));
-        HIPCHK(hipHostGetDevicePointer((void**)&d->d_sin, d->h_sin, 0));
-        HIPCHK(hipHostGetDevicePointer((void**)&d->d_sout, d->h_sout, 0));
+        if (!chk(hipHostMalloc(&d->h_sin, kSmallBytes + 128 + 8 * (kSmallDocs + 1), fl), "hipHostMalloc") ||
+            !chk(hipHostMalloc(&d->h_sout, kSmallOutBytes, fl), "hipHostMalloc") ||
+            !chk(hipHostGetDevicePointer((void**)&d->d_sin, d->h_sin, 0), "hipHostGetDevicePointer") ||
+            !chk(hipHostGetDevicePointer((void**)&d->d_sout, d->h_sout, 0), "hipHostGetDevicePointer"))
+            return;
         d->h_sout[SM_DONE] = 0;  // (recycled pinned memory may hold any value; small_seq starts at 1)
+    }
+    const bool hmm = rq[0]->hmm;
+    uint64_t nbytes = 0;
+    uint32_t nd = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        nbytes += rq[i]->doc_off[rq[i]->nd] - rq[i]->doc_off[0];
+        nd += rq[i]->nd;
     }
     const auto c0 = std::chrono::steady_clock::now();
     // a batch that fits the kernel arguments (96 bytes, 7 documents) travels in them (the kernel reads them from
@@ -932,71 +980,149 @@ static int cut_small(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
     const bool inl = nbytes <= kSmallInline && nd <= kSmallInlineDocs;
     SmallInline in;
     memset(&in, 0, sizeof in);
-    if (inl) {
-        if (nbytes) memcpy(in.txt, text + base, nbytes);
-        for (uint32_t k = 0; k <= nd; k++) in.doff[k] = (uint16_t)(doc_off[k] - base);
-    } else {
-        if (nbytes) memcpy(d->h_sin, text + base, nbytes);
+    uint8_t* const tx = inl ? in.txt : d->h_sin;
+    uint64_t* const hoff = reinterpret_cast<uint64_t*>(d->h_sin + kSmallBytes + 128);
+    uint64_t at = 0;
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const SmallReq& r = *rq[i];
+        const uint64_t base = r.doc_off[0], len = r.doc_off[r.nd] - base;
+        if (len) memcpy(tx + at, r.text + base, len);
+        for (uint32_t j = 0; j < r.nd; j++, k++) {
+            if (inl) in.doff[k] = (uint16_t)(at + r.doc_off[j] - base);
+            else hoff[k] = at + r.doc_off[j] - base;
+        }
+        at += len;
+    }
+    if (inl) in.doff[nd] = (uint16_t)nbytes;
+    else {
+        hoff[nd] = nbytes;
         memset(d->h_sin + nbytes, 0, 16);
-        uint64_t* const hoff = reinterpret_cast<uint64_t*>(d->h_sin + kSmallBytes + 128);
-        for (uint32_t k = 0; k <= nd; k++) hoff[k] = doc_off[k] - base;
     }
     // the kernel writes the call's sequence number after everything else (system-scope
     // release); spinning on it returns as soon as the results are in host memory
     const uint32_t seq = ++d->small_seq;
     volatile uint32_t* done = d->h_sout + SM_DONE;
-    const hipError_t e =
-        run_small(d->dim, inl ? nullptr : d->d_sin, (uint32_t)nbytes,
-                  inl ? nullptr : reinterpret_cast<const uint64_t*>(d->d_sin + kSmallBytes + 128), nd, hmm,
-                  d->d_sout, seq, in, d->sstream);
-    if (e != hipSuccess) return fail(JB_EDEVICE, "k_small launch: %s", hipGetErrorString(e));
+    if (!chk(run_small(d->dim, inl ? nullptr : d->d_sin, (uint32_t)nbytes, inl ? nullptr : reinterpret_cast<const uint64_t*>(
+                                                                                               d->d_sin + kSmallBytes + 128),
+                       nd, hmm, d->d_sout, seq, in, d->sstream),
+             "k_small launch"))
+        return;
     const auto c1 = std::chrono::steady_clock::now();
     for (uint32_t spin = 0; *done != seq; spin++) {
         if ((spin & 1023u) != 1023u) continue;
         const hipError_t q = hipStreamQuery(d->sstream);
         if (q == hipErrorNotReady) continue;
-        if (q != hipSuccess) return fail(JB_EDEVICE, "k_small: %s", hipGetErrorString(q));
-        if (*done != seq) return fail(JB_EDEVICE, "k_small finished without its completion word");
+        if (!chk(q, "k_small")) return;
+        if (*done != seq) {
+            fail_all(fail(JB_EDEVICE, "k_small finished without its completion word"));
+            return;
+        }
         break;
     }
     std::atomic_thread_fence(std::memory_order_acquire);
     const auto c2 = std::chrono::steady_clock::now();
     const uint32_t* h = d->h_sout;
-    memcpy(d->small_hdr, h, sizeof d->small_hdr);
-    d->last_small = true;
-    d->has_stats = true;
+    {
+        std::lock_guard<std::mutex> g(d->mu);  // (jb_last_stats reads these)
+        memcpy(d->small_hdr, h, sizeof d->small_hdr);
+        d->last_small = true;
+        d->has_stats = true;
+    }
     static const bool dbg = getenv("JB_DEBUG") != nullptr;
     if (dbg) {  // k_small's phase clocks (10 ns ticks from its start)
         auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
             return std::chrono::duration<double, std::micro>(b - a).count();
         };
-        fprintf(stderr, "[jb] k_small %llu bytes: stage+launch %.2f us, sync %.2f us; phases (us):",
-                (unsigned long long)nbytes, us(c0, c1), us(c1, c2));
-        for (int k = 0; k < 15; k++) fprintf(stderr, " %.2f", h[SM_CLK + k] * 0.01);
+        fprintf(stderr, "[jb] k_small %llu bytes, %u calls: stage+launch %.2f us, sync %.2f us; phases (us):",
+                (unsigned long long)nbytes, n, us(c0, c1), us(c1, c2));
+        for (int q = 0; q < 15; q++) fprintf(stderr, " %.2f", h[SM_CLK + q] * 0.01);
         fprintf(stderr, "; %u clocks", h[SM_CLK + 15]);
         fprintf(stderr, "\n");
     }
-    if (h[SM_ERR]) return fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)");
-    if (h[SM_NTOK] != h[SM_NTOKE])
-        return fail(JB_EDEVICE, "internal: %u token starts vs %u ends", h[SM_NTOK], h[SM_NTOKE]);
-    const uint32_t nt = h[SM_NTOK];
+    if (h[SM_ERR]) {  // the reference panics on some document: find whose (each call alone)
+        if (n > 1) {
+            for (uint32_t i = 0; i < n; i++) small_batch(d, rq + i, 1);
+            return;
+        }
+        fail_all(fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)"));
+        return;
+    }
+    if (h[SM_NTOK] != h[SM_NTOKE]) {
+        fail_all(fail(JB_EDEVICE, "internal: %u token starts vs %u ends", h[SM_NTOK], h[SM_NTOKE]));
+        return;
+    }
     const uint32_t* hs = h + kSmallHdr;
     const uint32_t* he = hs + kSmallBytes;
     const uint64_t* dt = reinterpret_cast<const uint64_t*>(he + kSmallBytes);
-    const bool write = out->reserve(out->n + nt);
-    if (!write && !out->external) return fail(JB_ENOMEM, "out of host memory for %u tokens", nt);
-    if (write) {
-        for (uint32_t k = 0; k < nt; k++) {
-            out->s[out->n + k] = base + hs[k];
-            out->e[out->n + k] = base + he[k];
+    at = 0;
+    k = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        SmallReq& r = *rq[i];
+        SpanBuf* out = r.out;
+        const uint64_t base = r.doc_off[0];
+        const uint64_t t0 = dt[k], t1 = dt[k + r.nd], nt = t1 - t0;
+        const bool write = out->reserve(out->n + nt);
+        if (!write && !out->external) {
+            r.rc = fail(JB_ENOMEM, "out of host memory for %llu tokens", (unsigned long long)nt);
+            r.err = g_err;
+        } else {
+            if (write) {
+                for (uint64_t t = 0; t < nt; t++) {  // (batch offsets -> this call's text)
+                    out->s[out->n + t] = base + hs[t0 + t] - at;
+                    out->e[out->n + t] = base + he[t0 + t] - at;
+                }
+            } else {  // caller arrays too small: count the rest, write nothing more
+                out->needed = out->n + nt;
+                out->cap = 0;
+            }
+            out->n += nt;
+            for (uint32_t j = 0; j < r.nd; j++) out->per_doc.push_back(dt[k + j + 1] - dt[k + j]);
         }
-    } else {  // caller arrays too small: count the rest, write nothing more
-        out->needed = out->n + nt;
-        out->cap = 0;
+        at += r.doc_off[r.nd] - base;
+        k += r.nd;
     }
-    out->n += nt;
-    for (uint32_t k = 0; k < nd; k++) out->per_doc.push_back(dt[k + 1] - dt[k]);
-    return JB_OK;
+}
+
+static int cut_small(Device* d, const uint8_t* text, const uint64_t* doc_off, uint32_t nd, bool hmm,
+                     SpanBuf* out) {
+    SmallReq r{text, doc_off, nd, hmm, out};
+    std::unique_lock<std::mutex> lk(d->small_mu);
+    d->small_q.push_back(&r);
+    while (!r.done) {
+        if (d->small_leader) {
+            d->small_cv.wait(lk, [&] { return r.done || !d->small_leader; });
+            continue;
+        }
+        d->small_leader = true;
+        while (!r.done) {  // lead until this call's own request is served
+            std::vector<SmallReq*> b;
+            uint64_t bytes = 0;
+            uint32_t docs = 0;
+            const bool h = d->small_q.front()->hmm;
+            for (auto it = d->small_q.begin(); it != d->small_q.end();) {
+                SmallReq* q = *it;
+                const uint64_t len = q->doc_off[q->nd] - q->doc_off[0];
+                if (q->hmm != h || bytes + len > d->lc.small_max || docs + q->nd > kSmallDocs) {
+                    ++it;
+                    continue;
+                }
+                bytes += len;
+                docs += q->nd;
+                b.push_back(q);
+                it = d->small_q.erase(it);
+            }
+            lk.unlock();
+            small_batch(d, b.data(), (uint32_t)b.size());
+            lk.lock();
+            for (SmallReq* q : b) q->done = true;
+            d->small_cv.notify_all();
+        }
+        d->small_leader = false;
+        d->small_cv.notify_all();  // a waiting caller takes the queue over
+    }
+    if (r.rc) g_err = r.err;
+    return r.rc;
 }
 
 // Caller-owned boundary masks (jb_cut_batch_mask): bit i of s / e is byte batch0 + i.
@@ -1058,19 +1184,15 @@ static bool host_pinned(const void* p, uint64_t n) {
 // widened to u64 batch offsets into `out` by kCopyThreads host threads.
 static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, uint32_t d0, uint32_t d1, bool hmm,
                      SpanBuf* out, const MaskDst* mask) {
-    std::lock_guard<std::mutex> g(d->mu);
-    HIPCHK(hipSetDevice(d->ordinal));
     if (d0 >= d1) return JB_OK;
-    for (uint32_t k = d0; k < d1; k++)
-        if (doc_off[k + 1] - doc_off[k] >= (1ull << 31))
-            return fail(JB_ELIMIT, "document %u is %llu bytes (limit 2 GiB)", k,
-                        (unsigned long long)(doc_off[k + 1] - doc_off[k]));
     const uint64_t r0 = doc_off[d0], rbytes = doc_off[d1] - r0;
     const uint32_t ndr = d1 - d0;
     // mask geometry: range word j = caller word rw + j; the range's first bit is bit rsh of word 0
     const uint64_t rrel = mask ? r0 - mask->batch0 : 0, rw = rrel >> 6, rsh = rrel & 63u;
     const uint64_t nw = mask ? (rsh + rbytes + 63u) >> 6 : 0;
     int rc;
+    // (small batches: k_small on its own stream and buffers, coalesced across callers, without
+    // the device lock that the pipeline below holds)
     if (d->lc.small_max && rbytes <= d->lc.small_max && ndr <= kSmallDocs) {
         if (!mask) return cut_small(d, text, doc_off + d0, ndr, hmm, out);
         SpanBuf tmp;
@@ -1089,6 +1211,12 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         tmp.release();
         return JB_OK;
     }
+    std::lock_guard<std::mutex> g(d->mu);
+    HIPCHK(hipSetDevice(d->ordinal));
+    for (uint32_t k = d0; k < d1; k++)
+        if (doc_off[k + 1] - doc_off[k] >= (1ull << 31))
+            return fail(JB_ELIMIT, "document %u is %llu bytes (limit 2 GiB)", k,
+                        (unsigned long long)(doc_off[k + 1] - doc_off[k]));
     const uint64_t kPiece = d->piece_bytes;
     struct Piece { uint32_t d0, d1; uint64_t off, slot; };  // documents, device text offset, offsets slot
     std::vector<Piece> pcs;

@@ -902,3 +902,33 @@ def test_document_bitmap_between_runs(small):
         for rep in range(2):
             for i, off in enumerate(layouts):
                 _cmp_batch(tk, o, buf, off, hmm, f"layout {i} rep {rep}")
+
+
+def test_concurrent_cut_calls(syn_small, tmp_path):
+    """16 threads x 1,000 jb_cut calls at once on one context (Go code calling Cut
+    from many goroutines; the reference takes only an RLock, tokenizer.go:151-153):
+    every result equals the oracle's, and the calls are coalesced into shared
+    k_small launches (tests/concurrent_cut.cpp prints both rates)."""
+    import subprocess
+    dp, ep, s = syn_small
+    exe = str(tmp_path / "concurrent_cut")
+    lib = os.path.join(ROOT, "jieba-go_amd", "lib")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-pthread", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "concurrent_cut.cpp"), "-L", lib, "-ljiebahip",
+                           "-Wl,-rpath," + lib, "-o", exe])
+    o = O.Oracle.from_files(dp, ep, 0)
+    buf, off, _ = s.corpus(synth.KIND_SENTENCES, 77, max_docs=300, target_bytes=1 << 30)
+    sents = [bytes(np.asarray(buf)[int(off[i]):int(off[i + 1])]) for i in range(len(off) - 1)]
+    sents = [x for x in sents if b"\n" not in x] + [SENTENCE.encode(), "abc 中文 x".encode(), b""]
+    with open(tmp_path / "sent.txt", "wb") as f:
+        f.write(b"\n".join(sents) + b"\n")
+    with open(tmp_path / "want.txt", "w") as f:
+        for x in sents:
+            a, b = o.cut_spans(x, True)
+            f.write(" ".join([str(len(a))] + [f"{int(p)} {int(q)}" for p, q in zip(a, b)]) + "\n")
+    r = subprocess.run([exe, dp, ep, str(tmp_path / "sent.txt"), str(tmp_path / "want.txt"), "16", "1000"],
+                       capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rates = {ln.split()[0]: float(ln.split()[-1]) for ln in r.stdout.splitlines()}
+    assert rates["concurrent"] > rates["serial"]
