@@ -2412,16 +2412,16 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                             }
                             f.finish();
                             P = f.bestP;
-                        } else if (cl == 0u) {  // one item: it is the answer (:573-576)
-                            P = W[cs][0] + b1;
-                        } else if (cl == 1u) {  // two: the second unless it is smaller
-                            P = max_f64(W[cs][0] + b1, W[cs][1] + RV[rs][0]);
                         } else {
+                            // one form for 1-4 items, no branch: absent items have NaN
+                            // weights, so their sums are NaN, every compare with them is
+                            // false and v_max_f64 (IEEE maxNum) returns the other operand
+                            // (one item: p1; two: max(p1, p2), the second unless smaller)
                             const double p1 = W[cs][0] + b1;
                             const double p2 = W[cs][1] + RV[rs][0];
                             const double p3 = W[cs][2] + RV[rs][1];
                             const double p4 = W[cs][3] + RV[rs][2];
-                            const double R = max_f64(p1, p2);  // (items 1, 2 exist: no NaN)
+                            const double R = max_f64(p1, p2);
                             const bool k3 = p3 >= p2, k4 = p4 >= p3;
                             const double p34 = k4 ? p4 : p3;
                             P = (k3 || k4) ? p34 : R;
