@@ -162,18 +162,21 @@ struct Device {
     jb_stats acc{};              // counters summed over the pieces of the last host range
     bool acc_valid = false;      // the last run was such a range
     // k_small's pinned, mapped host buffers (coherent: the kernel reads and writes them directly)
-    uint8_t* h_sin = nullptr;    // text (kSmallBytes + 128), then u64 doc offsets (kSmallDocs + 1)
-    uint32_t* h_sout = nullptr;  // header, spans, doc_tok (kSmallOutBytes)
-    uint8_t* d_sin = nullptr;    // their device addresses
-    uint32_t* d_sout = nullptr;
+    // per in-flight k_small batch (cut_small keeps up to kSmallSlots launched at once)
+    struct SmallSlot {
+        uint8_t* h_sin = nullptr;    // text (kSmallBytes + 128), then u64 doc offsets (kSmallDocs + 1)
+        uint32_t* h_sout = nullptr;  // header, spans, doc_tok (kSmallOutBytes)
+        uint8_t* d_sin = nullptr;    // their device addresses
+        uint32_t* d_sout = nullptr;
+        uint32_t seq = 0;            // the kernel writes this number last
+        bool busy = false;
+    } slots[4];
     bool last_small = false;     // the last batch took k_small (jb_last_stats reads small_hdr)
     hipStream_t sstream = nullptr;  // k_small's stream, masked to one CU (its code stays in that I-cache)
-    uint32_t small_seq = 0;         // k_small calls: the kernel writes this number last
     // concurrent small calls, coalesced into shared k_small launches (cut_small)
     std::mutex small_mu;
     std::condition_variable small_cv;
     std::deque<SmallReq*> small_q;
-    bool small_leader = false;
     uint32_t small_hdr[kSmallHdr] = {0};
     uint32_t ncu = 0;
     uint64_t piece_bytes = 64ull << 20;  // host-batch pipeline piece (JB_PIECE_KIB)
@@ -900,7 +903,11 @@ extern "C" void jb_close(jb_ctx* ctx) {
         dfree(d->text); dfree(d->doc_off);
         free_image_bufs(&d->ib);
         if (d->ws_done) (void)hipEventDestroy(d->ws_done);
-        hfree(d->h_text); hfree(d->h_misc); hfree(d->h_sin); hfree(d->h_sout);
+        hfree(d->h_text); hfree(d->h_misc);
+        for (auto& sl : d->slots) {
+            hfree(sl.h_sin);
+            hfree(sl.h_sout);
+        }
         free_outs(d.get());
         hfree(d->h_pcnt); dfree(d->d_mask); hfree(d->h_mask); hfree(d->h_zero);
         for (auto* v : {&d->ev_h2d, &d->ev_comp, &d->ev_d2h})
@@ -924,12 +931,13 @@ extern "C" const char* jb_last_error(void) { return g_err.c_str(); }
 // from mapped pinned host memory (or its kernel arguments) and writes the spans
 // there.  Concurrent calls on a device are coalesced (the reference runs Cut calls
 // side by side under RLock, tokenizer.go:151-153): each call queues a SmallReq;
-// whichever caller finds no leader becomes it, and launches the queue's head
-// requests (same hmm, up to the k_small limits together) as ONE k_small batch,
-// their documents back to back, then hands each caller its own spans by its
-// documents' doc_tok ranges.  A leader leads until its own request is done and then
-// passes the role on, so no caller serves others for long.  One caller alone: a
-// batch of one, as before.
+// a caller whose request is still queued takes a free slot (one of four pinned
+// input/output buffer pairs), launches the queue's head requests (same hmm, up to
+// the k_small limits together) as ONE k_small batch on it, their documents back to
+// back, waits for that batch's completion word and hands each caller its own spans
+// by its documents' doc_tok ranges.  Up to four batches are in flight (the stream
+// runs them in order), so staging and waking callers overlap the kernels.  One
+// caller alone: a batch of one, as before.
 namespace {
 struct SmallReq {
     const uint8_t* text;
@@ -939,13 +947,14 @@ struct SmallReq {
     SpanBuf* out;
     int rc = JB_OK;
     std::string err;
+    bool launched = false;  // taken into a k_small batch
     bool done = false;
 };
 }  // namespace
 
 // One k_small launch over requests rq[0..n) (together within the limits): stage, launch,
 // wait for the completion word, split the spans.  Sets each request's rc / err.
-static void small_batch(Device* d, SmallReq* const* rq, uint32_t n) {
+static void small_batch(Device* d, Device::SmallSlot* sl, SmallReq* const* rq, uint32_t n) {
     auto fail_all = [&](int rc) {
         for (uint32_t i = 0; i < n; i++) {
             rq[i]->rc = rc;
@@ -958,14 +967,14 @@ static void small_batch(Device* d, SmallReq* const* rq, uint32_t n) {
         return false;
     };
     if (!chk(hipSetDevice(d->ordinal), "hipSetDevice")) return;
-    if (!d->h_sin) {
+    if (!sl->h_sin) {
         const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
-        if (!chk(hipHostMalloc(&d->h_sin, kSmallBytes + 128 + 8 * (kSmallDocs + 1), fl), "hipHostMalloc") ||
-            !chk(hipHostMalloc(&d->h_sout, kSmallOutBytes, fl), "hipHostMalloc") ||
-            !chk(hipHostGetDevicePointer((void**)&d->d_sin, d->h_sin, 0), "hipHostGetDevicePointer") ||
-            !chk(hipHostGetDevicePointer((void**)&d->d_sout, d->h_sout, 0), "hipHostGetDevicePointer"))
+        if (!chk(hipHostMalloc(&sl->h_sin, kSmallBytes + 128 + 8 * (kSmallDocs + 1), fl), "hipHostMalloc") ||
+            !chk(hipHostMalloc(&sl->h_sout, kSmallOutBytes, fl), "hipHostMalloc") ||
+            !chk(hipHostGetDevicePointer((void**)&sl->d_sin, sl->h_sin, 0), "hipHostGetDevicePointer") ||
+            !chk(hipHostGetDevicePointer((void**)&sl->d_sout, sl->h_sout, 0), "hipHostGetDevicePointer"))
             return;
-        d->h_sout[SM_DONE] = 0;  // (recycled pinned memory may hold any value; small_seq starts at 1)
+        sl->h_sout[SM_DONE] = 0;  // (recycled pinned memory may hold any value; seq starts at 1)
     }
     const bool hmm = rq[0]->hmm;
     uint64_t nbytes = 0;
@@ -980,8 +989,8 @@ static void small_batch(Device* d, SmallReq* const* rq, uint32_t n) {
     const bool inl = nbytes <= kSmallInline && nd <= kSmallInlineDocs;
     SmallInline in;
     memset(&in, 0, sizeof in);
-    uint8_t* const tx = inl ? in.txt : d->h_sin;
-    uint64_t* const hoff = reinterpret_cast<uint64_t*>(d->h_sin + kSmallBytes + 128);
+    uint8_t* const tx = inl ? in.txt : sl->h_sin;
+    uint64_t* const hoff = reinterpret_cast<uint64_t*>(sl->h_sin + kSmallBytes + 128);
     uint64_t at = 0;
     uint32_t k = 0;
     for (uint32_t i = 0; i < n; i++) {
@@ -997,15 +1006,15 @@ static void small_batch(Device* d, SmallReq* const* rq, uint32_t n) {
     if (inl) in.doff[nd] = (uint16_t)nbytes;
     else {
         hoff[nd] = nbytes;
-        memset(d->h_sin + nbytes, 0, 16);
+        memset(sl->h_sin + nbytes, 0, 16);
     }
     // the kernel writes the call's sequence number after everything else (system-scope
     // release); spinning on it returns as soon as the results are in host memory
-    const uint32_t seq = ++d->small_seq;
-    volatile uint32_t* done = d->h_sout + SM_DONE;
-    if (!chk(run_small(d->dim, inl ? nullptr : d->d_sin, (uint32_t)nbytes, inl ? nullptr : reinterpret_cast<const uint64_t*>(
-                                                                                               d->d_sin + kSmallBytes + 128),
-                       nd, hmm, d->d_sout, seq, in, d->sstream),
+    const uint32_t seq = ++sl->seq;
+    volatile uint32_t* done = sl->h_sout + SM_DONE;
+    if (!chk(run_small(d->dim, inl ? nullptr : sl->d_sin, (uint32_t)nbytes,
+                       inl ? nullptr : reinterpret_cast<const uint64_t*>(sl->d_sin + kSmallBytes + 128), nd, hmm,
+                       sl->d_sout, seq, in, d->sstream),
              "k_small launch"))
         return;
     const auto c1 = std::chrono::steady_clock::now();
@@ -1022,7 +1031,7 @@ static void small_batch(Device* d, SmallReq* const* rq, uint32_t n) {
     }
     std::atomic_thread_fence(std::memory_order_acquire);
     const auto c2 = std::chrono::steady_clock::now();
-    const uint32_t* h = d->h_sout;
+    const uint32_t* h = sl->h_sout;
     {
         std::lock_guard<std::mutex> g(d->mu);  // (jb_last_stats reads these)
         memcpy(d->small_hdr, h, sizeof d->small_hdr);
@@ -1042,7 +1051,7 @@ static void small_batch(Device* d, SmallReq* const* rq, uint32_t n) {
     }
     if (h[SM_ERR]) {  // the reference panics on some document: find whose (each call alone)
         if (n > 1) {
-            for (uint32_t i = 0; i < n; i++) small_batch(d, rq + i, 1);
+            for (uint32_t i = 0; i < n; i++) small_batch(d, sl, rq + i, 1);
             return;
         }
         fail_all(fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)"));
@@ -1089,37 +1098,45 @@ static int cut_small(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
     SmallReq r{text, doc_off, nd, hmm, out};
     std::unique_lock<std::mutex> lk(d->small_mu);
     d->small_q.push_back(&r);
-    while (!r.done) {
-        if (d->small_leader) {
-            d->small_cv.wait(lk, [&] { return r.done || !d->small_leader; });
+    for (;;) {
+        if (r.done) break;
+        Device::SmallSlot* sl = nullptr;
+        if (!r.launched)
+            for (auto& x : d->slots)
+                if (!x.busy) {
+                    sl = &x;
+                    break;
+                }
+        if (!sl) {  // own request in flight (its launcher completes it), or every slot busy
+            d->small_cv.wait(lk);
             continue;
         }
-        d->small_leader = true;
-        while (!r.done) {  // lead until this call's own request is served
-            std::vector<SmallReq*> b;
-            uint64_t bytes = 0;
-            uint32_t docs = 0;
-            const bool h = d->small_q.front()->hmm;
-            for (auto it = d->small_q.begin(); it != d->small_q.end();) {
-                SmallReq* q = *it;
-                const uint64_t len = q->doc_off[q->nd] - q->doc_off[0];
-                if (q->hmm != h || bytes + len > d->lc.small_max || docs + q->nd > kSmallDocs) {
-                    ++it;
-                    continue;
-                }
-                bytes += len;
-                docs += q->nd;
-                b.push_back(q);
-                it = d->small_q.erase(it);
+        // launch the queue's head requests (same hmm, within the limits) on the free slot,
+        // then complete them: launches on other slots can go on meanwhile
+        std::vector<SmallReq*> b;
+        uint64_t bytes = 0;
+        uint32_t docs = 0;
+        const bool h = d->small_q.front()->hmm;
+        for (auto it = d->small_q.begin(); it != d->small_q.end();) {
+            SmallReq* q = *it;
+            const uint64_t len = q->doc_off[q->nd] - q->doc_off[0];
+            if (q->hmm != h || bytes + len > d->lc.small_max || docs + q->nd > kSmallDocs) {
+                ++it;
+                continue;
             }
-            lk.unlock();
-            small_batch(d, b.data(), (uint32_t)b.size());
-            lk.lock();
-            for (SmallReq* q : b) q->done = true;
-            d->small_cv.notify_all();
+            bytes += len;
+            docs += q->nd;
+            q->launched = true;
+            b.push_back(q);
+            it = d->small_q.erase(it);
         }
-        d->small_leader = false;
-        d->small_cv.notify_all();  // a waiting caller takes the queue over
+        sl->busy = true;
+        lk.unlock();
+        small_batch(d, sl, b.data(), (uint32_t)b.size());
+        lk.lock();
+        sl->busy = false;
+        for (SmallReq* q : b) q->done = true;
+        d->small_cv.notify_all();
     }
     if (r.rc) g_err = r.err;
     return r.rc;
