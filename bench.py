@@ -544,7 +544,8 @@ def roofline_latency(timeout=240):
     import subprocess
     if not os.path.exists(STAMPS_LIB):
         return None
-    env = dict(os.environ, JB_LIB=STAMPS_LIB, JB_STAMPS="1", JB_GRAPH="0")
+    # (JB_ZH_WIDE=1: the one-wave batch runs k_zh's wide form too, the form the headline batch gets)
+    env = dict(os.environ, JB_LIB=STAMPS_LIB, JB_STAMPS="1", JB_GRAPH="0", JB_ZH_WIDE="1")
     try:
         p = subprocess.run([sys.executable, os.path.abspath(__file__), "--latency-probe"], env=env,
                            capture_output=True, text=True, timeout=timeout)
@@ -563,7 +564,7 @@ def roofline_latency(timeout=240):
     return {"bound": "latency", "unit": "cycles per DP step per wave",
             "achieved": round(cl, 1), "floor": round(ca, 1), "frac": round(ca / cl, 4),
             "dp_share_of_k_zh": round(loaded[0] / loaded[2], 4), "dp_lane_use": loaded[3],
-            "waves_per_simd": 4, "phase_clocks_loaded": lines[-2:],
+            "waves_per_simd": 4, "workgroup_waves": 16, "phase_clocks_loaded": lines[-2:],
             "what": "k_zh's backward DP (calcDagProba + maxIndexProba): s_memtime cycles per step of a wave's "
                     "DP loop, every wave busy (first 128 MiB of the corpus) vs one wave alone (a 1 KiB batch); "
                     "STAMPS build of the same source, per-wave clocks cost a few %"}
