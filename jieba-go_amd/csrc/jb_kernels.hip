@@ -1188,40 +1188,6 @@ __device__ __forceinline__ double rec_fold_a3(uint64_t lp, const double w[4], ui
     return bP;
 }
 
-// The same fold with the ring values read a step ahead (ring_pf) and best(i + 1),
-// the value the previous step folded, from a register: an L = 1 field (an edge of one
-// rune, or a phantom) takes b1, the others the prefetched rv.  The step's own ring
-// reads, which waited for the LDS round trip every step, leave the chain: what is
-// left on it is the fold's adds, compares and selects.
-__device__ __forceinline__ double rec_fold_pf(uint64_t lp, const double w[4], const double rv[4], double b1,
-                                              uint32_t& bls) {
-    double pp[4];
-    uint32_t Ls[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        Ls[k] = (uint32_t)(lp >> (16 * k));
-        pp[k] = w[k] + (((Ls[k] & 0x1E00u) == 0x200u) ? b1 : rv[k]);
-    }
-    uint32_t bL = Ls[0];
-    double bP = pp[0];
-#pragma unroll
-    for (int k = 1; k < 4; k++) {
-        const bool take = pp[k] >= pp[k - 1];
-        bL = take ? Ls[k] : bL;
-        bP = take ? pp[k] : bP;
-    }
-    bls = bL;
-    return bP;
-}
-// best(i + L) of a record's fields for the rune whose ring position is cs1 >> 9, read
-// one step before its fold (its L = 1 fields read the slot the current step is about
-// to write: they take b1 instead)
-__device__ __forceinline__ void ring_pf(uint64_t lp, uint32_t cs1, const char* rb0, uint32_t lb, double rv[4]) {
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-        rv[k] = *reinterpret_cast<const double*>(rb0 + ring_off(cs1 - (uint32_t)(lp >> (16 * k)), lb));
-}
-
 // The same fold on a per-lane ring pointer (slot stride 64 doubles).  Returns L.
 __device__ __forceinline__ double rec_fold_g(uint64_t lp, const double w[4], uint32_t c, const double* ring,
                                              uint32_t& bl) {
@@ -1352,7 +1318,6 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
     auto ring_at = [&](uint32_t cs) -> double& {
         return *reinterpret_cast<double*>(const_cast<char*>(rb0) + ring_off(cs, lb));
     };
-    double b1 = 0.0;  // best(i + 1): the value the previous step folded
     auto setup = [&]() __attribute__((always_inline)) {  // (re)start at the last rune of [bs, be)
         key0 = be / 3u;
         q = be - 3u;
@@ -1360,7 +1325,6 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
         s = q / 3u;
         bi = (q - v.wb) / 3u;
         ring_at(0u) = 0.0;  // best(n), the {n, 0.0} sentinel
-        b1 = 0.0;           // (the block's last rune has L = 1 fields only: it takes best(n) from b1)
     };
     // The records of the lane's NEXT block's last two runes, E(s'-1) and E(s'), in one
     // 16-byte load issued when this block starts (after everything else of its prime),
@@ -1407,21 +1371,17 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
     // One rune.  wc: this rune's weights (loaded a step ago); wn: gets the next rune's.
     // Weight registers alternate between steps, so nothing is copied out of a
     // load's destination (a copy would wait for the load).
-    auto step = [&](const int P, double (&w)[4], double (&rv)[4]) __attribute__((always_inline)) -> bool {
+    auto step = [&](const int P, double (&wc)[4], double (&wn)[4]) __attribute__((always_inline)) -> bool {
         const bool more = q > bs;
         const uint64_t nx = P == 0 ? xl : (P == 1 ? yh : (P == 2 ? yl : xh));
         const uint64_t r1v = more ? nx : 0ull;  // the next rune's record (when it exists)
         const uint64_t ln = s_ltab[(uint32_t)r1v & 0xFFu];
+        rec_weights<WL>(im, r1v, wn);
         if (P == 0) ld_pair(s - 5u, xl, xh);
         if (P == 2) ld_pair(s - 5u, yl, yh);
         const uint32_t cs = c << 9;
         uint32_t bLs;
-        double bP = rec_fold_pf(lc, w, rv, b1, bLs);
-        // this rune's weights and ring values are read: the next rune's go into the same
-        // registers (one set of each, read a step before their fold)
-        __builtin_amdgcn_sched_barrier(0);
-        rec_weights<WL>(im, r1v, w);
-        ring_pf(ln, cs + 0x200u, rb0, lb, rv);  // (slots up to c - 1: all written)
+        double bP = rec_fold_a3(lc, wc, cs, rb0, lb, bLs);
         bool redo = false;
         if (lc & kLtabOvf) {  // overflowed record (rare)
             DpFold f;
@@ -1432,7 +1392,6 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
             redo = f.redo;
         }
         ring_at(cs) = bP;
-        b1 = bP;
         if (longm) gbest[key0 - c] = bP;
         v.bls[bi] = (uint8_t)(bLs >> 9);
         steps++;
@@ -1448,24 +1407,23 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
         if (redo) {  // an edge past the ring: this block again, every best value kept in gbest
             longm = true;
             setup();
-            prime((P + 1) & 3, w, ld_e(0), ld_e(2));  // (pre keeps the next block's records)
+            prime((P + 1) & 3, wn, ld_e(0), ld_e(2));  // (pre keeps the next block's records)
             return false;
         }
         if (!src.next(j, bs, be)) return true;
         longm = false;
         setup();
-        prime((P + 1) & 3, w, pre, pre0);  // the next step is the next kind
+        prime((P + 1) & 3, wn, pre, pre0);  // the next step is the next kind
         return false;
     };
-    double w[4];
-    double rv[4] = {0.0, 0.0, 0.0, 0.0};  // ring values read a step ahead
+    double wa[4], wb[4];
     setup();
-    prime(0, w, ld_e(0), ld_e(2));
+    prime(0, wa, ld_e(0), ld_e(2));
     for (;;) {
-        if (step(0, w, rv)) break;
-        if (step(1, w, rv)) break;
-        if (step(2, w, rv)) break;
-        if (step(3, w, rv)) break;
+        if (step(0, wa, wb)) break;
+        if (step(1, wb, wa)) break;
+        if (step(2, wa, wb)) break;
+        if (step(3, wb, wa)) break;
     }
     return steps;
 }

@@ -61,14 +61,15 @@ int main(int argc, char** argv) {
     // per rune: the largest weight index among its (at most 4) record fields
     std::vector<uint32_t> rune_max;
     std::vector<uint32_t> run;
-    uint64_t edges = 0, runes = 0;
+    uint64_t edges = 0, runes = 0, items_hist[9] = {0};
     auto flush = [&]() {
         for (size_t i = 0; i < run.size(); i++) {
             runes++;
-            uint32_t mx = 0;
+            uint32_t mx = 0, nit = 0;
             auto edge = [&](uint32_t widx) {
                 hits[widx]++;
                 edges++;
+                nit++;
                 mx = std::max(mx, widx);
             };
             const uint32_t row = jb_row(pm, run[i]);
@@ -77,6 +78,7 @@ int main(int argc, char** argv) {
             if (jb_cell_check(c) != JB_CHECK_ROOT) {
                 edge(JB_WIDX_ABSENT);
                 rune_max.push_back(mx);
+                items_hist[1]++;
                 continue;
             }
             edge(jb_cell_widx(c));  // (count 0 or a word: the L = 1 item)
@@ -91,6 +93,7 @@ int main(int argc, char** argv) {
                     c = ch;
                 }
             rune_max.push_back(mx);
+            items_hist[std::min(nit, 8u)]++;
         }
         run.clear();
     };
@@ -107,6 +110,9 @@ int main(int argc, char** argv) {
     flush();
     printf("distinct weights %zu, runes %llu, edges %llu (%.2f per rune)\n", img.wtab.size(),
            (unsigned long long)runes, (unsigned long long)edges, (double)edges / (double)runes);
+    printf("DAG items per rune (1..7, 8+):");
+    for (int k = 1; k <= 8; k++) printf(" %.4f", (double)items_hist[k] / (double)runes);
+    printf("\n");
     for (uint32_t H : {64u, 128u, 256u, 512u, 1024u, 2048u, 4096u}) {
         uint64_t cold = 0;
         for (size_t k = H; k < hits.size(); k++) cold += hits[k];
