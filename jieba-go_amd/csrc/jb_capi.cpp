@@ -177,6 +177,8 @@ struct Device {
     std::mutex small_mu;
     std::condition_variable small_cv;
     std::deque<SmallReq*> small_q;
+    std::atomic<uint32_t> small_gen{0};  // k_small batches completed (waiters spin on it)
+    uint32_t small_slots = 2;            // k_small batches in flight at most (JB_SMALL_SLOTS, 1..4)
     uint32_t small_hdr[kSmallHdr] = {0};
     uint32_t ncu = 0;
     uint64_t piece_bytes = 64ull << 20;  // host-batch pipeline piece (JB_PIECE_KIB)
@@ -672,6 +674,9 @@ static int init_launch_cfg(Device* d) {
     if (sm < 0 || sm > (int)kSmallBytes)
         return fail(JB_EINVAL, "JB_SMALL=%d: want 0 (off) .. %u bytes", sm, kSmallBytes);
     lc.small_max = (uint32_t)sm;
+    const int ss = env_int("JB_SMALL_SLOTS", 2);
+    if (ss < 1 || ss > 4) return fail(JB_EINVAL, "JB_SMALL_SLOTS=%d: want 1 .. 4", ss);
+    d->small_slots = (uint32_t)ss;
     return JB_OK;
 }
 
@@ -1102,13 +1107,26 @@ static int cut_small(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         if (r.done) break;
         Device::SmallSlot* sl = nullptr;
         if (!r.launched)
-            for (auto& x : d->slots)
-                if (!x.busy) {
-                    sl = &x;
+            for (uint32_t k = 0; k < d->small_slots; k++)
+                if (!d->slots[k].busy) {
+                    sl = &d->slots[k];
                     break;
                 }
         if (!sl) {  // own request in flight (its launcher completes it), or every slot busy
-            d->small_cv.wait(lk);
+            // spin up to ~100 us for the next completion before sleeping: a batch takes
+            // 20-30 us, and a sleeping caller's wake-up costs about as much again
+            const uint32_t g0 = d->small_gen.load(std::memory_order_relaxed);
+            lk.unlock();
+            bool moved = false;
+            const auto t0 = std::chrono::steady_clock::now();
+            for (uint32_t i = 1; !moved; i++) {
+                moved = d->small_gen.load(std::memory_order_acquire) != g0;
+                if (!moved && (i & 63u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(100))
+                    break;
+                __builtin_ia32_pause();
+            }
+            lk.lock();
+            if (!moved && d->small_gen.load(std::memory_order_relaxed) == g0) d->small_cv.wait(lk);
             continue;
         }
         // launch the queue's head requests (same hmm, within the limits) on the free slot,
@@ -1136,6 +1154,7 @@ static int cut_small(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         lk.lock();
         sl->busy = false;
         for (SmallReq* q : b) q->done = true;
+        d->small_gen.fetch_add(1, std::memory_order_release);
         d->small_cv.notify_all();
     }
     if (r.rc) g_err = r.err;

@@ -904,11 +904,13 @@ def test_document_bitmap_between_runs(small):
                 _cmp_batch(tk, o, buf, off, hmm, f"layout {i} rep {rep}")
 
 
-def test_concurrent_cut_calls(syn_small, tmp_path):
+@pytest.mark.parametrize("slots", [1, 2, 4])
+def test_concurrent_cut_calls(syn_small, tmp_path, slots):
     """16 threads x 1,000 jb_cut calls at once on one context (Go code calling Cut
     from many goroutines; the reference takes only an RLock, tokenizer.go:151-153):
     every result equals the oracle's, and the calls are coalesced into shared
-    k_small launches (tests/concurrent_cut.cpp prints both rates)."""
+    k_small launches (tests/concurrent_cut.cpp prints both rates), with 1, 2 or 4
+    batches in flight (JB_SMALL_SLOTS)."""
     import subprocess
     dp, ep, s = syn_small
     exe = str(tmp_path / "concurrent_cut")
@@ -927,7 +929,8 @@ def test_concurrent_cut_calls(syn_small, tmp_path):
             a, b = o.cut_spans(x, True)
             f.write(" ".join([str(len(a))] + [f"{int(p)} {int(q)}" for p, q in zip(a, b)]) + "\n")
     r = subprocess.run([exe, dp, ep, str(tmp_path / "sent.txt"), str(tmp_path / "want.txt"), "16", "1000"],
-                       capture_output=True, text=True, timeout=300)
+                       capture_output=True, text=True, timeout=300, env=dict(os.environ, JB_SMALL_SLOTS=str(slots)))
+    print(f"JB_SMALL_SLOTS={slots}")
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     rates = {ln.split()[0]: float(ln.split()[-1]) for ln in r.stdout.splitlines()}
