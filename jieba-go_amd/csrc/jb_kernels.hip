@@ -1104,7 +1104,7 @@ __device__ __forceinline__ void dp_walk_rune(const V& v, const DevImage& im, uin
 // step kept that unit saturated; LDS reads take the LDS pipe instead.
 typedef const __attribute__((address_space(1))) char gchar;  // global memory, whatever inference concludes
 typedef const __attribute__((address_space(3))) char lchar;  // LDS
-__shared__ double s_wt[kZhWtab];  // wtab1 in LDS (k_zh<.., kZhWgWide>: one copy per CU)
+__shared__ __attribute__((aligned(32))) double s_wt[kZhWtab];  // wtab1 in LDS (k_zh<.., kZhWgWide>: one copy per CU)
 template <bool WL = false>
 __device__ __forceinline__ void rec_weights(const DevImage& im, uint64_t rc, double w[4]) {
     gchar* const wb = (gchar*)im.wtab1;
@@ -1374,7 +1374,11 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
     auto step = [&](const int P, double (&wc)[4], double (&wn)[4]) __attribute__((always_inline)) -> bool {
         const bool more = q > bs;
         const uint64_t nx = P == 0 ? xl : (P == 1 ? yh : (P == 2 ? yl : xh));
-        const uint64_t r1v = more ? nx : 0ull;  // the next rune's record (when it exists)
+        // the next rune's record when it exists; past the block's first rune it is whatever
+        // precedes, and what it loads is replaced at the restart (prime) unused: with the
+        // weights in LDS a garbage index only reads other LDS words, from memory it could
+        // fault, so only that form masks it
+        const uint64_t r1v = (WL || more) ? nx : 0ull;
         const uint64_t ln = s_ltab[(uint32_t)r1v & 0xFFu];
         rec_weights<WL>(im, r1v, wn);
         if (P == 0) ld_pair(s - 5u, xl, xh);
