@@ -113,6 +113,7 @@ struct ImageBufs {
     uint32_t* code = nullptr;
     double* wtab = nullptr;
     uint64_t* l1row = nullptr;
+    uint64_t* hot = nullptr;  // hot level-1 rows: JB_HOT_SLOTS u64 values, then u16 tags
 };
 
 struct SmallReq;  // (cut_small)
@@ -471,6 +472,7 @@ static int upload(T** dst, const std::vector<T>& src) {
 
 static void free_image_bufs(ImageBufs* b) {
     dfree(b->pagemap); dfree(b->emit); dfree(b->cells); dfree(b->code); dfree(b->wtab); dfree(b->l1row);
+    dfree(b->hot);
     *b = ImageBufs{};
 }
 
@@ -489,10 +491,13 @@ static int stage_image(int ordinal, const Image& img, ImageBufs* b) {
     std::vector<double> wt1(img.wtab.size() + 1);
     wt1[0] = -HUGE_VAL;
     std::copy(img.wtab.begin(), img.wtab.end(), wt1.begin() + 1);
+    // hot level-1 rows (k_mark_walk keeps them in LDS)
+    std::vector<uint64_t> hot(JB_HOT_SLOTS + JB_HOT_SLOTS / 4u, 0ull);
+    build_hot_rows(img, hot.data(), reinterpret_cast<uint16_t*>(hot.data() + JB_HOT_SLOTS));
     int rc;
     if ((rc = upload(&b->pagemap, img.pagemap)) || (rc = upload(&b->emit, img.emit)) ||
         (rc = upload(&b->cells, img.cells)) || (rc = upload(&b->code, img.code)) ||
-        (rc = upload(&b->wtab, wt1)) || (rc = upload(&b->l1row, l1))) {
+        (rc = upload(&b->wtab, wt1)) || (rc = upload(&b->l1row, l1)) || (rc = upload(&b->hot, hot))) {
         free_image_bufs(b);
         return rc;
     }
@@ -506,6 +511,7 @@ static int install_image(Device* d, ImageBufs* b, const Image& img) {
     d->ib = *b;
     *b = ImageBufs{};
     d->dim.l1row = d->ib.l1row;
+    d->dim.hot = d->ib.hot;
     d->dim.pagemap = d->ib.pagemap;
     d->dim.emit = d->ib.emit;
     d->dim.cells = d->ib.cells;

@@ -77,6 +77,13 @@ JB_HD uint64_t jb_l1row_cell(uint64_t v) {
     return (v & ~0x3FFFFFull) | (((uint32_t)v & JB_L1_ROOTBIT) ? (uint64_t)JB_CHECK_ROOT : 0ull);
 }
 
+// Hot level-1 rows (device only, derived at upload, jb_image.cpp build_hot_rows): the
+// l1row values of the runes of U+3400..U+9FFF that text is likeliest to hold, in a
+// direct-mapped table of JB_HOT_SLOTS slots (value u64, then tag u16 = the rune,
+// 0 = empty).  k_mark_walk keeps it in LDS and gathers l1row only for the others.
+#define JB_HOT_SLOTS 512u
+JB_HD uint32_t jb_hot_slot(uint32_t r) { return (r * 0x9E3779B1u) >> 23; }
+
 // Pages U+3400..U+9FFF (CJK Ext-A + URO) sit at fixed page ids 1..108.
 #define JB_DIRECT_LO 0x3400u
 #define JB_DIRECT_N 0x6C00u

@@ -896,3 +896,54 @@ int load_image(const char* buf, size_t len, Dictionary* d, Emission* e, Image* i
 }
 
 }  // namespace jb
+
+void build_hot_rows(const Image& img, uint64_t* vals, uint16_t* tags) {
+    for (uint32_t k = 0; k < JB_HOT_SLOTS; k++) {
+        vals[k] = 0;
+        tags[k] = 0;
+    }
+    const size_t nc = img.cells.size();
+    if (!nc) return;
+    // summed frequency per code: every key (a cell with a positive count) adds its
+    // frequency, exp(weight) up to the common factor size, to each rune on its path
+    std::vector<double> score(img.ncodes + 1u, 0.0);
+    for (size_t t = 0; t < nc; t++) {
+        const uint64_t c = img.cells[t];
+        const uint32_t ck = jb_cell_check(c);
+        if (ck == 0u || jb_cell_fc(c) != JB_FC_POS) continue;
+        const uint32_t wi = jb_cell_widx(c);
+        if (wi >= img.wtab.size()) continue;
+        const double f = exp(img.wtab[wi]);
+        uint64_t node = t;
+        for (uint32_t depth = 0; depth < 4096u; depth++) {  // (bounded: a walk up the trie)
+            const uint32_t k = jb_cell_check(img.cells[node]);
+            if (k == JB_CHECK_ROOT) {
+                if (node < score.size()) score[node] += f;
+                break;
+            }
+            if (k == 0u || k - 1u >= nc) break;
+            const uint64_t parent = k - 1u;
+            const uint64_t code = node - jb_cell_base(img.cells[parent]);
+            if (code < score.size()) score[code] += f;
+            node = parent;
+        }
+    }
+    std::vector<std::pair<double, uint32_t>> rows;  // (score, row) of the direct rows
+    for (uint32_t r = JB_DIRECT_LO; r < JB_DIRECT_LO + JB_DIRECT_N; r++) {
+        const uint32_t row = r - 0x3300u;
+        if (row >= img.code.size()) continue;
+        const uint32_t cd = img.code[row];
+        if (cd == 0u || cd >= score.size() || !(score[cd] > 0.0)) continue;
+        rows.push_back({score[cd], row});
+    }
+    std::sort(rows.begin(), rows.end(), [](const auto& a, const auto& b) {
+        return a.first != b.first ? a.first > b.first : a.second < b.second;
+    });
+    for (const auto& sr : rows) {
+        const uint32_t r = sr.second + 0x3300u, slot = jb_hot_slot(r);
+        if (tags[slot]) continue;
+        const uint32_t cd = img.code[sr.second];
+        tags[slot] = (uint16_t)r;
+        vals[slot] = jb_l1row_make(cd, cd < nc ? img.cells[cd] : 0ull);
+    }
+}

@@ -61,6 +61,12 @@ struct Lookup {
 
 double go_log(double x);
 
+// The hot-row table of an image (JB_HOT_SLOTS values, then JB_HOT_SLOTS u16 tags):
+// runes of U+3400..U+9FFF ranked by the summed frequency of the keys that hold them
+// (each key's frequency from its weight), placed in descending rank at their slot
+// jb_hot_slot(rune) when it is still free.  The value is the rune's l1row entry.
+void build_hot_rows(const Image& img, uint64_t* vals, uint16_t* tags);
+
 // Parse dict.txt-format text with the two reference semantics
 // (kind 0: newPrefixDictionaryFromFile, kind 1: buildPrefixDictionary).
 // Returns 0 or a negative JB_E* code; err receives a message.

@@ -21,6 +21,8 @@ struct DevImage {
     // replaced by the code (bits 0-16) and bit 21 = "that check was the root",
     // so k_mark_walk gets code and level-1 cell in one load (jb_l1row_make)
     const uint64_t* l1row;
+    // hot level-1 rows (jb_common.h JB_HOT_SLOTS): u64 l1row values, then u16 tags
+    const uint64_t* hot;
     uint32_t nrows;
     uint32_t nw1;  // entries in wtab1 (distinct weights + 1)
     // 1: every weight is finite or -Inf (a dictionary whose size is > 0).  k_zh's

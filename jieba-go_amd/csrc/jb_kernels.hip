@@ -267,6 +267,9 @@ constexpr uint32_t kMwOffDb = kMwOffE + kTileEX * 4u;                     // u32
 constexpr uint32_t kMwOffWl = kMwOffDb + (kTileBytes / 32u + 3u) * 4u;    // u16 per entry
 constexpr uint32_t kMwOffScan = (kMwOffWl + kTileE * 2u + 3u) & ~3u;      // u32 x 8
 constexpr uint32_t kMwLds = kMwOffScan + 8u * 4u;
+constexpr uint32_t kMwOffHot = (kMwOffE + 15u) & ~15u;  // hot level-1 rows (phase 1 only), under the entries
+static_assert(kMwOffHot % 16u == 0u && kMwOffHot + 10u * JB_HOT_SLOTS <= kMwOffDb && JB_HOT_SLOTS == 512u,
+              "k_mark_walk: the hot rows fit under the entry list, 256 threads stage them");
 static_assert(kMwOffE >= kMwStage, "staged text must fit under the entry cells");
 static_assert(kTileBytes + kLABytes + 4u <= kMwStage - 16u && kTileBytes + kLABytes + 4u <= kTileBytes + 64u,
               "lookahead bytes are staged and have document bits");
@@ -411,6 +414,10 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         if (threadIdx.x < kMwStage / 16 - 256u && (uint64_t)g2 + 16 <= nbytes + 64)
             vb = *reinterpret_cast<const uint4*>(text + g2);
     }
+    // the hot level-1 rows (512 values and tags), staged into the entry list's space (free
+    // until the entries are written, after the level-1 lookups that read them)
+    const uint4 hv4 = reinterpret_cast<const uint4*>(im.hot)[threadIdx.x];
+    const uint32_t ht2 = reinterpret_cast<const uint32_t*>(im.hot + JB_HOT_SLOTS)[threadIdx.x];
     const uint64_t lastw = (nbytes + 31) >> 5;
     uint32_t dbw = 0;
     if (threadIdx.x < kTileBytes / 32 + 3) {
@@ -444,6 +451,8 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     reinterpret_cast<uint4*>(s_t)[threadIdx.x] = va;
     if (threadIdx.x < kMwStage / 16 - 256u) reinterpret_cast<uint4*>(s_t)[threadIdx.x + 256u] = vb;
     if (threadIdx.x < kTileBytes / 32 + 3) s_db[threadIdx.x] = dbw;
+    reinterpret_cast<uint4*>(s_raw + kMwOffHot)[threadIdx.x] = hv4;
+    reinterpret_cast<uint32_t*>(s_raw + kMwOffHot + 8u * JB_HOT_SLOTS)[threadIdx.x] = ht2;
     {  // clear the tile's words of the token bitmaps (k_zh and k_nonzh OR into them): no memset pass
         const uint64_t wz = (t0 >> 5) + (threadIdx.x & 127u);
         if (wz < lastw + 2u) __builtin_nontemporal_store(0u, (threadIdx.x < 128u ? sbits : ebits) + wz);
@@ -530,9 +539,25 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
 
     // ---- (2) Han rune entries of the tile, in text order ---------------------------
     uint32_t hs = ((hanb & ~covered & valid) >> 4) & 0xFFFFu;  // Han rune starts of the lane's bytes
+    {  // the level-1 rows, in flight during the entry scan: a hot rune's from LDS, the rest
+       // gathered (a gather costs the L1 one cycle per active lane, so the hot runes' are
+       // taken out of it, not just served faster)
+        const uint64_t* s_hv = reinterpret_cast<const uint64_t*>(s_raw + kMwOffHot);
+        const uint16_t* s_ht = reinterpret_cast<const uint16_t*>(s_raw + kMwOffHot + 8u * JB_HOT_SLOTS);
+        uint32_t hit = 0;  // (tags first, values after: fewer registers live at once)
 #pragma unroll
-    for (int i = 0; i < 7; i++)  // the level-1 loads, in flight during the entry scan
-        cl[i] = ((hsm >> i) & 1u) ? im.l1row[(rowp[i >> 1] >> (16 * (i & 1))) & 0xFFFFu] : 0ull;
+        for (int i = 0; i < 7; i++) {
+            const uint32_t r = ((rowp[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) + 0x3300u;
+            hit |= (((hsm >> i) & 1u) && s_ht[jb_hot_slot(r)] == r ? 1u : 0u) << i;
+        }
+#pragma unroll
+        for (int i = 0; i < 7; i++) {
+            const uint32_t row = (rowp[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+            cl[i] = 0ull;
+            if ((hit >> i) & 1u) cl[i] = s_hv[jb_hot_slot(row + 0x3300u)];
+            else if ((hsm >> i) & 1u) cl[i] = im.l1row[row];
+        }
+    }
     uint32_t nent;
     uint32_t o = block_scan_u32(__popc(hs), lds, &nent);
     bool has4 = false;  // a 4-byte Han rune starts in the lane's bytes

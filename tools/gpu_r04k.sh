@@ -8,3 +8,4 @@ tail -1 $OUT/pytest.log
 grep -E "JB_SMALL_SLOTS|serial threads|concurrent threads" $OUT/pytest.log
 timeout -k 10 300 python -u bench.py --workload long-oov --steps 5 --warmup 2 --no-e2e > $OUT/long_oov.json 2> $OUT/long_oov.err || { echo LONG_FAILED; tail -5 $OUT/long_oov.err; exit 1; }
 python -c "import json; d=json.load(open('$OUT/long_oov.json')); print('5b', d['ms_per_step'], d['kernels_ms']['k_long_dp'], d['parity']['bit_exact'])"
+TAG=${RUN:-r04k}/ab REPS=2 bash tools/abtest.sh lib base
