@@ -897,6 +897,7 @@ int load_image(const char* buf, size_t len, Dictionary* d, Emission* e, Image* i
 
 }  // namespace jb
 
+namespace jb {
 void build_hot_rows(const Image& img, uint64_t* vals, uint16_t* tags) {
     for (uint32_t k = 0; k < JB_HOT_SLOTS; k++) {
         vals[k] = 0;
@@ -947,3 +948,4 @@ void build_hot_rows(const Image& img, uint64_t* vals, uint16_t* tags) {
         vals[slot] = jb_l1row_make(cd, cd < nc ? img.cells[cd] : 0ull);
     }
 }
+}  // namespace jb
