@@ -2335,7 +2335,7 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                     for (int k = 0; k < 4; k++) d.w[k] = w[k];
 #pragma unroll
                     for (int k = 1; k < 4; k++) d.a[k - 1] = (uint32_t)k < m ? (((uint32_t)i + L[k]) & (kLdRing - 1u)) * 8u : 0u;
-                    d.flag = m >= 2u && L[1] == 2u ? 2u : 0u;  // item 2 reaches best(i + 2): the chain's b2
+                    d.flag = 0u;
                     cl = m == 1u ? 0u : (m == 2u ? 1u : 2u);
                 } else {  // more than 4 items, or none, or no L = 1 item (a negative count)
                     cl = 3u;
@@ -2368,20 +2368,15 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
         __syncthreads();
         if (wave == 0u) {
             // ---- the chain (calcDagProba + maxIndexProba, :502-578), lane 0 ----
-            // Step s: issue rune s-4's descriptor and rune s-2's ring reads, then
+            // Step s: issue rune s-3's descriptor and rune s-1's ring reads, then
             // fold rune s.  The reference's rule over items p1..p4 (:565-578) is
             // "the last k with p_k >= p_(k-1)" (p_0 = minFloat).  With L1 = 1 and
             // NaN for absent items that is: p4 if p4 >= p3, else p3 if p3 >= p2,
             // else max(p1, p2) (p1 < minFloat only when p1 = -Inf, and then
             // p2 >= p1 whenever item 2 exists; equal values are the same value).
-            // best(s + 1) and best(s + 2) are the last two steps' values, in
-            // registers (b1, b2): item 1 always has L = 1, and an item 2 with L = 2
-            // (descriptor flag bit 1) takes b2, so every ring read is for L >= 3
-            // and can be issued two steps before its fold.  Eight descriptor and
-            // ring register sets, a step's set is s & 7.
-            double W[8][4], RV[8][3];
-            uint32_t A[8][3], F[8];
-            double b1 = 0.0, b2 = 0.0;  // best(s + 1), best(s + 2)
+            double W[4][4], RV[2][3];
+            uint32_t A[4][3], F[4];
+            double b1 = 0.0;  // best(s + 1)
             auto ld_desc = [&](uint32_t set, uint32_t off) {  // off: byte offset in S.desc
                 const char* p = reinterpret_cast<const char*>(S.desc) + off;
                 const double2 x = *reinterpret_cast<const double2*>(p);
@@ -2396,42 +2391,42 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                 A[set][2] = z.z;
                 F[set] = z.w;
             };
-            auto ld_ring = [&](uint32_t set) {
+            auto ld_ring = [&](uint32_t rs, uint32_t set) {
 #pragma unroll
-                for (int k = 0; k < 3; k++) RV[set][k] = *reinterpret_cast<const double*>(rb + A[set][k]);
+                for (int k = 0; k < 3; k++) RV[rs][k] = *reinterpret_cast<const double*>(rb + A[set][k]);
             };
-            auto doff = [](int32_t i) { return ((uint32_t)i & (kLdDesc - 1u)) * 48u; };
-            const int32_t top = (int32_t)kLdWin * J - 1;  // (top & 7 == 7)
+            const int32_t top = (int32_t)kLdWin * J - 1;
             if (lane == 0u) {
-#pragma unroll
-                for (int k = 0; k < 4; k++) ld_desc((uint32_t)(7 - k), doff(top - k));
-                ld_ring(7u);
-                ld_ring(6u);
+                ld_desc(3u, ((uint32_t)top & (kLdDesc - 1u)) * 48u);
+                ld_desc(2u, ((uint32_t)(top - 1) & (kLdDesc - 1u)) * 48u);
+                ld_desc(1u, ((uint32_t)(top - 2) & (kLdDesc - 1u)) * 48u);
+                ld_ring(1u, 3u);
             }
-            // step forms of the 8 runes of the group up next (two LDS words, a group ahead)
-            uint32_t cwn0 = 0, cwn1 = 0;
-            if (lane == 0u) {
-                cwn0 = *reinterpret_cast<const uint32_t*>(S.cls + ((uint32_t)(top - 7) & (kLdDesc - 1u)));
-                cwn1 = *reinterpret_cast<const uint32_t*>(S.cls + ((uint32_t)(top - 3) & (kLdDesc - 1u)));
-            }
+            // step forms of the 4 runes of the group up next (one LDS word, a group ahead)
+            uint32_t cwn = 0;
+            if (lane == 0u) cwn = *reinterpret_cast<const uint32_t*>(S.cls + ((uint32_t)(top - 3) & (kLdDesc - 1u)));
             auto run = [&](auto chk, int32_t j) {
                 constexpr bool CHK = decltype(chk)::value;
                 const uint32_t b = (uint32_t)j & 3u;
-                for (int32_t g = (int32_t)kLdWin * j + (int32_t)kLdWin - 8; g >= (int32_t)kLdWin * j; g -= 8) {
-                    const uint32_t cw0 = __builtin_amdgcn_readfirstlane(cwn0), cw1 = __builtin_amdgcn_readfirstlane(cwn1);
-                    cwn0 = *reinterpret_cast<const uint32_t*>(S.cls + ((uint32_t)(g - 8) & (kLdDesc - 1u)));
-                    cwn1 = *reinterpret_cast<const uint32_t*>(S.cls + ((uint32_t)(g - 4) & (kLdDesc - 1u)));
+                for (int32_t g = (int32_t)kLdWin * j + (int32_t)kLdWin - 4; g >= (int32_t)kLdWin * j; g -= 4) {
+                    const uint32_t cw = __builtin_amdgcn_readfirstlane(cwn);
+                    cwn = *reinterpret_cast<const uint32_t*>(S.cls + ((uint32_t)(g - 4) & (kLdDesc - 1u)));
+                    // runes s = g + 3 - u, u = 0..3: descriptor set s & 3 = 3 - u, ring set s & 1
+                    const uint32_t dcur = ((uint32_t)g & (kLdDesc - 1u)) * 48u;
+                    const uint32_t dnxt = ((uint32_t)(g - 4) & (kLdDesc - 1u)) * 48u;
                     char* const rw = reinterpret_cast<char*>(S.ring) + ((uint32_t)g & (kLdRing - 1u)) * 8u;
 #pragma unroll
-                    for (int u = 0; u < 8; u++) {
-                        // rune s = g + 7 - u in set 7 - u; rune s - 4's descriptor, rune s - 2's ring reads
-                        const uint32_t cs = (uint32_t)(7 - u) & 7u;
-                        ld_desc((uint32_t)(3 - u) & 7u, doff(g + 3 - u));
-                        ld_ring((uint32_t)(5 - u) & 7u);
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t cs = (uint32_t)(3 - u) & 3u, c1 = (uint32_t)(2 - u) & 3u,
+                                       c3 = (uint32_t)(0 - u) & 3u;
+                        const uint32_t rs = (uint32_t)(3 - u) & 1u, r1 = (uint32_t)(2 - u) & 1u;
+                        // rune s - 3 is g - u: slot g (u = 0) or g - 4 + (4 - u)
+                        ld_desc(c3, u == 0 ? dcur : dnxt + (uint32_t)(4 - u) * 48u);
+                        ld_ring(r1, c1);
                         double P;
-                        const uint32_t cl = ((u < 4 ? cw1 : cw0) >> (8 * ((7 - u) & 3))) & 3u;  // rune s: byte 7 - u
+                        const uint32_t cl = (cw >> (8 * (3 - u))) & 3u;  // rune s = g + 3 - u: byte 3 - u
                         if (CHK && cl == 3u) {
-                            const uint32_t s = (uint32_t)(g + 7 - u), fl = F[cs];
+                            const uint32_t s = (uint32_t)(g + 3 - u), fl = F[cs];
                             DpFold f;
                             if (fl == kLdWalk) {
                                 long_items(text, im, erec, bs, be, s, [&](uint32_t L, double wt) {
@@ -2452,19 +2447,19 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                             // false and v_max_f64 (IEEE maxNum) returns the other operand
                             // (one item: p1; two: max(p1, p2), the second unless smaller)
                             const double p1 = W[cs][0] + b1;
-                            const double p2 = W[cs][1] + ((F[cs] & 2u) ? b2 : RV[cs][0]);
-                            const double p3 = W[cs][2] + RV[cs][1];
-                            const double p4 = W[cs][3] + RV[cs][2];
+                            const double p2 = W[cs][1] + RV[rs][0];
+                            const double p3 = W[cs][2] + RV[rs][1];
+                            const double p4 = W[cs][3] + RV[rs][2];
                             const double R = max_f64(p1, p2);
                             const bool k3 = p3 >= p2, k4 = p4 >= p3;
                             const double p34 = k4 ? p4 : p3;
                             P = (k3 || k4) ? p34 : R;
                         }
-                        *reinterpret_cast<double*>(rw + (uint32_t)(7 - u) * 8u) = P;
-                        b2 = b1;
+                        *reinterpret_cast<double*>(rw + (uint32_t)(3 - u) * 8u) = P;
                         b1 = P;
-                        // keep each step's loads ahead of their use: the scheduler would
-                        // otherwise hoist later steps' adds up to just-issued reads
+                        // keep each step's loads a whole step ahead of their use: the
+                        // scheduler would otherwise hoist the next step's adds up to
+                        // its just-issued ring reads and wait for them
                         __builtin_amdgcn_sched_barrier(0);
                     }
                 }
