@@ -171,15 +171,15 @@ struct Device {
         uint32_t* d_sout = nullptr;
         uint32_t seq = 0;            // the kernel writes this number last
         bool busy = false;
+        hipStream_t st = nullptr;    // this slot's stream, masked to its own CU
     } slots[4];
     bool last_small = false;     // the last batch took k_small (jb_last_stats reads small_hdr)
-    hipStream_t sstream = nullptr;  // k_small's stream, masked to one CU (its code stays in that I-cache)
     // concurrent small calls, coalesced into shared k_small launches (cut_small)
     std::mutex small_mu;
     std::condition_variable small_cv;
     std::deque<SmallReq*> small_q;
     std::atomic<uint32_t> small_gen{0};  // k_small batches completed (waiters spin on it)
-    uint32_t small_slots = 2;            // k_small batches in flight at most (JB_SMALL_SLOTS, 1..4)
+    uint32_t small_slots = 4;            // k_small batches in flight at most (JB_SMALL_SLOTS, 1..4)
     uint32_t small_hdr[kSmallHdr] = {0};
     uint32_t ncu = 0;
     uint64_t piece_bytes = 64ull << 20;  // host-batch pipeline piece (JB_PIECE_KIB)
@@ -680,7 +680,7 @@ static int init_launch_cfg(Device* d) {
     if (sm < 0 || sm > (int)kSmallBytes)
         return fail(JB_EINVAL, "JB_SMALL=%d: want 0 (off) .. %u bytes", sm, kSmallBytes);
     lc.small_max = (uint32_t)sm;
-    const int ss = env_int("JB_SMALL_SLOTS", 2);
+    const int ss = env_int("JB_SMALL_SLOTS", 4);
     if (ss < 1 || ss > 4) return fail(JB_EINVAL, "JB_SMALL_SLOTS=%d: want 1 .. 4", ss);
     d->small_slots = (uint32_t)ss;
     return JB_OK;
@@ -834,14 +834,20 @@ static int open_device(Device* d, int ordinal, const Image& img) {
     memset(d->h_zero, 0, 64);
     HIPCHK(hipStreamCreateWithFlags(&d->dstream, hipStreamNonBlocking));
     {
-        // k_small runs one workgroup per call: pinned to one CU (JB_SMALL_CU, default 0) it
-        // finds its 21 KB of code in that CU's instruction cache (and the trie's hot lines
-        // in that XCD's L2) instead of fetching them cold on whichever CU the dispatcher picks
-        const int cu = env_int("JB_SMALL_CU", 0);
-        if (cu < 0 || cu >= (int)d->ncu) return fail(JB_EINVAL, "JB_SMALL_CU=%d: %u CUs", cu, d->ncu);
-        std::vector<uint32_t> mask((d->ncu + 31) / 32, 0u);
-        mask[cu / 32] = 1u << (cu % 32);
-        HIPCHK(hipExtStreamCreateWithCUMask(&d->sstream, (uint32_t)mask.size(), mask.data()));
+        // k_small runs one workgroup per batch: each slot's stream is pinned to one CU
+        // (JB_SMALL_CU + slot x JB_SMALL_CU_STRIDE) so its batch finds its 21 KB of code in
+        // that CU's instruction cache (and the trie's hot lines in that XCD's L2) instead of
+        // fetching them cold on whichever CU the dispatcher picks, and so batches of
+        // different slots run side by side instead of one after another
+        const int cu = env_int("JB_SMALL_CU", 0), cs = env_int("JB_SMALL_CU_STRIDE", 1);
+        if (cu < 0 || cs < 0 || cu + 3 * cs >= (int)d->ncu)
+            return fail(JB_EINVAL, "JB_SMALL_CU=%d, JB_SMALL_CU_STRIDE=%d: %u CUs", cu, cs, d->ncu);
+        for (int k = 0; k < 4; k++) {
+            std::vector<uint32_t> mask((d->ncu + 31) / 32, 0u);
+            const int c = cu + k * cs;
+            mask[c / 32] = 1u << (c % 32);
+            HIPCHK(hipExtStreamCreateWithCUMask(&d->slots[k].st, (uint32_t)mask.size(), mask.data()));
+        }
     }
     ImageBufs b;
     if ((rc = stage_image(d->ordinal, img, &b))) return rc;
@@ -902,7 +908,8 @@ extern "C" void jb_close(jb_ctx* ctx) {
     for (auto& d : ctx->devs) {
         (void)hipSetDevice(d->ordinal);
         (void)hipStreamSynchronize(d->stream);
-        if (d->sstream) (void)hipStreamSynchronize(d->sstream);
+        for (auto& sl : d->slots)
+            if (sl.st) (void)hipStreamSynchronize(sl.st);
         d->timer.reset();
         // a jb_cut_device pipeline queued on a caller's stream may still use the workspace:
         // wait for its completion event before freeing anything (the caller's stream may be
@@ -926,7 +933,8 @@ extern "C" void jb_close(jb_ctx* ctx) {
         if (d->cstream) (void)hipStreamDestroy(d->cstream);
         if (d->dstream) (void)hipStreamDestroy(d->dstream);
         (void)hipStreamDestroy(d->stream);
-        if (d->sstream) (void)hipStreamDestroy(d->sstream);
+        for (auto& sl : d->slots)
+            if (sl.st) (void)hipStreamDestroy(sl.st);
     }
     delete ctx;
 }
@@ -943,12 +951,12 @@ extern "C" const char* jb_last_error(void) { return g_err.c_str(); }
 // there.  Concurrent calls on a device are coalesced (the reference runs Cut calls
 // side by side under RLock, tokenizer.go:151-153): each call queues a SmallReq;
 // a caller whose request is still queued takes a free slot (one of four pinned
-// input/output buffer pairs), launches the queue's head requests (same hmm, up to
-// the k_small limits together) as ONE k_small batch on it, their documents back to
-// back, waits for that batch's completion word and hands each caller its own spans
-// by its documents' doc_tok ranges.  Up to four batches are in flight (the stream
-// runs them in order), so staging and waking callers overlap the kernels.  One
-// caller alone: a batch of one, as before.
+// input/output buffer pairs, each with its own stream on its own CU), launches the
+// queue's head requests (same hmm, up to the k_small limits together) as ONE k_small
+// batch on it, their documents back to back, waits for that batch's completion word
+// and hands each caller its own spans by its documents' doc_tok ranges.  Up to
+// JB_SMALL_SLOTS batches run at once, side by side on their CUs.  One caller alone:
+// a batch of one, as before.
 namespace {
 struct SmallReq {
     const uint8_t* text;
@@ -1025,13 +1033,13 @@ static void small_batch(Device* d, Device::SmallSlot* sl, SmallReq* const* rq, u
     volatile uint32_t* done = sl->h_sout + SM_DONE;
     if (!chk(run_small(d->dim, inl ? nullptr : sl->d_sin, (uint32_t)nbytes,
                        inl ? nullptr : reinterpret_cast<const uint64_t*>(sl->d_sin + kSmallBytes + 128), nd, hmm,
-                       sl->d_sout, seq, in, d->sstream),
+                       sl->d_sout, seq, in, sl->st),
              "k_small launch"))
         return;
     const auto c1 = std::chrono::steady_clock::now();
     for (uint32_t spin = 0; *done != seq; spin++) {
         if ((spin & 1023u) != 1023u) continue;
-        const hipError_t q = hipStreamQuery(d->sstream);
+        const hipError_t q = hipStreamQuery(sl->st);
         if (q == hipErrorNotReady) continue;
         if (!chk(q, "k_small")) return;
         if (*done != seq) {

@@ -932,6 +932,9 @@ def test_concurrent_cut_calls(syn_small, tmp_path, slots):
                        capture_output=True, text=True, timeout=300, env=dict(os.environ, JB_SMALL_SLOTS=str(slots)))
     print(f"JB_SMALL_SLOTS={slots}")
     print(r.stdout)
+    if os.environ.get("JB_CONC_LOG"):  # (diagnostics: JB_DEBUG's per-batch lines)
+        with open(f"{os.environ['JB_CONC_LOG']}.slots{slots}.txt", "w") as f:
+            f.write(r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     rates = {ln.split()[0]: float(ln.split()[-1]) for ln in r.stdout.splitlines()}
     assert rates["concurrent"] > rates["serial"]
