@@ -377,6 +377,9 @@ __device__ __forceinline__ bool dat_hit(uint64_t child, uint32_t id) { return jb
 #ifndef JB_MW_SGPR
 #define JB_MW_SGPR 80
 #endif
+#ifndef JB_MW_WALKS
+#define JB_MW_WALKS 1  // trie walks per lane at once (2 measured slower)
+#endif
 #define JB_MW_ATTR __attribute__((amdgpu_num_sgpr(JB_MW_SGPR)))
 __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                    const uint32_t* __restrict__ docbits, DevImage im,
@@ -706,62 +709,89 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     // mask m and a shift register rw of weight indices + 1 (each new one enters
     // at the last field, kRecTop, pushing the earlier ones a field down: after n
     // edges they fill the last n fields, the record's layout, and the first
-    // 4 - n fields are still 0).  One trip = one probe, with selects instead of
-    // branches (k_mark_walk is issue-bound).
-    bool act = false, ovf = false;
-    uint32_t j = 0, js = 0, id = 0, base = 0, len = 0, nedge = 0, m = 0;
-    uint64_t rw = 0;
-    uint32_t en = 0;  // entry j + 1 (the next rune of the walk), read a trip ahead
+    // 4 - n fields are still 0).  One trip = one probe per walk, with selects
+    // instead of branches.  Each lane runs JB_MW_WALKS walks side by side (two:
+    // two probes in flight per lane and trip, so the wave pays the probe round
+    // trip half as often; the walk phase is latency-bound).
+    struct Walk {
+        bool act, ovf;
+        uint32_t j, js, id, base, len, nedge, m, en;
+        uint64_t rw;
+    };
+    Walk wk[JB_MW_WALKS];
+#pragma unroll
+    for (int q = 0; q < JB_MW_WALKS; q++) {
+        wk[q].act = wk[q].ovf = false;
+        wk[q].j = wk[q].js = wk[q].id = wk[q].base = wk[q].len = wk[q].nedge = wk[q].m = wk[q].en = 0u;
+        wk[q].rw = 0ull;
+    }
     for (;;) {
-        const uint64_t need = __ballot(!act);
-        const uint32_t rank =
-            __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-        const uint32_t j0 = head + rank;
-        const bool fresh = !act && j0 < hi;
-        head = min(hi, head + (uint32_t)__popcll(need));
-        if (fresh) {  // a walk from the list: its rune has children and the run goes on in the tile
-            js = s_wl[j0];
-            j = js;
-            const uint64_t c = s_c[j];
-            id = ent_code(ent[j]);  // its level-1 cell
-            base = jb_cell_base(c);
-            const bool pos = jb_cell_fc(c) == JB_FC_POS;  // (weight index < 2^14: checked by the run links)
-            m = pos ? 1u : 0u;
-            nedge = m;
-            rw = pos ? (uint64_t)(jb_cell_widx(c) + 1u) << kRecTop : 0ull;
-            len = 1u;
-            ovf = false;
-            act = true;
-            en = ent[j + 1u];
+#pragma unroll
+        for (int q = 0; q < JB_MW_WALKS; q++) {  // idle walks take the next starts of the wave's list
+            Walk& w = wk[q];
+            const uint64_t need = __ballot(!w.act);
+            const uint32_t rank =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+            const uint32_t j0 = head + rank;
+            const bool fresh = !w.act && j0 < hi;
+            head = min(hi, head + (uint32_t)__popcll(need));
+            if (fresh) {  // a walk from the list: its rune has children and the run goes on in the tile
+                w.js = s_wl[j0];
+                w.j = w.js;
+                const uint64_t c = s_c[w.j];
+                w.id = ent_code(ent[w.j]);  // its level-1 cell
+                w.base = jb_cell_base(c);
+                const bool pos = jb_cell_fc(c) == JB_FC_POS;  // (weight index < 2^14: checked by the run links)
+                w.m = pos ? 1u : 0u;
+                w.nedge = w.m;
+                w.rw = pos ? (uint64_t)(jb_cell_widx(c) + 1u) << kRecTop : 0ull;
+                w.len = 1u;
+                w.ovf = false;
+                w.act = true;
+                w.en = ent[w.j + 1u];
+            }
         }
-        if (act) {  // one round trip: the next rune's cell
-            const uint32_t t = base + ent_code(en);
-            const uint64_t child = im.cells[t];
-            const uint32_t en2 = ent[j + 2u];  // (used only when the walk goes on: then entry j + 2 exists)
-            const bool hit = dat_hit(child, id);
-            ++len;
-            const uint32_t wi = jb_cell_widx(child);
-            const bool pos = hit && jb_cell_fc(child) == JB_FC_POS;
-            const bool bad = pos && (len > kEdgeMaxL || nedge >= 4u || wi > kRecIdxMax);
-            const bool add = pos && !bad;
-            ovf |= bad;
-            m |= add ? 1u << ((len - 1u) & 7u) : 0u;
-            rw = add ? (rw >> kEdgeIdxBits) | ((uint64_t)(wi + 1u) << kRecTop) : rw;
-            nedge += add ? 1u : 0u;
-            const bool more = hit && jb_cell_hc(child) && !ovf;
-            const bool go = more && (en & kEntCont);
-            const bool dfr = more && !(en & kEntCont) && (en & kEntEdge);  // past the lookahead: k_zh walks it
-            ++j;
-            en = en2;
-            id = t;
-            base = jb_cell_base(child);
-            if (!go) {  // the record goes to the start entry's LDS cell (read when the walk began)
-                s_c[js] = (ovf || dfr) ? 0ull : ((uint64_t)m | rw);
-                act = false;
+        uint64_t child[JB_MW_WALKS];
+        uint32_t tt[JB_MW_WALKS], en2[JB_MW_WALKS];
+#pragma unroll
+        for (int q = 0; q < JB_MW_WALKS; q++) {  // every walk's probe issued before any is used
+            tt[q] = wk[q].base + ent_code(wk[q].en);
+            child[q] = wk[q].act ? im.cells[tt[q]] : 0ull;
+            en2[q] = ent[wk[q].j + 2u];  // (used only when the walk goes on: then entry j + 2 exists)
+        }
+#pragma unroll
+        for (int q = 0; q < JB_MW_WALKS; q++) {
+            Walk& w = wk[q];
+            if (w.act) {
+                const uint64_t ch = child[q];
+                const bool hit = dat_hit(ch, w.id);
+                ++w.len;
+                const uint32_t wi = jb_cell_widx(ch);
+                const bool pos = hit && jb_cell_fc(ch) == JB_FC_POS;
+                const bool bad = pos && (w.len > kEdgeMaxL || w.nedge >= 4u || wi > kRecIdxMax);
+                const bool add = pos && !bad;
+                w.ovf |= bad;
+                w.m |= add ? 1u << ((w.len - 1u) & 7u) : 0u;
+                w.rw = add ? (w.rw >> kEdgeIdxBits) | ((uint64_t)(wi + 1u) << kRecTop) : w.rw;
+                w.nedge += add ? 1u : 0u;
+                const bool more = hit && jb_cell_hc(ch) && !w.ovf;
+                const bool go = more && (w.en & kEntCont);
+                const bool dfr = more && !(w.en & kEntCont) && (w.en & kEntEdge);  // past the lookahead: k_zh walks it
+                ++w.j;
+                w.en = en2[q];
+                w.id = tt[q];
+                w.base = jb_cell_base(ch);
+                if (!go) {  // the record goes to the start entry's LDS cell (read when the walk began)
+                    s_c[w.js] = (w.ovf || dfr) ? 0ull : ((uint64_t)w.m | w.rw);
+                    w.act = false;
+                }
             }
         }
         trips++;
-        if (!__any(act) && head >= hi) break;
+        bool any = false;
+#pragma unroll
+        for (int q = 0; q < JB_MW_WALKS; q++) any |= wk[q].act;
+        if (!__any(any) && head >= hi) break;
     }
     if (stamps) c3 = __builtin_amdgcn_s_memtime();
     __syncthreads();
@@ -2154,6 +2184,9 @@ constexpr uint32_t kLongGrid = 64;    // k_long_dp workgroups (persistent over t
 #if JB_STAMPS
 constexpr uint32_t kDbgLong = 65536u * 4u;  // k_long_dp's diagnostic clocks in the debug buffer (u64 index)
 #endif
+#ifndef JB_LD_REGWIN
+#define JB_LD_REGWIN 2  // k_long_dp: groups of four runes with items L = 1..m take best(s + L) from registers
+#endif
 constexpr uint32_t kLdWin = 256;      // runes per descriptor window
 constexpr uint32_t kLdDesc = 1024;    // descriptor ring: 4 windows
 constexpr uint32_t kLdRing = 512;     // best-value ring (edges are at most 255 runes)
@@ -2176,7 +2209,7 @@ struct LItem {
 struct LongLds {
     double ring[kLdRing];  // best(i) at i & 511
     LDesc desc[kLdDesc];   // rune i at i & 1023
-    uint8_t cls[kLdDesc];  // rune i's step form: 0 one item, 1 two, 2 three or four, 3 slow
+    uint8_t cls[kLdDesc];  // rune i's step form: 0 items L = 1..m (m <= 4), 1 other fast forms, 3 slow
     LItem side[4][kLdSide];
     uint32_t sidecnt[4], wslow[4];
 };
@@ -2336,7 +2369,8 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
 #pragma unroll
                     for (int k = 1; k < 4; k++) d.a[k - 1] = (uint32_t)k < m ? (((uint32_t)i + L[k]) & (kLdRing - 1u)) * 8u : 0u;
                     d.flag = 0u;
-                    cl = m == 1u ? 0u : (m == 2u ? 1u : 2u);
+                    // 0: items exactly L = 1..m (the chain's register form), 1: other gaps
+                    cl = (m < 2u || L[1] == 2u) && (m < 3u || L[2] == 3u) && (m < 4u || L[3] == 4u) ? 0u : 1u;
                 } else {  // more than 4 items, or none, or no L = 1 item (a negative count)
                     cl = 3u;
                     const uint32_t off = atomicAdd(&S.sidecnt[b], m);
@@ -2367,6 +2401,137 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
         if (tid == 0u) S.ring[n & (kLdRing - 1u)] = 0.0;
         __syncthreads();
         if (wave == 0u) {
+#if JB_LD_REGWIN == 2
+            // ---- the chain (calcDagProba + maxIndexProba, :502-578), lane 0 ----
+            // By groups of four runes g..g+3 (taken g+3 first): the group's descriptors
+            // were loaded into registers during the group before (two register sets,
+            // alternate groups, no copies), and best(s+1 .. s+4) are in registers (H).
+            // A group whose runes all have items exactly L = 1..m (m <= 4; class word 0,
+            // most groups) folds from registers only.  Another group reads best(s + L_k)
+            // from the ring, one rune ahead, and its slow runes walk their item lists.
+            // The reference's rule over items p1..p4 (:565-578) is "the last k with
+            // p_k >= p_(k-1)" (p_0 = minFloat).  With L1 = 1 and NaN for absent items
+            // that is: p4 if p4 >= p3, else p3 if p3 >= p2, else max(p1, p2) (p1 <
+            // minFloat only when p1 = -Inf, and then p2 >= p1 whenever item 2 exists;
+            // equal values are the same value).
+            struct DSet {
+                double w[4][4];
+                uint32_t a[4][3], f[4];
+            };
+            DSet D0, D1;
+            double H[4] = {0.0, 0.0, 0.0, 0.0};  // best(s + 1 .. s + 4) before rune s
+            // a zero the compiler cannot see through: the descriptor addresses are
+            // uniform, and it would otherwise keep the loaded sets in SGPRs and wait
+            // for each load at once to move it there (readfirstlane), not a group later
+            uint32_t dz;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(dz));
+            double RV[2][3];
+            auto ld_grp = [&](DSet& D, int32_t g) __attribute__((always_inline)) {  // descriptors of runes g .. g+3 (index s & 3)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const char* p = reinterpret_cast<const char*>(S.desc) + (((uint32_t)(g + r) & (kLdDesc - 1u)) * 48u + dz);
+                    const double2 x = *reinterpret_cast<const double2*>(p);
+                    const double2 y = *reinterpret_cast<const double2*>(p + 16);
+                    const uint4 z = *reinterpret_cast<const uint4*>(p + 32);
+                    D.w[r][0] = x.x;
+                    D.w[r][1] = x.y;
+                    D.w[r][2] = y.x;
+                    D.w[r][3] = y.y;
+                    D.a[r][0] = z.x;
+                    D.a[r][1] = z.y;
+                    D.a[r][2] = z.z;
+                    D.f[r] = z.w;
+                }
+            };
+            auto ld_rv = [&](uint32_t k, const DSet& D, int r) __attribute__((always_inline)) {
+#pragma unroll
+                for (int q = 0; q < 3; q++) RV[k][q] = *reinterpret_cast<const double*>(rb + D.a[r][q]);
+            };
+            auto push = [&](double P) __attribute__((always_inline)) {
+                H[3] = H[2];
+                H[2] = H[1];
+                H[1] = H[0];
+                H[0] = P;
+            };
+            auto group = [&](auto chk, int32_t g, const DSet& C, DSet& N, uint32_t cw, uint32_t b) __attribute__((always_inline)) {
+                constexpr bool CHK = decltype(chk)::value;
+                ld_grp(N, g - 4);  // (the next group's, a whole group ahead)
+                char* const rw = reinterpret_cast<char*>(S.ring) + ((uint32_t)g & (kLdRing - 1u)) * 8u;
+                if (cw == 0u) {
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int r = 3 - u;
+                        const double p1 = C.w[r][0] + H[0];
+                        const double p2 = C.w[r][1] + H[1];
+                        const double p3 = C.w[r][2] + H[2];
+                        const double p4 = C.w[r][3] + H[3];
+                        const double R = max_f64(p1, p2);
+                        const bool k3 = p3 >= p2, k4 = p4 >= p3;
+                        const double p34 = k4 ? p4 : p3;
+                        const double P = (k3 || k4) ? p34 : R;
+                        *reinterpret_cast<double*>(rw + (uint32_t)r * 8u) = P;
+                        push(P);
+                    }
+                    return;
+                }
+                ld_rv(1u, C, 3);
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int r = 3 - u;
+                    const uint32_t rs = (uint32_t)(u + 1) & 1u;  // this rune's ring values (set 1 at u = 0)
+                    if (u < 3) ld_rv(rs ^ 1u, C, r - 1);  // the next rune's, a step ahead
+                    double P;
+                    const uint32_t cl = (cw >> (8 * r)) & 3u;
+                    if (CHK && cl == 3u) {
+                        const uint32_t s = (uint32_t)(g + r), fl = C.f[r];
+                        DpFold f;
+                        if (fl == kLdWalk) {
+                            long_items(text, im, erec, bs, be, s, [&](uint32_t L, double wt) {
+                                fold_item(f, L, wt + S.ring[(s + L) & (kLdRing - 1u)]);
+                            });
+                        } else {
+                            const uint32_t m = fl >> 16, off = (fl >> 1) & 0x7FFFu;
+                            for (uint32_t k = 0; k < m; k++) {
+                                const LItem it = S.side[b][off + k];
+                                fold_item(f, it.L, it.w + S.ring[(s + it.L) & (kLdRing - 1u)]);
+                            }
+                        }
+                        f.finish();
+                        P = f.bestP;
+                    } else {
+                        const double p1 = C.w[r][0] + H[0];
+                        const double p2 = C.w[r][1] + RV[rs][0];
+                        const double p3 = C.w[r][2] + RV[rs][1];
+                        const double p4 = C.w[r][3] + RV[rs][2];
+                        const double R = max_f64(p1, p2);
+                        const bool k3 = p3 >= p2, k4 = p4 >= p3;
+                        const double p34 = k4 ? p4 : p3;
+                        P = (k3 || k4) ? p34 : R;
+                    }
+                    *reinterpret_cast<double*>(rw + (uint32_t)r * 8u) = P;
+                    push(P);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            };
+            const int32_t top = (int32_t)kLdWin * J - 4;  // the first group
+            uint32_t cwn = 0;
+            if (lane == 0u) {
+                ld_grp(D0, top);
+                cwn = *reinterpret_cast<const uint32_t*>(S.cls + ((uint32_t)top & (kLdDesc - 1u)));
+            }
+            auto run = [&](auto chk, int32_t j) {
+                const uint32_t b = (uint32_t)j & 3u;
+                for (int32_t g = (int32_t)kLdWin * j + (int32_t)kLdWin - 4; g >= (int32_t)kLdWin * j; g -= 8) {
+                    uint32_t cw = __builtin_amdgcn_readfirstlane(cwn);
+                    cwn = *reinterpret_cast<const uint32_t*>(S.cls + ((uint32_t)(g - 4) & (kLdDesc - 1u)));
+                    group(chk, g, D0, D1, cw, b);
+                    cw = __builtin_amdgcn_readfirstlane(cwn);
+                    cwn = *reinterpret_cast<const uint32_t*>(S.cls + ((uint32_t)(g - 8) & (kLdDesc - 1u)));
+                    group(chk, g - 4, D1, D0, cw, b);
+                }
+            };
+            static_assert(kLdWin % 8u == 0u, "two groups per loop trip");
+#else
             // ---- the chain (calcDagProba + maxIndexProba, :502-578), lane 0 ----
             // Step s: issue rune s-3's descriptor and rune s-1's ring reads, then
             // fold rune s.  The reference's rule over items p1..p4 (:565-578) is
@@ -2376,8 +2541,21 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
             // p2 >= p1 whenever item 2 exists; equal values are the same value).
             double W[4][4], RV[2][3];
             uint32_t A[4][3], F[4];
-            double b1 = 0.0;  // best(s + 1)
+            // best(s + 1 .. s + 4) before rune s (H[0] = best(s + 1)): a group of four
+            // runes whose items are all L = 1..m (m <= 4) reads them from here, not
+            // from the ring (each LDS round trip stood on the chain, §4.4)
+            double H[4] = {0.0, 0.0, 0.0, 0.0};
             auto ld_desc = [&](uint32_t set, uint32_t off) {  // off: byte offset in S.desc
+#if defined(JB_EXP_LD_NODESC)  // timing experiment only (wrong results): one descriptor read per 4 runes
+                if (set != 0u) {
+#pragma unroll
+                    for (int k = 0; k < 4; k++) W[set][k] = W[0][k];
+#pragma unroll
+                    for (int k = 0; k < 3; k++) A[set][k] = A[0][k];
+                    F[set] = F[0];
+                    return;
+                }
+#endif
                 const char* p = reinterpret_cast<const char*>(S.desc) + off;
                 const double2 x = *reinterpret_cast<const double2*>(p);
                 const double2 y = *reinterpret_cast<const double2*>(p + 16);
@@ -2392,8 +2570,13 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                 F[set] = z.w;
             };
             auto ld_ring = [&](uint32_t rs, uint32_t set) {
+#if defined(JB_EXP_LD_NORING)  // timing experiment only (wrong results): no ring reads
+#pragma unroll
+                for (int k = 0; k < 3; k++) RV[rs][k] = W[set][k + 1];
+#else
 #pragma unroll
                 for (int k = 0; k < 3; k++) RV[rs][k] = *reinterpret_cast<const double*>(rb + A[set][k]);
+#endif
             };
             const int32_t top = (int32_t)kLdWin * J - 1;
             if (lane == 0u) {
@@ -2415,6 +2598,31 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                     const uint32_t dcur = ((uint32_t)g & (kLdDesc - 1u)) * 48u;
                     const uint32_t dnxt = ((uint32_t)(g - 4) & (kLdDesc - 1u)) * 48u;
                     char* const rw = reinterpret_cast<char*>(S.ring) + ((uint32_t)g & (kLdRing - 1u)) * 8u;
+#if JB_LD_REGWIN
+                    if (cw == 0u) {  // four runes of the register form
+#pragma unroll
+                        for (int u = 0; u < 4; u++) {
+                            const uint32_t cs = (uint32_t)(3 - u) & 3u, c1 = (uint32_t)(2 - u) & 3u,
+                                           c3 = (uint32_t)(0 - u) & 3u;
+                            ld_desc(c3, u == 0 ? dcur : dnxt + (uint32_t)(4 - u) * 48u);
+                            if (u == 3) ld_ring(1u, c1);  // (the next group's first rune, should it need them)
+                            const double p1 = W[cs][0] + H[0];
+                            const double p2 = W[cs][1] + H[1];
+                            const double p3 = W[cs][2] + H[2];
+                            const double p4 = W[cs][3] + H[3];
+                            const double R = max_f64(p1, p2);
+                            const bool k3 = p3 >= p2, k4 = p4 >= p3;
+                            const double p34 = k4 ? p4 : p3;
+                            const double P = (k3 || k4) ? p34 : R;
+                            *reinterpret_cast<double*>(rw + (uint32_t)(3 - u) * 8u) = P;
+                            H[3] = H[2];
+                            H[2] = H[1];
+                            H[1] = H[0];
+                            H[0] = P;
+                        }
+                        continue;
+                    }
+#endif
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
                         const uint32_t cs = (uint32_t)(3 - u) & 3u, c1 = (uint32_t)(2 - u) & 3u,
@@ -2446,7 +2654,7 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                             // weights, so their sums are NaN, every compare with them is
                             // false and v_max_f64 (IEEE maxNum) returns the other operand
                             // (one item: p1; two: max(p1, p2), the second unless smaller)
-                            const double p1 = W[cs][0] + b1;
+                            const double p1 = W[cs][0] + H[0];
                             const double p2 = W[cs][1] + RV[rs][0];
                             const double p3 = W[cs][2] + RV[rs][1];
                             const double p4 = W[cs][3] + RV[rs][2];
@@ -2456,7 +2664,10 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                             P = (k3 || k4) ? p34 : R;
                         }
                         *reinterpret_cast<double*>(rw + (uint32_t)(3 - u) * 8u) = P;
-                        b1 = P;
+                        H[3] = H[2];
+                        H[2] = H[1];
+                        H[1] = H[0];
+                        H[0] = P;
                         // keep each step's loads a whole step ahead of their use: the
                         // scheduler would otherwise hoist the next step's adds up to
                         // its just-issued ring reads and wait for them
@@ -2464,6 +2675,7 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                     }
                 }
             };
+#endif
             for (int32_t j = J - 1; j >= 0; --j) {
 #if JB_STAMPS
                 const uint64_t t0 = __builtin_amdgcn_s_memtime();
