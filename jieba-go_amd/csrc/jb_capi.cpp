@@ -798,6 +798,16 @@ static int launch_pipeline_(Device* d, const Work& w, const uint8_t* d_text, uin
                         (unsigned long long)sl[i * 8 + 2], (unsigned long long)sl[i * 8 + 3],
                         (unsigned long long)sl[i * 8 + 4], (unsigned long long)sl[i * 8 + 5]);
         HIPCHK(hipMemsetAsync(d->w.dbg + 65536 * 4, 0, sl.size() * 8, s));
+        if (const char* wo = getenv("JB_LDW_OUT")) {  // k_long_dp per-window records of block 0
+            std::vector<uint64_t> wr(65536 * 2 * 4);
+            HIPCHK(hipMemcpyAsync(wr.data(), d->w.dbg + 65536 * 8, wr.size() * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            if (FILE* f = fopen(wo, "wb")) {
+                fwrite(wr.data(), 8, wr.size(), f);
+                fclose(f);
+            }
+            HIPCHK(hipMemsetAsync(d->w.dbg + 65536 * 8, 0, wr.size() * 8, s));
+        }
     }
     return JB_OK;
 }

@@ -2183,9 +2183,8 @@ __global__ __launch_bounds__(NW * 64) JB_ZH_ATTR void k_zh(const uint8_t* __rest
 constexpr uint32_t kLongGrid = 64;    // k_long_dp workgroups (persistent over the long-block list)
 #if JB_STAMPS
 constexpr uint32_t kDbgLong = 65536u * 4u;  // k_long_dp's diagnostic clocks in the debug buffer (u64 index)
-#endif
-#ifndef JB_LD_REGWIN
-#define JB_LD_REGWIN 2  // k_long_dp: groups of four runes with items L = 1..m take best(s + L) from registers
+constexpr uint32_t kDbgLongWin = 65536u * 8u;  // per-window chain clocks and group counts of block 0
+constexpr uint32_t kDbgLongWinMax = 65536u * 2u;
 #endif
 constexpr uint32_t kLdWin = 256;      // runes per descriptor window
 constexpr uint32_t kLdDesc = 1024;    // descriptor ring: 4 windows
@@ -2401,7 +2400,6 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
         if (tid == 0u) S.ring[n & (kLdRing - 1u)] = 0.0;
         __syncthreads();
         if (wave == 0u) {
-#if JB_LD_REGWIN == 2
             // ---- the chain (calcDagProba + maxIndexProba, :502-578), lane 0 ----
             // By groups of four runes g..g+3 (taken g+3 first): the group's descriptors
             // were loaded into registers during the group before (two register sets,
@@ -2413,7 +2411,8 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
             // p_k >= p_(k-1)" (p_0 = minFloat).  With L1 = 1 and NaN for absent items
             // that is: p4 if p4 >= p3, else p3 if p3 >= p2, else max(p1, p2) (p1 <
             // minFloat only when p1 = -Inf, and then p2 >= p1 whenever item 2 exists;
-            // equal values are the same value).
+            // equal values are the same value; tests/test_long_fold.py checks this
+            // form against the oracle's rule).
             struct DSet {
                 double w[4][4];
                 uint32_t a[4][3], f[4];
@@ -2519,163 +2518,31 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                 ld_grp(D0, top);
                 cwn = *reinterpret_cast<const uint32_t*>(S.cls + ((uint32_t)top & (kLdDesc - 1u)));
             }
+#if JB_STAMPS
+            uint32_t st_wf = 0, st_w1 = 0, st_w3 = 0;  // per window: register-form groups, class-1 and class-3 runes
+            auto st_count = [&](uint32_t cw) {
+                const uint32_t x = cw & 0x03030303u;
+                st_wf += cw == 0u ? 1u : 0u;
+                st_w1 += (uint32_t)__popc(x & ~(x >> 1) & 0x01010101u);
+                st_w3 += (uint32_t)__popc(x & (x >> 1) & 0x01010101u);
+            };
+#else
+            auto st_count = [](uint32_t) {};
+#endif
             auto run = [&](auto chk, int32_t j) {
                 const uint32_t b = (uint32_t)j & 3u;
                 for (int32_t g = (int32_t)kLdWin * j + (int32_t)kLdWin - 4; g >= (int32_t)kLdWin * j; g -= 8) {
                     uint32_t cw = __builtin_amdgcn_readfirstlane(cwn);
                     cwn = *reinterpret_cast<const uint32_t*>(S.cls + ((uint32_t)(g - 4) & (kLdDesc - 1u)));
+                    st_count(cw);
                     group(chk, g, D0, D1, cw, b);
                     cw = __builtin_amdgcn_readfirstlane(cwn);
                     cwn = *reinterpret_cast<const uint32_t*>(S.cls + ((uint32_t)(g - 8) & (kLdDesc - 1u)));
+                    st_count(cw);
                     group(chk, g - 4, D1, D0, cw, b);
                 }
             };
             static_assert(kLdWin % 8u == 0u, "two groups per loop trip");
-#else
-            // ---- the chain (calcDagProba + maxIndexProba, :502-578), lane 0 ----
-            // Step s: issue rune s-3's descriptor and rune s-1's ring reads, then
-            // fold rune s.  The reference's rule over items p1..p4 (:565-578) is
-            // "the last k with p_k >= p_(k-1)" (p_0 = minFloat).  With L1 = 1 and
-            // NaN for absent items that is: p4 if p4 >= p3, else p3 if p3 >= p2,
-            // else max(p1, p2) (p1 < minFloat only when p1 = -Inf, and then
-            // p2 >= p1 whenever item 2 exists; equal values are the same value).
-            double W[4][4], RV[2][3];
-            uint32_t A[4][3], F[4];
-            // best(s + 1 .. s + 4) before rune s (H[0] = best(s + 1)): a group of four
-            // runes whose items are all L = 1..m (m <= 4) reads them from here, not
-            // from the ring (each LDS round trip stood on the chain, §4.4)
-            double H[4] = {0.0, 0.0, 0.0, 0.0};
-            auto ld_desc = [&](uint32_t set, uint32_t off) {  // off: byte offset in S.desc
-#if defined(JB_EXP_LD_NODESC)  // timing experiment only (wrong results): one descriptor read per 4 runes
-                if (set != 0u) {
-#pragma unroll
-                    for (int k = 0; k < 4; k++) W[set][k] = W[0][k];
-#pragma unroll
-                    for (int k = 0; k < 3; k++) A[set][k] = A[0][k];
-                    F[set] = F[0];
-                    return;
-                }
-#endif
-                const char* p = reinterpret_cast<const char*>(S.desc) + off;
-                const double2 x = *reinterpret_cast<const double2*>(p);
-                const double2 y = *reinterpret_cast<const double2*>(p + 16);
-                const uint4 z = *reinterpret_cast<const uint4*>(p + 32);
-                W[set][0] = x.x;
-                W[set][1] = x.y;
-                W[set][2] = y.x;
-                W[set][3] = y.y;
-                A[set][0] = z.x;
-                A[set][1] = z.y;
-                A[set][2] = z.z;
-                F[set] = z.w;
-            };
-            auto ld_ring = [&](uint32_t rs, uint32_t set) {
-#if defined(JB_EXP_LD_NORING)  // timing experiment only (wrong results): no ring reads
-#pragma unroll
-                for (int k = 0; k < 3; k++) RV[rs][k] = W[set][k + 1];
-#else
-#pragma unroll
-                for (int k = 0; k < 3; k++) RV[rs][k] = *reinterpret_cast<const double*>(rb + A[set][k]);
-#endif
-            };
-            const int32_t top = (int32_t)kLdWin * J - 1;
-            if (lane == 0u) {
-                ld_desc(3u, ((uint32_t)top & (kLdDesc - 1u)) * 48u);
-                ld_desc(2u, ((uint32_t)(top - 1) & (kLdDesc - 1u)) * 48u);
-                ld_desc(1u, ((uint32_t)(top - 2) & (kLdDesc - 1u)) * 48u);
-                ld_ring(1u, 3u);
-            }
-            // step forms of the 4 runes of the group up next (one LDS word, a group ahead)
-            uint32_t cwn = 0;
-            if (lane == 0u) cwn = *reinterpret_cast<const uint32_t*>(S.cls + ((uint32_t)(top - 3) & (kLdDesc - 1u)));
-            auto run = [&](auto chk, int32_t j) {
-                constexpr bool CHK = decltype(chk)::value;
-                const uint32_t b = (uint32_t)j & 3u;
-                for (int32_t g = (int32_t)kLdWin * j + (int32_t)kLdWin - 4; g >= (int32_t)kLdWin * j; g -= 4) {
-                    const uint32_t cw = __builtin_amdgcn_readfirstlane(cwn);
-                    cwn = *reinterpret_cast<const uint32_t*>(S.cls + ((uint32_t)(g - 4) & (kLdDesc - 1u)));
-                    // runes s = g + 3 - u, u = 0..3: descriptor set s & 3 = 3 - u, ring set s & 1
-                    const uint32_t dcur = ((uint32_t)g & (kLdDesc - 1u)) * 48u;
-                    const uint32_t dnxt = ((uint32_t)(g - 4) & (kLdDesc - 1u)) * 48u;
-                    char* const rw = reinterpret_cast<char*>(S.ring) + ((uint32_t)g & (kLdRing - 1u)) * 8u;
-#if JB_LD_REGWIN
-                    if (cw == 0u) {  // four runes of the register form
-#pragma unroll
-                        for (int u = 0; u < 4; u++) {
-                            const uint32_t cs = (uint32_t)(3 - u) & 3u, c1 = (uint32_t)(2 - u) & 3u,
-                                           c3 = (uint32_t)(0 - u) & 3u;
-                            ld_desc(c3, u == 0 ? dcur : dnxt + (uint32_t)(4 - u) * 48u);
-                            if (u == 3) ld_ring(1u, c1);  // (the next group's first rune, should it need them)
-                            const double p1 = W[cs][0] + H[0];
-                            const double p2 = W[cs][1] + H[1];
-                            const double p3 = W[cs][2] + H[2];
-                            const double p4 = W[cs][3] + H[3];
-                            const double R = max_f64(p1, p2);
-                            const bool k3 = p3 >= p2, k4 = p4 >= p3;
-                            const double p34 = k4 ? p4 : p3;
-                            const double P = (k3 || k4) ? p34 : R;
-                            *reinterpret_cast<double*>(rw + (uint32_t)(3 - u) * 8u) = P;
-                            H[3] = H[2];
-                            H[2] = H[1];
-                            H[1] = H[0];
-                            H[0] = P;
-                        }
-                        continue;
-                    }
-#endif
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const uint32_t cs = (uint32_t)(3 - u) & 3u, c1 = (uint32_t)(2 - u) & 3u,
-                                       c3 = (uint32_t)(0 - u) & 3u;
-                        const uint32_t rs = (uint32_t)(3 - u) & 1u, r1 = (uint32_t)(2 - u) & 1u;
-                        // rune s - 3 is g - u: slot g (u = 0) or g - 4 + (4 - u)
-                        ld_desc(c3, u == 0 ? dcur : dnxt + (uint32_t)(4 - u) * 48u);
-                        ld_ring(r1, c1);
-                        double P;
-                        const uint32_t cl = (cw >> (8 * (3 - u))) & 3u;  // rune s = g + 3 - u: byte 3 - u
-                        if (CHK && cl == 3u) {
-                            const uint32_t s = (uint32_t)(g + 3 - u), fl = F[cs];
-                            DpFold f;
-                            if (fl == kLdWalk) {
-                                long_items(text, im, erec, bs, be, s, [&](uint32_t L, double wt) {
-                                    fold_item(f, L, wt + S.ring[(s + L) & (kLdRing - 1u)]);
-                                });
-                            } else {
-                                const uint32_t m = fl >> 16, off = (fl >> 1) & 0x7FFFu;
-                                for (uint32_t k = 0; k < m; k++) {
-                                    const LItem it = S.side[b][off + k];
-                                    fold_item(f, it.L, it.w + S.ring[(s + it.L) & (kLdRing - 1u)]);
-                                }
-                            }
-                            f.finish();
-                            P = f.bestP;
-                        } else {
-                            // one form for 1-4 items, no branch: absent items have NaN
-                            // weights, so their sums are NaN, every compare with them is
-                            // false and v_max_f64 (IEEE maxNum) returns the other operand
-                            // (one item: p1; two: max(p1, p2), the second unless smaller)
-                            const double p1 = W[cs][0] + H[0];
-                            const double p2 = W[cs][1] + RV[rs][0];
-                            const double p3 = W[cs][2] + RV[rs][1];
-                            const double p4 = W[cs][3] + RV[rs][2];
-                            const double R = max_f64(p1, p2);
-                            const bool k3 = p3 >= p2, k4 = p4 >= p3;
-                            const double p34 = k4 ? p4 : p3;
-                            P = (k3 || k4) ? p34 : R;
-                        }
-                        *reinterpret_cast<double*>(rw + (uint32_t)(3 - u) * 8u) = P;
-                        H[3] = H[2];
-                        H[2] = H[1];
-                        H[1] = H[0];
-                        H[0] = P;
-                        // keep each step's loads a whole step ahead of their use: the
-                        // scheduler would otherwise hoist the next step's adds up to
-                        // its just-issued ring reads and wait for them
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-                }
-            };
-#endif
             for (int32_t j = J - 1; j >= 0; --j) {
 #if JB_STAMPS
                 const uint64_t t0 = __builtin_amdgcn_s_memtime();
@@ -2687,6 +2554,14 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
 #if JB_STAMPS
                 const uint64_t t1 = __builtin_amdgcn_s_memtime();
                 st_slow += S.wslow[j & 3] ? 1u : 0u;
+                if (blockIdx.x == 0u && lane == 0u && (uint32_t)j < kDbgLongWinMax) {  // per window of block 0
+                    uint64_t* o = dbg + kDbgLongWin + (uint64_t)j * 4u;
+                    o[0] = t1 - t0;
+                    o[1] = st_wf;
+                    o[2] = st_w1;
+                    o[3] = st_w3;
+                }
+                st_wf = st_w1 = st_w3 = 0u;
 #endif
                 __syncthreads();
 #if JB_STAMPS

@@ -1,0 +1,62 @@
+"""The closed form k_long_dp's chain folds a rune with (jb_kernels.hip, the
+chain's comment): for items in length order with L1 = 1, sums p1..pm and NaN
+for the absent p(m+1)..p4,
+    P = p4 if p4 >= p3, else p3 if p3 >= p2, else max(p1, p2)
+(v_max_f64 drops a NaN operand).  Checked against the oracle's maxIndexProba
+(tokenizer.go:565-578, oracle/jieba_oracle.c) on 1-4 items with ties and -Inf
+(count-0 weights).  The chain keeps only the taken item's value (k_long_seg
+recomputes the lengths), so the value is what must match, bit for bit.  The GPU
+parity tests run the kernel itself."""
+import itertools
+import math
+import random
+
+import pytest
+
+import oracle as O
+
+NAN = float("nan")
+INF = float("inf")
+
+
+def vmax(a, b):  # v_max_f64: IEEE maxNum (a NaN operand gives the other one)
+    if math.isnan(a):
+        return b
+    if math.isnan(b):
+        return a
+    return a if a >= b else b
+
+
+def chain_fold(p):
+    """The chain's fold of sums p (1-4 items, in length order)."""
+    p1, p2, p3, p4 = (list(p) + [NAN] * 4)[:4]
+    k3, k4 = p3 >= p2, p4 >= p3
+    return (p4 if k4 else p3) if (k3 or k4) else vmax(p1, p2)
+
+
+def reference(p):
+    return O.max_index_proba(list(enumerate(p)))[1]
+
+
+def _same(a, b):
+    return a == b or (math.isinf(a) and math.isinf(b) and (a > 0) == (b > 0))
+
+
+def test_chain_fold_random():
+    rng = random.Random(1)
+    pool = [-1.0, -2.0, -3.0, -0.5, -7.25, -INF]
+    bad = []
+    for _ in range(40000):
+        m = rng.randint(1, 4)
+        p = [rng.choice(pool + [rng.uniform(-80.0, 0.0)]) for _ in range(m)]
+        want, got = reference(p), chain_fold(p)
+        if not _same(want, got):
+            bad.append((p, want, got))
+    assert not bad, bad[:3]
+
+
+@pytest.mark.parametrize("m", [1, 2, 3, 4])
+def test_chain_fold_every_order(m):
+    """Every order of the items' sums, ties and -Inf included."""
+    for p in itertools.product([-4.0, -3.0, -2.0, -1.0, -INF], repeat=m):
+        assert _same(reference(list(p)), chain_fold(p)), p
