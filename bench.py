@@ -604,6 +604,13 @@ def load_backend():
     return getattr(importlib.import_module(mod), cls)()
 
 
+def share_gpu():
+    """JB_BENCH_SHARE_GPU=1 (testing only): every rank on GPU (LOCAL_RANK mod the GPUs
+    visible), so the N-rank path runs end to end on a one-GPU box; the line's `data`
+    and `config.ranks` say so, and it is never a scaling number."""
+    return os.environ.get("JB_BENCH_SHARE_GPU") == "1"
+
+
 def _free_port():
     import socket
     with socket.socket() as sk:
@@ -621,7 +628,7 @@ def launch(n, argv, backend):
     import signal
     import subprocess
     have = backend.device_count()
-    if have < n:
+    if have < n and not (share_gpu() and have >= 1):
         print(f"bench.py: --gpus {n} but only {have} GPU(s) visible; not running a smaller job in its place",
               file=sys.stderr)
         return 2
@@ -699,6 +706,8 @@ def main(argv=None):
         if args.gpus is not None and args.gpus != world:
             print(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world}", file=sys.stderr)
             return 2
+    if share_gpu() and backend.device_count() >= 1:
+        local %= backend.device_count()
     if local >= backend.device_count():
         print(f"bench.py: rank {rank} wants GPU {local}, only {backend.device_count()} visible", file=sys.stderr)
         return 2
@@ -755,6 +764,9 @@ def main(argv=None):
         launcher = os.environ.get("JB_BENCH_LAUNCHER") or ("torch.distributed.run" if world > 1 else "single process")
         line["config"]["ranks"] = {"launcher": launcher, "processes": world, "rank_to_gpu": "rank r -> GPU r",
                                    "host_group": "gloo (timing barriers + job sums; no RCCL)" if world > 1 else None}
+        if share_gpu():
+            line["config"]["ranks"]["rank_to_gpu"] = "TEST (JB_BENCH_SHARE_GPU): rank r -> GPU r mod the GPUs visible"
+            line["data"] = "TEST (JB_BENCH_SHARE_GPU, ranks share a GPU): not a scaling measurement; " + line["data"]
         if backend.name != "gpu":
             line["data"] = f"TEST BACKEND {backend.name}: not a measurement"
         if world == 1 and not args.no_e2e:

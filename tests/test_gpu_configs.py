@@ -320,3 +320,26 @@ def test_cut_device_into_unaligned_outputs(syn_small):
         _cmp(*got, *want, f"outputs {4 * sh} bytes past alignment")
         assert int(o_s[sh - 1].item()) == -1 and int(o_s[sh + n].item()) == -1  # nothing written outside
     tk.close()
+
+
+def test_bench_two_ranks_on_the_gpu(tmp_path):
+    """`bench.py --gpus 2` end to end on the GPU: the launcher starts two ranks
+    (JB_BENCH_SHARE_GPU puts both on GPU 0 of a one-GPU box, testing only), each cuts
+    its byte-balanced shard of the corpus through the C ABI and checks every token
+    against the oracle, and rank 0 prints one line with the job's aggregate
+    (the driver's N-GPU scaling run takes the same path with one GPU per rank)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, JB_BENCH_SHARE_GPU="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--corpus-mib", "32",
+                        "--steps", "2", "--warmup", "1", "--no-e2e", "--no-latency", "--no-profile",
+                        "--cpu1-sample-mib", "0"], capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["config"]["ranks"]["processes"] == 2
+    assert line["parity"]["bit_exact"] and line["parity"]["ranks_checked"] == 2, line["parity"]
+    assert "JB_BENCH_SHARE_GPU" in line["data"]
+    assert line["value"] > 0
