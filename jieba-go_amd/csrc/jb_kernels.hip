@@ -3634,17 +3634,26 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
             };
             if (lw == 0xFFu) {  // more than 4 edges: walk the rune again
                 sm_walk(s, im, s.hpos[h], [&](uint32_t L, uint32_t, double w) { item(L, w, s.sbest[h + L]); });
+                if (bestL == 0) {  // no item qualified: the last item (or none: tail -1)
+                    bestL = lastL;
+                    bestP = prevP;
+                }
             } else {
+                // Up to 4 items without a branch: an absent item (L = 0) has a NaN sum, which
+                // no compare takes.  The reference's "last item k with p_k >= p_(k-1)"
+                // (p_0 = minFloat; none: the last item) is then p3 if p3 >= p2, else p2 if
+                // p2 >= p1, else p1 if p1 >= p0, else p0 (the first item alone, or -Inf).
                 const uint32_t L0 = lw & 0xFFu, L1 = (lw >> 8) & 0xFFu, L2 = (lw >> 16) & 0xFFu, L3 = lw >> 24;
                 const double b0 = s.sbest[h + L0], b1 = s.sbest[h + L1], b2 = s.sbest[h + L2], b3 = s.sbest[h + L3];
-                if (L0) item(L0, w0, b0);
-                if (L1) item(L1, w1, b1);
-                if (L2) item(L2, w2, b2);
-                if (L3) item(L3, w3, b3);
-            }
-            if (bestL == 0) {  // no item qualified: the last item (or none: tail -1)
-                bestL = lastL;
-                bestP = prevP;
+                auto sum = [&](uint32_t L, double w, double nb) {  // pieceProba (:519-529)
+                    const double pp = w + (h + L == h1 ? 0.0 : (L == 1u ? bnx : nb));
+                    return L ? pp : __builtin_nan("");
+                };
+                const double p0 = sum(L0, w0, b0), p1 = sum(L1, w1, b1), p2 = sum(L2, w2, b2), p3 = sum(L3, w3, b3);
+                const bool c3 = p3 >= p2, c2 = p2 >= p1, c1 = p1 >= p0;
+                bestP = c3 ? p3 : (c2 ? p2 : (c1 ? p1 : p0));
+                bestL = c3 ? L3 : (c2 ? L2 : (c1 ? L1 : L0));
+                bestP = L0 ? bestP : JB_MIN_FLOAT;  // (no item: the reference panics later, sL = 0)
             }
             s.sbest[h] = bestP;
             s.sL[h] = (uint8_t)bestL;
