@@ -3632,17 +3632,27 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
                 prevP = pp;
                 lastL = L;
             };
-            if (lw == 0xFFu) {  // more than 4 edges: walk the rune again
-                sm_walk(s, im, s.hpos[h], [&](uint32_t L, uint32_t, double w) { item(L, w, s.sbest[h + L]); });
+            if (lw == 0xFFu || !im.plainw) {  // more than 4 edges (walk the rune again), or +Inf/NaN weights
+                if (lw == 0xFFu) {
+                    sm_walk(s, im, s.hpos[h], [&](uint32_t L, uint32_t, double w) { item(L, w, s.sbest[h + L]); });
+                } else {
+                    const uint32_t L0 = lw & 0xFFu, L1 = (lw >> 8) & 0xFFu, L2 = (lw >> 16) & 0xFFu, L3 = lw >> 24;
+                    if (L0) item(L0, w0, s.sbest[h + L0]);
+                    if (L1) item(L1, w1, s.sbest[h + L1]);
+                    if (L2) item(L2, w2, s.sbest[h + L2]);
+                    if (L3) item(L3, w3, s.sbest[h + L3]);
+                }
                 if (bestL == 0) {  // no item qualified: the last item (or none: tail -1)
                     bestL = lastL;
                     bestP = prevP;
                 }
             } else {
                 // Up to 4 items without a branch: an absent item (L = 0) has a NaN sum, which
-                // no compare takes.  The reference's "last item k with p_k >= p_(k-1)"
-                // (p_0 = minFloat; none: the last item) is then p3 if p3 >= p2, else p2 if
-                // p2 >= p1, else p1 if p1 >= p0, else p0 (the first item alone, or -Inf).
+                // no compare takes.  With finite or -Inf weights (plainw) the reference's "last
+                // item k with p_k >= p_(k-1)" (p_0 = minFloat; none: the last item) is then p3
+                // if p3 >= p2, else p2 if p2 >= p1, else p1 if p1 >= p0, else p0 (the first item
+                // alone, or -Inf).  (With NaN weights no item qualifies and the reference takes
+                // the last one: the literal fold above.)
                 const uint32_t L0 = lw & 0xFFu, L1 = (lw >> 8) & 0xFFu, L2 = (lw >> 16) & 0xFFu, L3 = lw >> 24;
                 const double b0 = s.sbest[h + L0], b1 = s.sbest[h + L1], b2 = s.sbest[h + L2], b3 = s.sbest[h + L3];
                 auto sum = [&](uint32_t L, double w, double nb) {  // pieceProba (:519-529)
