@@ -60,3 +60,26 @@ def test_chain_fold_every_order(m):
     """Every order of the items' sums, ties and -Inf included."""
     for p in itertools.product([-4.0, -3.0, -2.0, -1.0, -INF], repeat=m):
         assert _same(reference(list(p)), chain_fold(p)), p
+
+
+def small_fold(p):
+    """k_small's branch-free step (plainw weights): the chosen item's index by nested
+    selects, p3 if p3 >= p2, else p2 if p2 >= p1, else p1 if p1 >= p0, else p0."""
+    p0, p1, p2, p3 = (list(p) + [NAN] * 4)[:4]
+    return 3 if p3 >= p2 else (2 if p2 >= p1 else (1 if p1 >= p0 else 0))
+
+
+@pytest.mark.parametrize("m", [1, 2, 3, 4])
+def test_small_fold_every_order(m):
+    """k_small's step picks the reference's item (index, hence length and value) on every
+    order of 1-4 finite or -Inf sums."""
+    for p in itertools.product([-4.0, -3.0, -2.0, -1.0, -INF], repeat=m):
+        assert O.max_index_proba(list(enumerate(p)))[0] == small_fold(p), p
+
+
+def test_small_fold_needs_plain_weights():
+    """With NaN sums (a dictionary of size <= 0) no item qualifies and the reference
+    takes the last one, which the nested form does not: k_small keeps the literal fold
+    for !plainw (jb_kernels.hip)."""
+    p = [NAN, NAN]
+    assert O.max_index_proba(list(enumerate(p)))[0] == 1 and small_fold(p) == 0
