@@ -680,6 +680,9 @@ static int init_launch_cfg(Device* d) {
     if (sm < 0 || sm > (int)kSmallBytes)
         return fail(JB_EINVAL, "JB_SMALL=%d: want 0 (off) .. %u bytes", sm, kSmallBytes);
     lc.small_max = (uint32_t)sm;
+    const int ls = env_int("JB_LONG_SPEC", 1);
+    if (ls < 0 || ls > 2) return fail(JB_EINVAL, "JB_LONG_SPEC=%d: want 0, 1 (or 2: testing)", ls);
+    lc.long_spec = (uint32_t)ls;
     const int ss = env_int("JB_SMALL_SLOTS", 4);
     if (ss < 1 || ss > 4) return fail(JB_EINVAL, "JB_SMALL_SLOTS=%d: want 1 .. 4", ss);
     d->small_slots = (uint32_t)ss;

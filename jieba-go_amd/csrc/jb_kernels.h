@@ -99,7 +99,7 @@ struct Work {
 // Kernel ids for per-launch timing.
 enum KernelId {
     K_DOCBITS = 0, K_MARK_WALK, K_ZH, K_NONZH,
-    K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_LONG_DP, K_LONG_SEG, K_LONG_PATH, K_LONG_TAIL, K_MASK_MERGE,
+    K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_LONG_SPEC, K_LONG_DP, K_LONG_SEG, K_LONG_PATH, K_LONG_TAIL, K_MASK_MERGE,
     K_NUM
 };
 extern const char* const kKernelNames[K_NUM];
@@ -121,6 +121,8 @@ struct LaunchCfg {
     uint32_t small_max; // host batches up to this many bytes take k_small (0: never)
     uint32_t zh_tail;        // k_zh: about this many bytes at the batch end go in smaller groups (0: none)
     uint32_t zh_tail_group;  // ... of this many bytes (a multiple of 32, at most the group size)
+    uint32_t long_spec;      // long blocks: speculative choices + decided chain (JB_LONG_SPEC: 1 default, 0 off,
+                             // 2 testing: some choices wrong on purpose, the exact chain redoes the block)
 };
 
 // k_zh's group split: g1 groups of grp bytes, then groups of *sgrp bytes to the end.

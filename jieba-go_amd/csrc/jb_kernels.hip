@@ -40,7 +40,7 @@
 namespace jb {
 
 const char* const kKernelNames[K_NUM] = {"k_docbits", "k_mark_walk", "k_zh", "k_nonzh", "k_tok_count", "k_scan_tok",
-                                         "k_tok_write", "k_doc_tok", "k_long_dp", "k_long_seg", "k_long_path",
+                                         "k_tok_write", "k_doc_tok", "k_long_spec", "k_long_dp", "k_long_seg", "k_long_path",
                                          "k_long_tail", "k_mask_merge"};
 
 // newJiebaHMM literals (tokenizer.go:629-652)
@@ -2205,12 +2205,29 @@ struct LItem {
     double w;
     uint32_t L, pad;
 };
+// c ? a : b for a mask c of all ones or zero, as two v_bfi_b32 (a select the compiler
+// keeps: it turns ternaries whose arms are loads into exec-mask branches)
+__device__ __forceinline__ double bitsel64(uint32_t m, double a, double b) {
+    const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+    uint32_t lo, hi;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(lo) : "v"(m), "v"((uint32_t)ua), "v"((uint32_t)ub));
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(hi) : "v"(m), "v"((uint32_t)(ua >> 32)), "v"((uint32_t)(ub >> 32)));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+struct LSpec {  // a rune's speculative choice (k_long_spec): the chosen item's weight and length
+    double w;
+    uint32_t L, pad;
+};
 struct LongLds {
     double ring[kLdRing];  // best(i) at i & 511
-    LDesc desc[kLdDesc];   // rune i at i & 1023
+    union {
+        LDesc desc[kLdDesc];   // rune i at i & 1023
+        LSpec spec[kLdDesc];   // (the decided chain)
+    };
     uint8_t cls[kLdDesc];  // rune i's step form: 0 items L = 1..m (m <= 4), 1 other fast forms, 3 slow
     LItem side[4][kLdSide];
-    uint32_t sidecnt[4], wslow[4];
+    uint32_t sidecnt[4], wslow[4], bad;
 };
 
 // DAG items (L, weight) of rune i of an all-3-byte block [bs, be), ascending L
@@ -2290,13 +2307,71 @@ __device__ __forceinline__ uint32_t long_block_of(const uint32_t* __restrict__ l
     return lo;
 }
 
+// k_long_spec: the speculative choices of the long blocks' runes, in parallel.
+// One lane per 64-rune segment (grid-stride; the lane's DP ring in LDS): the DP
+// of calcDagProba + maxIndexProba (:502-578) from kSpecOver runes past the
+// segment, where best is taken as 0.0 (a guess; at the block's end it is the
+// true best(n) = 0.0), down to the segment's first rune.  Past a few hundred
+// runes the choices no longer depend on the guess (config 5b: none differ at
+// 1024, 1.1 % at 64: tools/spec_sim.cpp).  For each rune of the segment it
+// writes the chosen length to gbl and the chosen item's weight to gbest, which
+// k_long_dp's decided chain turns into the exact best values and verifies.
+constexpr uint32_t kSpecOver = 1024;
+constexpr uint32_t kSpecRing = 256;  // > the longest edge (255 runes)
+constexpr uint32_t kSpecGrid = 256;  // 64-lane workgroups, one per CU (128 KB of LDS each)
+__global__ __launch_bounds__(64) void k_long_spec(const uint8_t* __restrict__ text, DevImage im,
+                                                  const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
+                                                  const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ counters,
+                                                  uint8_t* __restrict__ gbl, double* __restrict__ gbest, uint32_t mode) {
+    __shared__ double s_ring[kSpecRing][64];
+    const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG], lane = threadIdx.x;
+    if (!im.plainw) return;  // (k_long_dp runs the exact chain)
+    for (uint32_t g = blockIdx.x * 64u + lane; g < nseg; g += gridDim.x * 64u) {
+        const uint32_t bi = long_block_of(lsegb, nlong, g);
+        const uint2 bb = longblk[bi];
+        const uint32_t bs = bb.x, be = bb.y, n = (be - bs) / 3u, s0 = bs / 3u;
+        const uint32_t a = (g - lsegb[bi]) * kSeg, lim = min(a + kSeg, n), top = min(lim + kSpecOver, n);
+        double bnx = 0.0;  // speculative best(i + 1)
+        for (uint32_t i = top; i-- > a;) {
+            double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT, bestW = 0.0, lastW = 0.0;
+            uint32_t bestL = 0, lastL = 0;
+            long_items(text, im, erec, bs, be, i, [&](uint32_t L, double wt) {
+                const uint32_t j = i + L;
+                const double b = j >= top ? 0.0 : (L == 1u ? bnx : s_ring[j & (kSpecRing - 1u)][lane]);
+                const double pp = wt + b;
+                if (pp >= prevP) {
+                    bestL = L;
+                    bestP = pp;
+                    bestW = wt;
+                }
+                prevP = pp;
+                lastL = L;
+                lastW = wt;
+            });
+            if (bestL == 0) {  // no item qualified: the last item (or none)
+                bestL = lastL;
+                bestP = prevP;
+                bestW = lastW;
+            }
+            s_ring[i & (kSpecRing - 1u)][lane] = bestP;
+            bnx = bestP;
+            if (i < lim) {
+                // (mode 2, testing only: some choices made wrong on purpose, so that
+                // k_long_dp's verification and exact chain run)
+                gbl[s0 + i] = (uint8_t)(mode == 2u && i % 97u == 0u && bestL > 1u ? 1u : bestL);
+                gbest[s0 + i] = bestW;
+            }
+        }
+    }
+}
+
 template <bool HMM>
 __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ text, DevImage im,
                                                  const uint64_t* __restrict__ erec, uint8_t* __restrict__ gbl,
                                                  double* __restrict__ gbest, const uint2* __restrict__ longblk,
                                                  uint32_t* __restrict__ counters, uint32_t* __restrict__ sbits,
                                                  uint32_t* __restrict__ ebits, uint32_t* __restrict__ lflag,
-                                                 uint64_t* __restrict__ dbg) {
+                                                 uint64_t* __restrict__ dbg, uint32_t spec) {
     __shared__ LongLds S;
 #if JB_STAMPS
     uint64_t st_run = 0, st_bar = 0, st_n = 0, st_slow = 0;  // diagnostic clocks (wave 0 and wave 1, lane 0)
@@ -2330,6 +2405,133 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
         }
         const uint32_t n = (be - bs) / 3u, s0 = bs / 3u;  // rune i: bytes bs + 3i, slot s0 + i
         const int32_t J = (int32_t)((n + kLdWin - 1u) / kLdWin);  // windows; runes [n, 256 J) are dummies
+        if (spec && im.plainw) {
+            // ---- the decided chain: best(s) = w_D(s) + best(s + L_D(s)) from k_long_spec's
+            // choices (the reference's pieceProba add for the chosen item, :519-529), one add
+            // per rune on lane 0; the helper waves stage the choices two windows ahead and
+            // verify each finished window: every rune's choice by maxIndexProba over the
+            // exact values.  The rightmost wrong choice would be the first one found, and
+            // every value right of it is exact; any wrong choice sends the block to the exact
+            // chain below, which recomputes all of it. ----
+            if (tid == 0u) S.bad = 0u;
+            __syncthreads();
+            auto stage = [&](int32_t jw, uint32_t t, uint32_t nt) {
+                for (uint32_t r = t; r < kLdWin; r += nt) {
+                    const int32_t i = jw * (int32_t)kLdWin + (int32_t)r;
+                    LSpec& d = S.spec[(uint32_t)i & (kLdDesc - 1u)];
+                    const bool real = i >= 0 && (uint32_t)i < n;  // (past the block: best = 0.0 + best(i + 1) = 0.0)
+                    const uint32_t L = real ? (uint32_t)gbl[s0 + (uint32_t)i] : 1u;
+                    d.w = real ? gbest[s0 + (uint32_t)i] : 0.0;
+                    d.L = L ? L : 1u;
+                    if (L == 0u) S.bad = 1u;  // no item (the reference panics later): the exact chain
+                }
+            };
+            auto verify = [&](int32_t jv, uint32_t t, uint32_t nt) {
+                bool bad = false;
+                for (uint32_t r = t; r < kLdWin; r += nt) {
+                    const uint32_t i = (uint32_t)jv * kLdWin + r;
+                    if (i >= n) continue;
+                    DpFold f;
+                    long_items(text, im, erec, bs, be, i, [&](uint32_t L, double wt) {
+                        fold_item(f, L, wt + (i + L == n ? 0.0 : gbest[s0 + i + L]));
+                    });
+                    f.finish();
+                    bad |= f.bestL != S.spec[i & (kLdDesc - 1u)].L;
+                }
+                if (bad) S.bad = 1u;
+            };
+            stage(J - 1, tid, 256u);
+            stage(J - 2, tid, 256u);
+            if (tid == 0u) S.ring[n & (kLdRing - 1u)] = 0.0;  // best(n), when rune n is no dummy
+            __syncthreads();
+            if (wave == 0u) {
+                double H0 = 0.0, H1 = 0.0;  // best(s + 1), best(s + 2)
+                // a zero the compiler cannot see through: the choices stay in VGPRs and the
+                // selects on them stay selects (uniform, they became scalar branches: 288
+                // cycles per rune instead of one add and a few selects)
+                uint32_t dz;
+                asm volatile("v_mov_b32 %0, 0" : "=v"(dz));
+                for (int32_t j = J - 1; j >= 0; --j) {
+#if JB_STAMPS
+                    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
+                    if (lane == 0u) {
+                        for (int32_t g = (int32_t)kLdWin * j + (int32_t)kLdWin - 4; g >= (int32_t)kLdWin * j; g -= 4) {
+                            double w[4], rv[4];
+                            uint32_t L[4];
+#pragma unroll
+                            for (int r = 0; r < 4; r++) {
+                                const LSpec d = S.spec[((uint32_t)(g + r) & (kLdDesc - 1u)) + dz];
+                                w[r] = d.w;
+                                L[r] = d.L;
+                            }
+                            // best(s + L) for L >= 3 from the ring: runes g+3, g+2, g+1 read values of
+                            // earlier groups now, rune g after rune g+3 has written best(g+3).  Always
+                            // read, and taken by bit selects the compiler cannot turn into branches.
+#pragma unroll
+                            for (int r = 1; r < 4; r++)
+                                rv[r] = S.ring[((uint32_t)g + (uint32_t)r + L[r]) & (kLdRing - 1u)];
+#pragma unroll
+                            for (int u = 0; u < 4; u++) {
+                                const int r = 3 - u;
+                                const uint32_t s = (uint32_t)(g + r);
+                                if (u == 1) rv[0] = S.ring[((uint32_t)g + L[0]) & (kLdRing - 1u)];
+                                // (s + L == n needs no case: best(n..) are the dummies' 0.0, in the
+                                // ring and in H0/H1)
+                                const double b = bitsel64(L[r] == 1u ? ~0u : 0u, H0,
+                                                          bitsel64(L[r] == 2u ? ~0u : 0u, H1, rv[r]));
+                                const double P = w[r] + b;
+                                S.ring[s & (kLdRing - 1u)] = P;
+                                // (a dummy's 0.0 lands on rune n - 1 before rune n - 1's own value)
+                                gbest[s0 + min(s, n - 1u)] = P;
+                                H1 = H0;
+                                H0 = P;
+                            }
+                        }
+                    }
+#if JB_STAMPS
+                    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+#endif
+                    __syncthreads();
+#if JB_STAMPS
+                    st_run += t1 - t0;
+                    st_bar += __builtin_amdgcn_s_memtime() - t1;
+                    st_n++;
+#endif
+                }
+                __syncthreads();
+            } else {
+                const uint32_t ht = tid - 64u;
+                for (int32_t j = J - 1; j >= 0; --j) {
+#if JB_STAMPS
+                    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
+                    stage(j - 2, ht, 192u);
+                    if (j + 1 < J) verify(j + 1, ht, 192u);
+#if JB_STAMPS
+                    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+#endif
+                    __syncthreads();
+#if JB_STAMPS
+                    st_run += t1 - t0;
+                    st_bar += __builtin_amdgcn_s_memtime() - t1;
+                    st_n++;
+#endif
+                }
+                verify(0, ht, 192u);
+                __syncthreads();
+            }
+            const bool bad = S.bad != 0u;
+#if JB_STAMPS
+            st_slow += bad ? 1000000u : 0u;  // (a block sent to the exact chain)
+#endif
+            if (!bad) {
+                if (tid == 0u) lflag[bi] = 2u;  // DP done here; k_long_path sets 1 (entries found)
+                __syncthreads();
+                continue;
+            }
+            __syncthreads();  // (every thread has read S.bad: the exact chain below reuses the LDS)
+        }
         if (tid < 4u) {
             S.sidecnt[tid] = 0u;
             S.wslow[tid] = 0u;
@@ -3840,14 +4042,19 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         // nbytes / 192 + nbytes / kZhLongMin segments), one wave per block
         const uint64_t segs = nbytes / (3u * kSeg) + nbytes / kZhLongMin + 2u;
         const uint32_t gseg = (uint32_t)std::min<uint64_t>(1024u, (segs + 255u) / 256u);
+        const uint32_t spec = lc.long_spec ? 1u : 0u;
+        if (spec)
+            JB_TIMED(K_LONG_SPEC, hipLaunchKernelGGL(k_long_spec, dim3(kSpecGrid), dim3(64), 0, stream, d_text, im,
+                                                     w.erec + kErecPad, w.longblk, w.lsegb, w.counters, w.gbl, w.gbest,
+                                                     lc.long_spec));
         if (hmm)
             JB_TIMED(K_LONG_DP, hipLaunchKernelGGL((k_long_dp<true>), dim3(kLongGrid), dim3(256), 0, stream, d_text, im,
                                                    w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters, w.sbits,
-                                                   w.ebits, w.lflag, w.dbg));
+                                                   w.ebits, w.lflag, w.dbg, spec));
         else
             JB_TIMED(K_LONG_DP, hipLaunchKernelGGL((k_long_dp<false>), dim3(kLongGrid), dim3(256), 0, stream, d_text, im,
                                                    w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters, w.sbits,
-                                                   w.ebits, w.lflag, w.dbg));
+                                                   w.ebits, w.lflag, w.dbg, spec));
         JB_TIMED(K_LONG_SEG, hipLaunchKernelGGL(k_long_seg, dim3(gseg), dim3(256), 0, stream, d_text, im,
                                                 w.erec + kErecPad, w.longblk, w.lsegb, w.counters, w.lflag, w.gbest,
                                                 w.gbl, w.lbp));

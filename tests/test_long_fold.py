@@ -83,3 +83,83 @@ def test_small_fold_needs_plain_weights():
     for !plainw (jb_kernels.hip)."""
     p = [NAN, NAN]
     assert O.max_index_proba(list(enumerate(p)))[0] == 1 and small_fold(p) == 0
+
+
+def _dag(rng, n):
+    """Per rune, items (L, weight) in length order; L = 1 always present (plainw)."""
+    dag = []
+    for i in range(n):
+        its = [(1, -rng.uniform(5.0, 15.0))]
+        for L in range(2, min(9, n - i + 1)):
+            if rng.random() < 0.3:
+                its.append((L, -rng.uniform(5.0, 20.0)))
+        dag.append(its)
+    return dag
+
+
+def _fold(items, best, n):
+    """maxIndexProba over pieceProba = w + best(i + L) (tokenizer.go:519-578), as the
+    oracle does: the chosen (L, w)."""
+    pr = [(L, w + (0.0 if L == 0 else best[L])) for L, w in items]
+    k, _ = O.max_index_proba([(j, p) for j, (_, p) in enumerate(pr)])
+    return items[k]
+
+
+def _exact(dag, n):
+    best = [0.0] * (n + 1)
+    for i in range(n - 1, -1, -1):
+        L, w = _fold(dag[i], {L: best[i + L] for L, _ in dag[i]}, n)
+        best[i] = w + best[i + L]
+    return best
+
+
+def _spec(dag, n, seg, over):
+    """k_long_spec: per segment, the DP from `over` runes past it with best = 0.0 there."""
+    ch = [None] * n
+    for a in range(0, n, seg):
+        lim, top = min(a + seg, n), min(a + seg + over, n)
+        b = {top: 0.0}
+        for i in range(top - 1, a - 1, -1):
+            L, w = _fold(dag[i], {L: (0.0 if i + L >= top else b[i + L]) for L, _ in dag[i]}, n)
+            b[i] = w + (0.0 if i + L >= top else b[i + L])
+            if i < lim:
+                ch[i] = (L, w)
+    return ch
+
+
+def _decided(dag, ch, n):
+    """k_long_dp's decided chain (one add per rune), then the helpers' verification:
+    every rune's choice by the rule over the chain's values."""
+    best = [0.0] * (n + 1)
+    for i in range(n - 1, -1, -1):
+        L, w = ch[i]
+        best[i] = w + best[i + L]
+    ok = all(_fold(dag[i], {L: best[i + L] for L, _ in dag[i]}, n)[0] == ch[i][0] for i in range(n))
+    return best, ok
+
+
+@pytest.mark.parametrize("over", [0, 4, 64])
+def test_decided_chain_is_exact_when_verified(over):
+    """Decide-add-verify (k_long_spec + k_long_dp's decided chain): when every choice
+    passes the rule over the added values, the values are the exact DP's bit for bit
+    (same adds, same operands); a wrong choice never passes.  With a short overlap the
+    guesses go wrong and the block takes the exact chain."""
+    rng = random.Random(7 + over)
+    seen_ok = seen_bad = 0
+    for _ in range(6):
+        n = rng.randint(50, 400)
+        dag = _dag(rng, n)
+        exact = _exact(dag, n)
+        ch = _spec(dag, n, 16, over)
+        best, ok = _decided(dag, ch, n)
+        right = all(ch[i][0] == _fold(dag[i], {L: exact[i + L] for L, _ in dag[i]}, n)[0] for i in range(n))
+        assert ok == right
+        if ok:
+            assert best == exact
+            seen_ok += 1
+        else:
+            seen_bad += 1
+    if over == 64:
+        assert seen_ok
+    if over == 0:
+        assert seen_bad
