@@ -2215,15 +2215,23 @@ __device__ __forceinline__ double bitsel64(uint32_t m, double a, double b) {
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
-struct LSpec {  // a rune's speculative choice (k_long_spec): the chosen item's weight and length
-    double w;
-    uint32_t L, pad;
+struct LSpec {  // a rune's speculative choice (k_long_spec) as the decided chain takes it
+    double w;     // the chosen item's weight
+    uint32_t ra;  // byte offset in dring of best(i + L)
+    uint32_t m1;  // all ones if L is 1
 };
+struct LDecided {  // the decided chain's LDS (rune i at i & 1023)
+    LSpec spec[kLdDesc];
+    double dring[kLdDesc];  // best(i): the chain writes, the helpers verify and publish
+    uint32_t m2[kLdDesc];   // all ones if L is 2
+    uint32_t L[kLdDesc];    // the chosen length (verification)
+};
+constexpr uint32_t kSpWin = 192;  // the decided chain's window: 48 groups, 16 loop trips
 struct LongLds {
     double ring[kLdRing];  // best(i) at i & 511
     union {
         LDesc desc[kLdDesc];   // rune i at i & 1023
-        LSpec spec[kLdDesc];   // (the decided chain)
+        LDecided dc;           // (the decided chain)
     };
     uint8_t cls[kLdDesc];  // rune i's step form: 0 items L = 1..m (m <= 4), 1 other fast forms, 3 slow
     LItem side[4][kLdSide];
@@ -2413,80 +2421,118 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
             // exact values.  The rightmost wrong choice would be the first one found, and
             // every value right of it is exact; any wrong choice sends the block to the exact
             // chain below, which recomputes all of it. ----
+            const int32_t Jd = (int32_t)((n + kSpWin - 1u) / kSpWin);  // windows; runes [n, 192 Jd) are dummies
             if (tid == 0u) S.bad = 0u;
             __syncthreads();
             auto stage = [&](int32_t jw, uint32_t t, uint32_t nt) {
-                for (uint32_t r = t; r < kLdWin; r += nt) {
-                    const int32_t i = jw * (int32_t)kLdWin + (int32_t)r;
-                    LSpec& d = S.spec[(uint32_t)i & (kLdDesc - 1u)];
+                for (uint32_t r = t; r < kSpWin; r += nt) {
+                    const int32_t i = jw * (int32_t)kSpWin + (int32_t)r;
+                    const uint32_t k = (uint32_t)i & (kLdDesc - 1u);
                     const bool real = i >= 0 && (uint32_t)i < n;  // (past the block: best = 0.0 + best(i + 1) = 0.0)
-                    const uint32_t L = real ? (uint32_t)gbl[s0 + (uint32_t)i] : 1u;
-                    d.w = real ? gbest[s0 + (uint32_t)i] : 0.0;
-                    d.L = L ? L : 1u;
-                    if (L == 0u) S.bad = 1u;  // no item (the reference panics later): the exact chain
+                    uint32_t L = real ? (uint32_t)gbl[s0 + (uint32_t)i] : 1u;
+                    if (L == 0u) {  // no item (the reference panics later): the exact chain
+                        S.bad = 1u;
+                        L = 1u;
+                    }
+                    S.dc.spec[k].w = real ? gbest[s0 + (uint32_t)i] : 0.0;
+                    S.dc.spec[k].ra = (((uint32_t)i + L) & (kLdDesc - 1u)) * 8u;
+                    S.dc.spec[k].m1 = L == 1u ? ~0u : 0u;
+                    S.dc.m2[k] = L == 2u ? ~0u : 0u;
+                    S.dc.L[k] = L;
                 }
             };
+            // every rune's choice by maxIndexProba over the exact values; then the window's
+            // values go to gbest (k_long_seg, k_long_path read them)
             auto verify = [&](int32_t jv, uint32_t t, uint32_t nt) {
                 bool bad = false;
-                for (uint32_t r = t; r < kLdWin; r += nt) {
-                    const uint32_t i = (uint32_t)jv * kLdWin + r;
+                for (uint32_t r = t; r < kSpWin; r += nt) {
+                    const uint32_t i = (uint32_t)jv * kSpWin + r;
                     if (i >= n) continue;
                     DpFold f;
                     long_items(text, im, erec, bs, be, i, [&](uint32_t L, double wt) {
-                        fold_item(f, L, wt + (i + L == n ? 0.0 : gbest[s0 + i + L]));
+                        fold_item(f, L, wt + (i + L == n ? 0.0 : S.dc.dring[(i + L) & (kLdDesc - 1u)]));
                     });
                     f.finish();
-                    bad |= f.bestL != S.spec[i & (kLdDesc - 1u)].L;
+                    bad |= f.bestL != S.dc.L[i & (kLdDesc - 1u)];
+                    gbest[s0 + i] = S.dc.dring[i & (kLdDesc - 1u)];
                 }
                 if (bad) S.bad = 1u;
             };
-            stage(J - 1, tid, 256u);
-            stage(J - 2, tid, 256u);
-            if (tid == 0u) S.ring[n & (kLdRing - 1u)] = 0.0;  // best(n), when rune n is no dummy
+            stage(Jd - 1, tid, 256u);
+            stage(Jd - 2, tid, 256u);
+            if (tid == 0u) S.dc.dring[n & (kLdDesc - 1u)] = 0.0;  // best(n), when rune n is no dummy
             __syncthreads();
             if (wave == 0u) {
-                double H0 = 0.0, H1 = 0.0;  // best(s + 1), best(s + 2)
-                // a zero the compiler cannot see through: the choices stay in VGPRs and the
-                // selects on them stay selects (uniform, they became scalar branches: 288
-                // cycles per rune instead of one add and a few selects)
+                // best(s + 1), best(s + 2) in registers; best(s + L) for L >= 3 from dring, read
+                // three runes ahead (right after rune s + 3 is written: LDS accesses of a wave
+                // complete in order).  A group's choices are loaded a group ahead of their first
+                // use, into one of three register sets (three groups per loop trip, so the sets
+                // rotate without copies).  Values are taken by bit selects, which the compiler
+                // cannot turn into branches.  Per rune: four v_bfi_b32, one v_add_f64, one LDS
+                // write and one LDS read.
+                double H0 = 0.0, H1 = 0.0;
+                // a zero the compiler cannot see through: the choices stay in VGPRs (uniform,
+                // the compiler moved them to SGPRs and branched on them: 288 cycles per rune)
                 uint32_t dz;
                 asm volatile("v_mov_b32 %0, 0" : "=v"(dz));
-                for (int32_t j = J - 1; j >= 0; --j) {
+                const char* const ringb = reinterpret_cast<const char*>(S.dc.dring);
+                for (int32_t j = Jd - 1; j >= 0; --j) {
 #if JB_STAMPS
                     const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
                     if (lane == 0u) {
-                        for (int32_t g = (int32_t)kLdWin * j + (int32_t)kLdWin - 4; g >= (int32_t)kLdWin * j; g -= 4) {
-                            double w[4], rv[4];
-                            uint32_t L[4];
+                        struct Set {
+                            double w[4];
+                            uint32_t ra[4], m1[4], m2[4];
+                        };
+                        auto load = [&](Set& X, uint32_t g) {
+                            const uint32_t k = (g & (kLdDesc - 1u)) + dz;  // (g: a multiple of 4)
 #pragma unroll
                             for (int r = 0; r < 4; r++) {
-                                const LSpec d = S.spec[((uint32_t)(g + r) & (kLdDesc - 1u)) + dz];
-                                w[r] = d.w;
-                                L[r] = d.L;
+                                const LSpec d = S.dc.spec[k + (uint32_t)r];
+                                X.w[r] = d.w;
+                                X.ra[r] = d.ra;
+                                X.m1[r] = d.m1;
                             }
-                            // best(s + L) for L >= 3 from the ring: runes g+3, g+2, g+1 read values of
-                            // earlier groups now, rune g after rune g+3 has written best(g+3).  Always
-                            // read, and taken by bit selects the compiler cannot turn into branches.
-#pragma unroll
-                            for (int r = 1; r < 4; r++)
-                                rv[r] = S.ring[((uint32_t)g + (uint32_t)r + L[r]) & (kLdRing - 1u)];
+                            const uint4 m2 = *reinterpret_cast<const uint4*>(&S.dc.m2[k]);
+                            X.m2[0] = m2.x;
+                            X.m2[1] = m2.y;
+                            X.m2[2] = m2.z;
+                            X.m2[3] = m2.w;
+                        };
+                        double rv[4];  // best(s + L) of rune s at index s & 3
+                        // group g from set X (the ring reads of the next group from set Y); set Z
+                        // loaded for the group after the next
+                        auto group = [&](const Set& X, const Set& Y, Set& Z, uint32_t g) {
+                            load(Z, g - 8u);
+                            __builtin_amdgcn_sched_barrier(0);
+                            double* const rg = &S.dc.dring[g & (kLdDesc - 1u)];  // (g + 3 does not wrap)
 #pragma unroll
                             for (int u = 0; u < 4; u++) {
                                 const int r = 3 - u;
-                                const uint32_t s = (uint32_t)(g + r);
-                                if (u == 1) rv[0] = S.ring[((uint32_t)g + L[0]) & (kLdRing - 1u)];
-                                // (s + L == n needs no case: best(n..) are the dummies' 0.0, in the
-                                // ring and in H0/H1)
-                                const double b = bitsel64(L[r] == 1u ? ~0u : 0u, H0,
-                                                          bitsel64(L[r] == 2u ? ~0u : 0u, H1, rv[r]));
-                                const double P = w[r] + b;
-                                S.ring[s & (kLdRing - 1u)] = P;
-                                // (a dummy's 0.0 lands on rune n - 1 before rune n - 1's own value)
-                                gbest[s0 + min(s, n - 1u)] = P;
+                                const double b = bitsel64(X.m1[r], H0, bitsel64(X.m2[r], H1, rv[r]));
+                                const double P = X.w[r] + b;
+                                rg[r] = P;
+                                // rune g + r - 3: g from X, g - 1 .. g - 3 from Y
+                                rv[(r + 1) & 3] = *reinterpret_cast<const double*>(ringb + (r == 3 ? X.ra[0] : Y.ra[r + 1]));
                                 H1 = H0;
                                 H0 = P;
+                                // (the scheduler sank the ring reads to their use, a full LDS
+                                // round trip per rune; keep them here)
+                                __builtin_amdgcn_sched_barrier(0);
                             }
+                        };
+                        const uint32_t top = kSpWin * (uint32_t)j + kSpWin;
+                        Set A, B, C;
+                        load(A, top - 4u);
+                        load(B, top - 8u);
+#pragma unroll
+                        for (int r = 1; r < 4; r++) rv[r] = *reinterpret_cast<const double*>(ringb + A.ra[r]);
+                        uint32_t g = top - 4u;
+                        for (uint32_t t = 0; t < kSpWin / 12u; t++, g -= 12u) {
+                            group(A, B, C, g);
+                            group(B, C, A, g - 4u);
+                            group(C, A, B, g - 8u);
                         }
                     }
 #if JB_STAMPS
@@ -2502,12 +2548,12 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                 __syncthreads();
             } else {
                 const uint32_t ht = tid - 64u;
-                for (int32_t j = J - 1; j >= 0; --j) {
+                for (int32_t j = Jd - 1; j >= 0; --j) {
 #if JB_STAMPS
                     const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
                     stage(j - 2, ht, 192u);
-                    if (j + 1 < J) verify(j + 1, ht, 192u);
+                    if (j + 1 < Jd) verify(j + 1, ht, 192u);
 #if JB_STAMPS
                     const uint64_t t1 = __builtin_amdgcn_s_memtime();
 #endif
