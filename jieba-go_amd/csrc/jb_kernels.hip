@@ -2464,13 +2464,16 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
             __syncthreads();
             if (wave == 0u) {
                 // best(s + 1), best(s + 2) in registers; best(s + L) for L >= 3 from dring, read
-                // three runes ahead (right after rune s + 3 is written: LDS accesses of a wave
+                // two to three runes ahead (right after rune s + 3 is written: LDS accesses of a wave
                 // complete in order).  A group's choices are loaded a group ahead of their first
                 // use, into one of three register sets (three groups per loop trip, so the sets
                 // rotate without copies).  Values are taken by bit selects, which the compiler
                 // cannot turn into branches.  Per rune: four v_bfi_b32, one v_add_f64, one LDS
                 // write and one LDS read.
-                double H0 = 0.0, H1 = 0.0;
+                double H0 = 0.0;  // best(s + 1)
+                // the next rune's L = 2 / L >= 3 select, made one step ahead (the window's top
+                // rune takes L = 1: a dummy, or rune n - 1)
+                double inner = 0.0;
                 // a zero the compiler cannot see through: the choices stay in VGPRs (uniform,
                 // the compiler moved them to SGPRs and branched on them: 288 cycles per rune)
                 uint32_t dz;
@@ -2510,15 +2513,17 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
 #pragma unroll
                             for (int u = 0; u < 4; u++) {
                                 const int r = 3 - u;
-                                const double b = bitsel64(X.m1[r], H0, bitsel64(X.m2[r], H1, rv[r]));
+                                const double b = bitsel64(X.m1[r], H0, inner);
                                 const double P = X.w[r] + b;
+                                __builtin_amdgcn_sched_barrier(0);
+                                // the inner select of rune g + r - 1 (its best(s + 2) is H0 now),
+                                // while the add is in flight
+                                inner = r ? bitsel64(X.m2[r - 1], H0, rv[r - 1]) : bitsel64(Y.m2[3], H0, rv[3]);
+                                __builtin_amdgcn_sched_barrier(0);
                                 rg[r] = P;
                                 // rune g + r - 3: g from X, g - 1 .. g - 3 from Y
                                 rv[(r + 1) & 3] = *reinterpret_cast<const double*>(ringb + (r == 3 ? X.ra[0] : Y.ra[r + 1]));
-                                H1 = H0;
                                 H0 = P;
-                                // (the scheduler sank the ring reads to their use, a full LDS
-                                // round trip per rune; keep them here)
                                 __builtin_amdgcn_sched_barrier(0);
                             }
                         };
