@@ -2221,12 +2221,12 @@ struct LSpec {  // a rune's speculative choice (k_long_spec) as the decided chai
     uint32_t m1;  // all ones if L is 1
 };
 struct LDecided {  // the decided chain's LDS (rune i at i & 1023)
-    LSpec spec[kLdDesc];
+    LSpec spec[16 + kLdDesc];  // (rune i at 16 + (i & 1023): the chain's prefetch past a window reads the 16 below)
     double dring[kLdDesc];  // best(i): the chain writes, the helpers verify and publish
-    uint32_t m2[kLdDesc];   // all ones if L is 2
+    uint32_t m2[16 + kLdDesc];  // all ones if L is 2 (as spec)
     uint32_t L[kLdDesc];    // the chosen length (verification)
 };
-constexpr uint32_t kSpWin = 192;  // the decided chain's window: 48 groups, 16 loop trips
+constexpr uint32_t kSpWin = 256;  // the decided chain's window (ring slots (j & 3) * 256 ..: no wrap inside): 16 loop trips of 4 groups
 struct LongLds {
     double ring[kLdRing];  // best(i) at i & 511
     union {
@@ -2434,10 +2434,10 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                         S.bad = 1u;
                         L = 1u;
                     }
-                    S.dc.spec[k].w = real ? gbest[s0 + (uint32_t)i] : 0.0;
-                    S.dc.spec[k].ra = (((uint32_t)i + L) & (kLdDesc - 1u)) * 8u;
-                    S.dc.spec[k].m1 = L == 1u ? ~0u : 0u;
-                    S.dc.m2[k] = L == 2u ? ~0u : 0u;
+                    S.dc.spec[16u + k].w = real ? gbest[s0 + (uint32_t)i] : 0.0;
+                    S.dc.spec[16u + k].ra = (((uint32_t)i + L) & (kLdDesc - 1u)) * 8u;
+                    S.dc.spec[16u + k].m1 = L == 1u ? ~0u : 0u;
+                    S.dc.m2[16u + k] = L == 2u ? ~0u : 0u;
                     S.dc.L[k] = L;
                 }
             };
@@ -2465,15 +2465,14 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
             if (wave == 0u) {
                 // best(s + 1), best(s + 2) in registers; best(s + L) for L >= 3 from dring, read
                 // two to three runes ahead (right after rune s + 3 is written: LDS accesses of a wave
-                // complete in order).  A group's choices are loaded a group ahead of their first
-                // use, into one of three register sets (three groups per loop trip, so the sets
-                // rotate without copies).  Values are taken by bit selects, which the compiler
-                // cannot turn into branches.  Per rune: four v_bfi_b32, one v_add_f64, one LDS
-                // write and one LDS read.
-                double H0 = 0.0;  // best(s + 1)
-                // the next rune's L = 2 / L >= 3 select, made one step ahead (the window's top
-                // rune takes L = 1: a dummy, or rune n - 1)
-                double inner = 0.0;
+                // complete in order).  A group's choices are loaded three groups ahead into one of
+                // four register sets (four groups per loop trip, so the sets rotate without
+                // copies); a window's slots do not wrap, so a trip's loads and stores are one base
+                // address and immediate offsets.  Values are taken by bit selects, which the
+                // compiler cannot turn into branches.  Per rune: four v_bfi_b32, one v_add_f64,
+                // one LDS write and one LDS read.
+                double H0 = 0.0, H1 = 0.0;  // best(s + 1), best(s + 2)
+                double inner = 0.0;  // the next rune's L = 2 / L >= 3 select, made one step ahead
                 // a zero the compiler cannot see through: the choices stay in VGPRs (uniform,
                 // the compiler moved them to SGPRs and branched on them: 288 cycles per rune)
                 uint32_t dz;
@@ -2488,56 +2487,63 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                             double w[4];
                             uint32_t ra[4], m1[4], m2[4];
                         };
-                        auto load = [&](Set& X, uint32_t g) {
-                            const uint32_t k = (g & (kLdDesc - 1u)) + dz;  // (g: a multiple of 4)
+                        const uint32_t kwin = ((uint32_t)j & 3u) * kSpWin;  // the window's first slot
+                        const LSpec* const sp = S.dc.spec + (16u + kwin + dz);
+                        const uint32_t* const mp = S.dc.m2 + (16u + kwin + dz);
+                        double* const rw = S.dc.dring + kwin;
+                        // the group at window offset p (a multiple of 4, >= -16)
+                        auto load = [&](Set& X, int32_t p) {
 #pragma unroll
                             for (int r = 0; r < 4; r++) {
-                                const LSpec d = S.dc.spec[k + (uint32_t)r];
+                                const LSpec d = sp[p + r];
                                 X.w[r] = d.w;
                                 X.ra[r] = d.ra;
                                 X.m1[r] = d.m1;
                             }
-                            const uint4 m2 = *reinterpret_cast<const uint4*>(&S.dc.m2[k]);
+                            const uint4 m2 = *reinterpret_cast<const uint4*>(mp + p);
                             X.m2[0] = m2.x;
                             X.m2[1] = m2.y;
                             X.m2[2] = m2.z;
                             X.m2[3] = m2.w;
                         };
                         double rv[4];  // best(s + L) of rune s at index s & 3
-                        // group g from set X (the ring reads of the next group from set Y); set Z
-                        // loaded for the group after the next
-                        auto group = [&](const Set& X, const Set& Y, Set& Z, uint32_t g) {
-                            load(Z, g - 8u);
+                        // group p from set X (the ring reads of the next group from set Y); set Z
+                        // (the last group's) loaded for the group three ahead
+                        auto group = [&](const Set& X, const Set& Y, Set& Z, int32_t p) {
+                            load(Z, p - 12);
                             __builtin_amdgcn_sched_barrier(0);
-                            double* const rg = &S.dc.dring[g & (kLdDesc - 1u)];  // (g + 3 does not wrap)
 #pragma unroll
                             for (int u = 0; u < 4; u++) {
                                 const int r = 3 - u;
                                 const double b = bitsel64(X.m1[r], H0, inner);
                                 const double P = X.w[r] + b;
                                 __builtin_amdgcn_sched_barrier(0);
-                                // the inner select of rune g + r - 1 (its best(s + 2) is H0 now),
+                                // the inner select of rune p + r - 1 (its best(s + 2) is H0 now),
                                 // while the add is in flight
                                 inner = r ? bitsel64(X.m2[r - 1], H0, rv[r - 1]) : bitsel64(Y.m2[3], H0, rv[3]);
                                 __builtin_amdgcn_sched_barrier(0);
-                                rg[r] = P;
-                                // rune g + r - 3: g from X, g - 1 .. g - 3 from Y
+                                rw[p + r] = P;
+                                // rune p + r - 3: p from X, p - 1 .. p - 3 from Y
                                 rv[(r + 1) & 3] = *reinterpret_cast<const double*>(ringb + (r == 3 ? X.ra[0] : Y.ra[r + 1]));
+                                H1 = H0;
                                 H0 = P;
                                 __builtin_amdgcn_sched_barrier(0);
                             }
                         };
-                        const uint32_t top = kSpWin * (uint32_t)j + kSpWin;
-                        Set A, B, C;
-                        load(A, top - 4u);
-                        load(B, top - 8u);
+                        Set A, B, C, D;
+                        const int32_t top = (int32_t)kSpWin;
+                        load(A, top - 4);
+                        load(B, top - 8);
+                        load(C, top - 12);
 #pragma unroll
                         for (int r = 1; r < 4; r++) rv[r] = *reinterpret_cast<const double*>(ringb + A.ra[r]);
-                        uint32_t g = top - 4u;
-                        for (uint32_t t = 0; t < kSpWin / 12u; t++, g -= 12u) {
-                            group(A, B, C, g);
-                            group(B, C, A, g - 4u);
-                            group(C, A, B, g - 8u);
+                        // (the window's top rune: a dummy or rune n - 1, L = 1, in the top window)
+                        inner = bitsel64(A.m2[3], H1, rv[3]);
+                        for (int32_t p = top - 4; p > 0; p -= 16) {
+                            group(A, B, D, p);
+                            group(B, C, A, p - 4);
+                            group(C, D, B, p - 8);
+                            group(D, A, C, p - 12);
                         }
                     }
 #if JB_STAMPS
