@@ -2516,11 +2516,12 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                             for (int u = 0; u < 4; u++) {
                                 const int r = 3 - u;
                                 const double b = bitsel64(X.m1[r], H0, inner);
-                                const double P = X.w[r] + b;
-                                __builtin_amdgcn_sched_barrier(0);
-                                // the inner select of rune p + r - 1 (its best(s + 2) is H0 now),
-                                // while the add is in flight
+                                // the inner select of rune p + r - 1 (its best(s + 2) is H0 now)
+                                // between this rune's select and add (after the add instead, a
+                                // hazard s_nop per rune and 5.8 % slower: profiles/ab/r04z6_chain_order_ab.txt)
                                 inner = r ? bitsel64(X.m2[r - 1], H0, rv[r - 1]) : bitsel64(Y.m2[3], H0, rv[3]);
+                                __builtin_amdgcn_sched_barrier(0);
+                                const double P = X.w[r] + b;
                                 __builtin_amdgcn_sched_barrier(0);
                                 rw[p + r] = P;
                                 // rune p + r - 3: p from X, p - 1 .. p - 3 from Y
