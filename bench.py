@@ -265,23 +265,47 @@ def job_sums(dist, agg_dev, vals, op="sum"):
     return [float(x) for x in t.tolist()]
 
 
-def roofline_of(kernels, units, traffic_of):
-    """Algorithmic bytes: 1 B read per byte of a kernel's units +
-    2 output bits per byte = 1.25 B per unit byte.  Units: every input byte for
-    k_mark_walk (it classifies and walks the whole batch), the Han bytes for
-    k_zh / k_long_dp (DP + Viterbi over zh blocks)."""
+# The timed step's output (jb_cut_device): u32 (start, end) spans, 8 B per token
+# ("with (start,end) uint32 spans: 8 B x tokens").
+OUTPUT_FORMAT = "u32 (start, end) token spans, 8 B per token"
+SPAN_BYTES = 8
+
+
+def alg_bytes_per_byte(step_bytes, step_tokens):
+    """SURVEY.md §8d's algorithmic bytes per input byte of the timed step: 1 B read
+    + the output written, here the spans (8 B per token) spread over the input bytes."""
+    return 1.0 + SPAN_BYTES * step_tokens / step_bytes if step_bytes else 1.0
+
+
+def roofline_of(kernels, units, traffic_of, per_byte):
+    """Per kernel: algorithmic bytes per launch = `per_byte` (alg_bytes_per_byte of the
+    step) x the unit bytes the launch processes, over its average launch time.  Units:
+    every input byte for k_mark_walk (it classifies and walks the whole batch), the Han
+    bytes for k_zh / k_long_dp (DP + Viterbi over zh blocks)."""
     out = {}
     for kname, u in units.items():
         kk = kernels.get(kname)
         if not kk or not u:
             continue
-        alg = 1.25 * u
+        alg = per_byte * u
         achieved = alg / (kk["avg_ms"] * 1e-3) / 1e9
         out[kname] = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic_of(kname),
-                      "kernel": kname, "alg_bytes_per_launch": alg, "avg_launch_ms": kk["avg_ms"],
+                      "kernel": kname, "output_format": OUTPUT_FORMAT, "alg_bytes_per_unit_byte": round(per_byte, 5),
+                      "alg_bytes_per_launch": alg, "avg_launch_ms": kk["avg_ms"],
                       "frac_of_measured_copy": round(achieved / HBM_MEASURED_GBS, 5)}
     return out
+
+
+def roofline_step(step_bytes, step_tokens, ms_per_step):
+    """The whole timed step against HBM: its algorithmic bytes (input read + spans
+    written) over ms_per_step."""
+    alg = step_bytes + SPAN_BYTES * step_tokens
+    achieved = alg / (ms_per_step * 1e-3) / 1e9 if ms_per_step else 0.0
+    return {"bound": "hbm", "output_format": OUTPUT_FORMAT, "alg_bytes_per_step": int(alg),
+            "input_bytes": int(step_bytes), "tokens": int(step_tokens), "ms_per_step": ms_per_step,
+            "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5)}
 
 
 def run(args, world, rank, dist, agg_dev, make_cutter, open_oracle, log=print):
@@ -322,6 +346,7 @@ def run(args, world, rank, dist, agg_dev, make_cutter, open_oracle, log=print):
         dist.barrier()
     results = cutter.results()
     ties = cutter.ties()
+    ntok = int(len(results[0]))
 
     kprof, prof_ms = ({}, None) if args.no_profile else cutter.profile(args.steps)
     kernels = {k: {"avg_ms": ms / n, "launches": int(n)} for k, (ms, n) in kprof.items() if n}
@@ -341,8 +366,18 @@ def run(args, world, rank, dist, agg_dev, make_cutter, open_oracle, log=print):
     sums = job_sums(dist, agg_dev, [nrunes, nbytes, hbytes, len(soff) - 1, ties,
                                     par["mismatches"] if par else 0, par["tokens"] if par else 0,
                                     0 if par is None else (0 if par["ok"] else 1),
-                                    par["oracle_ties"] if par else 0])
-    tot_runes, tot_bytes, tot_han, tot_docs, tot_ties, tot_mism, tot_tok, bad_ranks, tot_oties = sums
+                                    par["oracle_ties"] if par else 0, ntok])
+    tot_runes, tot_bytes, tot_han, tot_docs, tot_ties, tot_mism, tot_tok, bad_ranks, tot_oties, tot_gtok = sums
+    # every rank's own numbers (an N > 1 line shows a straggler)
+    mine = {"rank": rank, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
+            "shard_bytes": nbytes, "shard_docs": len(soff) - 1, "shard_chars": nrunes, "first_doc": d0,
+            "tokens": ntok, "bit_exact": None if par is None else par["ok"]}
+    if dist is not None and world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+    else:
+        per_rank = [mine]
 
     cpu = None
     if rank == 0 and world == 1 and par is not None:
@@ -370,7 +405,7 @@ def run(args, world, rank, dist, agg_dev, make_cutter, open_oracle, log=print):
     if args.workload == "long-oov":  # one unpunctuated block: its Han bytes all go through the k_long_* chain
         units["k_long_dp"] = float(hbytes)
     wkey = f"{args.workload}:{nbytes}:{'hmm' if args.hmm else 'nohmm'}:{args.dict_kind}"
-    rooflines = roofline_of(kernels, units, lambda k: load_pmc_traffic(k, wkey))
+    rooflines = roofline_of(kernels, units, lambda k: load_pmc_traffic(k, wkey), alg_bytes_per_byte(nbytes, ntok))
     roof = None
     if kernels:
         dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
@@ -395,9 +430,11 @@ def run(args, world, rank, dist, agg_dev, make_cutter, open_oracle, log=print):
                                f"{'NewJiebaTokenizer (prefix dict, size 60,101,967)' if args.dict_kind == 'prefix' else 'NewTokenizer(dict.txt)'}",
                    "corpus_bytes": int(tot_bytes), "corpus_chars": int(tot_runes), "corpus_han_bytes": int(tot_han),
                    "corpus_docs": int(tot_docs), "rank0_shard_bytes": nbytes, "dict_words": s.nwords,
-                   "parallelism": f"doc-shard x{world} (byte-balanced contiguous ranges), no collectives"},
+                   "parallelism": f"doc-shard x{world} (byte-balanced contiguous ranges), no collectives",
+                   "per_rank": per_rank},
         "roofline": roof,
         "roofline_kernels": rooflines,
+        "roofline_step": roofline_step(tot_bytes, tot_gtok, ms_per_step),
         "cpu_baseline": cpu,
         "parity": parity,
         "viterbi_ties": {"gpu": int(tot_ties), "oracle": int(tot_oties) if par else None,
@@ -763,7 +800,8 @@ def main(argv=None):
         line, (sbuf, soff, _) = out
         launcher = os.environ.get("JB_BENCH_LAUNCHER") or ("torch.distributed.run" if world > 1 else "single process")
         line["config"]["ranks"] = {"launcher": launcher, "processes": world, "rank_to_gpu": "rank r -> GPU r",
-                                   "host_group": "gloo (timing barriers + job sums; no RCCL)" if world > 1 else None}
+                                   "host_group": "gloo (timing barriers + job sums; no RCCL)" if world > 1 else None,
+                                   "per_rank": line["config"].pop("per_rank")}
         if share_gpu():
             line["config"]["ranks"]["rank_to_gpu"] = "TEST (JB_BENCH_SHARE_GPU): rank r -> GPU r mod the GPUs visible"
             line["data"] = "TEST (JB_BENCH_SHARE_GPU, ranks share a GPU): not a scaling measurement; " + line["data"]

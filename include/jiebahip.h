@@ -200,7 +200,10 @@ int jb_dict_get(jb_ctx *ctx, const char *word, size_t len, int64_t *freq); /* 1 
 int64_t jb_dict_size(jb_ctx *ctx);
 
 /* Counters of the last cut on each device of ctx, summed over the devices (a host
- * batch cut in pieces: summed over its pieces).  Synchronises the devices' streams. */
+ * batch cut in pieces: summed over its pieces).  Synchronises the devices' streams.
+ * Concurrent small calls (jb_cut of at most 4 KiB) are coalesced into shared k_small
+ * batches: after one, the counters are those of the k_small batch that finished last
+ * on the device, which may hold other callers' documents beside this caller's. */
 typedef struct {
     uint64_t tokens;       /* tokens written */
     uint64_t blocks;       /* splitText blocks, zh and non-zh (tokenizer.go:165-210) */

@@ -173,6 +173,10 @@ struct Device {
         bool busy = false;
         hipStream_t st = nullptr;    // this slot's stream, masked to its own CU
     } slots[4];
+    // jb_last_stats' view of the last batch: last_small, small_hdr and has_stats, under
+    // stats_mu alone (a finished k_small batch publishes them without waiting for d->mu,
+    // which a host-batch pipeline holds for its whole run; lock order: mu, then stats_mu)
+    std::mutex stats_mu;
     bool last_small = false;     // the last batch took k_small (jb_last_stats reads small_hdr)
     // concurrent small calls, coalesced into shared k_small launches (cut_small)
     std::mutex small_mu;
@@ -533,7 +537,7 @@ static int install_image(Device* d, ImageBufs* b, const Image& img) {
 static void free_work(Work* w) {
     dfree(w->docbits); dfree(w->tile_cnt);
     dfree(w->ttile_cnt); dfree(w->supt); dfree(w->alnum16); dfree(w->erec); dfree(w->lanemask);
-    dfree(w->gbl); dfree(w->lsegb); dfree(w->lent); dfree(w->lflag); dfree(w->lbp); dfree(w->gbest); dfree(w->tile4); dfree(w->longblk);
+    dfree(w->gbl); dfree(w->lsegb); dfree(w->lmap); dfree(w->lcx); dfree(w->lflag); dfree(w->lbp); dfree(w->gbest); dfree(w->tile4); dfree(w->longblk);
     dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters); dfree(w->dbg); dfree(w->dbg_walk);
     *w = Work{};
 }
@@ -564,8 +568,12 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
     HIPCHK(hipMalloc(&w.gbl, nb / 3 + 8 + 512));
     HIPCHK(hipMalloc(&w.lflag, (nb / kZhLongMin + 2) * 4));
     HIPCHK(hipMalloc(&w.lsegb, (nb / kZhLongMin + 2) * 4));
-    HIPCHK(hipMalloc(&w.lent, (nb / (3 * kSeg) + nb / kZhLongMin + 4) * 4));
-    HIPCHK(hipMalloc(&w.lbp, nb / 3 + 64));
+    {
+        const uint64_t nchunk = (nb / (3 * kSeg) + nb / kZhLongMin + 4) / kSeg + 2;  // 64-segment chunks
+        HIPCHK(hipMalloc(&w.lmap, nchunk * 256));
+        HIPCHK(hipMalloc(&w.lcx, nchunk));
+    }
+    HIPCHK(hipMalloc(&w.lbp, nb / 3 + 256));
     HIPCHK(hipMalloc(&w.tile4, ntiles * 4));
     HIPCHK(hipMalloc(&w.longblk, (nb / kZhLongMin + 2) * sizeof(uint2)));
     HIPCHK(hipMalloc(&w.gbest, (nb / 3 + 8) * sizeof(double)));
@@ -706,7 +714,10 @@ static int launch_pipeline_(Device* d, const Work& w, const uint8_t* d_text, uin
     static const bool dbg = getenv("JB_DEBUG") != nullptr;
     const LaunchCfg& lc = d->lc;
     d->last_nbytes = nbytes;
-    d->last_small = false;
+    {
+        std::lock_guard<std::mutex> g(d->stats_mu);
+        d->last_small = false;
+    }
     if (dbg)
         fprintf(stderr, "[jb] nbytes=%llu ndocs=%u zh_waves=%u/%u wide=%d zh_group=%u\n", (unsigned long long)nbytes,
                 ndocs, lc.zh_waves, lc.zh_waves_wide, lc.zh_wide, lc.zh_group ? lc.zh_group : zh_group_for(nbytes));
@@ -826,7 +837,10 @@ static int launch(Device* d, const Work& w, const uint8_t* d_text, uint64_t nbyt
     if (rc) return rc;
     HIPCHK(hipEventRecord(d->ws_done, s));
     d->ws_stream = s;
-    d->has_stats = true;
+    {
+        std::lock_guard<std::mutex> g(d->stats_mu);
+        d->has_stats = true;
+    }
     d->acc_valid = false;
     return JB_OK;
 }
@@ -846,6 +860,10 @@ static int open_device(Device* d, int ordinal, const Image& img) {
     HIPCHK(hipHostMalloc(&d->h_zero, 64, hipHostMallocDefault));
     memset(d->h_zero, 0, 64);
     HIPCHK(hipStreamCreateWithFlags(&d->dstream, hipStreamNonBlocking));
+    ImageBufs b;
+    if ((rc = stage_image(d->ordinal, img, &b))) return rc;
+    if ((rc = install_image(d, &b, img))) return rc;
+    if ((rc = init_launch_cfg(d))) return rc;  // (sets small_slots)
     {
         // k_small runs one workgroup per batch: each slot's stream is pinned to one CU
         // (JB_SMALL_CU + slot x JB_SMALL_CU_STRIDE) so its batch finds its 21 KB of code in
@@ -853,19 +871,19 @@ static int open_device(Device* d, int ordinal, const Image& img) {
         // fetching them cold on whichever CU the dispatcher picks, and so batches of
         // different slots run side by side instead of one after another
         const int cu = env_int("JB_SMALL_CU", 0), cs = env_int("JB_SMALL_CU_STRIDE", 1);
-        if (cu < 0 || cs < 0 || cu + 3 * cs >= (int)d->ncu)
-            return fail(JB_EINVAL, "JB_SMALL_CU=%d, JB_SMALL_CU_STRIDE=%d: %u CUs", cu, cs, d->ncu);
-        for (int k = 0; k < 4; k++) {
+        const int last = cu + ((int)d->small_slots - 1) * cs;  // (only the slots in use get a stream)
+        if (cu < 0 || cs < 0 || last >= (int)d->ncu)
+            return fail(JB_EINVAL,
+                        "JB_SMALL_CU=%d, JB_SMALL_CU_STRIDE=%d, JB_SMALL_SLOTS=%u: slot k runs on CU "
+                        "JB_SMALL_CU + k x JB_SMALL_CU_STRIDE, and the last one (%d) is past the device's %u CUs",
+                        cu, cs, d->small_slots, last, d->ncu);
+        for (int k = 0; k < (int)d->small_slots; k++) {
             std::vector<uint32_t> mask((d->ncu + 31) / 32, 0u);
             const int c = cu + k * cs;
             mask[c / 32] = 1u << (c % 32);
             HIPCHK(hipExtStreamCreateWithCUMask(&d->slots[k].st, (uint32_t)mask.size(), mask.data()));
         }
     }
-    ImageBufs b;
-    if ((rc = stage_image(d->ordinal, img, &b))) return rc;
-    if ((rc = install_image(d, &b, img))) return rc;
-    if ((rc = init_launch_cfg(d))) return rc;
     return JB_OK;
 }
 
@@ -1065,7 +1083,7 @@ static void small_batch(Device* d, Device::SmallSlot* sl, SmallReq* const* rq, u
     const auto c2 = std::chrono::steady_clock::now();
     const uint32_t* h = sl->h_sout;
     {
-        std::lock_guard<std::mutex> g(d->mu);  // (jb_last_stats reads these)
+        std::lock_guard<std::mutex> g(d->stats_mu);  // (jb_last_stats reads these; not d->mu: see Device)
         memcpy(d->small_hdr, h, sizeof d->small_hdr);
         d->last_small = true;
         d->has_stats = true;
@@ -1323,7 +1341,10 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
             return rc;
         HIPCHK(run_zero(d->d_mask, 2 * nw * 8, d->stream));
     }
-    d->last_small = false;
+    {
+        std::lock_guard<std::mutex> g(d->stats_mu);
+        d->last_small = false;
+    }
     jb_stats acc{};
     auto drain = [&](int code) {  // an error with work in flight: let the streams finish first
         (void)hipStreamSynchronize(d->cstream);
@@ -1788,7 +1809,7 @@ static int cut_sharded(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off
         if (split) *unit_doc = un.doc;
     }
     for (auto& d : ctx->devs) {  // jb_last_stats: only the devices this batch reaches
-        std::lock_guard<std::mutex> g(d->mu);
+        std::lock_guard<std::mutex> g(d->stats_mu);
         d->has_stats = false;
     }
     if (mask)  // the words a device range shares with its neighbours are ORed into: clear them first
@@ -2014,7 +2035,7 @@ static int cut_device(jb_ctx* ctx, const uint8_t* d_text, uint64_t nbytes, const
     if (((uintptr_t)d_text & 15u) != 0) return fail(JB_EINVAL, "d_text must be 16-byte aligned");
     std::shared_lock<std::shared_mutex> rl(ctx->lock);
     for (size_t k = 1; k < ctx->devs.size(); k++) {
-        std::lock_guard<std::mutex> g(ctx->devs[k]->mu);
+        std::lock_guard<std::mutex> g(ctx->devs[k]->stats_mu);
         ctx->devs[k]->has_stats = false;
     }
     Device* d = ctx->devs[0].get();
@@ -2175,15 +2196,18 @@ extern "C" int jb_last_stats(jb_ctx* ctx, jb_stats* out) {
     memset(out, 0, sizeof *out);
     std::shared_lock<std::shared_mutex> rl(ctx->lock);
     for (auto& d : ctx->devs) {
-        std::lock_guard<std::mutex> g(d->mu);
-        if (!d->has_stats) continue;  // not reached by the last batch (its counters are older)
-        if (d->last_small) {  // k_small's counters came back with its spans
-            out->tokens += d->small_hdr[SM_NTOK];
-            out->blocks += d->small_hdr[SM_BLOCKS];
-            out->zh_blocks += d->small_hdr[SM_ZHBLOCKS];
-            out->viterbi_ties += d->small_hdr[SM_TIES];
-            continue;
+        {
+            std::lock_guard<std::mutex> sg(d->stats_mu);
+            if (!d->has_stats) continue;  // not reached by the last batch (its counters are older)
+            if (d->last_small) {  // k_small's counters came back with its spans (no device lock needed)
+                out->tokens += d->small_hdr[SM_NTOK];
+                out->blocks += d->small_hdr[SM_BLOCKS];
+                out->zh_blocks += d->small_hdr[SM_ZHBLOCKS];
+                out->viterbi_ties += d->small_hdr[SM_TIES];
+                continue;
+            }
         }
+        std::lock_guard<std::mutex> g(d->mu);
         if (d->acc_valid) {  // a host range cut in pieces: summed as they came back
             out->tokens += d->acc.tokens;
             out->blocks += d->acc.blocks;

@@ -79,12 +79,13 @@ struct Work {
                            // their blocks from these bits: a block ends at the next start)
     uint2* longblk;        // (start, end) of each long zh block (k_zh -> k_long_*)
     uint32_t* lsegb;       // per long block: its first segment (ascending with the block index)
-    uint32_t* lent;        // per segment: offset of the path's first piece start (0xFF none) | one-rune piece ends there << 8
+    uint8_t* lmap;         // per 64-segment chunk of a long block: its path-state map (k_long_seg -> k_long_path)
+    uint8_t* lcx;          // per chunk: the path state at its start (k_long_path -> k_long_tail)
     uint32_t* tile4;       // per tile: a 4-byte Han rune starts in it
     uint8_t* gbl;          // per Han rune: chosen piece length, then Viterbi back-pointers / labels
                            // (+512 bytes: k_zh_long reads 256-slot windows)
     uint32_t* lflag;       // per long block: 0 cut by k_long_dp's one-lane path, 2 DP done, 1 entries found
-    uint8_t* lbp;          // long blocks, per slot: exit codes (k_long_seg -> k_long_path), then Viterbi back-pointers / labels (k_long_tail)
+    uint8_t* lbp;          // long blocks, per slot: path exit codes (k_long_seg -> k_long_path, k_long_tail)
     double* gbest;         // per Han rune: best proba, kept only for blocks with an edge > 8 runes
     uint32_t* tok_start;
     uint32_t* tok_end;

@@ -266,7 +266,12 @@ constexpr uint32_t kMwOffE = kTileEX * 8u;                                // aft
 constexpr uint32_t kMwOffDb = kMwOffE + kTileEX * 4u;                     // u32 per 32 bytes of the tile, +2
 constexpr uint32_t kMwOffWl = kMwOffDb + (kTileBytes / 32u + 3u) * 4u;    // u16 per entry
 constexpr uint32_t kMwOffScan = (kMwOffWl + kTileE * 2u + 3u) & ~3u;      // u32 x 8
-constexpr uint32_t kMwLds = kMwOffScan + 8u * 4u;
+#ifndef JB_MW_SORT
+#define JB_MW_SORT 1  // the walk list grouped by the line of each walk's first probe
+#endif
+constexpr uint32_t kMwSortB = 64u;                   // buckets of the walk-list sort
+constexpr uint32_t kMwOffHist = kMwOffScan + 8u * 4u;  // u32 per bucket
+constexpr uint32_t kMwLds = kMwOffHist + (JB_MW_SORT ? kMwSortB * 4u : 0u);
 constexpr uint32_t kMwOffHot = (kMwOffE + 15u) & ~15u;  // hot level-1 rows (phase 1 only), under the entries
 static_assert(kMwOffHot % 16u == 0u && kMwOffHot + 10u * JB_HOT_SLOTS <= kMwOffDb && JB_HOT_SLOTS == 512u,
               "k_mark_walk: the hot rows fit under the entry list, 256 threads stage them");
@@ -431,6 +436,10 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         s_nla = 0;
         s_nwl = 0;
     }
+#if JB_MW_SORT
+    uint32_t* const s_hist = reinterpret_cast<uint32_t*>(s_raw + kMwOffHist);
+    if (threadIdx.x < kMwSortB) s_hist[threadIdx.x] = 0u;
+#endif
     const uint64_t p0 = t0 + threadIdx.x * 16u;
     // doc-start / past-the-end mask, bit k <-> byte p0 - 4 + k (k < 24)
     uint64_t M;
@@ -667,7 +676,8 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     // has no children or ends its Han run gets its record now (in its LDS cell,
     // which only its own walk would read); the others go on the walk list.
     const uint32_t nla = s_nla;
-    for (uint32_t i = threadIdx.x; i < nent; i += 256u) {
+    [[maybe_unused]] uint32_t wm = 0;  // (JB_MW_SORT) which of the thread's entries went on the walk list
+    for (uint32_t i = threadIdx.x, k = 0; i < nent; i += 256u, k++) {
         const uint32_t e = s_e[i];
         const uint32_t nxt = ent_pos(e) + ent_w(e);
         uint32_t f = 0;
@@ -692,11 +702,45 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
             r1 = 0ull;
             go = false;
         }
-        if (!go) s_c[i] = r1;
-        else s_wl[atomicAdd(&s_nwl, 1u)] = (uint16_t)i;
+        if (!go) {
+            s_c[i] = r1;
+        } else {
+#if JB_MW_SORT
+            // Walks whose first probes fall in one 128-byte line of cells go next to each
+            // other on the list, so that a wave's gather asks L2 for fewer lines: a
+            // counting sort by a hash of that line (the order within a bucket does not
+            // matter).  The bucket and the rank in it wait in the entry cell's check
+            // field, which a walk never reads (its check is the root).
+            const uint32_t ln = (jb_cell_base(c1) + ent_code(s_e[i + 1u])) >> 4;
+            const uint32_t b = (ln * 0x9E3779B1u) >> 26;
+            static_assert(kMwSortB == 64u && kTileEX <= 2048u, "bucket (6 bits) and rank (11 bits) in the check field");
+            const uint32_t rk = atomicAdd(&s_hist[b], 1u);
+            s_c[i] = (c1 & ~0x3FFFFFull) | (b << 11) | rk;
+            wm |= 1u << k;
+#else
+            s_wl[atomicAdd(&s_nwl, 1u)] = (uint16_t)i;
+#endif
+        }
     }
     const int any4 = __syncthreads_or(has4);  // (also the barrier after the run links)
     if (threadIdx.x == 0) tile4[blockIdx.x] = any4 ? 1u : 0u;  // k_zh: general rune stepping near this tile
+#if JB_MW_SORT
+    if (threadIdx.x < 64u) {  // bucket offsets: wave 0, a bucket per lane
+        const uint32_t h = s_hist[threadIdx.x];
+        const uint32_t x = wave_incl_scan(h);
+        s_hist[threadIdx.x] = x - h;
+        if (threadIdx.x == 63u) s_nwl = x;
+    }
+    __syncthreads();
+    for (uint32_t k = 0; wm >> k; k++) {
+        if ((wm >> k) & 1u) {
+            const uint32_t i = threadIdx.x + 256u * k;
+            const uint32_t ck = (uint32_t)s_c[i] & 0x3FFFFFu;
+            s_wl[s_hist[ck >> 11] + (ck & 2047u)] = (uint16_t)i;
+        }
+    }
+    __syncthreads();
+#endif
     if (stamps) c2 = __builtin_amdgcn_s_memtime();
     // ---- walks: wave w takes a quarter of the walk list ------------------------------
     const uint32_t* ent = s_e;
@@ -2330,12 +2374,30 @@ constexpr uint32_t kSpecGrid = 256;  // 64-lane workgroups, one per CU (128 KB o
 __global__ __launch_bounds__(64) void k_long_spec(const uint8_t* __restrict__ text, DevImage im,
                                                   const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
                                                   const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ counters,
-                                                  uint8_t* __restrict__ gbl, double* __restrict__ gbest, uint32_t mode) {
+                                                  const uint32_t* __restrict__ tile4, uint8_t* __restrict__ gbl,
+                                                  double* __restrict__ gbest, uint32_t mode) {
     __shared__ double s_ring[kSpecRing][64];
     const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG], lane = threadIdx.x;
     if (!im.plainw) return;  // (k_long_dp runs the exact chain)
-    for (uint32_t g = blockIdx.x * 64u + lane; g < nseg; g += gridDim.x * 64u) {
-        const uint32_t bi = long_block_of(lsegb, nlong, g);
+    for (uint32_t g0 = blockIdx.x * 64u; g0 < nseg; g0 += gridDim.x * 64u) {  // (wave-uniform)
+        const uint32_t g = g0 + lane;
+        const bool act = g < nseg;
+        const uint32_t bi = act ? long_block_of(lsegb, nlong, g) : 0xFFFFFFFFu;
+        // A block with a 4-byte Han rune takes k_long_dp's general path, which ignores these
+        // choices; its runes are not all 3 bytes, so slots bs / 3 + i are not all rune starts
+        // written in this batch (a record there may be stale), and it is skipped.  The
+        // wave checks the tile4 flags of its segments' blocks, one block at a time.
+        bool skip = !act;
+        for (uint64_t pend = __ballot(act); pend;) {
+            const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bi, (int)__builtin_ctzll(pend));
+            const uint2 bb0 = longblk[b0];
+            bool f = false;
+            for (uint32_t t = bb0.x / kTileBytes + lane; t <= (bb0.y - 1u) / kTileBytes; t += 64u) f |= tile4[t] != 0u;
+            const bool has4 = __ballot(f) != 0ull;
+            if (bi == b0) skip = has4;
+            pend &= ~__ballot(bi == b0);
+        }
+        if (skip) continue;
         const uint2 bb = longblk[bi];
         const uint32_t bs = bb.x, be = bb.y, n = (be - bs) / 3u, s0 = bs / 3u;
         const uint32_t a = (g - lsegb[bi]) * kSeg, lim = min(a + kSeg, n), top = min(lim + kSpecOver, n);
@@ -2869,6 +2931,29 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
 #endif
 }
 
+// Path states at segment boundaries (findDagPath, :552-562, over a long block cut
+// in 64-rune segments).  Where the path goes on at the start of a segment is one
+// byte x, the same code k_long_seg writes for each rune:
+//   0..254  the next piece starts x runes past the segment's start (x >= 64: the
+//           piece before spans the whole segment)
+//   0xFF    it starts at offset 0, and the piece before is one rune (so a run of
+//           single-rune pieces enters the segment)
+// Crossing segment s maps x to the state at the next boundary: kLpNext.  The
+// state at every boundary follows from composing these maps, which is integer
+// work: exact in any association (unlike the f64 values).
+__device__ __forceinline__ uint32_t lp_next(const uint8_t* codes, uint32_t x) {  // codes: the segment's 64 exit codes
+    return x >= 64u && x != 0xFFu ? x - 64u : codes[x == 0xFFu ? 0u : x];
+}
+// the segment's entry as k_long_tail takes it: first piece start | a one-rune piece ends there << 8;
+// 0xFFFFFFFF when no piece starts in it (or the path ended: runes past the block's n)
+__device__ __forceinline__ uint32_t lp_entry(uint32_t x, uint32_t a, uint32_t n) {
+    const uint32_t o = x == 0xFFu ? 0u : x;
+    if (o >= 64u || a + o >= n) return 0xFFFFFFFFu;
+    return o | (x == 0xFFu ? 256u : 0u);
+}
+constexpr uint32_t kLpMap = 256;    // a chunk map: next state for each of the 256 states
+constexpr uint32_t kLpBatch = 128;  // chunk maps k_long_path stages in LDS at a time (32 KB)
+
 // k_long_seg: one lane per 64-rune segment of a long block that k_long_dp ran
 // the chain for.  The chosen lengths are maxIndexProba over the same sums
 // w + best(i + L) the chain formed (the same float64 adds of the same values),
@@ -2877,72 +2962,120 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
 // lands at or past the segment's end (its offset past the end, 0..254), or
 // 0xFF when that is the end itself and the last piece before it is one rune
 // (so the next segment knows a run of single-rune pieces enters it).
+// A wave holds 64 consecutive segments, chunk c = g / 64.  When they are all one
+// block's and the block goes on past them, the wave composes their boundary maps
+// into the chunk's map (lmap[c]: state at the chunk's start -> state at its end),
+// four states per lane walked through the 64 segments' codes in LDS.
 __global__ __launch_bounds__(256) void k_long_seg(const uint8_t* __restrict__ text, DevImage im,
                                                   const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
                                                   const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ counters,
                                                   const uint32_t* __restrict__ lflag, const double* __restrict__ gbest,
-                                                  uint8_t* __restrict__ gbl, uint8_t* __restrict__ lcode) {
+                                                  uint8_t* __restrict__ gbl, uint8_t* __restrict__ lcode,
+                                                  uint8_t* __restrict__ lmap) {
     __shared__ uint8_t s_bl[256][kSeg];
-    const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG];
+    const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG], lane = threadIdx.x & 63u;
     uint8_t* const my = s_bl[threadIdx.x];
-    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < nseg; g += gridDim.x * blockDim.x) {
-        const uint32_t bi = long_block_of(lsegb, nlong, g);
-        if (lflag[bi] != 2u) continue;
-        const uint2 bb = longblk[bi];
-        const uint32_t bs = bb.x, be = bb.y, n = (be - bs) / 3u, s0 = bs / 3u;
-        const uint32_t a = (g - lsegb[bi]) * kSeg, lim = min(a + kSeg, n);
-        for (uint32_t i = a; i < lim; i++) {
-            DpFold f;
-            long_items(text, im, erec, bs, be, i, [&](uint32_t L, double wt) {
-                fold_item(f, L, wt + (i + L == n ? 0.0 : gbest[s0 + i + L]));
-            });
-            f.finish();
-            my[i - a] = (uint8_t)f.bestL;
-            gbl[s0 + i] = (uint8_t)f.bestL;
+    for (uint32_t gw = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); gw < nseg; gw += gridDim.x * blockDim.x) {
+        const uint32_t g = gw + lane;  // (the loop is wave-uniform: the chunk map needs the whole wave)
+        uint32_t bi = 0xFFFFFFFFu, n = 0, a = 0;
+        bool act = g < nseg;
+        if (act) {
+            bi = long_block_of(lsegb, nlong, g);
+            act = lflag[bi] == 2u;
         }
-        for (uint32_t p = lim; p-- > a;) {
-            // (a rune with no piece walks on as if it had one: if the true path
-            // comes to it, k_long_tail reports it)
-            const uint32_t L = max(1u, (uint32_t)my[p - a]), q = p + L;
-            const uint8_t c = q >= lim ? (L == 1u ? (uint8_t)0xFFu : (uint8_t)(q - lim)) : my[q - a];
-            my[p - a] = c;
-            lcode[s0 + p] = c;
+        if (act) {
+            const uint2 bb = longblk[bi];
+            const uint32_t bs = bb.x, be = bb.y, s0 = bs / 3u;
+            n = (be - bs) / 3u;
+            a = (g - lsegb[bi]) * kSeg;
+            const uint32_t lim = min(a + kSeg, n);
+            for (uint32_t i = a; i < lim; i++) {
+                DpFold f;
+                long_items(text, im, erec, bs, be, i, [&](uint32_t L, double wt) {
+                    fold_item(f, L, wt + (i + L == n ? 0.0 : gbest[s0 + i + L]));
+                });
+                f.finish();
+                my[i - a] = (uint8_t)f.bestL;
+                gbl[s0 + i] = (uint8_t)f.bestL;
+            }
+            for (uint32_t p = lim; p-- > a;) {
+                // (a rune with no piece walks on as if it had one: if the true path
+                // comes to it, k_long_tail reports it)
+                const uint32_t L = max(1u, (uint32_t)my[p - a]), q = p + L;
+                const uint8_t c = q >= lim ? (L == 1u ? (uint8_t)0xFFu : (uint8_t)(q - lim)) : my[q - a];
+                my[p - a] = c;
+                lcode[s0 + p] = c;
+            }
         }
+        // the chunk map: 64 whole segments of one block, and more of the block after them
+        const uint32_t b0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)bi);
+        const bool inner = act && bi == b0 && a + kSeg < n;
+        if (__ballot(inner) == ~0ull) {
+            wave_sync();  // (every lane's codes are in LDS)
+            const uint8_t(*sc)[kSeg] = s_bl + (threadIdx.x & ~63u);
+            uint32_t x0 = lane, x1 = lane + 64u, x2 = lane + 128u, x3 = lane + 192u;
+            for (uint32_t k = 0; k < kSeg; k++) {  // (four independent chains per lane)
+                x0 = lp_next(sc[k], x0);
+                x1 = lp_next(sc[k], x1);
+                x2 = lp_next(sc[k], x2);
+                x3 = lp_next(sc[k], x3);
+            }
+            uint8_t* const m = lmap + (uint64_t)(gw / kSeg) * kLpMap;
+            m[lane] = (uint8_t)x0;
+            m[lane + 64u] = (uint8_t)x1;
+            m[lane + 128u] = (uint8_t)x2;
+            m[lane + 192u] = (uint8_t)x3;
+        }
+        wave_sync();  // (the next iteration's codes overwrite these)
     }
 }
 
-// k_long_path: one wave per long block: findDagPath (:552-562) hop by hop over
-// the segments, one exit-code lookup per segment, staged 64 segments at a time
-// in LDS.  Per segment: the offset of the path's first piece start in it (0xFF:
-// none, a piece spans the segment) and whether a one-rune piece ends there.
+// k_long_path: one wave per long block: the path state (lp_next) at the start of
+// every 64-segment chunk the block spans past its first (lcx[c]).  The segments
+// before the first chunk boundary are crossed one by one (their codes staged in
+// LDS), then each chunk by its map (k_long_seg), the maps staged kLpBatch at a
+// time: one LDS lookup per chunk instead of one hop per segment (the serial walk
+// over 15.6K segments of config 5b took 2.1 ms).  k_long_tail finds each
+// segment's entry from these states.
 __global__ __launch_bounds__(64) void k_long_path(const uint2* __restrict__ longblk, const uint32_t* __restrict__ lsegb,
                                                   const uint32_t* __restrict__ counters, uint32_t* __restrict__ lflag,
-                                                  const uint8_t* __restrict__ lcode, uint32_t* __restrict__ lent) {
-    __shared__ uint32_t s_c32[kSeg * kSeg / 4u];  // exit codes of 64 segments
-    const uint8_t* const s_c = reinterpret_cast<const uint8_t*>(s_c32);
+                                                  const uint8_t* __restrict__ lcode, const uint8_t* __restrict__ lmap,
+                                                  uint8_t* __restrict__ lcx) {
+    __shared__ uint32_t s_m32[kLpBatch * kLpMap / 4u];
+    const uint8_t* const s_m = reinterpret_cast<const uint8_t*>(s_m32);
+    static_assert(kSeg * kSeg <= kLpBatch * kLpMap, "the first partial chunk's codes fit the map space");
     const uint32_t lane = threadIdx.x;
     const uint32_t nlong = counters[CNT_NLONG];
     for (uint32_t bi = blockIdx.x; bi < nlong; bi += gridDim.x) {
         if (lflag[bi] != 2u) continue;
         const uint2 bb = longblk[bi];
         const uint32_t n = (bb.y - bb.x) / 3u, s0 = bb.x / 3u, sb = lsegb[bi];
-        const uint32_t nsg = (n + kSeg - 1u) / kSeg;
-        uint32_t E = 0, single = 0;
-        for (uint32_t b0 = 0; b0 < nsg; b0 += 64u) {
-            const uint32_t base = b0 * kSeg, top = min(n, base + kSeg * kSeg);
-            const uint32_t nw = (top - base + 3u) / 4u;  // (lcode has 512 bytes of slack)
-            for (uint32_t k = lane; k < nw; k += 64u) s_c32[k] = ld4(lcode, (uint64_t)s0 + base + 4u * k);
-            __syncthreads();
-            uint32_t ent = 0xFFFFFFFFu;  // lane t: segment b0 + t
-            while (E < top) {
-                const uint32_t seg = E / kSeg, lim = min(seg * kSeg + kSeg, n);
-                const uint32_t c = s_c[E - base];
-                ent = lane == seg - b0 ? ((E - seg * kSeg) | (single << 8)) : ent;
-                single = c == 0xFFu;
-                E = lim + (single ? 0u : c);
+        const uint32_t gend = sb + (n + kSeg - 1u) / kSeg;  // past the block's last segment
+        const uint32_t g1 = min(gend, (sb + kSeg - 1u) & ~(kSeg - 1u));  // the first chunk boundary
+        uint32_t x = 0;  // the state at the block's start: its first rune, no piece before
+        if (g1 < gend) {
+            if (g1 > sb) {  // the segments before it, one by one (lcode has 512 bytes of slack)
+                const uint32_t nw = (g1 - sb) * (kSeg / 4u);
+                for (uint32_t k = lane; k < nw; k += 64u) s_m32[k] = ld4(lcode, (uint64_t)s0 + 4u * k);
+                __syncthreads();
+                for (uint32_t j = 0; j < g1 - sb; j++) x = lp_next(s_m + j * kSeg, x);
+                __syncthreads();
             }
-            if (b0 + lane < nsg) lent[sb + b0 + lane] = ent;
-            __syncthreads();
+            for (uint32_t c0 = g1 / kSeg; c0 * kSeg < gend; c0 += kLpBatch) {
+                // chunks c0 .. (the maps of the ones wholly inside the block with more after them)
+                const uint32_t cend = min(c0 + kLpBatch, (gend + kSeg - 1u) / kSeg);
+                uint32_t cmap = cend;
+                while (cmap > c0 && (cmap * kSeg >= gend)) --cmap;  // chunks c0..cmap-1 have a map
+                const uint32_t nw = (cmap - c0) * (kLpMap / 4u);
+                const uint32_t* gm = reinterpret_cast<const uint32_t*>(lmap + (uint64_t)c0 * kLpMap);
+                for (uint32_t k = lane; k < nw; k += 64u) s_m32[k] = gm[k];
+                __syncthreads();
+                for (uint32_t c = c0; c < cend; c++) {
+                    if (lane == 0u) lcx[c] = (uint8_t)x;
+                    if (c < cmap) x = s_m[(c - c0) * kLpMap + x];
+                }
+                __syncthreads();
+            }
         }
         if (lane == 0u) lflag[bi] = 1u;
     }
@@ -3009,29 +3142,67 @@ __device__ void long_viterbi(const uint8_t* __restrict__ text, const DevImage& i
     }
 }
 
-// k_long_tail: one lane per segment of a long block, from the entry
-// k_long_path found: the pieces that start in the segment become tokens, and
-// every run of one-rune pieces that starts there gets its Viterbi (+ cutHMM);
+// k_long_tail: one lane per segment of a long block.  A wave holds the 64
+// segments of chunk c = g / 64: it stages their exit codes in LDS and crosses
+// them in order from the chunk's state (k_long_path's lcx[c], or the block's
+// start state where a block begins), which gives each segment its entry (the
+// hop-by-hop walk of findDagPath, :552-562, over 64 segments at a time).  From
+// its entry each lane makes the pieces that start in its segment tokens, and
+// runs every run of one-rune pieces that starts there through Viterbi (+ cutHMM);
 // a run that entered from the previous segment belongs to that segment's lane.
+// The Viterbi back-pointers go to bp (gbest's bytes, free by now), not over the
+// exit codes other waves still read.
 template <bool HMM>
 __global__ __launch_bounds__(256) void k_long_tail(const uint8_t* __restrict__ text, DevImage im,
                                                    const uint8_t* __restrict__ gbl, const uint2* __restrict__ longblk,
                                                    const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ lflag,
-                                                   uint32_t* __restrict__ counters, const uint32_t* __restrict__ lent,
-                                                   uint8_t* __restrict__ bp, uint32_t* __restrict__ sbits,
-                                                   uint32_t* __restrict__ ebits) {
-    const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG];
+                                                   uint32_t* __restrict__ counters, const uint8_t* __restrict__ lcode,
+                                                   const uint8_t* __restrict__ lcx, uint8_t* __restrict__ bp,
+                                                   uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits) {
+    __shared__ uint4 s_cd[256][kSeg / 16u];  // each lane's segment's exit codes
+    const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG], lane = threadIdx.x & 63u;
     Emitter em(sbits, ebits);
     bool bad = false;
-    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < nseg; g += gridDim.x * blockDim.x) {
-        const uint32_t bi = long_block_of(lsegb, nlong, g);
-        if (lflag[bi] != 1u) continue;  // cut by the one-lane path
-        const uint32_t ent = lent[g];
-        if (ent == 0xFFFFFFFFu) continue;  // no piece starts here
+    for (uint32_t gw = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); gw < nseg; gw += gridDim.x * blockDim.x) {
+        const uint32_t g = gw + lane;  // (wave-uniform loop)
+        uint32_t bi = 0, a = 0, n = 0;
+        bool act = g < nseg;
+        if (act) {
+            bi = long_block_of(lsegb, nlong, g);
+            act = lflag[bi] == 1u;  // (else cut by the one-lane path)
+        }
+        bool first = false;  // the block's first segment
+        if (act) {
+            const uint2 bb = longblk[bi];
+            const uint32_t sg = lsegb[bi];
+            n = (bb.y - bb.x) / 3u;
+            a = (g - sg) * kSeg;
+            first = g == sg;
+            uint32_t* d = reinterpret_cast<uint32_t*>(s_cd[threadIdx.x]);  // (lcode has 256 bytes of slack)
+#pragma unroll
+            for (uint32_t k = 0; k < kSeg / 4u; k++) d[k] = ld4(lcode, (uint64_t)bb.x / 3u + a + 4u * k);
+        }
+        const uint64_t am = __ballot(act), fm = __ballot(first);
+        wave_sync();
+        // the wave's segments in order: every lane runs the same walk (LDS reads of one
+        // address: broadcast) and keeps its own segment's entry
+        uint32_t x = lcx[gw / kSeg], ent = 0xFFFFFFFFu;
+        for (uint32_t k = 0; k < 64u; k++) {
+            if (!((am >> k) & 1ull)) continue;  // (uniform)
+            if ((fm >> k) & 1ull) x = 0u;
+            const uint32_t ak = (uint32_t)__builtin_amdgcn_readlane((int)a, (int)k);
+            const uint32_t nk = (uint32_t)__builtin_amdgcn_readlane((int)n, (int)k);
+            const uint32_t e = lp_entry(x, ak, nk);
+            if (lane == k) ent = e;
+            if (e != 0xFFFFFFFFu || (x != 0xFFu && x >= 64u))
+                x = lp_next(reinterpret_cast<const uint8_t*>(s_cd[(threadIdx.x & ~63u) + k]), x);
+        }
+        wave_sync();  // (the next iteration overwrites the codes)
+        if (!act || ent == 0xFFFFFFFFu) continue;  // no piece starts here
         const uint2 bb = longblk[bi];
-        const uint32_t bs = bb.x, n = (bb.y - bb.x) / 3u, s0 = bs / 3u;
+        const uint32_t bs = bb.x, s0 = bs / 3u;
         auto len = [&](uint32_t j) { return (uint32_t)gbl[s0 + j]; };
-        const uint32_t c0 = (g - lsegb[bi]) * kSeg, c1 = min(n, c0 + kSeg);
+        const uint32_t c0 = a, c1 = min(n, c0 + kSeg);
         uint32_t q = c0 + (ent & 0xFFu);
         if (HMM && (ent >> 8))  // a run of one-rune pieces enters: its owner cuts it
             while (q < n && len(q) == 1u) q++;
@@ -4103,8 +4274,8 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         const uint32_t spec = lc.long_spec ? 1u : 0u;
         if (spec)
             JB_TIMED(K_LONG_SPEC, hipLaunchKernelGGL(k_long_spec, dim3(kSpecGrid), dim3(64), 0, stream, d_text, im,
-                                                     w.erec + kErecPad, w.longblk, w.lsegb, w.counters, w.gbl, w.gbest,
-                                                     lc.long_spec));
+                                                     w.erec + kErecPad, w.longblk, w.lsegb, w.counters, w.tile4, w.gbl,
+                                                     w.gbest, lc.long_spec));
         if (hmm)
             JB_TIMED(K_LONG_DP, hipLaunchKernelGGL((k_long_dp<true>), dim3(kLongGrid), dim3(256), 0, stream, d_text, im,
                                                    w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters, w.sbits,
@@ -4115,16 +4286,18 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                                    w.ebits, w.lflag, w.dbg, spec));
         JB_TIMED(K_LONG_SEG, hipLaunchKernelGGL(k_long_seg, dim3(gseg), dim3(256), 0, stream, d_text, im,
                                                 w.erec + kErecPad, w.longblk, w.lsegb, w.counters, w.lflag, w.gbest,
-                                                w.gbl, w.lbp));
+                                                w.gbl, w.lbp, w.lmap));
         JB_TIMED(K_LONG_PATH, hipLaunchKernelGGL(k_long_path, dim3(kLongGrid), dim3(64), 0, stream, w.longblk, w.lsegb,
-                                                 w.counters, w.lflag, w.lbp, w.lent));
+                                                 w.counters, w.lflag, w.lbp, w.lmap, w.lcx));
+        // (the Viterbi back-pointers go to gbest's bytes: the exit codes in lbp are read to the end)
+        uint8_t* const bp = reinterpret_cast<uint8_t*>(w.gbest);
         if (hmm)
             JB_TIMED(K_LONG_TAIL, hipLaunchKernelGGL((k_long_tail<true>), dim3(gseg), dim3(256), 0, stream, d_text, im,
-                                                     w.gbl, w.longblk, w.lsegb, w.lflag, w.counters, w.lent, w.lbp,
+                                                     w.gbl, w.longblk, w.lsegb, w.lflag, w.counters, w.lbp, w.lcx, bp,
                                                      w.sbits, w.ebits));
         else
             JB_TIMED(K_LONG_TAIL, hipLaunchKernelGGL((k_long_tail<false>), dim3(gseg), dim3(256), 0, stream, d_text, im,
-                                                     w.gbl, w.longblk, w.lsegb, w.lflag, w.counters, w.lent, w.lbp,
+                                                     w.gbl, w.longblk, w.lsegb, w.lflag, w.counters, w.lbp, w.lcx, bp,
                                                      w.sbits, w.ebits));
     }
     {

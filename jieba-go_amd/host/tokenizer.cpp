@@ -90,6 +90,15 @@ void Tokenizer::AddWord(const std::string& word, int freq) {
     check(jb_add_word(ctx_, word.data(), word.size(), freq));
 }
 
+void Tokenizer::AddWord(const std::string& word, int freq, const std::function<double(double)>& log) {
+    int64_t f = freq;
+    if (freq < 1) check(jb_suggest_freq(ctx_, word.data(), word.size(), &f));  // (tokenizer.go:373-375)
+    const int64_t keys[2] = {f, jb_dict_size(ctx_) + f};
+    const double vals[2] = {log((double)keys[0]), log((double)keys[1])};
+    check(jb_add_log(ctx_, keys, vals, 2));
+    check(jb_add_word(ctx_, word.data(), word.size(), f));
+}
+
 void Tokenizer::Save(const std::string& path) { check(jb_save(ctx_, path.c_str())); }
 
 }  // namespace jiebago

@@ -9,6 +9,7 @@
 // log.Fatal / panic (constructor load errors, tokenizer.go:397-416,443,452,656,660;
 // the cutDAG slice panic), this mirror throws jiebago::Error.
 #pragma once
+#include <functional>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -49,8 +50,13 @@ public:
     std::vector<std::string> CutParallel(const std::string& text, bool hmm, int numWorkers, bool ordered);
     // Many documents in one device pass (what CutParallel is used for).
     std::vector<std::vector<std::string>> CutBatch(const std::vector<std::string>& docs, bool hmm);
-    // AddWord (tokenizer.go:372) without the reference's self-deadlock.
+    // AddWord (tokenizer.go:372) without the reference's self-deadlock.  The new
+    // weights use the library's restatement of Go's math.Log (jb_go_log).
     void AddWord(const std::string& word, int freq);
+    // The same with the caller's logarithm (the Go binding passes math.Log): log(f) of
+    // the new frequency and log(size + f) of the new pd.size (addTerm, tokenizer.go:580-585)
+    // go to jb_add_log first, so the rebuilt weights use exactly those values.
+    void AddWord(const std::string& word, int freq, const std::function<double(double)>& log);
     // Write the current image (AddWord changes included) for FromImage.
     void Save(const std::string& path);
 

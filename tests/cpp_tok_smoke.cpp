@@ -60,6 +60,9 @@ int main(int argc, char** argv) {
         for (const auto& d : docs) line("batch_doc", d);
         tk->AddWord(argv[3], 0);
         line("cut_added", tk->Cut(text, true));
+        // the caller-log overload, as a Go AddWord passes math.Log (here the library's restatement)
+        tk->AddWord("\xe8\xa8\x8e\xe8\xab\x96\xe9\x87\x8f\xe5\xad\x90", 7, [](double x) { return jb_go_log(x); });
+        line("cut_added_log", tk->Cut(text, true));
         tk->Save(argv[4]);
         auto img = jiebago::Tokenizer::FromImage(argv[4]);
         line("cut_image", img->Cut(text, true));

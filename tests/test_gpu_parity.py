@@ -502,6 +502,29 @@ def test_long_blocks_many(tmp_path, syn_small, kind, spec, monkeypatch):
         tk.close()
 
 
+def test_long_block_4byte_rune_after_junk(tmp_path, syn_small, monkeypatch):
+    """A long block with a 4-byte Han rune, cut in a workspace that the batch before
+    filled with DAG records: its stride-3 slots past the 4-byte rune are
+    not rune starts, so k_long_spec must leave such a block alone (k_long_dp takes it
+    on its general path) instead of reading the stale records there."""
+    monkeypatch.setenv("JB_LONG_SPEC", "1")
+    dp, ep, _ = syn_small
+    tk, o = _pair(dp, ep)
+    try:
+        rng = random.Random(11)
+        pool = [chr(c) for c in range(0x4E00, 0x4E00 + 2000)]
+        han = "".join(rng.choice(pool) for _ in range(12000))
+        junk = [han[:6000], han[6000:]]  # every slot of both blocks gets a record
+        with4 = [han[:1500] + "\U00020000" + han[1500:5999], "\U00020000" + han[6000:11999]]
+        assert sum(len(t.encode()) for t in with4) <= sum(len(t.encode()) for t in junk)
+        for hmm in (False, True):
+            for texts in (junk, with4):
+                buf, off = _batch_of(texts)
+                _cmp_batch(tk, o, buf, off, hmm, f"4-byte rune after junk hmm={hmm}")
+    finally:
+        tk.close()
+
+
 def test_synthetic_golden_vectors(syn_golden):
     """The GPU path reproduces the committed golden vectors (oracle output frozen in tests/golden)."""
     g, docs, dp, ep = syn_golden
@@ -669,6 +692,8 @@ def test_cpp_tokenizer_mirror(syn_small, tmp_path):
     tk.close()
     o.add_term(word, f)
     assert got["cut_added"][0] == o.cut(t, True)
+    o.add_term("討論量子", 7)  # (AddWord with the caller's log function)
+    assert got["cut_added_log"][0] == o.cut(t, True)
     assert got["cut_image"][0] == o.cut(t, True)
 
 

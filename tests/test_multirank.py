@@ -124,6 +124,19 @@ def test_bench_two_ranks_gloo(syn_small, corrupt_rank):
     assert line["parity"]["mismatches"] == (0 if corrupt_rank < 0 else 1)
     assert line["cpu_baseline"] is None  # (rank 0 at N = 1 only)
     assert abs(line["value"] - nr * 3 / (line["ms_per_step"] * 3e-3)) / line["value"] < 0.05  # (ms rounded)
+    # every rank's own step time, kernel times and shard (a straggler shows in the line)
+    pr = line["config"]["per_rank"]
+    assert [r["rank"] for r in pr] == [0, 1]
+    assert [r["shard_docs"] for r in pr] == [cut[1] - cut[0], cut[2] - cut[1]]
+    assert [r["shard_bytes"] for r in pr] == [int(off[cut[1]] - off[cut[0]]), int(off[cut[2]] - off[cut[1]])]
+    assert [r["first_doc"] for r in pr] == [0, cut[1]]
+    assert sum(r["shard_chars"] for r in pr) == nr
+    assert max(r["ms_per_step"] for r in pr) == pytest.approx(line["ms_per_step"], rel=1e-3, abs=1e-3)
+    assert [r["bit_exact"] for r in pr] == [True, corrupt_rank != 1]
+    assert all(isinstance(r["kernels_ms"], dict) for r in pr)
+    st = line["roofline_step"]
+    assert st["tokens"] == sum(r["tokens"] for r in pr) and st["input_bytes"] == int(off[-1])
+    assert st["alg_bytes_per_step"] == int(off[-1]) + 8 * st["tokens"]
 
 
 def _bench_cmd(*extra):
@@ -162,6 +175,28 @@ def test_bench_launcher_two_ranks(corrupt_rank):
     assert line["parity"]["mismatches"] == (0 if corrupt_rank < 0 else 1)
     assert line["data"].startswith("TEST BACKEND")
     assert line["value"] > 0 and line["cpu_baseline"] is None
+    pr = line["config"]["ranks"]["per_rank"]
+    assert [r["rank"] for r in pr] == [0, 1] and sum(r["shard_bytes"] for r in pr) == line["config"]["corpus_bytes"]
+    assert [r["bit_exact"] for r in pr] == [True, corrupt_rank != 1]
+
+
+def test_roofline_charges_the_output_format():
+    """bench.roofline_of charges SURVEY.md §8d's bytes for the format the timed step
+    writes: 1 B read per input byte + 8 B per u32 (start, end) span."""
+    import bench
+    nbytes, ntok, han = 1_000_000, 123_457, 700_002
+    per = bench.alg_bytes_per_byte(nbytes, ntok)
+    assert per == pytest.approx(1.0 + 8.0 * ntok / nbytes)
+    kern = {"k_mark_walk": {"avg_ms": 2.0}, "k_zh": {"avg_ms": 1.0}}
+    r = bench.roofline_of(kern, {"k_mark_walk": float(nbytes), "k_zh": float(han)}, lambda k: None, per)
+    assert r["k_mark_walk"]["alg_bytes_per_launch"] == pytest.approx(nbytes + 8 * ntok)
+    assert r["k_zh"]["alg_bytes_per_launch"] == pytest.approx(han * per)
+    assert r["k_mark_walk"]["achieved"] == pytest.approx((nbytes + 8 * ntok) / 2e-3 / 1e9, abs=0.01)
+    assert "spans" in r["k_mark_walk"]["output_format"]
+    st = bench.roofline_step(nbytes, ntok, 0.5)
+    assert st["alg_bytes_per_step"] == nbytes + 8 * ntok
+    assert st["achieved"] == pytest.approx((nbytes + 8 * ntok) / 0.5e-3 / 1e9, abs=0.01)
+    assert st["frac"] == pytest.approx(st["achieved"] / bench.HBM_PEAK_GBS, abs=1e-5)
 
 
 def test_bench_launcher_refuses_missing_devices():
