@@ -1096,7 +1096,8 @@ static void small_batch(Device* d, Device::SmallSlot* sl, SmallReq* const* rq, u
         fprintf(stderr, "[jb] k_small %llu bytes, %u calls: stage+launch %.2f us, sync %.2f us; phases (us):",
                 (unsigned long long)nbytes, n, us(c0, c1), us(c1, c2));
         for (int q = 0; q < 15; q++) fprintf(stderr, " %.2f", h[SM_CLK + q] * 0.01);
-        fprintf(stderr, "; %u clocks", h[SM_CLK + 15]);
+        fprintf(stderr, "; %u clocks (walk end %u, viterbi fwd %u, traceback %u)", h[SM_CLK + 15], h[SM_CLK + 16],
+                h[SM_CLK + 17], h[SM_CLK + 18]);
         fprintf(stderr, "\n");
     }
     if (h[SM_ERR]) {  // the reference panics on some document: find whose (each call alone)

@@ -3688,6 +3688,8 @@ __global__ __launch_bounds__(256) void k_mask_merge(const uint32_t* __restrict__
 //   7  token bitmaps -> spans, per-document first tokens, counters
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSmallSlots = kSmallBytes / 3u + 2u;
+constexpr uint32_t kSmZero = kSmallSlots - 1u;  // (Han ordinals are < kSmallBytes / 3 + 1)
+constexpr uint32_t kSmM1 = 0x8000u;
 constexpr uint32_t kSmallWords = kSmallBytes / 32u + 2u;
 
 struct SmallLds {
@@ -3710,8 +3712,11 @@ struct SmallLds {
     uint16_t hord[kSmallSlots];   // Han ordinal, at the slot
     // per Han rune, by ordinal h (the runes of a block have consecutive ordinals)
     uint32_t rlw[kSmallSlots];       // DAG edge lengths, a byte each, ascending (0: none); 0xFF: more than 4
-    alignas(16) double rw[kSmallSlots][4];  // their weights (pieceFreq, :511-519)
-    double sbest[kSmallSlots];
+    alignas(16) double rw[kSmallSlots][4];  // their weights (pieceFreq, :511-519); NaN past the last
+    alignas(8) uint16_t ra[kSmallSlots][4];  // byte offset in sbest of best(h + L) per item (kSmZero's at the block's end);
+                                             // item 0's bit 15 (kSmM1): L = 1 inside the block (the chain's register)
+    uint32_t slowb[kSmallSlots / 32u + 1u];  // by the ordinal of a block's first Han rune: the block needs the literal fold
+    double sbest[kSmallSlots];       // (index kSmZero holds 0.0: best(n), :522-525)
     uint8_t sL[kSmallSlots];         // chosen piece length (0: none, the reference panics)
     uint8_t sbl[kSmallSlots];        // Viterbi labels (traceback)
     uint8_t bp4[kSmallSlots][4];     // Viterbi back-pointer of each state (quad lane = state)
@@ -3777,7 +3782,8 @@ __device__ __forceinline__ double quad_perm_f64(double x) {
 // (stateChange, :24-29) from the other lanes with DPP, so a rune is one short
 // chain instead of four serial routes.  Lane 0 then runs the traceback and emits.
 template <class E>
-__device__ void sm_viterbi(SmallLds& s, uint32_t ha, uint32_t re, uint32_t m, E& em, uint32_t ql) {
+__device__ void sm_viterbi(SmallLds& s, uint32_t ha, uint32_t re, uint32_t m, E& em, uint32_t ql,
+                           uint64_t* xc = nullptr) {
     const uint32_t rs = s.hpos[ha];
     if (m == 1) {  // always "S" for a single rune (:672-674)
         if (ql == 0) em.token(rs, re);
@@ -3805,6 +3811,7 @@ __device__ void sm_viterbi(SmallLds& s, uint32_t ha, uint32_t re, uint32_t m, E&
     }
     em.ties += nt;
     const double vE = quad_perm_f64<0xAA>(vv), vS = quad_perm_f64<0xFF>(vv);
+    if (xc) xc[1] = __builtin_amdgcn_s_memtime();  // (JB_DEBUG sub-phase clocks: forward half done)
     if (ql != 0) return;
     // traceback (:715-729): stops at the first "" route, and cutHMM then labels the
     // runes from the run start (viterbi_back)
@@ -3824,6 +3831,51 @@ __device__ void sm_viterbi(SmallLds& s, uint32_t ha, uint32_t re, uint32_t m, E&
         --t;
         --h;
     }
+    if (xc) xc[2] = __builtin_amdgcn_s_memtime();  // (traceback done)
+    uint32_t ts = rs;
+    for (uint32_t k = 0; k < m - reset; k++) {
+        const uint32_t lab = s.sbl[h + k];
+        const uint32_t qa = ha + k + 1u < ha + m ? s.hpos[ha + k + 1u] : re;  // end of rune k
+        if (lab >= (uint32_t)JB_E) {
+            em.token(ts, qa);
+            ts = qa;
+        }
+    }
+}
+
+// The end of a run's viterbi (:723-729) + traceback + cutHMM, after its forward half
+// ran inside the fused forward walk (k_small): vv is lane ql's value of state ql at the
+// run's last rune; the run is ordinals [ha, ha + m), ending at byte re.
+template <class E>
+__device__ void sm_vit_finish(SmallLds& s, uint32_t ha, uint32_t re, uint32_t m, double vv, E& em, uint32_t ql,
+                              uint64_t* xc) {
+    const uint32_t rs = s.hpos[ha];
+    if (m == 1) {  // always "S" for a single rune (:672-674)
+        if (ql == 0) em.token(rs, re);
+        return;
+    }
+    const double vE = quad_perm_f64<0xAA>(vv), vS = quad_perm_f64<0xFF>(vv);
+    if (xc) xc[1] = __builtin_amdgcn_s_memtime();
+    if (ql != 0) return;
+    // traceback (:715-729): stops at the first "" route, and cutHMM then labels the
+    // runes from the run start (viterbi_back)
+    uint32_t st = vE > vS ? (uint32_t)JB_E : (uint32_t)JB_S, t = m - 1u, reset = 0, h = ha + m - 1u;
+    for (;;) {
+        if (t == 0) {
+            s.sbl[h] = (uint8_t)st;
+            break;
+        }
+        const uint32_t code = s.bp4[h][st];
+        s.sbl[h] = (uint8_t)st;
+        if (code == 2u) {
+            reset = t;
+            break;
+        }
+        st = (st == JB_B || st == JB_S) ? 2u + code : code;  // B,S <- {E,S}; M,E <- {B,M}
+        --t;
+        --h;
+    }
+    if (xc) xc[2] = __builtin_amdgcn_s_memtime();
     uint32_t ts = rs;
     for (uint32_t k = 0; k < m - reset; k++) {
         const uint32_t lab = s.sbl[h + k];
@@ -3880,10 +3932,14 @@ __device__ void sm_nonzh(const uint8_t* tx, uint32_t bs, uint32_t be, E& em) {
 // threads, 4 bytes each in the byte phases (16 bytes each ran every phase as one long
 // dependent instruction chain per wave); a batch gets as many waves as its bytes need.
 constexpr uint32_t kSmallThreads = 1024;
-constexpr uint32_t kSmallPer = kSmallBytes / kSmallThreads;  // bytes per thread in the byte phases
-static_assert(kSmallPer == 4u, "a thread's bytes are one 4-bit field of a 32-bit word");
+static_assert(kSmallBytes / kSmallThreads == 4u, "4 bytes per thread at most in the byte phases");
+constexpr uint32_t kSmallOneByte = 64;  // a batch up to this many bytes: one wave, one byte per lane
 
-template <bool HMM>
+// PER: bytes per thread in the byte phases (a thread's bytes are one PER-bit field of a
+// 32-bit bitmap word): 4, or 1 for a batch of at most kSmallOneByte bytes, whose one
+// wave then runs every byte phase as one step instead of a loop of four (a sentence's
+// widths phase took 1.6 us as four dependent rounds of LDS reads)
+template <bool HMM, uint32_t PER>
 __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restrict__ text, uint32_t nbytes,
                                                          const uint64_t* __restrict__ doc_off, uint32_t ndocs,
                                                          DevImage im, uint32_t* __restrict__ out, uint32_t seq,
@@ -3892,6 +3948,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
     const uint32_t t = threadIdx.x;
     const uint32_t nw = (nbytes + 31u) / 32u;
     uint64_t clk[16];  // phase clocks (100 MHz), thread 0: header words SM_CLK..
+    uint64_t xc[3] = {0, 0, 0};  // sub-phase shader clocks of the last block (thread 0): header words 24..26
     uint64_t cyc0 = 0;
     if (t == 0) {
         clk[0] = __builtin_amdgcn_s_memrealtime();
@@ -3917,6 +3974,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
     for (uint32_t d = t; d <= ndocs; d += nt)
         s.doff[d] = doc_off ? (uint16_t)min(doc_off[d], (uint64_t)nbytes) : in.doff[d];
     for (uint32_t i = t; i < kSmallWords; i += nt) s.docb[i] = s.rsb[i] = s.hsb[i] = s.bsb[i] = s.sb[i] = s.eb[i] = 0u;
+    for (uint32_t i = t; i < kSmallSlots / 32u + 1u; i += nt) s.slowb[i] = 0u;
     if (t == 0) s.err = s.ties = s.nzh = 0u;
     __syncthreads();
     if (t == 0) clk[1] = __builtin_amdgcn_s_memrealtime();
@@ -3927,10 +3985,11 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
     __syncthreads();
     if (t == 0) clk[2] = __builtin_amdgcn_s_memrealtime();
     // widths at lead bytes: thread t owns bytes [4t, 4t + 4)
-    const uint32_t p0 = kSmallPer * t, sh = p0 & 31u;
+    static_assert(PER == 1u || PER == 4u, "PER bytes per thread");
+    const uint32_t p0 = PER * t, sh = p0 & 31u;
     uint32_t hanm = 0;  // Han lead bytes of the thread's 4
 #pragma unroll
-    for (uint32_t k = 0; k < kSmallPer; k++) {
+    for (uint32_t k = 0; k < PER; k++) {
         const uint32_t p = p0 + k;
         uint32_t w = 1;
         if (p < nbytes && s.txt[p] >= 0xC0u) {
@@ -3948,7 +4007,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
     // 2. rune starts: bytes that no valid sequence of the 3 bytes before covers
     uint32_t rs4 = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < kSmallPer; k++) {
+    for (uint32_t k = 0; k < PER; k++) {
         const uint32_t p = p0 + k;
         const bool cov = (p >= 1u && s.wd[p - 1u] >= 2u) || (p >= 2u && s.wd[p - 2u] >= 3u) ||
                          (p >= 3u && s.wd[p - 3u] >= 4u);
@@ -4013,18 +4072,36 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
     }
     __syncthreads();
     if (t == 0) clk[6] = __builtin_amdgcn_s_memrealtime();
-    // 5. DAG edges of every Han rune
+    // 5. DAG edges of every Han rune, and the DP step's descriptor: weights (NaN for
+    // absent items), where each item's best(h + L) is, and whether item 0 takes
+    // best(h + 1) from the chain's register
+    if (t == 0) s.sbest[kSmZero] = 0.0;
     for (uint32_t h = t; h < nh; h += nt) {
         const uint32_t p = s.hpos[h];
         uint32_t n = 0, lw = 0;
-        sm_walk(s, im, p, [&](uint32_t L, uint32_t, double w) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            s.rw[h][k] = __builtin_nan("");
+            s.ra[h][k] = (uint16_t)(kSmZero * 8u);
+        }
+        sm_walk(s, im, p, [&](uint32_t L, uint32_t qe, double w) {
             if (n < 4u) {
                 lw |= L << (8u * n);
                 s.rw[h][n] = w;
+                // the piece ends at the block's end unless a Han rune of the same block starts at qe
+                const bool inside = sm_bit(s.hsb, qe) && !sm_bit(s.bsb, qe);
+                s.ra[h][n] = (uint16_t)((inside ? h + L : kSmZero) * 8u | (n == 0u && L == 1u && inside ? kSmM1 : 0u));
             }
             n++;
         });
         s.rlw[h] = n <= 4u ? lw : 0xFFu;
+        if (n > 4u || n == 0u || !im.plainw) {  // (no item: the reference panics later)
+            // the literal fold for this rune's block: its bit at the block's first Han rune
+            uint32_t w = p >> 5, m = s.bsb[w] & (0xFFFFFFFFu >> (31u - (p & 31u)));
+            while (!m) m = s.bsb[--w];
+            const uint32_t h0 = s.hord[(32u * w + 31u - (uint32_t)__builtin_clz(m)) / 3u];
+            atomicOr(&s.slowb[h0 >> 5], 1u << (h0 & 31u));
+        }
     }
     __syncthreads();
     if (t == 0) clk[7] = __builtin_amdgcn_s_memrealtime();
@@ -4042,69 +4119,177 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
             continue;
         }
         // backward DP (calcDagProba, :502-548) over the block's runes, ordinals [h0, h1):
-        // best(h) from best(h + L), best(h1) = 0.0.  The next rune's record is read
-        // while this one folds; best(h + 1) stays in a register, the others come from LDS.
+        // best(h) from best(h + L), best(h1) = 0.0.  A step is the chain of item 0's sum
+        // (best(h + 1) from a register, or its LDS value) into the closed fold below; the
+        // next rune's descriptor was read a step earlier and its best(h + L >= 2) values
+        // are read at the start of this step (they were written by the steps before:
+        // a wave's LDS accesses complete in order), so no LDS round trip is on the chain.
         const uint32_t h0 = s.hord[bs / 3u], h1 = s.hord[z_prev(v, be, bs) / 3u] + 1u;
         uint32_t h = h1 - 1u;
-        uint32_t lw = s.rlw[h];
-        double w0 = s.rw[h][0], w1 = s.rw[h][1], w2 = s.rw[h][2], w3 = s.rw[h][3];
-        double bnx = 0.0;
-        for (;;) {
-            const uint32_t hp = h > h0 ? h - 1u : h;
-            const uint32_t lwn = s.rlw[hp];
-            const double n0 = s.rw[hp][0], n1 = s.rw[hp][1], n2 = s.rw[hp][2], n3 = s.rw[hp][3];
-            double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT;  // maxIndexProba's state (:565-578)
-            uint32_t bestL = 0, lastL = 0;
-            auto item = [&](uint32_t L, double w, double nb) {
-                const double pp = w + (h + L == h1 ? 0.0 : (L == 1u ? bnx : nb));  // pieceProba (:519-529)
-                const bool take = pp >= prevP;
-                bestL = take ? L : bestL;
-                bestP = take ? pp : bestP;
-                prevP = pp;
-                lastL = L;
+        if (!((s.slowb[h0 >> 5] >> (h0 & 31u)) & 1u)) {
+            // Up to 4 items per rune without a branch: an absent item has a NaN weight, so
+            // its sum is NaN and no compare takes it.  With finite or -Inf weights (plainw)
+            // the reference's "last item k with p_k >= p_(k-1)" (p_0 = minFloat; none: the
+            // last item) is then p3 if p3 >= p2, else p2 if p2 >= p1, else p1 if p1 >= p0,
+            // else p0 (the first item alone, or -Inf).  The selects are v_bfi_b32 on masks
+            // (bitsel64: as ternaries the compiler made branches of them), and the register
+            // sets of three consecutive runes rotate by unrolling, not by copies.
+            struct Rn {
+                double w0, w1, w2, w3, b0, b1, b2, b3;
+                uint32_t ra0, ra1, lw;
             };
-            if (lw == 0xFFu || !im.plainw) {  // more than 4 edges (walk the rune again), or +Inf/NaN weights
+            auto load_desc = [&](Rn& r, uint32_t i) {
+                const double4 w = *reinterpret_cast<const double4*>(s.rw[i]);
+                r.w0 = w.x; r.w1 = w.y; r.w2 = w.z; r.w3 = w.w;
+                const uint2 a = *reinterpret_cast<const uint2*>(s.ra[i]);
+                r.ra0 = a.x;
+                r.ra1 = a.y;
+                r.lw = s.rlw[i];
+            };
+            auto load_b = [&](Rn& r) {  // (item 0's L = 1 value is the chain's register)
+                const char* const sb = reinterpret_cast<const char*>(s.sbest);
+                r.b0 = *reinterpret_cast<const double*>(sb + (r.ra0 & 0x7FFFu));
+                r.b1 = *reinterpret_cast<const double*>(sb + (r.ra0 >> 16));
+                r.b2 = *reinterpret_cast<const double*>(sb + (r.ra1 & 0xFFFFu));
+                r.b3 = *reinterpret_cast<const double*>(sb + (r.ra1 >> 16));
+            };
+            auto fold = [&](const Rn& r, uint32_t hh, double bnx) {
+                const uint32_t m1 = (r.ra0 & kSmM1) ? ~0u : 0u;
+                const double p0 = r.w0 + bitsel64(m1, bnx, r.b0);  // pieceProba (:519-529)
+                const double p1 = r.w1 + r.b1, p2 = r.w2 + r.b2, p3 = r.w3 + r.b3;
+                const uint32_t k3 = p3 >= p2 ? ~0u : 0u, k2 = p2 >= p1 ? ~0u : 0u, k1 = p1 >= p0 ? ~0u : 0u;
+                const uint32_t kh = k3 | k2;
+                const double best = bitsel64(kh, bitsel64(k3, p3, p2), bitsel64(k1, p1, p0));
+                const uint32_t sh = (kh & k3 & 24u) | (kh & ~k3 & 16u) | (~kh & k1 & 8u);  // 8 x the item's index
+                s.sbest[hh] = best;
+                s.sL[hh] = (uint8_t)(r.lw >> sh);
+                return best;
+            };
+            auto clampd = [&](uint32_t i, uint32_t d) { return i >= h0 + d ? i - d : h0; };
+            Rn A, B, C;
+            load_desc(A, h);
+            load_b(A);
+            load_desc(B, clampd(h, 1u));
+            double bnx = 0.0;
+            for (;;) {
+                load_b(B);  // rune h - 1's best(h - 1 + L >= 2): written by the steps before
+                load_desc(C, clampd(h, 2u));
+                bnx = fold(A, h, bnx);
+                if (h == h0) break;
+                --h;
+                load_b(C);
+                load_desc(A, clampd(h, 2u));
+                bnx = fold(B, h, bnx);
+                if (h == h0) break;
+                --h;
+                load_b(A);
+                load_desc(B, clampd(h, 2u));
+                bnx = fold(C, h, bnx);
+                if (h == h0) break;
+                --h;
+            }
+        } else {
+            // a rune with more than 4 edges (walked again), none, or +Inf/NaN weights: the
+            // literal rule of maxIndexProba (:565-578) over the block, from LDS
+            for (double bnx = 0.0;; --h) {
+                double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT;
+                uint32_t bestL = 0, lastL = 0;
+                auto item = [&](uint32_t L, double w) {
+                    const double pp = w + (h + L == h1 ? 0.0 : (L == 1u ? bnx : s.sbest[h + L]));  // (:519-529)
+                    const bool take = pp >= prevP;
+                    bestL = take ? L : bestL;
+                    bestP = take ? pp : bestP;
+                    prevP = pp;
+                    lastL = L;
+                };
+                const uint32_t lw = s.rlw[h];
                 if (lw == 0xFFu) {
-                    sm_walk(s, im, s.hpos[h], [&](uint32_t L, uint32_t, double w) { item(L, w, s.sbest[h + L]); });
+                    sm_walk(s, im, s.hpos[h], [&](uint32_t L, uint32_t, double w) { item(L, w); });
                 } else {
                     const uint32_t L0 = lw & 0xFFu, L1 = (lw >> 8) & 0xFFu, L2 = (lw >> 16) & 0xFFu, L3 = lw >> 24;
-                    if (L0) item(L0, w0, s.sbest[h + L0]);
-                    if (L1) item(L1, w1, s.sbest[h + L1]);
-                    if (L2) item(L2, w2, s.sbest[h + L2]);
-                    if (L3) item(L3, w3, s.sbest[h + L3]);
+                    if (L0) item(L0, s.rw[h][0]);
+                    if (L1) item(L1, s.rw[h][1]);
+                    if (L2) item(L2, s.rw[h][2]);
+                    if (L3) item(L3, s.rw[h][3]);
                 }
                 if (bestL == 0) {  // no item qualified: the last item (or none: tail -1)
                     bestL = lastL;
                     bestP = prevP;
                 }
-            } else {
-                // Up to 4 items without a branch: an absent item (L = 0) has a NaN sum, which
-                // no compare takes.  With finite or -Inf weights (plainw) the reference's "last
-                // item k with p_k >= p_(k-1)" (p_0 = minFloat; none: the last item) is then p3
-                // if p3 >= p2, else p2 if p2 >= p1, else p1 if p1 >= p0, else p0 (the first item
-                // alone, or -Inf).  (With NaN weights no item qualifies and the reference takes
-                // the last one: the literal fold above.)
-                const uint32_t L0 = lw & 0xFFu, L1 = (lw >> 8) & 0xFFu, L2 = (lw >> 16) & 0xFFu, L3 = lw >> 24;
-                const double b0 = s.sbest[h + L0], b1 = s.sbest[h + L1], b2 = s.sbest[h + L2], b3 = s.sbest[h + L3];
-                auto sum = [&](uint32_t L, double w, double nb) {  // pieceProba (:519-529)
-                    const double pp = w + (h + L == h1 ? 0.0 : (L == 1u ? bnx : nb));
-                    return L ? pp : __builtin_nan("");
-                };
-                const double p0 = sum(L0, w0, b0), p1 = sum(L1, w1, b1), p2 = sum(L2, w2, b2), p3 = sum(L3, w3, b3);
-                const bool c3 = p3 >= p2, c2 = p2 >= p1, c1 = p1 >= p0;
-                bestP = c3 ? p3 : (c2 ? p2 : (c1 ? p1 : p0));
-                bestL = c3 ? L3 : (c2 ? L2 : (c1 ? L1 : L0));
-                bestP = L0 ? bestP : JB_MIN_FLOAT;  // (no item: the reference panics later, sL = 0)
+                s.sbest[h] = bestP;
+                s.sL[h] = (uint8_t)bestL;
+                bnx = bestP;
+                if (h == h0) break;
             }
-            s.sbest[h] = bestP;
-            s.sL[h] = (uint8_t)bestL;
-            if (h == h0) break;
-            bnx = bestP;
-            h = hp;
-            lw = lwn;
-            w0 = n0; w1 = n1; w2 = n2; w3 = n3;
         }
         if (t == 0) clk[12] = __builtin_amdgcn_s_memrealtime();
+#ifndef JB_SM_FUSED
+#define JB_SM_FUSED 1
+#endif
+#if JB_SM_FUSED
+        // forward path (findDagPath, :552-562) fused with the forward half of each HMM
+        // run's viterbi (cutZh, :221-255; viterbi, :668-730): a single-rune piece is one
+        // Viterbi step of the run it extends (lane ql of the quad holds state ql and takes
+        // its two candidates from the other lanes by DPP).  The next piece's length, start
+        // and emission are read a piece ahead, during this piece's step.
+        bool ok = true;
+        {
+            // B <- (E, S), M <- (B, M), E <- (B, M), S <- (E, S)
+            const double ta = ql == 0 ? T_EB : (ql == 1 ? T_BM : (ql == 2 ? T_BE : T_ES));
+            const double tb = ql == 0 ? T_SB : (ql == 1 ? T_MM : (ql == 2 ? T_ME : T_SS));
+            const double st0 = ql == 0 ? START_B : (ql == 3 ? START_S : JB_MIN_FLOAT);
+            uint32_t m = 0, run_h = 0, nt = 0;
+            double vv = 0.0;
+            h = h0;
+            uint32_t L = s.sL[h], p = s.hpos[h];
+            double e = HMM ? s.sem[h][ql] : 0.0;
+            while (h < h1) {
+                if (L == 0) {  // tail index -1: cutDAG's slice panics in the reference
+                    ok = false;
+                    break;
+                }
+                const uint32_t hn = h + L, hq = hn < h1 ? hn : h;  // (the next piece; past the block: unused)
+                const uint32_t Ln = s.sL[hq], pq = s.hpos[hq];
+                const double en = HMM ? s.sem[hq][ql] : 0.0;
+                const uint32_t pn = hn < h1 ? pq : be;
+                if (HMM && L == 1u) {
+                    if (m == 0) {
+                        vv = st0 + e;
+                        run_h = h;
+                    } else {
+                        const double a = quad_perm_f64<2 | (0 << 2) | (0 << 4) | (2 << 6)>(vv) + ta;
+                        const double b = quad_perm_f64<3 | (1 << 2) | (1 << 4) | (3 << 6)>(vv) + tb;
+                        // stateTransitionRoute (:736-756): strict '>' against minFloat, code 2 = no route
+                        uint32_t c = 2u;
+                        double best = JB_MIN_FLOAT;
+                        if (a > best) { c = 0u; best = a; }
+                        if (b > best) { c = 1u; best = b; }
+                        nt += (a == b && a > JB_MIN_FLOAT) ? 1u : 0u;
+                        vv = best + e;
+                        s.bp4[h][ql] = (uint8_t)c;
+                    }
+                    m++;
+                } else {
+                    if (HMM && m) {
+                        sm_vit_finish(s, run_h, p, m, vv, em, ql, nullptr);
+                        m = 0;
+                    }
+                    if (ql == 0) em.token(p, pn);
+                }
+                h = hn;
+                L = Ln;
+                p = pn;
+                e = en;
+            }
+            em.ties += nt;
+            if (t == 0) xc[0] = __builtin_amdgcn_s_memtime();  // (forward walk done)
+            if (HMM && ok && m) sm_vit_finish(s, run_h, be, m, vv, em, ql, t == 0 ? xc : nullptr);
+        }
+        if (!ok) {
+            if (ql == 0) s.err = 1u;
+            continue;
+        }
+#else
         // forward path (findDagPath, :552-562) + HMM runs (cutZh, :221-255)
         uint32_t run_h = 0, run_n = 0;
         bool ok = true;
@@ -4133,7 +4318,9 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
             if (ql == 0) s.err = 1u;
             continue;
         }
-        if (HMM && run_n) sm_viterbi(s, run_h, be, run_n, em, ql);
+        if (t == 0) xc[0] = __builtin_amdgcn_s_memtime();  // (forward walk done)
+        if (HMM && run_n) sm_viterbi(s, run_h, be, run_n, em, ql, t == 0 ? xc : nullptr);
+#endif
         if (t == 0) clk[13] = __builtin_amdgcn_s_memrealtime();
     }
     em.flush();
@@ -4176,6 +4363,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
         out[SM_ZHBLOCKS] = s.nzh;
         for (int k = 1; k < 16; k++) out[SM_CLK + k - 1] = (uint32_t)(clk[k] - clk[0]);
         out[SM_CLK + 15] = (uint32_t)(__builtin_amdgcn_s_memtime() - cyc0);  // shader clock cycles
+        for (int k = 0; k < 3; k++) out[SM_CLK + 16 + k] = xc[k] ? (uint32_t)(xc[k] - cyc0) : 0u;
     }
     // every thread's writes reach host memory before the completion word
     __threadfence_system();
@@ -4193,14 +4381,18 @@ hipError_t run_small(const DevImage& im, const uint8_t* text, uint32_t nbytes, c
     if ((!text || !doc_off) && (text || doc_off || nbytes > kSmallInline || ndocs > kSmallInlineDocs))
         return hipErrorInvalidValue;
     // as many waves as the byte phases need (4 bytes per thread): a sentence is one
-    // wave, whose barriers and scans cost next to nothing
+    // wave, whose barriers and scans cost next to nothing (and up to 64 bytes, one byte per lane)
     const uint32_t nt = std::max(64u, (nbytes + 4u * 64u - 1u) / (4u * 64u) * 64u);
-    if (hmm)
-        hipLaunchKernelGGL((k_small<true>), dim3(1), dim3(nt), 0, stream, text, nbytes, doc_off, ndocs, im, out, seq,
-                           in);
-    else
-        hipLaunchKernelGGL((k_small<false>), dim3(1), dim3(nt), 0, stream, text, nbytes, doc_off, ndocs, im, out, seq,
-                           in);
+#define JB_SMALL_LAUNCH(H, P)                                                                                    \
+    hipLaunchKernelGGL((k_small<H, P>), dim3(1), dim3(nt), 0, stream, text, nbytes, doc_off, ndocs, im, out, seq, in)
+    if (nbytes <= kSmallOneByte) {
+        if (hmm) JB_SMALL_LAUNCH(true, 1u);
+        else JB_SMALL_LAUNCH(false, 1u);
+    } else {
+        if (hmm) JB_SMALL_LAUNCH(true, 4u);
+        else JB_SMALL_LAUNCH(false, 4u);
+    }
+#undef JB_SMALL_LAUNCH
     return hipGetLastError();
 }
 

@@ -515,7 +515,7 @@ def test_long_block_4byte_rune_after_junk(tmp_path, syn_small, monkeypatch):
         pool = [chr(c) for c in range(0x4E00, 0x4E00 + 2000)]
         han = "".join(rng.choice(pool) for _ in range(12000))
         junk = [han[:6000], han[6000:]]  # every slot of both blocks gets a record
-        with4 = [han[:1500] + "\U00020000" + han[1500:5999], "\U00020000" + han[6000:11999]]
+        with4 = [han[:1500] + "\U00020000" + han[1502:6000], "\U00020000" + han[6002:12000]]
         assert sum(len(t.encode()) for t in with4) <= sum(len(t.encode()) for t in junk)
         for hmm in (False, True):
             for texts in (junk, with4):

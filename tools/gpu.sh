@@ -17,6 +17,7 @@
 #   conc              the concurrent-Cut test (16 threads x 1,000 jb_cut calls), its rates printed
 #   hostprobe         the host-batch tests and tools/host_probe.py (host-memory pipeline clocks)
 #   stamps:V          per-wave phase clocks of the headline from STAMPS build V (lib_st or a variant)
+#   sclk:V            k_small phase clocks (JB_DEBUG) on the benchmark sentence and a 4 KiB batch, library V
 # usage: RUN=r05a bash tools/gpu.sh test ab:nosort req:lib req:nosort
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -109,6 +110,11 @@ EOF
       JB_LIB=$L JB_STAMPS=1 timeout -k 10 200 python -u bench.py --no-parity --no-e2e --no-profile --no-latency \
         --steps 2 --warmup 1 ${BENCH_ARGS:-} > "$OUT/stamps_$v.json" 2> "$OUT/stamps_$v.err" || fail "$step" "$OUT/stamps_$v.err"
       grep "\[jb\]" "$OUT/stamps_$v.err" | tail -3 ;;
+    sclk:*)
+      v=${step#sclk:}
+      JB_LIB=$(libof "$v") JB_DEBUG=1 timeout -k 10 200 python -u tools/small_clocks.py > "$OUT/sclk_$v.log" 2> "$OUT/sclk_$v.err" \
+        || fail "$step" "$OUT/sclk_$v.err"
+      cat "$OUT/sclk_$v.log"; grep "k_small" "$OUT/sclk_$v.err" | tail -1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
