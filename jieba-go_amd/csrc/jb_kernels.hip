@@ -3703,6 +3703,7 @@ struct SmallLds {
     uint32_t eb[kSmallWords];      // token last bytes
     uint32_t swp[kSmallWords];     // token starts before each word
     uint32_t scan[16];
+    uint64_t clk[19];  // phase clocks of thread 0 (JB_DEBUG): 0..15 realtime, 16..18 shader cycles of the last run
     uint32_t nh, nblk, nzh, err, ties;
     uint16_t doff[kSmallDocs + 1];  // document offsets
     uint16_t hpos[kSmallSlots];     // Han rune starts, text order
@@ -3947,12 +3948,13 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
     __shared__ SmallLds s;
     const uint32_t t = threadIdx.x;
     const uint32_t nw = (nbytes + 31u) / 32u;
-    uint64_t clk[16];  // phase clocks (100 MHz), thread 0: header words SM_CLK..
-    uint64_t xc[3] = {0, 0, 0};  // sub-phase shader clocks of the last block (thread 0): header words 24..26
+    uint64_t* const clk = s.clk;  // phase clocks (100 MHz), thread 0: header words SM_CLK.. (in LDS: no registers)
+    uint64_t* const xc = s.clk + 16;  // sub-phase shader clocks of the last run (thread 0): header words 24..26
     uint64_t cyc0 = 0;
     if (t == 0) {
         clk[0] = __builtin_amdgcn_s_memrealtime();
         cyc0 = __builtin_amdgcn_s_memtime();
+        xc[0] = xc[1] = xc[2] = 0;
     }
     const uint32_t nt = blockDim.x;  // a multiple of 64 with 4 * nt >= nbytes (run_small)
     // 1. text (zero past nbytes, up to 64 bytes on) and document offsets -> LDS (one
@@ -4238,25 +4240,24 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
             const double ta = ql == 0 ? T_EB : (ql == 1 ? T_BM : (ql == 2 ? T_BE : T_ES));
             const double tb = ql == 0 ? T_SB : (ql == 1 ? T_MM : (ql == 2 ? T_ME : T_SS));
             const double st0 = ql == 0 ? START_B : (ql == 3 ? START_S : JB_MIN_FLOAT);
-            uint32_t m = 0, run_h = 0, nt = 0;
-            double vv = 0.0;
+            auto rd = [&](uint32_t i) { return min(i, kSmallSlots - 1u); };  // (reads past the block: unused)
+            uint32_t nt = 0;
             h = h0;
-            uint32_t L = s.sL[h], p = s.hpos[h];
-            double e = HMM ? s.sem[h][ql] : 0.0;
+            uint32_t L = s.sL[h];
             while (h < h1) {
                 if (L == 0) {  // tail index -1: cutDAG's slice panics in the reference
                     ok = false;
                     break;
                 }
-                const uint32_t hn = h + L, hq = hn < h1 ? hn : h;  // (the next piece; past the block: unused)
-                const uint32_t Ln = s.sL[hq], pq = s.hpos[hq];
-                const double en = HMM ? s.sem[hq][ql] : 0.0;
-                const uint32_t pn = hn < h1 ? pq : be;
                 if (HMM && L == 1u) {
-                    if (m == 0) {
-                        vv = st0 + e;
-                        run_h = h;
-                    } else {
+                    // a run of single-rune pieces from h: its viterbi's forward half rune by rune,
+                    // the next rune's emission and piece length read a step ahead into register
+                    // sets that alternate (nothing copied out of a load's destination)
+                    const uint32_t ha = h;
+                    double vv = st0 + s.sem[h][ql];
+                    double ea = s.sem[rd(h + 1u)][ql], eb = 0.0;
+                    uint32_t La = s.sL[rd(h + 1u)], Lb = 0, Lx;
+                    auto vstep = [&](double e) {  // rune h + 1
                         const double a = quad_perm_f64<2 | (0 << 2) | (0 << 4) | (2 << 6)>(vv) + ta;
                         const double b = quad_perm_f64<3 | (1 << 2) | (1 << 4) | (3 << 6)>(vv) + tb;
                         // stateTransitionRoute (:736-756): strict '>' against minFloat, code 2 = no route
@@ -4266,24 +4267,41 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
                         if (b > best) { c = 1u; best = b; }
                         nt += (a == b && a > JB_MIN_FLOAT) ? 1u : 0u;
                         vv = best + e;
-                        s.bp4[h][ql] = (uint8_t)c;
+                        s.bp4[h + 1u][ql] = (uint8_t)c;
+                    };
+                    for (;;) {
+                        if (h + 1u >= h1 || La != 1u) {
+                            Lx = La;
+                            break;
+                        }
+                        eb = s.sem[rd(h + 2u)][ql];
+                        Lb = s.sL[rd(h + 2u)];
+                        vstep(ea);
+                        ++h;
+                        if (h + 1u >= h1 || Lb != 1u) {
+                            Lx = Lb;
+                            break;
+                        }
+                        ea = s.sem[rd(h + 2u)][ql];
+                        La = s.sL[rd(h + 2u)];
+                        vstep(eb);
+                        ++h;
                     }
-                    m++;
-                } else {
-                    if (HMM && m) {
-                        sm_vit_finish(s, run_h, p, m, vv, em, ql, nullptr);
-                        m = 0;
-                    }
-                    if (ql == 0) em.token(p, pn);
+                    ++h;  // the run is [ha, h)
+                    const uint32_t re = h < h1 ? s.hpos[h] : be;
+                    if (t == 0) xc[0] = __builtin_amdgcn_s_memtime();  // (JB_DEBUG: the last run's forward half done)
+                    sm_vit_finish(s, ha, re, h - ha, vv, em, ql, t == 0 ? xc : nullptr);
+                    L = Lx;
+                    continue;
                 }
+                const uint32_t hn = h + L, p = s.hpos[h];
+                const uint32_t pn = hn < h1 ? s.hpos[hn] : be;
+                const uint32_t Ln = s.sL[rd(hn)];
+                if (ql == 0) em.token(p, pn);
                 h = hn;
                 L = Ln;
-                p = pn;
-                e = en;
             }
             em.ties += nt;
-            if (t == 0) xc[0] = __builtin_amdgcn_s_memtime();  // (forward walk done)
-            if (HMM && ok && m) sm_vit_finish(s, run_h, be, m, vv, em, ql, t == 0 ? xc : nullptr);
         }
         if (!ok) {
             if (ql == 0) s.err = 1u;
