@@ -17,6 +17,7 @@
 #   conc              the concurrent-Cut test (16 threads x 1,000 jb_cut calls), its rates printed
 #   hostprobe         the host-batch tests and tools/host_probe.py (host-memory pipeline clocks)
 #   stamps:V          per-wave phase clocks of the headline from STAMPS build V (lib_st or a variant)
+#   envab:W:K=V       workload W with the in-tree library, default env against K=V, REPS rounds
 #   sclk:V            k_small phase clocks (JB_DEBUG) on the benchmark sentence and a 4 KiB batch, library V
 # usage: RUN=r05a bash tools/gpu.sh test ab:nosort req:lib req:nosort
 set -o pipefail
@@ -110,6 +111,16 @@ EOF
       JB_LIB=$L JB_STAMPS=1 timeout -k 10 200 python -u bench.py --no-parity --no-e2e --no-profile --no-latency \
         --steps 2 --warmup 1 ${BENCH_ARGS:-} > "$OUT/stamps_$v.json" 2> "$OUT/stamps_$v.err" || fail "$step" "$OUT/stamps_$v.err"
       grep "\[jb\]" "$OUT/stamps_$v.err" | tail -3 ;;
+    envab:*)
+      rest=${step#envab:}; w=${rest%%:*}; kv=${rest#*:}
+      for r in $(seq 1 ${REPS:-2}); do
+        for e in "" "$kv"; do
+          tag=$( [ -z "$e" ] && echo default || echo "${e//=/_}" )
+          env $e timeout -k 10 300 python bench.py --workload "$w" --no-e2e --no-parity ${BENCH_ARGS:-} \
+            > "$OUT/envab_${w}_$tag.$r.json" 2> "$OUT/envab_${w}_$tag.$r.err" || fail "$step" "$OUT/envab_${w}_$tag.$r.err"
+          python -c "import json; d=json.load(open('$OUT/envab_${w}_$tag.$r.json')); print('$w', '$tag', d['ms_per_step'], {k: round(x, 4) for k, x in (d.get('kernels_ms') or {}).items()})"
+        done
+      done ;;
     sclk:*)
       v=${step#sclk:}
       JB_LIB=$(libof "$v") JB_DEBUG=1 timeout -k 10 200 python -u tools/small_clocks.py > "$OUT/sclk_$v.log" 2> "$OUT/sclk_$v.err" \
