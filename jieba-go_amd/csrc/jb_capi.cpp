@@ -537,7 +537,7 @@ static int install_image(Device* d, ImageBufs* b, const Image& img) {
 static void free_work(Work* w) {
     dfree(w->docbits); dfree(w->tile_cnt);
     dfree(w->ttile_cnt); dfree(w->supt); dfree(w->alnum16); dfree(w->erec); dfree(w->lanemask);
-    dfree(w->gbl); dfree(w->lsegb); dfree(w->lmap); dfree(w->lcx); dfree(w->lflag); dfree(w->lbp); dfree(w->gbest); dfree(w->tile4); dfree(w->longblk);
+    dfree(w->gbl); dfree(w->lsegb); dfree(w->lmap); dfree(w->lcx); dfree(w->lpath); dfree(w->lflag); dfree(w->lbp); dfree(w->gbest); dfree(w->tile4); dfree(w->longblk);
     dfree(w->tok_start); dfree(w->tok_end); dfree(w->doc_tok); dfree(w->counters); dfree(w->dbg); dfree(w->dbg_walk);
     *w = Work{};
 }
@@ -572,6 +572,7 @@ static int ensure_work(Device* d, uint64_t nbytes, uint32_t ndocs) {
         const uint64_t nchunk = (nb / (3 * kSeg) + nb / kZhLongMin + 4) / kSeg + 2;  // 64-segment chunks
         HIPCHK(hipMalloc(&w.lmap, nchunk * 256));
         HIPCHK(hipMalloc(&w.lcx, nchunk));
+        HIPCHK(hipMalloc(&w.lpath, nchunk * kSeg * sizeof(uint64_t)));  // per segment
     }
     HIPCHK(hipMalloc(&w.lbp, nb / 3 + 256));
     HIPCHK(hipMalloc(&w.tile4, ntiles * 4));
@@ -689,7 +690,7 @@ static int init_launch_cfg(Device* d) {
         return fail(JB_EINVAL, "JB_SMALL=%d: want 0 (off) .. %u bytes", sm, kSmallBytes);
     lc.small_max = (uint32_t)sm;
     const int ls = env_int("JB_LONG_SPEC", 1);
-    if (ls < 0 || ls > 2) return fail(JB_EINVAL, "JB_LONG_SPEC=%d: want 0, 1 (or 2: testing)", ls);
+    if (ls < 0 || ls > 3) return fail(JB_EINVAL, "JB_LONG_SPEC=%d: want 0, 1, 3 (or 2: testing)", ls);
     lc.long_spec = (uint32_t)ls;
     const int ss = env_int("JB_SMALL_SLOTS", 4);
     if (ss < 1 || ss > 4) return fail(JB_EINVAL, "JB_SMALL_SLOTS=%d: want 1 .. 4", ss);
@@ -801,16 +802,19 @@ static int launch_pipeline_(Device* d, const Work& w, const uint8_t* d_text, uin
         fprintf(stderr, "[jb] k_mark_walk clocks/wave: mark %.0f (staging %.0f) entries %.0f (loads %.0f) walk %.0f "
                         "tail %.0f; trips/wave %.2f\n",
                 b[0] / m, b[6] / m, b[1] / m, b[7] / m, b[2] / m, b[3] / m, b[4] / m);
-        std::vector<uint64_t> sl(64 * 8);
+        std::vector<uint64_t> sl(64 * 16);
         HIPCHK(hipMemcpyAsync(sl.data(), d->w.dbg + 65536 * 4, sl.size() * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        for (int i = 0; i < 64; i++)
-            if (sl[i * 8 + 2])
+        for (int i = 0; i < 64; i++) {  // per wave: run, barrier, windows, slow
+            const uint64_t* o = sl.data() + i * 16;
+            if (o[2])
                 fprintf(stderr, "[jb] k_long_dp wg %d: chain run %llu bar %llu windows %llu slow %llu | "
-                                "helpers run %llu bar %llu\n", i,
-                        (unsigned long long)sl[i * 8], (unsigned long long)sl[i * 8 + 1],
-                        (unsigned long long)sl[i * 8 + 2], (unsigned long long)sl[i * 8 + 3],
-                        (unsigned long long)sl[i * 8 + 4], (unsigned long long)sl[i * 8 + 5]);
+                                "wave 1 run %llu bar %llu | wave 2 run %llu bar %llu (%llu) | wave 3 run %llu bar %llu\n", i,
+                        (unsigned long long)o[0], (unsigned long long)o[1], (unsigned long long)o[2],
+                        (unsigned long long)o[3], (unsigned long long)o[4], (unsigned long long)o[5],
+                        (unsigned long long)o[8], (unsigned long long)o[9], (unsigned long long)o[11],
+                        (unsigned long long)o[12], (unsigned long long)o[13]);
+        }
         HIPCHK(hipMemsetAsync(d->w.dbg + 65536 * 4, 0, sl.size() * 8, s));
         if (const char* wo = getenv("JB_LDW_OUT")) {  // k_long_dp per-window records of block 0
             std::vector<uint64_t> wr(65536 * 2 * 4);

@@ -81,10 +81,12 @@ struct Work {
     uint32_t* lsegb;       // per long block: its first segment (ascending with the block index)
     uint8_t* lmap;         // per 64-segment chunk of a long block: its path-state map (k_long_seg -> k_long_path)
     uint8_t* lcx;          // per chunk: the path state at its start (k_long_path -> k_long_tail)
+    uint64_t* lpath;       // per segment: the runes where a piece of the decided path starts (k_long_pbits -> k_long_dp)
     uint32_t* tile4;       // per tile: a 4-byte Han rune starts in it
     uint8_t* gbl;          // per Han rune: chosen piece length, then Viterbi back-pointers / labels
                            // (+512 bytes: k_zh_long reads 256-slot windows)
-    uint32_t* lflag;       // per long block: 0 cut by k_long_dp's one-lane path, 2 DP done, 1 entries found
+    uint32_t* lflag;       // per long block: 3 decided by k_long_spec (the path chain's), then k_long_dp's
+                           // verdict: 0 cut by its one-lane path, 2 DP done, 1 entries found (or path verified)
     uint8_t* lbp;          // long blocks, per slot: path exit codes (k_long_seg -> k_long_path, k_long_tail)
     double* gbest;         // per Han rune: best proba, kept only for blocks with an edge > 8 runes
     uint32_t* tok_start;
@@ -101,6 +103,7 @@ struct Work {
 enum KernelId {
     K_DOCBITS = 0, K_MARK_WALK, K_ZH, K_NONZH,
     K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_LONG_SPEC, K_LONG_DP, K_LONG_SEG, K_LONG_PATH, K_LONG_TAIL, K_MASK_MERGE,
+    K_LONG_PBITS,
     K_NUM
 };
 extern const char* const kKernelNames[K_NUM];
@@ -122,8 +125,9 @@ struct LaunchCfg {
     uint32_t small_max; // host batches up to this many bytes take k_small (0: never)
     uint32_t zh_tail;        // k_zh: about this many bytes at the batch end go in smaller groups (0: none)
     uint32_t zh_tail_group;  // ... of this many bytes (a multiple of 32, at most the group size)
-    uint32_t long_spec;      // long blocks: speculative choices + decided chain (JB_LONG_SPEC: 1 default, 0 off,
-                             // 2 testing: some choices wrong on purpose, the exact chain redoes the block)
+    uint32_t long_spec;      // long blocks: speculative choices, then (JB_LONG_SPEC) 1 the path chain (default),
+                             // 3 the decided chain (round 4), 0 neither (the exact chain); 2 testing: as 1 with
+                             // some choices wrong on purpose, so that the exact chain redoes the block
 };
 
 // k_zh's group split: g1 groups of grp bytes, then groups of *sgrp bytes to the end.

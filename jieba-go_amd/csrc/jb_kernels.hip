@@ -41,7 +41,7 @@ namespace jb {
 
 const char* const kKernelNames[K_NUM] = {"k_docbits", "k_mark_walk", "k_zh", "k_nonzh", "k_tok_count", "k_scan_tok",
                                          "k_tok_write", "k_doc_tok", "k_long_spec", "k_long_dp", "k_long_seg", "k_long_path",
-                                         "k_long_tail", "k_mask_merge"};
+                                         "k_long_tail", "k_mask_merge", "k_long_pbits"};
 
 // newJiebaHMM literals (tokenizer.go:629-652)
 #define START_B (-0.26268660809250016)
@@ -2271,11 +2271,68 @@ struct LDecided {  // the decided chain's LDS (rune i at i & 1023)
     uint32_t L[kLdDesc];    // the chosen length (verification)
 };
 constexpr uint32_t kSpWin = 256;  // the decided chain's window (ring slots (j & 3) * 256 ..: no wrap inside): 16 loop trips of 4 groups
+// Path states at segment boundaries (findDagPath, :552-562, over a long block cut
+// in 64-rune segments).  Where the path goes on at the start of a segment is one
+// byte x, the same code k_long_seg writes for each rune:
+//   0..254  the next piece starts x runes past the segment's start (x >= 64: the
+//           piece before spans the whole segment)
+//   0xFF    it starts at offset 0, and the piece before is one rune (so a run of
+//           single-rune pieces enters the segment)
+// Crossing segment s maps x to the state at the next boundary: kLpNext.  The
+// state at every boundary follows from composing these maps, which is integer
+// work: exact in any association (unlike the f64 values, VERDICT r04 item 3).
+__device__ __forceinline__ uint32_t lp_next(const uint8_t* codes, uint32_t x) {  // codes: the segment's 64 exit codes
+    return x >= 64u && x != 0xFFu ? x - 64u : codes[x == 0xFFu ? 0u : x];
+}
+// the segment's entry as k_long_tail takes it: first piece start | a one-rune piece ends there << 8;
+// 0xFFFFFFFF when no piece starts in it (or the path ended: runes past the block's n)
+__device__ __forceinline__ uint32_t lp_entry(uint32_t x, uint32_t a, uint32_t n) {
+    const uint32_t o = x == 0xFFu ? 0u : x;
+    if (o >= 64u || a + o >= n) return 0xFFFFFFFFu;
+    return o | (x == 0xFFu ? 256u : 0u);
+}
+constexpr uint32_t kLpMap = 256;    // a chunk map: next state for each of the 256 states
+constexpr uint32_t kLpBatch = 128;  // chunk maps k_long_path stages in LDS at a time (32 KB)
+
+// The 256-entry map of a chunk (64 consecutive segments of one block, each segment's
+// 64 exit codes at sc[k]): the state at the chunk's end for each state at its start,
+// four states per lane walked through the segments (a wave; k_long_spec, k_long_seg).
+__device__ __forceinline__ void lp_compose(const uint8_t (*sc)[kSeg], uint8_t* __restrict__ m, uint32_t lane) {
+    uint32_t x0 = lane, x1 = lane + 64u, x2 = lane + 128u, x3 = lane + 192u;
+    for (uint32_t k = 0; k < kSeg; k++) {  // (four independent chains per lane)
+        x0 = lp_next(sc[k], x0);
+        x1 = lp_next(sc[k], x1);
+        x2 = lp_next(sc[k], x2);
+        x3 = lp_next(sc[k], x3);
+    }
+    m[lane] = (uint8_t)x0;
+    m[lane + 64u] = (uint8_t)x1;
+    m[lane + 128u] = (uint8_t)x2;
+    m[lane + 192u] = (uint8_t)x3;
+}
+
+// The path chain's LDS (k_long_dp, round 5): window jw of kSpWin runes in buffer jw & 3,
+// rune i at ring slot i & 1023.
+struct LPath {
+    double pw[4][kSpWin];     // the window's path runes right to left: w_D, then (the chain) best
+    double dring[kLdDesc];    // best(i)
+    double wd[kLdDesc];       // w_D(i): the decided item's weight (k_long_spec)
+    uint8_t L[kLdDesc];       // D(i): the decided item's length
+    uint64_t pbits[4][kSpWin / kSeg];  // the window's path runes, a bit each
+    uint32_t pcnt[4];
+};
+struct LPrep {  // its prologue: chunk states, then per wave a chunk's exit codes and decisions
+    uint8_t maps[kLpBatch * kLpMap];
+    uint8_t codes[4][kSeg][kSeg];
+    uint8_t decs[4][kSeg][kSeg];
+};
 struct LongLds {
     double ring[kLdRing];  // best(i) at i & 511
     union {
         LDesc desc[kLdDesc];   // rune i at i & 1023
         LDecided dc;           // (the decided chain)
+        LPath lp;              // (the path chain)
+        LPrep pr;              // (its prologue)
     };
     uint8_t cls[kLdDesc];  // rune i's step form: 0 items L = 1..m (m <= 4), 1 other fast forms, 3 slow
     LItem side[4][kLdSide];
@@ -2285,12 +2342,11 @@ struct LongLds {
 // DAG items (L, weight) of rune i of an all-3-byte block [bs, be), ascending L
 // (buildDag's pieces and calcDagProba's pieceFreq, :462-497,511-519): from the
 // rune's record, or by walking the trie when the record overflowed.
+// (long_items_rc: the rune's record rc = erec[bs / 3 + i] already loaded)
 template <class F>
-__device__ __forceinline__ void long_items(const uint8_t* __restrict__ text, const DevImage& im,
-                                           const uint64_t* __restrict__ erec, uint32_t bs, uint32_t be, uint32_t i,
-                                           F&& f) {
+__device__ __forceinline__ void long_items_rc(const uint8_t* __restrict__ text, const DevImage& im, uint64_t rc,
+                                              uint32_t bs, uint32_t be, uint32_t i, F&& f) {
     const uint32_t q = bs + 3u * i;
-    const uint64_t rc = erec[q / 3u];
     uint32_t mk = (uint32_t)rc & 0xFFu;
     if (mk) {  // the edges are in the last popc(mk) fields (the first ones are phantoms)
         for (int k = 4 - __popc(mk); k < 4; k++) {
@@ -2328,6 +2384,13 @@ __device__ __forceinline__ void long_items(const uint8_t* __restrict__ text, con
         id = tt;
         cc = ch;
     }
+}
+
+template <class F>
+__device__ __forceinline__ void long_items(const uint8_t* __restrict__ text, const DevImage& im,
+                                           const uint64_t* __restrict__ erec, uint32_t bs, uint32_t be, uint32_t i,
+                                           F&& f) {
+    long_items_rc(text, im, erec[bs / 3u + i], bs, be, i, f);
 }
 
 // max of two float64 sums that are never NaN: one v_max_f64 (fmax would add a
@@ -2375,8 +2438,10 @@ __global__ __launch_bounds__(64) void k_long_spec(const uint8_t* __restrict__ te
                                                   const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
                                                   const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ counters,
                                                   const uint32_t* __restrict__ tile4, uint8_t* __restrict__ gbl,
-                                                  double* __restrict__ gbest, uint32_t mode) {
+                                                  double* __restrict__ gbest, uint8_t* __restrict__ lcode,
+                                                  uint8_t* __restrict__ lmap, uint32_t* __restrict__ lflag, uint32_t mode) {
     __shared__ double s_ring[kSpecRing][64];
+    __shared__ uint8_t s_cd[64][kSeg];  // the lane's segment: its decisions, then its exit codes
     const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG], lane = threadIdx.x;
     if (!im.plainw) return;  // (k_long_dp runs the exact chain)
     for (uint32_t g0 = blockIdx.x * 64u; g0 < nseg; g0 += gridDim.x * 64u) {  // (wave-uniform)
@@ -2397,10 +2462,16 @@ __global__ __launch_bounds__(64) void k_long_spec(const uint8_t* __restrict__ te
             if (bi == b0) skip = has4;
             pend &= ~__ballot(bi == b0);
         }
-        if (skip) continue;
+        // the block's flag: 3 for k_long_dp's path chain (k_long_path and k_long_pbits find
+        // the path of these choices first); 0 for the others (k_long_dp writes every flag)
+        if (act && g == lsegb[bi]) lflag[bi] = skip || mode == 3u ? 0u : 3u;
+        uint32_t n = 0, a = 0;
+        if (!skip) {
         const uint2 bb = longblk[bi];
-        const uint32_t bs = bb.x, be = bb.y, n = (be - bs) / 3u, s0 = bs / 3u;
-        const uint32_t a = (g - lsegb[bi]) * kSeg, lim = min(a + kSeg, n), top = min(lim + kSpecOver, n);
+        const uint32_t bs = bb.x, be = bb.y, s0 = bs / 3u;
+        n = (be - bs) / 3u;
+        a = (g - lsegb[bi]) * kSeg;
+        const uint32_t lim = min(a + kSeg, n), top = min(lim + kSpecOver, n);
         double bnx = 0.0;  // speculative best(i + 1)
         for (uint32_t i = top; i-- > a;) {
             double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT, bestW = 0.0, lastW = 0.0;
@@ -2428,10 +2499,28 @@ __global__ __launch_bounds__(64) void k_long_spec(const uint8_t* __restrict__ te
             if (i < lim) {
                 // (mode 2, testing only: some choices made wrong on purpose, so that
                 // k_long_dp's verification and exact chain run)
-                gbl[s0 + i] = (uint8_t)(mode == 2u && i % 97u == 0u && bestL > 1u ? 1u : bestL);
+                const uint8_t d = (uint8_t)(mode == 2u && i % 97u == 0u && bestL > 1u ? 1u : bestL);
+                gbl[s0 + i] = d;
                 gbest[s0 + i] = bestW;
+                s_cd[lane][i - a] = d;
             }
         }
+        // the segment's exit codes under these choices (k_long_seg's rule; the path chain
+        // finds the path of the decisions from them)
+        for (uint32_t p = lim; p-- > a;) {
+            const uint32_t L = max(1u, (uint32_t)s_cd[lane][p - a]), q = p + L;
+            const uint8_t c = q >= lim ? (L == 1u ? (uint8_t)0xFFu : (uint8_t)(q - lim)) : s_cd[lane][q - a];
+            s_cd[lane][p - a] = c;
+            lcode[s0 + p] = c;
+        }
+        }
+        // the chunk map of the wave's 64 segments (one block's, with more of it after them)
+        const uint32_t b0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)bi);
+        if (__ballot(!skip && bi == b0 && a + kSeg < n) == ~0ull) {
+            wave_sync();
+            lp_compose(s_cd, lmap + (uint64_t)(g0 / kSeg) * kLpMap, lane);
+        }
+        wave_sync();  // (the next iteration overwrites s_cd)
     }
 }
 
@@ -2441,6 +2530,7 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
                                                  double* __restrict__ gbest, const uint2* __restrict__ longblk,
                                                  uint32_t* __restrict__ counters, uint32_t* __restrict__ sbits,
                                                  uint32_t* __restrict__ ebits, uint32_t* __restrict__ lflag,
+                                                 const uint32_t* __restrict__ lsegb, const uint64_t* __restrict__ lpath,
                                                  uint64_t* __restrict__ dbg, uint32_t spec) {
     __shared__ LongLds S;
 #if JB_STAMPS
@@ -2475,8 +2565,303 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
         }
         const uint32_t n = (be - bs) / 3u, s0 = bs / 3u;  // rune i: bytes bs + 3i, slot s0 + i
         const int32_t J = (int32_t)((n + kLdWin - 1u) / kLdWin);  // windows; runes [n, 256 J) are dummies
-        if (spec && im.plainw) {
-            // ---- the decided chain: best(s) = w_D(s) + best(s + L_D(s)) from k_long_spec's
+        const uint32_t lf = lflag[bi];  // (k_long_spec's; every thread reads it before thread 0 rewrites it)
+        if (lf == 3u) {
+            // ---- the path chain (round 5): only the runes on findDagPath's path through
+            // k_long_spec's choices (k_long_pbits' lpath bits) are a serial chain, best(p) =
+            // w_D(p) + best(next path rune), one f64 add each on lane 0 (wave 0); from their
+            // values every other rune's, best(i) = w_D(i) + best(i + L_D(i)), in parallel (wave
+            // 2: the decided paths off the path soon join it); then every rune's choice is
+            // verified by maxIndexProba over these values (wave 3), as for the decided chain:
+            // the same adds of the same values, so if all choices pass, all values are exact.
+            // Window jw of kSpWin runes: stage (wave 1) at step jw + 1, chain at jw, fill at
+            // jw - 1, verify at jw - 2; buffers jw & 3 (4 windows in flight), a barrier per step. ----
+            const int32_t Jd = (int32_t)((n + kSpWin - 1u) / kSpWin);
+            const uint32_t sb = lsegb[bi];
+            if (tid == 0u) {
+                S.bad = 0u;
+                S.lp.dring[n & (kLdDesc - 1u)] = 0.0;  // best(n), when rune n is past the last window
+            }
+            // window jw's choices (wave 1): w_D and L_D of every rune at its ring slot, and the
+            // path runes' w_D right to left in pw.  Its loads
+            // are issued a step before (stage_load; a barrier does not wait for them).
+            struct StageIn {
+                uint64_t pm[4];  // the four segments' path bits
+                double w[4];     // w_D of rune base + 64 q + lane
+                uint32_t L[4];   // L_D
+            };
+            auto stage_load = [&](int32_t jw, StageIn& X) {
+                const uint32_t base = (uint32_t)jw * kSpWin;
+#pragma unroll
+                for (uint32_t q = 0; q < 4u; q++) {
+                    const uint32_t i = base + kSeg * q + lane;
+                    X.pm[q] = base + kSeg * q < n ? lpath[sb + (uint32_t)jw * 4u + q] : 0ull;
+                    X.w[q] = i < n ? gbest[s0 + i] : 0.0;
+                    X.L[q] = i < n ? (uint32_t)gbl[s0 + i] : 1u;
+                }
+            };
+            auto stage = [&](int32_t jw, const StageIn& X) {
+                const uint32_t b = (uint32_t)jw & 3u, kb = b * kSpWin;
+                const uint32_t c3 = (uint32_t)__popcll(X.pm[3]), c2 = (uint32_t)__popcll(X.pm[2]);
+                const uint32_t c1 = (uint32_t)__popcll(X.pm[1]), c0 = (uint32_t)__popcll(X.pm[0]);
+                const uint32_t above[4] = {c3 + c2 + c1, c3 + c2, c3, 0u};  // path runes in the words above
+                const uint32_t cnt = c3 + c2 + c1 + c0;
+                bool none = false;
+#pragma unroll
+                for (uint32_t q = 0; q < 4u; q++) {
+                    const uint32_t r = kSeg * q + lane;
+                    none |= X.L[q] == 0u;  // no item (the reference panics later): the exact chain
+                    S.lp.wd[kb + r] = X.w[q];
+                    S.lp.L[kb + r] = (uint8_t)max(1u, X.L[q]);
+                    const uint64_t hi = X.pm[q] >> lane;
+                    if (hi & 1ull) S.lp.pw[b][above[q] + (uint32_t)__popcll(hi >> 1)] = X.w[q];
+                }
+                if (none) S.bad = 1u;
+                // (the chain runs to a multiple of 16: x + -0.0 is x, bit for bit)
+                if (cnt + lane < ((cnt + 15u) & ~15u)) S.lp.pw[b][cnt + lane] = -0.0;
+                if (lane == 0u) {
+                    S.lp.pcnt[b] = cnt;
+#pragma unroll
+                    for (uint32_t q = 0; q < 4u; q++) S.lp.pbits[b][q] = X.pm[q];
+                }
+            };
+            // the chain over window j's path runes (wave 0, lane 0), in place in pw: 16 at a
+            // time from registers, the next 16 loaded meanwhile
+            double acc = 0.0;  // best of the path rune after the window (best(n) = 0.0 first)
+            auto chain = [&](int32_t j) {
+                const uint32_t b = (uint32_t)j & 3u;
+                const uint32_t c16 = (uint32_t)__builtin_amdgcn_readfirstlane((int)((S.lp.pcnt[b] + 15u) & ~15u));
+                double* const pw = S.lp.pw[b];
+                struct V16 {
+                    double v[16];
+                };
+                V16 A, B;
+                auto ld = [&](V16& X, uint32_t k) __attribute__((always_inline)) {
+#pragma unroll
+                    for (int t = 0; t < 8; t++) {
+                        const double2 v = *reinterpret_cast<const double2*>(pw + k + 2u * t);
+                        X.v[2 * t] = v.x;
+                        X.v[2 * t + 1] = v.y;
+                    }
+                };
+                // (the 16 sums in 16 registers, stored after the adds: a store's source
+                // register rewritten by the next add held that add back)
+                auto run = [&](const V16& X, uint32_t k) __attribute__((always_inline)) {
+                    double a[16];
+#pragma unroll
+                    for (int t = 0; t < 16; t++) {
+                        acc = X.v[t] + acc;
+                        a[t] = acc;
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int t = 0; t < 8; t++)
+                        *reinterpret_cast<double2*>(pw + k + 2u * t) = make_double2(a[2 * t], a[2 * t + 1]);
+                };
+#if JB_STAMPS
+                st_slow += c16;
+#endif
+                ld(A, 0u);  // (loads past c16 stay inside S and are not used)
+                for (uint32_t k = 0; k < c16; k += 32u) {
+                    ld(B, k + 16u);
+                    __builtin_amdgcn_sched_barrier(0);
+                    run(A, k);
+                    // B used here, before the branch: otherwise the compiler sinks its loads past
+                    // the branch to their use, and the half waits a whole LDS round trip (the
+                    // loads are done by now: this costs nothing)
+                    asm volatile("" ::"v"(B.v[0]), "v"(B.v[2]), "v"(B.v[4]), "v"(B.v[6]), "v"(B.v[8]), "v"(B.v[10]),
+                                 "v"(B.v[12]), "v"(B.v[14]));
+                    if (k + 16u >= c16) break;
+                    ld(A, k + 32u);
+                    run(B, k + 16u);
+                }
+            };
+            // window jw's best values into the ring (wave 2): the path runes', then each other
+            // rune's once its successor's is known, by rounds.  An unknown value is a NaN in the
+            // ring (under plainw no best value is NaN: weights are finite or -Inf, and nothing
+            // adds +Inf); a rune's w_D and successor slot stay in registers, and every round
+            // reads all four successors' values at once.
+            auto fill = [&](int32_t jw) {
+                const uint32_t b = (uint32_t)jw & 3u, base = (uint32_t)jw * kSpWin, kb = b * kSpWin;
+                uint32_t sq[4];
+                double wq[4], vq[4];
+                uint64_t pm[4];
+#pragma unroll
+                for (uint32_t q = 0; q < 4u; q++) pm[q] = S.lp.pbits[b][q];
+                const uint32_t c3 = (uint32_t)__popcll(pm[3]), c2 = (uint32_t)__popcll(pm[2]);
+                const uint32_t c1 = (uint32_t)__popcll(pm[1]);
+                const uint32_t above[4] = {c3 + c2 + c1, c3 + c2, c3, 0u};
+                // a path rune's value from pw (its rank from the right), a rune past the block
+                // 0.0 (so best(n) = 0.0), any other NaN
+#pragma unroll
+                for (uint32_t q = 0; q < 4u; q++) {
+                    const uint32_t r = kSeg * q + lane;
+                    const uint64_t hi = pm[q] >> lane;
+                    const double pv = S.lp.pw[b][(above[q] + (uint32_t)__popcll(hi >> 1)) & (kSpWin - 1u)];
+                    vq[q] = (hi & 1ull) ? pv : base + r >= n ? 0.0 : __builtin_nan("");
+                    sq[q] = (kb + r + S.lp.L[kb + r]) & (kLdDesc - 1u);
+                    wq[q] = S.lp.wd[kb + r];
+                }
+#pragma unroll
+                for (uint32_t q = 0; q < 4u; q++) S.lp.dring[kb + kSeg * q + lane] = vq[q];
+                // a round: every rune still NaN takes w_D + its successor's value (NaN while
+                // that is unknown); all four reads, then all four writes, no branch
+                uint32_t rounds = 0;
+                while (__ballot(vq[0] != vq[0] || vq[1] != vq[1] || vq[2] != vq[2] || vq[3] != vq[3]) != 0ull) {
+                    double v[4];
+#pragma unroll
+                    for (uint32_t q = 0; q < 4u; q++) v[q] = S.lp.dring[sq[q]];
+#pragma unroll
+                    for (uint32_t q = 0; q < 4u; q++) {
+                        vq[q] = vq[q] != vq[q] ? wq[q] + v[q] : vq[q];
+                        S.lp.dring[kb + kSeg * q + lane] = vq[q];
+                    }
+                    rounds++;
+                }
+#if JB_STAMPS
+                st_slow += rounds;
+#else
+                (void)rounds;
+#endif
+            };
+            // every rune's choice by maxIndexProba over the values (wave 3).  A record's items
+            // are the last popc(mk) of its four fields, lengths the bits of mk ascending; an
+            // overflowed record (mk 0) walks the trie (long_items_rc).  The loads run two steps
+            // ahead: at step j the records of window j, the weights of window j + 1 (all 16
+            // fields of each lane's four runes at once), the fold of window j + 2.
+            uint64_t vrc[4];    // records of window j + 1 (loaded the step before)
+            double vwv[4][4];   // weights of window j + 2
+            uint32_t vmk = 0;   // its item masks, a byte per rune
+            auto verify = [&](int32_t j) {
+                uint64_t rn[4];
+                if (j >= 0) {
+#pragma unroll
+                    for (uint32_t q = 0; q < 4u; q++) {
+                        const uint32_t i = (uint32_t)j * kSpWin + kSeg * q + lane;
+                        rn[q] = i < n ? erec[s0 + i] : 0x1ull;  // (past the block: one phantom item)
+                    }
+                }
+                double wn[4][4];
+                uint32_t mkn = 0;
+                if (j + 1 >= 0 && j + 1 < Jd) {
+#pragma unroll
+                    for (uint32_t q = 0; q < 4u; q++) {
+                        mkn |= ((uint32_t)vrc[q] & 0xFFu) << (8u * q);
+#pragma unroll
+                        for (uint32_t k = 0; k < 4u; k++)
+                            wn[q][k] = im.wtab1[(uint32_t)(vrc[q] >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u)];
+                    }
+                }
+                if (j + 2 < Jd) {
+                    // the items' sums: all 16 ring reads at once (an absent field reads best(i + 1),
+                    // unused; the ring holds best(n) = 0.0, so no case for i + L = n), then
+                    // maxIndexProba (:565-578) by selects over the present items, ascending L
+                    const int32_t jv = j + 2;
+                    const uint32_t kb = ((uint32_t)jv & 3u) * kSpWin, base = (uint32_t)jv * kSpWin;
+                    uint32_t Lk[4][4];
+                    double rv[4][4];
+#pragma unroll
+                    for (uint32_t q = 0; q < 4u; q++) {
+                        const uint32_t i = base + kSeg * q + lane;
+                        uint32_t mk = (vmk >> (8u * q)) & 0xFFu;
+                        const uint32_t k0 = 4u - (uint32_t)__popc(mk);
+#pragma unroll
+                        for (uint32_t k = 0; k < 4u; k++) {
+                            const bool pres = k >= k0;
+                            Lk[q][k] = pres ? (uint32_t)__builtin_ctz(mk) + 1u : 0u;
+                            mk = pres ? mk & (mk - 1u) : mk;
+                            rv[q][k] = S.lp.dring[(i + max(1u, Lk[q][k])) & (kLdDesc - 1u)];
+                        }
+                    }
+                    bool bad = false;
+#pragma unroll
+                    for (uint32_t q = 0; q < 4u; q++) {
+                        const uint32_t i = base + kSeg * q + lane;
+                        double prevP = JB_MIN_FLOAT;
+                        uint32_t bestL = 0, lastL = 0;
+#pragma unroll
+                        for (uint32_t k = 0; k < 4u; k++) {
+                            const uint32_t L = Lk[q][k];
+                            const double pp = vwv[q][k] + rv[q][k];
+                            bestL = L != 0u && pp >= prevP ? L : bestL;
+                            prevP = L != 0u ? pp : prevP;
+                            lastL = L != 0u ? L : lastL;
+                        }
+                        bestL = bestL ? bestL : lastL;
+                        if (((vmk >> (8u * q)) & 0xFFu) == 0u && i < n) {  // an overflowed record: walk
+                            DpFold f;
+                            long_items_rc(text, im, 0ull, bs, be, i, [&](uint32_t L, double wt) {
+                                fold_item(f, L, wt + (i + L == n ? 0.0 : S.lp.dring[(i + L) & (kLdDesc - 1u)]));
+                            });
+                            f.finish();
+                            bestL = f.bestL;
+                        }
+                        bad |= i < n && bestL != S.lp.L[kb + kSeg * q + lane];
+                    }
+                    if (bad) S.bad = 1u;
+                }
+#pragma unroll
+                for (uint32_t q = 0; q < 4u; q++) {
+                    vrc[q] = rn[q];
+#pragma unroll
+                    for (uint32_t k = 0; k < 4u; k++) vwv[q][k] = wn[q][k];
+                }
+                vmk = mkn;
+            };
+            // steps j = Jd - 1 .. -2, a barrier each (verify's first fold, of window Jd - 1, at
+            // step Jd - 3); each wave its own loop (one loop with a branch per wave merged the
+            // waves' registers at its join, and waited there for verify's loads in flight)
+#if JB_STAMPS
+#define JB_LP_STEP(body)                                          \
+    for (int32_t j = Jd - 1; j >= -2; --j) {                      \
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();         \
+        body;                                                     \
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();         \
+        __syncthreads();                                          \
+        st_run += t1 - t0;                                        \
+        st_bar += __builtin_amdgcn_s_memtime() - t1;              \
+        st_n++;                                                   \
+    }
+#else
+#define JB_LP_STEP(body)                     \
+    for (int32_t j = Jd - 1; j >= -2; --j) { \
+        body;                                \
+        __syncthreads();                     \
+    }
+#endif
+            if (wave == 0u) {
+                __syncthreads();
+                JB_LP_STEP(if (j >= 0 && lane == 0u) chain(j));
+            } else if (wave == 1u) {
+                StageIn sx;
+                stage_load(Jd - 1, sx);
+                stage(Jd - 1, sx);
+                if (Jd >= 2) stage_load(Jd - 2, sx);
+                __syncthreads();
+                JB_LP_STEP(if (j >= 1) {
+                    stage(j - 1, sx);
+                    if (j >= 2) stage_load(j - 2, sx);
+                });
+            } else if (wave == 2u) {
+                __syncthreads();
+                JB_LP_STEP(if (j >= -1 && j + 1 < Jd) fill(j + 1));
+            } else {
+                __syncthreads();
+                JB_LP_STEP(verify(j));
+            }
+#undef JB_LP_STEP
+            const bool bad = S.bad != 0u;
+#if JB_STAMPS
+            st_slow += bad ? 1000000u : 0u;  // (a block sent to the exact chain)
+#endif
+            if (!bad) {
+                if (tid == 0u) lflag[bi] = 1u;  // the path is the decided one: k_long_seg, k_long_path skip it
+                __syncthreads();
+                continue;
+            }
+            __syncthreads();  // (every thread has read S.bad: the exact chain below reuses the LDS)
+        } else if (spec == 3u && im.plainw) {
+            // ---- the decided chain (round 4, JB_LONG_SPEC=3): best(s) = w_D(s) + best(s + L_D(s)) from k_long_spec's
             // choices (the reference's pieceProba add for the chosen item, :519-529), one add
             // per rune on lane 0; the helper waves stage the choices two windows ahead and
             // verify each finished window: every rune's choice by maxIndexProba over the
@@ -2919,8 +3304,8 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
         __syncthreads();
     }
 #if JB_STAMPS
-    if (lane == 0u && wave < 2u) {  // [0..3] chain: run, barrier, windows, slow windows; [4..7] helper wave 1
-        uint64_t* o = dbg + kDbgLong + blockIdx.x * 8u + wave * 4u;
+    if (lane == 0u) {  // per wave w, [4w .. 4w + 3]: run, barrier, windows, slow (wave 0: the chain)
+        uint64_t* o = dbg + kDbgLong + blockIdx.x * 16u + wave * 4u;
         o[0] = st_run;
         o[1] = st_bar;
         o[2] = st_n;
@@ -2931,28 +3316,6 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
 #endif
 }
 
-// Path states at segment boundaries (findDagPath, :552-562, over a long block cut
-// in 64-rune segments).  Where the path goes on at the start of a segment is one
-// byte x, the same code k_long_seg writes for each rune:
-//   0..254  the next piece starts x runes past the segment's start (x >= 64: the
-//           piece before spans the whole segment)
-//   0xFF    it starts at offset 0, and the piece before is one rune (so a run of
-//           single-rune pieces enters the segment)
-// Crossing segment s maps x to the state at the next boundary: kLpNext.  The
-// state at every boundary follows from composing these maps, which is integer
-// work: exact in any association (unlike the f64 values, VERDICT r04 item 3).
-__device__ __forceinline__ uint32_t lp_next(const uint8_t* codes, uint32_t x) {  // codes: the segment's 64 exit codes
-    return x >= 64u && x != 0xFFu ? x - 64u : codes[x == 0xFFu ? 0u : x];
-}
-// the segment's entry as k_long_tail takes it: first piece start | a one-rune piece ends there << 8;
-// 0xFFFFFFFF when no piece starts in it (or the path ended: runes past the block's n)
-__device__ __forceinline__ uint32_t lp_entry(uint32_t x, uint32_t a, uint32_t n) {
-    const uint32_t o = x == 0xFFu ? 0u : x;
-    if (o >= 64u || a + o >= n) return 0xFFFFFFFFu;
-    return o | (x == 0xFFu ? 256u : 0u);
-}
-constexpr uint32_t kLpMap = 256;    // a chunk map: next state for each of the 256 states
-constexpr uint32_t kLpBatch = 128;  // chunk maps k_long_path stages in LDS at a time (32 KB)
 
 // k_long_seg: one lane per 64-rune segment of a long block that k_long_dp ran
 // the chain for.  The chosen lengths are maxIndexProba over the same sums
@@ -3012,19 +3375,7 @@ __global__ __launch_bounds__(256) void k_long_seg(const uint8_t* __restrict__ te
         const bool inner = act && bi == b0 && a + kSeg < n;
         if (__ballot(inner) == ~0ull) {
             wave_sync();  // (every lane's codes are in LDS)
-            const uint8_t(*sc)[kSeg] = s_bl + (threadIdx.x & ~63u);
-            uint32_t x0 = lane, x1 = lane + 64u, x2 = lane + 128u, x3 = lane + 192u;
-            for (uint32_t k = 0; k < kSeg; k++) {  // (four independent chains per lane)
-                x0 = lp_next(sc[k], x0);
-                x1 = lp_next(sc[k], x1);
-                x2 = lp_next(sc[k], x2);
-                x3 = lp_next(sc[k], x3);
-            }
-            uint8_t* const m = lmap + (uint64_t)(gw / kSeg) * kLpMap;
-            m[lane] = (uint8_t)x0;
-            m[lane + 64u] = (uint8_t)x1;
-            m[lane + 128u] = (uint8_t)x2;
-            m[lane + 192u] = (uint8_t)x3;
+            lp_compose(s_bl + (threadIdx.x & ~63u), lmap + (uint64_t)(gw / kSeg) * kLpMap, lane);
         }
         wave_sync();  // (the next iteration's codes overwrite these)
     }
@@ -3040,14 +3391,14 @@ __global__ __launch_bounds__(256) void k_long_seg(const uint8_t* __restrict__ te
 __global__ __launch_bounds__(64) void k_long_path(const uint2* __restrict__ longblk, const uint32_t* __restrict__ lsegb,
                                                   const uint32_t* __restrict__ counters, uint32_t* __restrict__ lflag,
                                                   const uint8_t* __restrict__ lcode, const uint8_t* __restrict__ lmap,
-                                                  uint8_t* __restrict__ lcx) {
+                                                  uint8_t* __restrict__ lcx, uint32_t want, uint32_t set) {
     __shared__ uint32_t s_m32[kLpBatch * kLpMap / 4u];
     const uint8_t* const s_m = reinterpret_cast<const uint8_t*>(s_m32);
     static_assert(kSeg * kSeg <= kLpBatch * kLpMap, "the first partial chunk's codes fit the map space");
     const uint32_t lane = threadIdx.x;
     const uint32_t nlong = counters[CNT_NLONG];
     for (uint32_t bi = blockIdx.x; bi < nlong; bi += gridDim.x) {
-        if (lflag[bi] != 2u) continue;
+        if (lflag[bi] != want) continue;
         const uint2 bb = longblk[bi];
         const uint32_t n = (bb.y - bb.x) / 3u, s0 = bb.x / 3u, sb = lsegb[bi];
         const uint32_t gend = sb + (n + kSeg - 1u) / kSeg;  // past the block's last segment
@@ -3077,7 +3428,67 @@ __global__ __launch_bounds__(64) void k_long_path(const uint2* __restrict__ long
                 __syncthreads();
             }
         }
-        if (lane == 0u) lflag[bi] = 1u;
+        if (lane == 0u) lflag[bi] = set;
+    }
+}
+
+// k_long_pbits: for the blocks k_long_dp takes by the path chain (lflag 3), the path of
+// findDagPath (:552-562) through k_long_spec's choices, one lane per segment: its entry
+// as k_long_tail finds it (the wave's 64 segments' exit codes crossed in order from
+// the chunk's state, k_long_path's lcx), then the pieces from there by the choices
+// (in LDS); lpath[g] has a bit for each rune where a piece starts.
+__global__ __launch_bounds__(256) void k_long_pbits(const uint2* __restrict__ longblk, const uint32_t* __restrict__ lsegb,
+                                                    const uint32_t* __restrict__ counters,
+                                                    const uint32_t* __restrict__ lflag, const uint8_t* __restrict__ gbl,
+                                                    const uint8_t* __restrict__ lcode, const uint8_t* __restrict__ lcx,
+                                                    uint64_t* __restrict__ lpath) {
+    __shared__ uint4 s_cd[256][kSeg / 16u];  // each lane's segment's exit codes, then its choices
+    const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG], lane = threadIdx.x & 63u;
+    uint32_t* const d = reinterpret_cast<uint32_t*>(s_cd[threadIdx.x]);
+    for (uint32_t gw = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); gw < nseg; gw += gridDim.x * blockDim.x) {
+        const uint32_t g = gw + lane;  // (wave-uniform loop)
+        uint32_t bi = 0, a = 0, n = 0, s0 = 0;
+        bool act = g < nseg;
+        if (act) {
+            bi = long_block_of(lsegb, nlong, g);
+            act = lflag[bi] == 3u;
+        }
+        bool first = false;  // the block's first segment
+        if (act) {
+            const uint2 bb = longblk[bi];
+            const uint32_t sg = lsegb[bi];
+            n = (bb.y - bb.x) / 3u;
+            s0 = bb.x / 3u;
+            a = (g - sg) * kSeg;
+            first = g == sg;
+#pragma unroll
+            for (uint32_t k = 0; k < kSeg / 4u; k++) d[k] = ld4(lcode, (uint64_t)s0 + a + 4u * k);  // (256 bytes of slack)
+        }
+        const uint64_t am = __ballot(act), fm = __ballot(first);
+        wave_sync();
+        uint32_t x = lcx[gw / kSeg], ent = 0xFFFFFFFFu;
+        for (uint32_t k = 0; k < 64u; k++) {
+            if (!((am >> k) & 1ull)) continue;  // (uniform)
+            if ((fm >> k) & 1ull) x = 0u;
+            const uint32_t ak = (uint32_t)__builtin_amdgcn_readlane((int)a, (int)k);
+            const uint32_t nk = (uint32_t)__builtin_amdgcn_readlane((int)n, (int)k);
+            const uint32_t e = lp_entry(x, ak, nk);
+            if (lane == k) ent = e;
+            if (e != 0xFFFFFFFFu || (x != 0xFFu && x >= 64u))
+                x = lp_next(reinterpret_cast<const uint8_t*>(s_cd[(threadIdx.x & ~63u) + k]), x);
+        }
+        wave_sync();  // (every lane is done with the codes)
+        if (act) {
+#pragma unroll
+            for (uint32_t k = 0; k < kSeg / 4u; k++) d[k] = ld4(gbl, (uint64_t)s0 + a + 4u * k);  // (512 bytes of slack)
+            const uint8_t* const dl = reinterpret_cast<const uint8_t*>(d);
+            const uint32_t lim = min(kSeg, n - a);
+            uint64_t bits = 0;
+            if (ent != 0xFFFFFFFFu)
+                for (uint32_t o = ent & 0xFFu; o < lim; o += max(1u, (uint32_t)dl[o])) bits |= 1ull << o;
+            lpath[g] = bits;
+        }
+        wave_sync();  // (the next iteration overwrites the LDS rows)
     }
 }
 
@@ -4481,24 +4892,30 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         // nbytes / 192 + nbytes / kZhLongMin segments), one wave per block
         const uint64_t segs = nbytes / (3u * kSeg) + nbytes / kZhLongMin + 2u;
         const uint32_t gseg = (uint32_t)std::min<uint64_t>(1024u, (segs + 255u) / 256u);
-        const uint32_t spec = lc.long_spec ? 1u : 0u;
+        const uint32_t spec = lc.long_spec;
         if (spec)
             JB_TIMED(K_LONG_SPEC, hipLaunchKernelGGL(k_long_spec, dim3(kSpecGrid), dim3(64), 0, stream, d_text, im,
                                                      w.erec + kErecPad, w.longblk, w.lsegb, w.counters, w.tile4, w.gbl,
-                                                     w.gbest, lc.long_spec));
+                                                     w.gbest, w.lbp, w.lmap, w.lflag, lc.long_spec));
+        if (spec && lc.long_spec != 3u) {  // the path of the decided choices (the path chain's blocks, lflag 3)
+            JB_TIMED(K_LONG_PATH, hipLaunchKernelGGL(k_long_path, dim3(kLongGrid), dim3(64), 0, stream, w.longblk,
+                                                     w.lsegb, w.counters, w.lflag, w.lbp, w.lmap, w.lcx, 3u, 3u));
+            JB_TIMED(K_LONG_PBITS, hipLaunchKernelGGL(k_long_pbits, dim3(gseg), dim3(256), 0, stream, w.longblk, w.lsegb,
+                                                      w.counters, w.lflag, w.gbl, w.lbp, w.lcx, w.lpath));
+        }
         if (hmm)
             JB_TIMED(K_LONG_DP, hipLaunchKernelGGL((k_long_dp<true>), dim3(kLongGrid), dim3(256), 0, stream, d_text, im,
                                                    w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters, w.sbits,
-                                                   w.ebits, w.lflag, w.dbg, spec));
+                                                   w.ebits, w.lflag, w.lsegb, w.lpath, w.dbg, spec));
         else
             JB_TIMED(K_LONG_DP, hipLaunchKernelGGL((k_long_dp<false>), dim3(kLongGrid), dim3(256), 0, stream, d_text, im,
                                                    w.erec + kErecPad, w.gbl, w.gbest, w.longblk, w.counters, w.sbits,
-                                                   w.ebits, w.lflag, w.dbg, spec));
+                                                   w.ebits, w.lflag, w.lsegb, w.lpath, w.dbg, spec));
         JB_TIMED(K_LONG_SEG, hipLaunchKernelGGL(k_long_seg, dim3(gseg), dim3(256), 0, stream, d_text, im,
                                                 w.erec + kErecPad, w.longblk, w.lsegb, w.counters, w.lflag, w.gbest,
                                                 w.gbl, w.lbp, w.lmap));
         JB_TIMED(K_LONG_PATH, hipLaunchKernelGGL(k_long_path, dim3(kLongGrid), dim3(64), 0, stream, w.longblk, w.lsegb,
-                                                 w.counters, w.lflag, w.lbp, w.lmap, w.lcx));
+                                                 w.counters, w.lflag, w.lbp, w.lmap, w.lcx, 2u, 1u));
         // (the Viterbi back-pointers go to gbest's bytes: the exit codes in lbp are read to the end)
         uint8_t* const bp = reinterpret_cast<uint8_t*>(w.gbest);
         if (hmm)
