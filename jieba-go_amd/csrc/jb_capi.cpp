@@ -692,6 +692,10 @@ static int init_launch_cfg(Device* d) {
     const int ls = env_int("JB_LONG_SPEC", 1);
     if (ls < 0 || ls > 3) return fail(JB_EINVAL, "JB_LONG_SPEC=%d: want 0, 1, 3 (or 2: testing)", ls);
     lc.long_spec = (uint32_t)ls;
+    const int lf = env_int("JB_LONG_FUSED", 1);
+    if (lf < 0 || lf > 1) return fail(JB_EINVAL, "JB_LONG_FUSED=%d: want 0 or 1", lf);
+    lc.long_fused = (uint32_t)lf;
+    lc.ncu = std::max(1u, d->ncu);
     const int ss = env_int("JB_SMALL_SLOTS", 4);
     if (ss < 1 || ss > 4) return fail(JB_EINVAL, "JB_SMALL_SLOTS=%d: want 1 .. 4", ss);
     d->small_slots = (uint32_t)ss;
@@ -1439,6 +1443,7 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         const Piece& p = pcs[k];
         HIPCHK(hipEventSynchronize(d->ev_comp[k]));
         const volatile uint32_t* c = d->h_pcnt + k * kSnapWords;
+        if (c[CNT_ERR] & 2u) return fail(JB_EDEVICE, "k_long: a grid barrier ran out of polls");
         if (c[CNT_ERR]) return fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)");
         if (c[CNT_NTOK] != c[CNT_NTOKE])
             return fail(JB_EDEVICE, "internal: %u token starts vs %u ends", c[CNT_NTOK], c[CNT_NTOKE]);

@@ -35,8 +35,10 @@ struct DevImage {
 enum {
     CNT_NTOK = 2,   // token starts
     CNT_NTOKE = 3,  // token ends (== CNT_NTOK when consistent)
-    CNT_ERR = 4,    // bit 0: a zh block reached a tail index -1 (the reference panics)
+    CNT_ERR = 4,    // bit 0: a zh block reached a tail index -1 (the reference panics); bit 1: a k_long
+                    // grid barrier ran out of polls
     CNT_WORK = 5,   // k_zh work counter: next group (kZhGroupBytes of text)
+    CNT_GSYNC = 6,  // k_long's grid barriers (arrivals)
     CNT_TIES = 7,   // exact Viterbi route ties (Q12)
     CNT_NWORDS = 8, // u64 token count lives at u32 slots 8-9 (byte offset 32)
     CNT_NLONG = 10, // long zh blocks k_zh left to k_long_* (u64 with CNT_NLSEG: one atomic)
@@ -103,7 +105,7 @@ struct Work {
 enum KernelId {
     K_DOCBITS = 0, K_MARK_WALK, K_ZH, K_NONZH,
     K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_LONG_SPEC, K_LONG_DP, K_LONG_SEG, K_LONG_PATH, K_LONG_TAIL, K_MASK_MERGE,
-    K_LONG_PBITS,
+    K_LONG_PBITS, K_LONG,
     K_NUM
 };
 extern const char* const kKernelNames[K_NUM];
@@ -128,6 +130,8 @@ struct LaunchCfg {
     uint32_t long_spec;      // long blocks: speculative choices, then (JB_LONG_SPEC) 1 the path chain (default),
                              // 3 the decided chain (round 4), 0 neither (the exact chain); 2 testing: as 1 with
                              // some choices wrong on purpose, so that the exact chain redoes the block
+    uint32_t long_fused;     // the long-block kernels as one launch, k_long (JB_LONG_FUSED: 1 default, 0 separate)
+    uint32_t ncu;            // the device's CUs (k_long's grid: at most one workgroup per CU)
 };
 
 // k_zh's group split: g1 groups of grp bytes, then groups of *sgrp bytes to the end.

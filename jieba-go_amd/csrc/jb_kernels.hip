@@ -41,7 +41,7 @@ namespace jb {
 
 const char* const kKernelNames[K_NUM] = {"k_docbits", "k_mark_walk", "k_zh", "k_nonzh", "k_tok_count", "k_scan_tok",
                                          "k_tok_write", "k_doc_tok", "k_long_spec", "k_long_dp", "k_long_seg", "k_long_path",
-                                         "k_long_tail", "k_mask_merge", "k_long_pbits"};
+                                         "k_long_tail", "k_mask_merge", "k_long_pbits", "k_long"};
 
 // newJiebaHMM literals (tokenizer.go:629-652)
 #define START_B (-0.26268660809250016)
@@ -2321,18 +2321,12 @@ struct LPath {
     uint64_t pbits[4][kSpWin / kSeg];  // the window's path runes, a bit each
     uint32_t pcnt[4];
 };
-struct LPrep {  // its prologue: chunk states, then per wave a chunk's exit codes and decisions
-    uint8_t maps[kLpBatch * kLpMap];
-    uint8_t codes[4][kSeg][kSeg];
-    uint8_t decs[4][kSeg][kSeg];
-};
 struct LongLds {
     double ring[kLdRing];  // best(i) at i & 511
     union {
         LDesc desc[kLdDesc];   // rune i at i & 1023
         LDecided dc;           // (the decided chain)
         LPath lp;              // (the path chain)
-        LPrep pr;              // (its prologue)
     };
     uint8_t cls[kLdDesc];  // rune i's step form: 0 items L = 1..m (m <= 4), 1 other fast forms, 3 slow
     LItem side[4][kLdSide];
@@ -2434,17 +2428,16 @@ __device__ __forceinline__ uint32_t long_block_of(const uint32_t* __restrict__ l
 constexpr uint32_t kSpecOver = 1024;
 constexpr uint32_t kSpecRing = 256;  // > the longest edge (255 runes)
 constexpr uint32_t kSpecGrid = 256;  // 64-lane workgroups, one per CU (128 KB of LDS each)
-__global__ __launch_bounds__(64) void k_long_spec(const uint8_t* __restrict__ text, DevImage im,
+__device__ __forceinline__ void long_spec_body(const uint8_t* __restrict__ text, DevImage im,
                                                   const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
                                                   const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ counters,
                                                   const uint32_t* __restrict__ tile4, uint8_t* __restrict__ gbl,
                                                   double* __restrict__ gbest, uint8_t* __restrict__ lcode,
-                                                  uint8_t* __restrict__ lmap, uint32_t* __restrict__ lflag, uint32_t mode) {
-    __shared__ double s_ring[kSpecRing][64];
-    __shared__ uint8_t s_cd[64][kSeg];  // the lane's segment: its decisions, then its exit codes
-    const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG], lane = threadIdx.x;
+                                                  uint8_t* __restrict__ lmap, uint32_t* __restrict__ lflag, uint32_t mode,
+        uint32_t wg, uint32_t ng, double (*s_ring)[64], uint8_t (*s_cd)[kSeg]) {
+    const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG], lane = threadIdx.x & 63u;
     if (!im.plainw) return;  // (k_long_dp runs the exact chain)
-    for (uint32_t g0 = blockIdx.x * 64u; g0 < nseg; g0 += gridDim.x * 64u) {  // (wave-uniform)
+    for (uint32_t g0 = wg * 64u; g0 < nseg; g0 += ng * 64u) {  // (wave-uniform)
         const uint32_t g = g0 + lane;
         const bool act = g < nseg;
         const uint32_t bi = act ? long_block_of(lsegb, nlong, g) : 0xFFFFFFFFu;
@@ -2473,37 +2466,108 @@ __global__ __launch_bounds__(64) void k_long_spec(const uint8_t* __restrict__ te
         a = (g - lsegb[bi]) * kSeg;
         const uint32_t lim = min(a + kSeg, n), top = min(lim + kSpecOver, n);
         double bnx = 0.0;  // speculative best(i + 1)
-        for (uint32_t i = top; i-- > a;) {
-            double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT, bestW = 0.0, lastW = 0.0;
-            uint32_t bestL = 0, lastL = 0;
-            long_items(text, im, erec, bs, be, i, [&](uint32_t L, double wt) {
-                const uint32_t j = i + L;
-                const double b = j >= top ? 0.0 : (L == 1u ? bnx : s_ring[j & (kSpecRing - 1u)][lane]);
-                const double pp = wt + b;
-                if (pp >= prevP) {
-                    bestL = L;
-                    bestP = pp;
-                    bestW = wt;
+        // By groups of four runes g .. g + 3, from the top down.  The loads run ahead of the
+        // DP, which then waits only on LDS: a group's records two groups before it, their
+        // weights (all 16 fields at once) one group before.
+        auto ld_rc = [&](int32_t g, uint64_t (&rc)[4]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int32_t r = 0; r < 4; r++) {
+                const int32_t i = g + r;
+                rc[r] = g >= (int32_t)a && i < (int32_t)top ? erec[s0 + (uint32_t)i] : 0x1ull;  // (else unused)
+            }
+        };
+        auto ld_w = [&](const uint64_t (&rc)[4], double (&w)[4][4]) __attribute__((always_inline)) {
+#pragma unroll
+            for (uint32_t r = 0; r < 4u; r++)
+#pragma unroll
+                for (uint32_t k = 0; k < 4u; k++)
+                    w[r][k] = im.wtab1[(uint32_t)(rc[r] >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u)];
+        };
+        auto masks = [](const uint64_t (&rc)[4]) {
+            return ((uint32_t)rc[0] & 0xFFu) | (((uint32_t)rc[1] & 0xFFu) << 8) | (((uint32_t)rc[2] & 0xFFu) << 16) |
+                   (((uint32_t)rc[3] & 0xFFu) << 24);
+        };
+        const int32_t gtop = (int32_t)(a + ((top - a + 3u) & ~3u)) - 4;
+        uint64_t rcn[4];
+        double wc[4][4];
+        uint32_t mkc;
+        {
+            uint64_t rc0[4];
+            ld_rc(gtop, rc0);
+            ld_w(rc0, wc);
+            mkc = masks(rc0);
+            ld_rc(gtop - 4, rcn);
+        }
+        for (int32_t g = gtop; g >= (int32_t)a; g -= 4) {
+            uint64_t rcnn[4];
+            ld_rc(g - 8, rcnn);
+            double wn[4][4];
+            ld_w(rcn, wn);
+            const uint32_t mkn = masks(rcn);
+#pragma unroll
+            for (int32_t r = 3; r >= 0; r--) {
+                const uint32_t i = (uint32_t)(g + r);
+                if (i >= top) continue;  // (the first group's runes past the top)
+                double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT, bestW = 0.0, lastW = 0.0;
+                uint32_t bestL = 0, lastL = 0;
+                uint32_t mk = (mkc >> (8 * r)) & 0xFFu;
+                if (mk) {  // the record's items, the last popc(mk) fields, by selects
+                    const uint32_t k0 = 4u - (uint32_t)__popc(mk);
+#pragma unroll
+                    for (uint32_t k = 0; k < 4u; k++) {
+                        const bool pres = k >= k0;
+                        const uint32_t L = pres ? (uint32_t)__builtin_ctz(mk) + 1u : 1u;
+                        mk = pres ? mk & (mk - 1u) : mk;
+                        const uint32_t j = i + L;
+                        const double rv = s_ring[j & (kSpecRing - 1u)][lane];
+                        const double wt = wc[r][k];
+                        const double pp = wt + (j >= top ? 0.0 : (L == 1u ? bnx : rv));
+                        const bool take = pres && pp >= prevP;
+                        bestL = take ? L : bestL;
+                        bestP = take ? pp : bestP;
+                        bestW = take ? wt : bestW;
+                        prevP = pres ? pp : prevP;
+                        lastL = pres ? L : lastL;
+                        lastW = pres ? wt : lastW;
+                    }
+                } else {  // an overflowed record: walk the trie
+                    long_items_rc(text, im, 0ull, bs, be, i, [&](uint32_t L, double wt) {
+                        const uint32_t j = i + L;
+                        const double b = j >= top ? 0.0 : (L == 1u ? bnx : s_ring[j & (kSpecRing - 1u)][lane]);
+                        const double pp = wt + b;
+                        if (pp >= prevP) {
+                            bestL = L;
+                            bestP = pp;
+                            bestW = wt;
+                        }
+                        prevP = pp;
+                        lastL = L;
+                        lastW = wt;
+                    });
                 }
-                prevP = pp;
-                lastL = L;
-                lastW = wt;
-            });
-            if (bestL == 0) {  // no item qualified: the last item (or none)
-                bestL = lastL;
-                bestP = prevP;
-                bestW = lastW;
+                if (bestL == 0) {  // no item qualified: the last item (or none)
+                    bestL = lastL;
+                    bestP = prevP;
+                    bestW = lastW;
+                }
+                s_ring[i & (kSpecRing - 1u)][lane] = bestP;
+                bnx = bestP;
+                if (i < lim) {
+                    // (mode 2, testing only: some choices made wrong on purpose, so that
+                    // k_long_dp's verification and exact chain run)
+                    const uint8_t d = (uint8_t)(mode == 2u && i % 97u == 0u && bestL > 1u ? 1u : bestL);
+                    gbl[s0 + i] = d;
+                    gbest[s0 + i] = bestW;
+                    s_cd[lane][i - a] = d;
+                }
             }
-            s_ring[i & (kSpecRing - 1u)][lane] = bestP;
-            bnx = bestP;
-            if (i < lim) {
-                // (mode 2, testing only: some choices made wrong on purpose, so that
-                // k_long_dp's verification and exact chain run)
-                const uint8_t d = (uint8_t)(mode == 2u && i % 97u == 0u && bestL > 1u ? 1u : bestL);
-                gbl[s0 + i] = d;
-                gbest[s0 + i] = bestW;
-                s_cd[lane][i - a] = d;
+#pragma unroll
+            for (uint32_t r = 0; r < 4u; r++) {
+                rcn[r] = rcnn[r];
+#pragma unroll
+                for (uint32_t k = 0; k < 4u; k++) wc[r][k] = wn[r][k];
             }
+            mkc = mkn;
         }
         // the segment's exit codes under these choices (k_long_seg's rule; the path chain
         // finds the path of the decisions from them)
@@ -2524,15 +2588,26 @@ __global__ __launch_bounds__(64) void k_long_spec(const uint8_t* __restrict__ te
     }
 }
 
+__global__ __launch_bounds__(64) void k_long_spec(const uint8_t* __restrict__ text, DevImage im,
+                                                  const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
+                                                  const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ counters,
+                                                  const uint32_t* __restrict__ tile4, uint8_t* __restrict__ gbl,
+                                                  double* __restrict__ gbest, uint8_t* __restrict__ lcode,
+                                                  uint8_t* __restrict__ lmap, uint32_t* __restrict__ lflag, uint32_t mode) {
+    __shared__ double s_ring[kSpecRing][64];
+    __shared__ uint8_t s_cd[64][kSeg];  // the lane's segment: its decisions, then its exit codes
+    long_spec_body(text, im, erec, longblk, lsegb, counters, tile4, gbl, gbest, lcode, lmap, lflag, mode, blockIdx.x, gridDim.x, s_ring, s_cd);
+}
+
 template <bool HMM>
-__global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ text, DevImage im,
+__device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, DevImage im,
                                                  const uint64_t* __restrict__ erec, uint8_t* __restrict__ gbl,
                                                  double* __restrict__ gbest, const uint2* __restrict__ longblk,
                                                  uint32_t* __restrict__ counters, uint32_t* __restrict__ sbits,
                                                  uint32_t* __restrict__ ebits, uint32_t* __restrict__ lflag,
                                                  const uint32_t* __restrict__ lsegb, const uint64_t* __restrict__ lpath,
-                                                 uint64_t* __restrict__ dbg, uint32_t spec) {
-    __shared__ LongLds S;
+                                                 uint64_t* __restrict__ dbg, uint32_t spec,
+        uint32_t wg, uint32_t ng, LongLds& S) {
 #if JB_STAMPS
     uint64_t st_run = 0, st_bar = 0, st_n = 0, st_slow = 0;  // diagnostic clocks (wave 0 and wave 1, lane 0)
 #endif
@@ -2540,7 +2615,7 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
     const uint32_t nlong = counters[CNT_NLONG];
     const char* const rb = reinterpret_cast<const char*>(S.ring);
     s_ltab[tid] = ltab_entry(tid);  // (zh_dp's record lengths; 256 threads, read after the barriers below)
-    for (uint32_t bi = blockIdx.x; bi < nlong; bi += gridDim.x) {
+    for (uint32_t bi = wg; bi < nlong; bi += ng) {
         const uint2 bb = longblk[bi];
         const uint32_t bs = bb.x, be = bb.y;
         bool any4 = false;  // a 4-byte Han rune (lead >= 0xF0) anywhere in the block
@@ -3261,7 +3336,7 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
 #if JB_STAMPS
                 const uint64_t t1 = __builtin_amdgcn_s_memtime();
                 st_slow += S.wslow[j & 3] ? 1u : 0u;
-                if (blockIdx.x == 0u && lane == 0u && (uint32_t)j < kDbgLongWinMax) {  // per window of block 0
+                if (wg == 0u && lane == 0u && (uint32_t)j < kDbgLongWinMax) {  // per window of block 0
                     uint64_t* o = dbg + kDbgLongWin + (uint64_t)j * 4u;
                     o[0] = t1 - t0;
                     o[1] = st_wf;
@@ -3305,7 +3380,7 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
     }
 #if JB_STAMPS
     if (lane == 0u) {  // per wave w, [4w .. 4w + 3]: run, barrier, windows, slow (wave 0: the chain)
-        uint64_t* o = dbg + kDbgLong + blockIdx.x * 16u + wave * 4u;
+        uint64_t* o = dbg + kDbgLong + wg * 16u + wave * 4u;
         o[0] = st_run;
         o[1] = st_bar;
         o[2] = st_n;
@@ -3314,6 +3389,18 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
 #else
     (void)dbg;
 #endif
+}
+
+template <bool HMM>
+__global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ text, DevImage im,
+                                                 const uint64_t* __restrict__ erec, uint8_t* __restrict__ gbl,
+                                                 double* __restrict__ gbest, const uint2* __restrict__ longblk,
+                                                 uint32_t* __restrict__ counters, uint32_t* __restrict__ sbits,
+                                                 uint32_t* __restrict__ ebits, uint32_t* __restrict__ lflag,
+                                                 const uint32_t* __restrict__ lsegb, const uint64_t* __restrict__ lpath,
+                                                 uint64_t* __restrict__ dbg, uint32_t spec) {
+    __shared__ LongLds S;
+    long_dp_body<HMM>(text, im, erec, gbl, gbest, longblk, counters, sbits, ebits, lflag, lsegb, lpath, dbg, spec, blockIdx.x, gridDim.x, S);
 }
 
 
@@ -3329,16 +3416,16 @@ __global__ __launch_bounds__(256) void k_long_dp(const uint8_t* __restrict__ tex
 // block's and the block goes on past them, the wave composes their boundary maps
 // into the chunk's map (lmap[c]: state at the chunk's start -> state at its end),
 // four states per lane walked through the 64 segments' codes in LDS.
-__global__ __launch_bounds__(256) void k_long_seg(const uint8_t* __restrict__ text, DevImage im,
+__device__ __forceinline__ void long_seg_body(const uint8_t* __restrict__ text, DevImage im,
                                                   const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
                                                   const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ counters,
                                                   const uint32_t* __restrict__ lflag, const double* __restrict__ gbest,
                                                   uint8_t* __restrict__ gbl, uint8_t* __restrict__ lcode,
-                                                  uint8_t* __restrict__ lmap) {
-    __shared__ uint8_t s_bl[256][kSeg];
+                                                  uint8_t* __restrict__ lmap,
+        uint32_t wg, uint32_t ng, uint8_t (*s_bl)[kSeg]) {
     const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG], lane = threadIdx.x & 63u;
     uint8_t* const my = s_bl[threadIdx.x];
-    for (uint32_t gw = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); gw < nseg; gw += gridDim.x * blockDim.x) {
+    for (uint32_t gw = wg * blockDim.x + (threadIdx.x & ~63u); gw < nseg; gw += ng * blockDim.x) {
         const uint32_t g = gw + lane;  // (the loop is wave-uniform: the chunk map needs the whole wave)
         uint32_t bi = 0xFFFFFFFFu, n = 0, a = 0;
         bool act = g < nseg;
@@ -3381,6 +3468,16 @@ __global__ __launch_bounds__(256) void k_long_seg(const uint8_t* __restrict__ te
     }
 }
 
+__global__ __launch_bounds__(256) void k_long_seg(const uint8_t* __restrict__ text, DevImage im,
+                                                  const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
+                                                  const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ counters,
+                                                  const uint32_t* __restrict__ lflag, const double* __restrict__ gbest,
+                                                  uint8_t* __restrict__ gbl, uint8_t* __restrict__ lcode,
+                                                  uint8_t* __restrict__ lmap) {
+    __shared__ uint8_t s_bl[256][kSeg];
+    long_seg_body(text, im, erec, longblk, lsegb, counters, lflag, gbest, gbl, lcode, lmap, blockIdx.x, gridDim.x, s_bl);
+}
+
 // k_long_path: one wave per long block: the path state (lp_next) at the start of
 // every 64-segment chunk the block spans past its first (lcx[c]).  The segments
 // before the first chunk boundary are crossed one by one (their codes staged in
@@ -3388,16 +3485,16 @@ __global__ __launch_bounds__(256) void k_long_seg(const uint8_t* __restrict__ te
 // time: one LDS lookup per chunk instead of one hop per segment (the serial walk
 // over 15.6K segments of config 5b took 2.1 ms).  k_long_tail finds each
 // segment's entry from these states.
-__global__ __launch_bounds__(64) void k_long_path(const uint2* __restrict__ longblk, const uint32_t* __restrict__ lsegb,
+__device__ __forceinline__ void long_path_body(const uint2* __restrict__ longblk, const uint32_t* __restrict__ lsegb,
                                                   const uint32_t* __restrict__ counters, uint32_t* __restrict__ lflag,
                                                   const uint8_t* __restrict__ lcode, const uint8_t* __restrict__ lmap,
-                                                  uint8_t* __restrict__ lcx, uint32_t want, uint32_t set) {
-    __shared__ uint32_t s_m32[kLpBatch * kLpMap / 4u];
+                                                  uint8_t* __restrict__ lcx, uint32_t want, uint32_t set,
+        uint32_t wg, uint32_t ng, uint32_t* s_m32) {
     const uint8_t* const s_m = reinterpret_cast<const uint8_t*>(s_m32);
     static_assert(kSeg * kSeg <= kLpBatch * kLpMap, "the first partial chunk's codes fit the map space");
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nlong = counters[CNT_NLONG];
-    for (uint32_t bi = blockIdx.x; bi < nlong; bi += gridDim.x) {
+    for (uint32_t bi = wg; bi < nlong; bi += ng) {
         if (lflag[bi] != want) continue;
         const uint2 bb = longblk[bi];
         const uint32_t n = (bb.y - bb.x) / 3u, s0 = bb.x / 3u, sb = lsegb[bi];
@@ -3408,9 +3505,9 @@ __global__ __launch_bounds__(64) void k_long_path(const uint2* __restrict__ long
             if (g1 > sb) {  // the segments before it, one by one (lcode has 512 bytes of slack)
                 const uint32_t nw = (g1 - sb) * (kSeg / 4u);
                 for (uint32_t k = lane; k < nw; k += 64u) s_m32[k] = ld4(lcode, (uint64_t)s0 + 4u * k);
-                __syncthreads();
+                wave_sync();
                 for (uint32_t j = 0; j < g1 - sb; j++) x = lp_next(s_m + j * kSeg, x);
-                __syncthreads();
+                wave_sync();
             }
             for (uint32_t c0 = g1 / kSeg; c0 * kSeg < gend; c0 += kLpBatch) {
                 // chunks c0 .. (the maps of the ones wholly inside the block with more after them)
@@ -3420,16 +3517,24 @@ __global__ __launch_bounds__(64) void k_long_path(const uint2* __restrict__ long
                 const uint32_t nw = (cmap - c0) * (kLpMap / 4u);
                 const uint32_t* gm = reinterpret_cast<const uint32_t*>(lmap + (uint64_t)c0 * kLpMap);
                 for (uint32_t k = lane; k < nw; k += 64u) s_m32[k] = gm[k];
-                __syncthreads();
+                wave_sync();
                 for (uint32_t c = c0; c < cend; c++) {
                     if (lane == 0u) lcx[c] = (uint8_t)x;
                     if (c < cmap) x = s_m[(c - c0) * kLpMap + x];
                 }
-                __syncthreads();
+                wave_sync();
             }
         }
         if (lane == 0u) lflag[bi] = set;
     }
+}
+
+__global__ __launch_bounds__(64) void k_long_path(const uint2* __restrict__ longblk, const uint32_t* __restrict__ lsegb,
+                                                  const uint32_t* __restrict__ counters, uint32_t* __restrict__ lflag,
+                                                  const uint8_t* __restrict__ lcode, const uint8_t* __restrict__ lmap,
+                                                  uint8_t* __restrict__ lcx, uint32_t want, uint32_t set) {
+    __shared__ uint32_t s_m32[kLpBatch * kLpMap / 4u];
+    long_path_body(longblk, lsegb, counters, lflag, lcode, lmap, lcx, want, set, blockIdx.x, gridDim.x, s_m32);
 }
 
 // k_long_pbits: for the blocks k_long_dp takes by the path chain (lflag 3), the path of
@@ -3437,15 +3542,15 @@ __global__ __launch_bounds__(64) void k_long_path(const uint2* __restrict__ long
 // as k_long_tail finds it (the wave's 64 segments' exit codes crossed in order from
 // the chunk's state, k_long_path's lcx), then the pieces from there by the choices
 // (in LDS); lpath[g] has a bit for each rune where a piece starts.
-__global__ __launch_bounds__(256) void k_long_pbits(const uint2* __restrict__ longblk, const uint32_t* __restrict__ lsegb,
+__device__ __forceinline__ void long_pbits_body(const uint2* __restrict__ longblk, const uint32_t* __restrict__ lsegb,
                                                     const uint32_t* __restrict__ counters,
                                                     const uint32_t* __restrict__ lflag, const uint8_t* __restrict__ gbl,
                                                     const uint8_t* __restrict__ lcode, const uint8_t* __restrict__ lcx,
-                                                    uint64_t* __restrict__ lpath) {
-    __shared__ uint4 s_cd[256][kSeg / 16u];  // each lane's segment's exit codes, then its choices
+                                                    uint64_t* __restrict__ lpath,
+        uint32_t wg, uint32_t ng, uint4 (*s_cd)[kSeg / 16u]) {
     const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG], lane = threadIdx.x & 63u;
     uint32_t* const d = reinterpret_cast<uint32_t*>(s_cd[threadIdx.x]);
-    for (uint32_t gw = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); gw < nseg; gw += gridDim.x * blockDim.x) {
+    for (uint32_t gw = wg * blockDim.x + (threadIdx.x & ~63u); gw < nseg; gw += ng * blockDim.x) {
         const uint32_t g = gw + lane;  // (wave-uniform loop)
         uint32_t bi = 0, a = 0, n = 0, s0 = 0;
         bool act = g < nseg;
@@ -3490,6 +3595,15 @@ __global__ __launch_bounds__(256) void k_long_pbits(const uint2* __restrict__ lo
         }
         wave_sync();  // (the next iteration overwrites the LDS rows)
     }
+}
+
+__global__ __launch_bounds__(256) void k_long_pbits(const uint2* __restrict__ longblk, const uint32_t* __restrict__ lsegb,
+                                                    const uint32_t* __restrict__ counters,
+                                                    const uint32_t* __restrict__ lflag, const uint8_t* __restrict__ gbl,
+                                                    const uint8_t* __restrict__ lcode, const uint8_t* __restrict__ lcx,
+                                                    uint64_t* __restrict__ lpath) {
+    __shared__ uint4 s_cd[256][kSeg / 16u];  // each lane's segment's exit codes, then its choices
+    long_pbits_body(longblk, lsegb, counters, lflag, gbl, lcode, lcx, lpath, blockIdx.x, gridDim.x, s_cd);
 }
 
 // Viterbi (tokenizer.go:668-730) + cutHMM (:273-285) of the run of single-rune
@@ -3564,17 +3678,17 @@ __device__ void long_viterbi(const uint8_t* __restrict__ text, const DevImage& i
 // The Viterbi back-pointers go to bp (gbest's bytes, free by now), not over the
 // exit codes other waves still read.
 template <bool HMM>
-__global__ __launch_bounds__(256) void k_long_tail(const uint8_t* __restrict__ text, DevImage im,
+__device__ __forceinline__ void long_tail_body(const uint8_t* __restrict__ text, DevImage im,
                                                    const uint8_t* __restrict__ gbl, const uint2* __restrict__ longblk,
                                                    const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ lflag,
                                                    uint32_t* __restrict__ counters, const uint8_t* __restrict__ lcode,
                                                    const uint8_t* __restrict__ lcx, uint8_t* __restrict__ bp,
-                                                   uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits) {
-    __shared__ uint4 s_cd[256][kSeg / 16u];  // each lane's segment's exit codes
+                                                   uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
+        uint32_t wg, uint32_t ng, uint4 (*s_cd)[kSeg / 16u]) {
     const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG], lane = threadIdx.x & 63u;
     Emitter em(sbits, ebits);
     bool bad = false;
-    for (uint32_t gw = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); gw < nseg; gw += gridDim.x * blockDim.x) {
+    for (uint32_t gw = wg * blockDim.x + (threadIdx.x & ~63u); gw < nseg; gw += ng * blockDim.x) {
         const uint32_t g = gw + lane;  // (wave-uniform loop)
         uint32_t bi = 0, a = 0, n = 0;
         bool act = g < nseg;
@@ -3641,6 +3755,99 @@ __global__ __launch_bounds__(256) void k_long_tail(const uint8_t* __restrict__ t
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) t += (uint32_t)__shfl_xor((int)t, d, 64);
     if ((threadIdx.x & 63u) == 0u && t) atomicAdd(counters + CNT_TIES, t);
+}
+
+template <bool HMM>
+__global__ __launch_bounds__(256) void k_long_tail(const uint8_t* __restrict__ text, DevImage im,
+                                                   const uint8_t* __restrict__ gbl, const uint2* __restrict__ longblk,
+                                                   const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ lflag,
+                                                   uint32_t* __restrict__ counters, const uint8_t* __restrict__ lcode,
+                                                   const uint8_t* __restrict__ lcx, uint8_t* __restrict__ bp,
+                                                   uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits) {
+    __shared__ uint4 s_cd[256][kSeg / 16u];  // each lane's segment's exit codes
+    long_tail_body<HMM>(text, im, gbl, longblk, lsegb, lflag, counters, lcode, lcx, bp, sbits, ebits, blockIdx.x, gridDim.x, s_cd);
+}
+
+// ---------------------------------------------------------------------------
+// k_long: the long-block kernels above as the phases of one launch (VERDICT r04
+// item 5), so that a batch without a long block (CNT_NLONG 0: every batch of
+// short documents) pays one launch instead of seven.  A grid barrier between the
+// phases (DESIGN §6's rule for inter-workgroup waits: every thread's stores made
+// visible at agent scope, a counter bumped by one thread per workgroup, polled with
+// agent-scope atomic loads, an acquire fence after; the wait is bounded and sets
+// CNT_ERR bit 1 when it runs out).  One workgroup per CU at most (the phases' LDS,
+// unioned, is 132 KB), and the grid is at most the CU count, so all its workgroups
+// are resident together.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kGridSpins = 1u << 21;  // polls before a grid barrier gives up (seconds)
+__device__ __forceinline__ void grid_sync(uint32_t* cnt, uint32_t target, uint32_t* err) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // (every thread: its stores, device-wide)
+    __syncthreads();
+    if (threadIdx.x == 0u) {
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t spins = 0;
+        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins == kGridSpins) {
+                __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (every thread: the others' stores)
+}
+
+union LongAll {  // the phases' LDS
+    struct {
+        double ring[kSpecRing][64];
+        uint8_t cd[64][kSeg];
+    } sp;                             // k_long_spec (wave 0)
+    LongLds dp;                       // k_long_dp
+    uint32_t m32[kLpBatch * kLpMap / 4u];  // k_long_path (wave 0)
+    uint4 cd4[256][kSeg / 16u];       // k_long_pbits, k_long_tail
+    uint8_t bl[256][kSeg];            // k_long_seg
+};
+
+template <bool HMM>
+__global__ __launch_bounds__(256) void k_long(const uint8_t* __restrict__ text, DevImage im,
+                                              const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
+                                              const uint32_t* __restrict__ lsegb, uint32_t* __restrict__ counters,
+                                              const uint32_t* __restrict__ tile4, uint8_t* __restrict__ gbl,
+                                              double* __restrict__ gbest, uint8_t* __restrict__ lcode,
+                                              uint8_t* __restrict__ lmap, uint8_t* __restrict__ lcx,
+                                              uint64_t* __restrict__ lpath, uint32_t* __restrict__ lflag,
+                                              uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
+                                              uint64_t* __restrict__ dbg, uint32_t spec) {
+    __shared__ LongAll U;
+    if (counters[CNT_NLONG] == 0u) return;  // (the whole grid: k_zh wrote it before this launch)
+    const uint32_t wg = blockIdx.x, ng = gridDim.x;
+    const bool w0 = threadIdx.x < 64u;  // (the one-wave phases)
+    uint32_t* const gs = counters + CNT_GSYNC;
+    uint32_t* const err = counters + CNT_ERR;
+    uint32_t bar = 0;
+    if (spec) {
+        if (w0)
+            long_spec_body(text, im, erec, longblk, lsegb, counters, tile4, gbl, gbest, lcode, lmap, lflag, spec, wg,
+                           ng, U.sp.ring, U.sp.cd);
+        grid_sync(gs, ++bar * ng, err);
+        if (spec != 3u) {
+            if (w0) long_path_body(longblk, lsegb, counters, lflag, lcode, lmap, lcx, 3u, 3u, wg, ng, U.m32);
+            grid_sync(gs, ++bar * ng, err);
+            long_pbits_body(longblk, lsegb, counters, lflag, gbl, lcode, lcx, lpath, wg, ng, U.cd4);
+            grid_sync(gs, ++bar * ng, err);
+        }
+    }
+    long_dp_body<HMM>(text, im, erec, gbl, gbest, longblk, counters, sbits, ebits, lflag, lsegb, lpath, dbg, spec,
+                      wg, ng, U.dp);
+    grid_sync(gs, ++bar * ng, err);
+    long_seg_body(text, im, erec, longblk, lsegb, counters, lflag, gbest, gbl, lcode, lmap, wg, ng, U.bl);
+    grid_sync(gs, ++bar * ng, err);
+    if (w0) long_path_body(longblk, lsegb, counters, lflag, lcode, lmap, lcx, 2u, 1u, wg, ng, U.m32);
+    grid_sync(gs, ++bar * ng, err);
+    // (the Viterbi back-pointers go to gbest's bytes: the exit codes in lcode are read to the end)
+    long_tail_body<HMM>(text, im, gbl, longblk, lsegb, lflag, counters, lcode, lcx, reinterpret_cast<uint8_t*>(gbest),
+                        sbits, ebits, wg, ng, U.cd4);
 }
 
 // ---------------------------------------------------------------------------
@@ -4893,6 +5100,20 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         const uint64_t segs = nbytes / (3u * kSeg) + nbytes / kZhLongMin + 2u;
         const uint32_t gseg = (uint32_t)std::min<uint64_t>(1024u, (segs + 255u) / 256u);
         const uint32_t spec = lc.long_spec;
+        if (lc.long_fused) {
+            // one workgroup per 64 segments (k_long_spec's lanes), at most one per CU
+            const uint32_t gl = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(lc.ncu, (segs + 63u) / 64u));
+            if (hmm)
+                JB_TIMED(K_LONG, hipLaunchKernelGGL((k_long<true>), dim3(gl), dim3(256), 0, stream, d_text, im,
+                                                    w.erec + kErecPad, w.longblk, w.lsegb, w.counters, w.tile4, w.gbl,
+                                                    w.gbest, w.lbp, w.lmap, w.lcx, w.lpath, w.lflag, w.sbits, w.ebits,
+                                                    w.dbg, spec));
+            else
+                JB_TIMED(K_LONG, hipLaunchKernelGGL((k_long<false>), dim3(gl), dim3(256), 0, stream, d_text, im,
+                                                    w.erec + kErecPad, w.longblk, w.lsegb, w.counters, w.tile4, w.gbl,
+                                                    w.gbest, w.lbp, w.lmap, w.lcx, w.lpath, w.lflag, w.sbits, w.ebits,
+                                                    w.dbg, spec));
+        } else {
         if (spec)
             JB_TIMED(K_LONG_SPEC, hipLaunchKernelGGL(k_long_spec, dim3(kSpecGrid), dim3(64), 0, stream, d_text, im,
                                                      w.erec + kErecPad, w.longblk, w.lsegb, w.counters, w.tile4, w.gbl,
@@ -4926,6 +5147,7 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
             JB_TIMED(K_LONG_TAIL, hipLaunchKernelGGL((k_long_tail<false>), dim3(gseg), dim3(256), 0, stream, d_text, im,
                                                      w.gbl, w.longblk, w.lsegb, w.lflag, w.counters, w.lbp, w.lcx, bp,
                                                      w.sbits, w.ebits));
+        }
     }
     {
         const uint32_t nw = (uint32_t)((nbytes + 1023u) / 1024u);  // alnum16 words

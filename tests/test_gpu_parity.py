@@ -465,9 +465,10 @@ def test_record_overflow_paths(tmp_path, syn_small, kind, nfill):
         tk.close()
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("spec", ["1", "0", "2", "3"])
 @pytest.mark.parametrize("kind", [J.JB_DICT_TXT, J.JB_DICT_PREFIX])
-def test_long_blocks_many(tmp_path, syn_small, kind, spec, monkeypatch):
+def test_long_blocks_many(tmp_path, syn_small, kind, spec, fused, monkeypatch):
     """The k_long_* kernels: several long blocks in one batch, sharing path-bitmap
     words across a 1-byte gap and across a document boundary; edges longer than
     a 64-rune segment (a piece spans whole segments); runes with more than 4
@@ -475,8 +476,10 @@ def test_long_blocks_many(tmp_path, syn_small, kind, spec, monkeypatch):
     walks the trie itself).  With the speculative choices and the path chain
     (JB_LONG_SPEC=1, the default), with the decided chain (3), with the exact chain
     alone (0), and with wrong choices planted (2: the verification must send every
-    block to the exact chain)."""
+    block to the exact chain).  The long-block kernels as one launch (k_long, JB_LONG_FUSED=1,
+    the default: phases behind grid barriers) and as separate launches (0)."""
     monkeypatch.setenv("JB_LONG_SPEC", spec)
+    monkeypatch.setenv("JB_LONG_FUSED", fused)
     _, ep, _ = syn_small
     rng = random.Random(5)
     pool = [chr(c) for c in range(0x4E00, 0x4E00 + 300)]
