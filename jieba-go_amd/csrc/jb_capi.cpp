@@ -667,9 +667,8 @@ static int init_launch_cfg(Device* d) {
     lc.zh_wide = wide;
     const int grp = env_int("JB_ZH_GROUP", 0);
     if (grp != 0) {
-        if (grp < (int)kZhGroupSmall || grp > (int)kZhGroupBytes || grp % 32 != 0)
-            return fail(JB_EINVAL, "JB_ZH_GROUP=%d: want a multiple of 32 in [%u, %u]", grp, kZhGroupSmall,
-                        kZhGroupBytes);
+        if (grp < 256 || grp > (int)kZhGroupBytes || grp % 32 != 0)
+            return fail(JB_EINVAL, "JB_ZH_GROUP=%d: want a multiple of 32 in [256, %u]", grp, kZhGroupBytes);
         lc.zh_group = (uint32_t)grp;
     }
     const int zt = env_int("JB_ZH_TAIL_KIB", 0), ztg = env_int("JB_ZH_TAIL_GROUP", 1024);

@@ -2314,7 +2314,8 @@ __device__ __forceinline__ void lp_compose(const uint8_t (*sc)[kSeg], uint8_t* _
 // The path chain's LDS (k_long_dp, round 5): window jw of kSpWin runes in buffer jw & 3,
 // rune i at ring slot i & 1023.
 struct LPath {
-    double pw[4][kSpWin];     // the window's path runes right to left: w_D, then (the chain) best
+    double pw[4][kSpWin];     // the window's path runes right to left: w_D, then (fill) best
+    double ck[4][kSpWin / 16u + 1u];  // the chain's sum before the window, then after every 16 path runes
     double dring[kLdDesc];    // best(i)
     double wd[kLdDesc];       // w_D(i): the decided item's weight (k_long_spec)
     uint8_t L[kLdDesc];       // D(i): the decided item's length
@@ -2700,8 +2701,11 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
                     for (uint32_t q = 0; q < 4u; q++) S.lp.pbits[b][q] = X.pm[q];
                 }
             };
-            // the chain over window j's path runes (wave 0, lane 0), in place in pw: 16 at a
-            // time from registers, the next 16 loaded meanwhile
+            // the chain over window j's path runes (wave 0, lane 0): 16 at a time from
+            // registers, the next 16 loaded meanwhile.  It stores only its sum before the window
+            // and after every 16 runes (ck): one wave's LDS stores cost it more than its adds
+            // (a 16-byte store per two sums: 24 cycles per sum against 12.6 with these
+            // checkpoints, tools/diag/pchain.hip); fill redoes the same adds from them.
             double acc = 0.0;  // best of the path rune after the window (best(n) = 0.0 first)
             auto chain = [&](int32_t j) {
                 const uint32_t b = (uint32_t)j & 3u;
@@ -2719,23 +2723,17 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
                         X.v[2 * t + 1] = v.y;
                     }
                 };
-                // (the 16 sums in 16 registers, stored after the adds: a store's source
-                // register rewritten by the next add held that add back)
+                double* const ck = S.lp.ck[b];
                 auto run = [&](const V16& X, uint32_t k) __attribute__((always_inline)) {
-                    double a[16];
 #pragma unroll
-                    for (int t = 0; t < 16; t++) {
-                        acc = X.v[t] + acc;
-                        a[t] = acc;
-                    }
+                    for (int t = 0; t < 16; t++) acc = X.v[t] + acc;
                     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int t = 0; t < 8; t++)
-                        *reinterpret_cast<double2*>(pw + k + 2u * t) = make_double2(a[2 * t], a[2 * t + 1]);
+                    ck[k / 16u + 1u] = acc;
                 };
 #if JB_STAMPS
                 st_slow += c16;
 #endif
+                ck[0] = acc;
                 ld(A, 0u);  // (loads past c16 stay inside S and are not used)
                 for (uint32_t k = 0; k < c16; k += 32u) {
                     ld(B, k + 16u);
@@ -2758,6 +2756,27 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
             // reads all four successors' values at once.
             auto fill = [&](int32_t jw) {
                 const uint32_t b = (uint32_t)jw & 3u, base = (uint32_t)jw * kSpWin, kb = b * kSpWin;
+                {  // the path runes' values: the chain's adds again, 16 per lane from its checkpoints
+                    const uint32_t c16 = (S.lp.pcnt[b] + 15u) & ~15u;
+                    if (lane < c16 / 16u) {
+                        double a = S.lp.ck[b][lane];
+                        double* const pw = S.lp.pw[b] + 16u * lane;
+                        double x[16];
+#pragma unroll
+                        for (int t = 0; t < 8; t++) {
+                            const double2 v = reinterpret_cast<const double2*>(pw)[t];
+                            x[2 * t] = v.x;
+                            x[2 * t + 1] = v.y;
+                        }
+#pragma unroll
+                        for (int t = 0; t < 16; t++) {
+                            a = x[t] + a;
+                            x[t] = a;
+                        }
+#pragma unroll
+                        for (int t = 0; t < 8; t++) reinterpret_cast<double2*>(pw)[t] = make_double2(x[2 * t], x[2 * t + 1]);
+                    }
+                }
                 uint32_t sq[4];
                 double wq[4], vq[4];
                 uint64_t pm[4];
@@ -2863,6 +2882,9 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
                             lastL = L != 0u ? L : lastL;
                         }
                         bestL = bestL ? bestL : lastL;
+#if JB_STAMPS
+                        st_slow += (uint64_t)__popcll(__ballot(((vmk >> (8u * q)) & 0xFFu) == 0u && i < n));
+#endif
                         if (((vmk >> (8u * q)) & 0xFFu) == 0u && i < n) {  // an overflowed record: walk
                             DpFold f;
                             long_items_rc(text, im, 0ull, bs, be, i, [&](uint32_t L, double wt) {
