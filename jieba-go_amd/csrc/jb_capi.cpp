@@ -805,7 +805,7 @@ static int launch_pipeline_(Device* d, const Work& w, const uint8_t* d_text, uin
         fprintf(stderr, "[jb] k_mark_walk clocks/wave: mark %.0f (staging %.0f) entries %.0f (loads %.0f) walk %.0f "
                         "tail %.0f; trips/wave %.2f\n",
                 b[0] / m, b[6] / m, b[1] / m, b[7] / m, b[2] / m, b[3] / m, b[4] / m);
-        std::vector<uint64_t> sl(64 * 16);
+        std::vector<uint64_t> sl(64 * 32);
         HIPCHK(hipMemcpyAsync(sl.data(), d->w.dbg + 65536 * 4, sl.size() * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         for (int i = 0; i < 64; i++) {  // per wave: run, barrier, windows, slow
@@ -817,6 +817,16 @@ static int launch_pipeline_(Device* d, const Work& w, const uint8_t* d_text, uin
                         (unsigned long long)o[3], (unsigned long long)o[4], (unsigned long long)o[5],
                         (unsigned long long)o[8], (unsigned long long)o[9], (unsigned long long)o[11],
                         (unsigned long long)o[12], (unsigned long long)o[13]);
+            const uint64_t* p = sl.data() + 64 * 16 + i * 16;
+            if (o[2])
+                fprintf(stderr, "[jb] k_long_dp wg %d sub-phases: w0 %llu %llu %llu %llu | w1 %llu %llu %llu %llu | "
+                                "w2 %llu %llu %llu %llu | w3 %llu %llu %llu %llu\n", i,
+                        (unsigned long long)p[0], (unsigned long long)p[1], (unsigned long long)p[2],
+                        (unsigned long long)p[3], (unsigned long long)p[4], (unsigned long long)p[5],
+                        (unsigned long long)p[6], (unsigned long long)p[7], (unsigned long long)p[8],
+                        (unsigned long long)p[9], (unsigned long long)p[10], (unsigned long long)p[11],
+                        (unsigned long long)p[12], (unsigned long long)p[13], (unsigned long long)p[14],
+                        (unsigned long long)p[15]);
         }
         HIPCHK(hipMemsetAsync(d->w.dbg + 65536 * 4, 0, sl.size() * 8, s));
         if (const char* wo = getenv("JB_LDW_OUT")) {  // k_long_dp per-window records of block 0

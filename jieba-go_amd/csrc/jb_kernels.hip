@@ -2610,7 +2610,8 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
                                                  uint64_t* __restrict__ dbg, uint32_t spec,
         uint32_t wg, uint32_t ng, LongLds& S) {
 #if JB_STAMPS
-    uint64_t st_run = 0, st_bar = 0, st_n = 0, st_slow = 0;  // diagnostic clocks (wave 0 and wave 1, lane 0)
+    uint64_t st_run = 0, st_bar = 0, st_n = 0, st_slow = 0;  // diagnostic clocks (lane 0 of each wave)
+    uint64_t st_p[4] = {0, 0, 0, 0};  // sub-phase clocks (the path chain's fill and verify)
 #endif
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const uint32_t nlong = counters[CNT_NLONG];
@@ -2756,6 +2757,9 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
             // reads all four successors' values at once.
             auto fill = [&](int32_t jw) {
                 const uint32_t b = (uint32_t)jw & 3u, base = (uint32_t)jw * kSpWin, kb = b * kSpWin;
+#if JB_STAMPS
+                const uint64_t f0 = __builtin_amdgcn_s_memtime();
+#endif
                 {  // the path runes' values: the chain's adds again, 16 per lane from its checkpoints
                     const uint32_t c16 = (S.lp.pcnt[b] + 15u) & ~15u;
                     if (lane < c16 / 16u) {
@@ -2777,43 +2781,67 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
                         for (int t = 0; t < 8; t++) reinterpret_cast<double2*>(pw)[t] = make_double2(x[2 * t], x[2 * t + 1]);
                     }
                 }
-                uint32_t sq[4];
-                double wq[4], vq[4];
+#if JB_STAMPS
+                const uint64_t f1 = __builtin_amdgcn_s_memtime();
+#endif
+                // each lane four consecutive runes r0 .. r0 + 3: a successor inside the lane is
+                // taken from the register of its value in the same round (the four right to left),
+                // so a run of off-path runes resolves a lane at a time
+                const uint32_t r0 = 4u * lane;
                 uint64_t pm[4];
 #pragma unroll
                 for (uint32_t q = 0; q < 4u; q++) pm[q] = S.lp.pbits[b][q];
+                const uint32_t wsel = lane >> 4;  // the word of the lane's four bits
+                const uint64_t pmw = wsel == 0u ? pm[0] : wsel == 1u ? pm[1] : wsel == 2u ? pm[2] : pm[3];
                 const uint32_t c3 = (uint32_t)__popcll(pm[3]), c2 = (uint32_t)__popcll(pm[2]);
                 const uint32_t c1 = (uint32_t)__popcll(pm[1]);
-                const uint32_t above[4] = {c3 + c2 + c1, c3 + c2, c3, 0u};
+                const uint32_t abv = wsel == 0u ? c3 + c2 + c1 : wsel == 1u ? c3 + c2 : wsel == 2u ? c3 : 0u;
+                const uint32_t L4 = *reinterpret_cast<const uint32_t*>(S.lp.L + kb + r0);
+                const double2 w01 = *reinterpret_cast<const double2*>(S.lp.wd + kb + r0);
+                const double2 w23 = *reinterpret_cast<const double2*>(S.lp.wd + kb + r0 + 2u);
+                const double wq[4] = {w01.x, w01.y, w23.x, w23.y};
+                uint32_t tq[4];
+                double vq[4];
                 // a path rune's value from pw (its rank from the right), a rune past the block
                 // 0.0 (so best(n) = 0.0), any other NaN
 #pragma unroll
                 for (uint32_t q = 0; q < 4u; q++) {
-                    const uint32_t r = kSeg * q + lane;
-                    const uint64_t hi = pm[q] >> lane;
-                    const double pv = S.lp.pw[b][(above[q] + (uint32_t)__popcll(hi >> 1)) & (kSpWin - 1u)];
-                    vq[q] = (hi & 1ull) ? pv : base + r >= n ? 0.0 : __builtin_nan("");
-                    sq[q] = (kb + r + S.lp.L[kb + r]) & (kLdDesc - 1u);
-                    wq[q] = S.lp.wd[kb + r];
+                    const uint64_t hi = (pmw >> ((r0 + q) & 63u));
+                    const double pv = S.lp.pw[b][(abv + (uint32_t)__popcll(hi >> 1)) & (kSpWin - 1u)];
+                    vq[q] = (hi & 1ull) ? pv : base + r0 + q >= n ? 0.0 : __builtin_nan("");
+                    tq[q] = r0 + q + ((L4 >> (8u * q)) & 0xFFu);  // the successor's window offset
                 }
-#pragma unroll
-                for (uint32_t q = 0; q < 4u; q++) S.lp.dring[kb + kSeg * q + lane] = vq[q];
+                double2* const dw = reinterpret_cast<double2*>(S.lp.dring + kb + r0);
+                dw[0] = make_double2(vq[0], vq[1]);
+                dw[1] = make_double2(vq[2], vq[3]);
+#if JB_STAMPS
+                const uint64_t f2 = __builtin_amdgcn_s_memtime();
+#endif
                 // a round: every rune still NaN takes w_D + its successor's value (NaN while
-                // that is unknown); all four reads, then all four writes, no branch
+                // that is unknown); the ring reads, the lane's runes right to left, two stores
                 uint32_t rounds = 0;
                 while (__ballot(vq[0] != vq[0] || vq[1] != vq[1] || vq[2] != vq[2] || vq[3] != vq[3]) != 0ull) {
                     double v[4];
 #pragma unroll
-                    for (uint32_t q = 0; q < 4u; q++) v[q] = S.lp.dring[sq[q]];
+                    for (uint32_t q = 0; q < 4u; q++) v[q] = S.lp.dring[(kb + tq[q]) & (kLdDesc - 1u)];
 #pragma unroll
-                    for (uint32_t q = 0; q < 4u; q++) {
-                        vq[q] = vq[q] != vq[q] ? wq[q] + v[q] : vq[q];
-                        S.lp.dring[kb + kSeg * q + lane] = vq[q];
+                    for (int q = 3; q >= 0; q--) {
+                        double sv = v[q];
+                        if (q <= 2) sv = tq[q] == r0 + 3u ? vq[3] : sv;
+                        if (q <= 1) sv = tq[q] == r0 + 2u ? vq[2] : sv;
+                        if (q == 0) sv = tq[q] == r0 + 1u ? vq[1] : sv;
+                        vq[q] = vq[q] != vq[q] ? wq[q] + sv : vq[q];
                     }
+                    dw[0] = make_double2(vq[0], vq[1]);
+                    dw[1] = make_double2(vq[2], vq[3]);
                     rounds++;
                 }
 #if JB_STAMPS
                 st_slow += rounds;
+                const uint64_t f3 = __builtin_amdgcn_s_memtime();
+                st_p[0] += f1 - f0;  // the path runes' values
+                st_p[1] += f2 - f1;  // setup
+                st_p[2] += f3 - f2;  // rounds
 #else
                 (void)rounds;
 #endif
@@ -2827,6 +2855,9 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
             double vwv[4][4];   // weights of window j + 2
             uint32_t vmk = 0;   // its item masks, a byte per rune
             auto verify = [&](int32_t j) {
+#if JB_STAMPS
+                const uint64_t v0 = __builtin_amdgcn_s_memtime();
+#endif
                 uint64_t rn[4];
                 if (j >= 0) {
 #pragma unroll
@@ -2846,6 +2877,10 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
                             wn[q][k] = im.wtab1[(uint32_t)(vrc[q] >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u)];
                     }
                 }
+#if JB_STAMPS
+                const uint64_t v1 = __builtin_amdgcn_s_memtime();
+                uint64_t v2 = v1, v3 = v1;
+#endif
                 if (j + 2 < Jd) {
                     // the items' sums: all 16 ring reads at once (an absent field reads best(i + 1),
                     // unused; the ring holds best(n) = 0.0, so no case for i + L = n), then
@@ -2867,6 +2902,9 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
                             rv[q][k] = S.lp.dring[(i + max(1u, Lk[q][k])) & (kLdDesc - 1u)];
                         }
                     }
+#if JB_STAMPS
+                    v2 = __builtin_amdgcn_s_memtime();
+#endif
                     bool bad = false;
 #pragma unroll
                     for (uint32_t q = 0; q < 4u; q++) {
@@ -2896,7 +2934,15 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
                         bad |= i < n && bestL != S.lp.L[kb + kSeg * q + lane];
                     }
                     if (bad) S.bad = 1u;
+#if JB_STAMPS
+                    v3 = __builtin_amdgcn_s_memtime();
+#endif
                 }
+#if JB_STAMPS
+                st_p[0] += v1 - v0;  // loads issued
+                st_p[1] += v2 - v1;  // ring reads
+                st_p[2] += v3 - v2;  // fold
+#endif
 #pragma unroll
                 for (uint32_t q = 0; q < 4u; q++) {
                     vrc[q] = rn[q];
@@ -3407,6 +3453,8 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
         o[1] = st_bar;
         o[2] = st_n;
         o[3] = st_slow;
+        uint64_t* p = dbg + kDbgLong + 64u * 16u + wg * 16u + wave * 4u;
+        for (int k = 0; k < 4; k++) p[k] = st_p[k];
     }
 #else
     (void)dbg;
