@@ -2315,7 +2315,7 @@ __device__ __forceinline__ void lp_compose(const uint8_t (*sc)[kSeg], uint8_t* _
 // rune i at ring slot i & 1023.
 struct LPath {
     double pw[4][kSpWin];     // the window's path runes right to left: w_D, then (fill) best
-    double ck[4][kSpWin / 16u + 1u];  // the chain's sum before the window, then after every 16 path runes
+    double ck[4][kSpWin / 8u + 2u];  // the chain's sum before the window, then after every 8 path runes
     double dring[kLdDesc];    // best(i)
     double wd[kLdDesc];       // w_D(i): the decided item's weight (k_long_spec)
     uint8_t L[kLdDesc];       // D(i): the decided item's length
@@ -2704,7 +2704,7 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
             };
             // the chain over window j's path runes (wave 0, lane 0): 16 at a time from
             // registers, the next 16 loaded meanwhile.  It stores only its sum before the window
-            // and after every 16 runes (ck): one wave's LDS stores cost it more than its adds
+            // and after every 8 runes (ck): one wave's LDS stores cost it more than its adds
             // (a 16-byte store per two sums: 24 cycles per sum against 12.6 with these
             // checkpoints, tools/diag/pchain.hip); fill redoes the same adds from them.
             double acc = 0.0;  // best of the path rune after the window (best(n) = 0.0 first)
@@ -2727,9 +2727,13 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
                 double* const ck = S.lp.ck[b];
                 auto run = [&](const V16& X, uint32_t k) __attribute__((always_inline)) {
 #pragma unroll
-                    for (int t = 0; t < 16; t++) acc = X.v[t] + acc;
+                    for (int t = 0; t < 8; t++) acc = X.v[t] + acc;
+                    const double a8 = acc;
+#pragma unroll
+                    for (int t = 8; t < 16; t++) acc = X.v[t] + acc;
                     __builtin_amdgcn_sched_barrier(0);
-                    ck[k / 16u + 1u] = acc;
+                    ck[k / 8u + 1u] = a8;
+                    ck[k / 8u + 2u] = acc;
                 };
 #if JB_STAMPS
                 st_slow += c16;
@@ -2760,33 +2764,7 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
 #if JB_STAMPS
                 const uint64_t f0 = __builtin_amdgcn_s_memtime();
 #endif
-                {  // the path runes' values: the chain's adds again, 16 per lane from its checkpoints
-                    const uint32_t c16 = (S.lp.pcnt[b] + 15u) & ~15u;
-                    if (lane < c16 / 16u) {
-                        double a = S.lp.ck[b][lane];
-                        double* const pw = S.lp.pw[b] + 16u * lane;
-                        double x[16];
-#pragma unroll
-                        for (int t = 0; t < 8; t++) {
-                            const double2 v = reinterpret_cast<const double2*>(pw)[t];
-                            x[2 * t] = v.x;
-                            x[2 * t + 1] = v.y;
-                        }
-#pragma unroll
-                        for (int t = 0; t < 16; t++) {
-                            a = x[t] + a;
-                            x[t] = a;
-                        }
-#pragma unroll
-                        for (int t = 0; t < 8; t++) reinterpret_cast<double2*>(pw)[t] = make_double2(x[2 * t], x[2 * t + 1]);
-                    }
-                }
-#if JB_STAMPS
-                const uint64_t f1 = __builtin_amdgcn_s_memtime();
-#endif
-                // each lane four consecutive runes r0 .. r0 + 3: a successor inside the lane is
-                // taken from the register of its value in the same round (the four right to left),
-                // so a run of off-path runes resolves a lane at a time
+                // (the lane's inputs first: their reads do not wait for the stores below)
                 const uint32_t r0 = 4u * lane;
                 uint64_t pm[4];
 #pragma unroll
@@ -2799,6 +2777,33 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
                 const uint32_t L4 = *reinterpret_cast<const uint32_t*>(S.lp.L + kb + r0);
                 const double2 w01 = *reinterpret_cast<const double2*>(S.lp.wd + kb + r0);
                 const double2 w23 = *reinterpret_cast<const double2*>(S.lp.wd + kb + r0 + 2u);
+                {  // the path runes' values: the chain's adds again, 8 per lane from its checkpoints
+                    const uint32_t c16 = (S.lp.pcnt[b] + 15u) & ~15u;
+                    if (lane < c16 / 8u) {
+                        double a = S.lp.ck[b][lane];
+                        double* const pw = S.lp.pw[b] + 8u * lane;
+                        double x[8];
+#pragma unroll
+                        for (int t = 0; t < 4; t++) {
+                            const double2 v = reinterpret_cast<const double2*>(pw)[t];
+                            x[2 * t] = v.x;
+                            x[2 * t + 1] = v.y;
+                        }
+#pragma unroll
+                        for (int t = 0; t < 8; t++) {
+                            a = x[t] + a;
+                            x[t] = a;
+                        }
+#pragma unroll
+                        for (int t = 0; t < 4; t++) reinterpret_cast<double2*>(pw)[t] = make_double2(x[2 * t], x[2 * t + 1]);
+                    }
+                }
+#if JB_STAMPS
+                const uint64_t f1 = __builtin_amdgcn_s_memtime();
+#endif
+                // each lane four consecutive runes r0 .. r0 + 3: a successor inside the lane is
+                // taken from the register of its value in the same round (the four right to left),
+                // so a run of off-path runes resolves a lane at a time
                 const double wq[4] = {w01.x, w01.y, w23.x, w23.y};
                 uint32_t tq[4];
                 double vq[4];
@@ -2851,17 +2856,25 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
             // overflowed record (mk 0) walks the trie (long_items_rc).  The loads run two steps
             // ahead: at step j the records of window j, the weights of window j + 1 (all 16
             // fields of each lane's four runes at once), the fold of window j + 2.
-            uint64_t vrc[4];    // records of window j + 1 (loaded the step before)
-            double vwv[4][4];   // weights of window j + 2
-            uint32_t vmk = 0;   // its item masks, a byte per rune
-            auto verify = [&](int32_t j) {
+            // Runes 64 q + lane for q in [Q0, Q1): wave 3 takes q = 0..2, wave 1 (after its
+            // stage) q = 3, each with its own loads in flight (VState).
+            struct VState {
+                uint64_t vrc[4];    // records of window j + 1 (loaded the step before)
+                double vwv[4][4];   // weights of window j + 2
+                uint32_t vmk = 0;   // its item masks, a byte per rune
+            };
+            auto verify = [&](int32_t j, auto Q0c, auto Q1c, VState& vs) {
+                constexpr uint32_t Q0 = decltype(Q0c)::value, Q1 = decltype(Q1c)::value;
+                uint64_t(&vrc)[4] = vs.vrc;
+                double(&vwv)[4][4] = vs.vwv;
+                uint32_t& vmk = vs.vmk;
 #if JB_STAMPS
                 const uint64_t v0 = __builtin_amdgcn_s_memtime();
 #endif
                 uint64_t rn[4];
                 if (j >= 0) {
 #pragma unroll
-                    for (uint32_t q = 0; q < 4u; q++) {
+                    for (uint32_t q = Q0; q < Q1; q++) {
                         const uint32_t i = (uint32_t)j * kSpWin + kSeg * q + lane;
                         rn[q] = i < n ? erec[s0 + i] : 0x1ull;  // (past the block: one phantom item)
                     }
@@ -2870,7 +2883,7 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
                 uint32_t mkn = 0;
                 if (j + 1 >= 0 && j + 1 < Jd) {
 #pragma unroll
-                    for (uint32_t q = 0; q < 4u; q++) {
+                    for (uint32_t q = Q0; q < Q1; q++) {
                         mkn |= ((uint32_t)vrc[q] & 0xFFu) << (8u * q);
 #pragma unroll
                         for (uint32_t k = 0; k < 4u; k++)
@@ -2890,7 +2903,7 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
                     uint32_t Lk[4][4];
                     double rv[4][4];
 #pragma unroll
-                    for (uint32_t q = 0; q < 4u; q++) {
+                    for (uint32_t q = Q0; q < Q1; q++) {
                         const uint32_t i = base + kSeg * q + lane;
                         uint32_t mk = (vmk >> (8u * q)) & 0xFFu;
                         const uint32_t k0 = 4u - (uint32_t)__popc(mk);
@@ -2907,7 +2920,7 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
 #endif
                     bool bad = false;
 #pragma unroll
-                    for (uint32_t q = 0; q < 4u; q++) {
+                    for (uint32_t q = Q0; q < Q1; q++) {
                         const uint32_t i = base + kSeg * q + lane;
                         double prevP = JB_MIN_FLOAT;
                         uint32_t bestL = 0, lastL = 0;
@@ -2944,7 +2957,7 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
                 st_p[2] += v3 - v2;  // fold
 #endif
 #pragma unroll
-                for (uint32_t q = 0; q < 4u; q++) {
+                for (uint32_t q = Q0; q < Q1; q++) {
                     vrc[q] = rn[q];
 #pragma unroll
                     for (uint32_t k = 0; k < 4u; k++) vwv[q][k] = wn[q][k];
@@ -2981,16 +2994,18 @@ __device__ __forceinline__ void long_dp_body(const uint8_t* __restrict__ text, D
                 stage(Jd - 1, sx);
                 if (Jd >= 2) stage_load(Jd - 2, sx);
                 __syncthreads();
+                VState vs;
                 JB_LP_STEP(if (j >= 1) {
                     stage(j - 1, sx);
                     if (j >= 2) stage_load(j - 2, sx);
-                });
+                } verify(j, std::integral_constant<uint32_t, 3>{}, std::integral_constant<uint32_t, 4>{}, vs));
             } else if (wave == 2u) {
                 __syncthreads();
                 JB_LP_STEP(if (j >= -1 && j + 1 < Jd) fill(j + 1));
             } else {
+                VState vs;
                 __syncthreads();
-                JB_LP_STEP(verify(j));
+                JB_LP_STEP(verify(j, std::integral_constant<uint32_t, 0>{}, std::integral_constant<uint32_t, 3>{}, vs));
             }
 #undef JB_LP_STEP
             const bool bad = S.bad != 0u;
