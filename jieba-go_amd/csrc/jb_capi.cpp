@@ -790,6 +790,9 @@ static int launch_pipeline_(Device* d, const Work& w, const uint8_t* d_text, uin
                         "the window per chunk %.3f; Viterbi lane use %.2f (longest lane %.1f runes per chunk)\n",
                 a[0] / n, a[1] / n, a[8] / n, a[9] / n, a[2] / n, a[6] / n, a[3] / n, a[4] / n, 64.0 * a[5] / n,
                 a[4] / (64.0 * a[5] + 1e-9), a[7] / (a[3] + 1e-9), a[10] / (64.0 * a[11] + 1e-9), a[11] / (a[3] + 1e-9));
+        fprintf(stderr, "[jb] k_zh Viterbi forward half per chunk: longest lane %.2f runes, longest single run %.2f, "
+                        "the wave's runes split evenly %.2f\n",
+                a[11] / (a[3] + 1e-9), a[12] / (a[3] + 1e-9), a[13] / (a[3] + 1e-9));
         HIPCHK(hipMemsetAsync(d->w.dbg, 0, (size_t)nwv * 128, s));
         const uint64_t nww = (nbytes + kTileBytes - 1) / kTileBytes * 4;
         std::vector<uint64_t> sw(nww * 8);

@@ -1839,19 +1839,24 @@ __device__ __forceinline__ void zh_chunk_main(const uint8_t* __restrict__ text, 
             const uint32_t nr = min(*nrun, kZhRuns * 64u);  // the pool's entries k = lane + 64 r are this lane's
             rl.n = nr > lane ? (nr - lane + 63u) / 64u : 0u;
             if (st) {  // Viterbi lane use: the lanes' summed run lengths against 64 x their maximum
-                uint32_t s = 0;
+                uint32_t s = 0, l1 = 0;
                 for (uint32_t r = 0; r < rl.n; r++) {
                     const uint32_t y = runs[r * 64u];
-                    s += ((y >> 16) - (y & 0xFFFFu)) / 3u;
+                    const uint32_t len = ((y >> 16) - (y & 0xFFFFu)) / 3u;
+                    s += len;
+                    l1 = max(l1, len);
                 }
                 uint32_t mx = s, sm = s;
 #pragma unroll
                 for (int d = 32; d >= 1; d >>= 1) {
                     mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
                     sm += (uint32_t)__shfl_xor((int)sm, d, 64);
+                    l1 = max(l1, (uint32_t)__shfl_xor((int)l1, d, 64));
                 }
                 st[10] += sm;
                 st[11] += mx;
+                st[12] += l1;              // the longest single run: no dealing goes below it
+                st[13] += (sm + 63u) / 64u;  // the wave's runes split evenly over its lanes
             }
         } else {
             ok = zh_fwd_lane<HMM>(v, im, src, le, rlp);
@@ -1982,7 +1987,7 @@ __global__ __launch_bounds__(NW * 64) JB_ZH_ATTR void k_zh(const uint8_t* __rest
     __syncthreads();
     // diagnostic per-wave clocks (JB_ABLATE bit 8): [0] setup [1] DP [2] forward+Viterbi+flush [3] chunks
     // [4] sum of lane DP steps [5] sum of per-chunk max lane DP steps [6] blocks past the window [7] scratch
-    uint64_t stv[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // [8] forward walk [9] Viterbi forward half
+    uint64_t stv[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // [8] forward walk [9] Viterbi forward half
     // [10] lanes' summed Viterbi run runes [11] 64 x max ... (Viterbi lane use)
 #if JB_STAMPS
     uint64_t* st = (diag & 0x100u) ? stv : nullptr;
@@ -2188,6 +2193,8 @@ __global__ __launch_bounds__(NW * 64) JB_ZH_ATTR void k_zh(const uint8_t* __rest
             o[9] = stv[9];
             o[10] = stv[10];
             o[11] = stv[11];
+            o[12] = stv[12];
+            o[13] = stv[13];
             o[0] = stv[0];
             o[1] = stv[1];
             o[2] = stv[2];
