@@ -2434,17 +2434,23 @@ __device__ __forceinline__ uint32_t long_block_of(const uint32_t* __restrict__ l
 // writes the chosen length to gbl and the chosen item's weight to gbest, which
 // k_long_dp's decided chain turns into the exact best values and verifies.
 constexpr uint32_t kSpecOver = 1024;
-constexpr uint32_t kSpecRing = 256;  // > the longest edge (255 runes)
-constexpr uint32_t kSpecGrid = 256;  // 64-lane workgroups, one per CU (128 KB of LDS each)
+constexpr uint32_t kSpecRing = 128;  // best values kept per lane (an item longer takes the guess)
+constexpr uint32_t kSpecGrid = 256;  // 64-lane workgroups, one per CU (140 KB of LDS each)
 __device__ __forceinline__ void long_spec_body(const uint8_t* __restrict__ text, DevImage im,
                                                   const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
                                                   const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ counters,
                                                   const uint32_t* __restrict__ tile4, uint8_t* __restrict__ gbl,
                                                   double* __restrict__ gbest, uint8_t* __restrict__ lcode,
                                                   uint8_t* __restrict__ lmap, uint32_t* __restrict__ lflag, uint32_t mode,
-        uint32_t wg, uint32_t ng, double (*s_ring)[64], uint8_t (*s_cd)[kSeg]) {
+        uint32_t wg, uint32_t ng, double (*s_ring)[64], uint8_t (*s_cd)[kSeg], double* s_wtl, double (*s_bw)[kSeg]) {
     const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG], lane = threadIdx.x & 63u;
     if (!im.plainw) return;  // (k_long_dp runs the exact chain)
+    // the weight table in LDS when it fits (kZhWtab entries, as k_zh's wide form)
+    double* const s_wt = im.nw1 <= kZhWtab ? s_wtl : nullptr;
+    if (s_wt)
+        for (uint32_t k = lane; k < im.nw1; k += 64u) s_wt[k] = im.wtab1[k];
+    for (uint32_t k = lane; k < 256u; k += 64u) s_ltab[k] = ltab_entry(k);  // (the records' lengths)
+    wave_sync();
     for (uint32_t g0 = wg * 64u; g0 < nseg; g0 += ng * 64u) {  // (wave-uniform)
         const uint32_t g = g0 + lane;
         const bool act = g < nseg;
@@ -2473,75 +2479,69 @@ __device__ __forceinline__ void long_spec_body(const uint8_t* __restrict__ text,
         n = (be - bs) / 3u;
         a = (g - lsegb[bi]) * kSeg;
         const uint32_t lim = min(a + kSeg, n), top = min(lim + kSpecOver, n);
-        double bnx = 0.0;  // speculative best(i + 1)
-        // By groups of four runes g .. g + 3, from the top down.  The loads run ahead of the
-        // DP, which then waits only on LDS: a group's records two groups before it, their
-        // weights (all 16 fields at once) one group before.
+        // By groups of four runes g .. g + 3, from the top down.  The records are loaded
+        // three groups ahead (the DP waits only on LDS).  With the weight table in LDS (WL:
+        // at most kZhWtab weights) a group's 16 weights are LDS reads at its start; else
+        // they are gathered a group ahead.  An item of kSpecRing runes or more takes the
+        // guess 0.0 for best(i + L), as past the top (only the speculation's quality depends
+        // on it: k_long_dp verifies every choice).
+        // (unconditional loads, the index clamped into the block: a rune past the top or a
+        // group below the segment is never used, and a conditional load made every later
+        // write of its register wait for all loads in flight)
         auto ld_rc = [&](int32_t g, uint64_t (&rc)[4]) __attribute__((always_inline)) {
 #pragma unroll
             for (int32_t r = 0; r < 4; r++) {
-                const int32_t i = g + r;
-                rc[r] = g >= (int32_t)a && i < (int32_t)top ? erec[s0 + (uint32_t)i] : 0x1ull;  // (else unused)
+                const int32_t i = min(max(g + r, 0), (int32_t)n - 1);
+                rc[r] = erec[s0 + (uint32_t)i];
             }
         };
-        auto ld_w = [&](const uint64_t (&rc)[4], double (&w)[4][4]) __attribute__((always_inline)) {
+        auto fidx = [](uint64_t rc, uint32_t k) {
+            return (uint32_t)(rc >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u);
+        };
+        auto ld_w = [&](const uint64_t (&rc)[4], double (&w)[4][4], const double* __restrict__ wt)
+                        __attribute__((always_inline)) {
 #pragma unroll
             for (uint32_t r = 0; r < 4u; r++)
 #pragma unroll
-                for (uint32_t k = 0; k < 4u; k++)
-                    w[r][k] = im.wtab1[(uint32_t)(rc[r] >> (8 + kEdgeIdxBits * k)) & ((1u << kEdgeIdxBits) - 1u)];
-        };
-        auto masks = [](const uint64_t (&rc)[4]) {
-            return ((uint32_t)rc[0] & 0xFFu) | (((uint32_t)rc[1] & 0xFFu) << 8) | (((uint32_t)rc[2] & 0xFFu) << 16) |
-                   (((uint32_t)rc[3] & 0xFFu) << 24);
+                for (uint32_t k = 0; k < 4u; k++) w[r][k] = wt[fidx(rc[r], k)];
         };
         const int32_t gtop = (int32_t)(a + ((top - a + 3u) & ~3u)) - 4;
-        uint64_t rcn[4];
-        double wc[4][4];
-        uint32_t mkc;
-        {
-            uint64_t rc0[4];
-            ld_rc(gtop, rc0);
-            ld_w(rc0, wc);
-            mkc = masks(rc0);
-            ld_rc(gtop - 4, rcn);
-        }
-        for (int32_t g = gtop; g >= (int32_t)a; g -= 4) {
-            uint64_t rcnn[4];
-            ld_rc(g - 8, rcnn);
-            double wn[4][4];
-            ld_w(rcn, wn);
-            const uint32_t mkn = masks(rcn);
+        double bnx = 0.0;  // speculative best(i + 1)
+        // the DP of group g's runes, right to left, its weights in wc
+        auto group = [&](int32_t g, const uint64_t (&rcg)[4], const double (&wc)[4][4]) __attribute__((always_inline)) {
 #pragma unroll
             for (int32_t r = 3; r >= 0; r--) {
                 const uint32_t i = (uint32_t)(g + r);
                 if (i >= top) continue;  // (the first group's runes past the top)
                 double prevP = JB_MIN_FLOAT, bestP = JB_MIN_FLOAT, bestW = 0.0, lastW = 0.0;
                 uint32_t bestL = 0, lastL = 0;
-                uint32_t mk = (mkc >> (8 * r)) & 0xFFu;
-                if (mk) {  // the record's items, the last popc(mk) fields, by selects
-                    const uint32_t k0 = 4u - (uint32_t)__popc(mk);
+                const uint32_t mk = (uint32_t)rcg[r] & 0xFFu;
+                if (mk) {
+                    // the record's four fields, phantoms (weight -Inf, L = 1) first, by k_zh's
+                    // fold (rec_fold_a3's reading of maxIndexProba: the first field taken
+                    // outright, each later one if its proba is >= the one before; the same item
+                    // under plainw).  best(i + L) for i + L >= top is 0.0 from the ring (set
+                    // below the top before the loop), best(i + 1) from a register.
+                    const uint64_t lt = s_ltab[mk];
+                    double prv = 0.0;
 #pragma unroll
                     for (uint32_t k = 0; k < 4u; k++) {
-                        const bool pres = k >= k0;
-                        const uint32_t L = pres ? (uint32_t)__builtin_ctz(mk) + 1u : 1u;
-                        mk = pres ? mk & (mk - 1u) : mk;
-                        const uint32_t j = i + L;
-                        const double rv = s_ring[j & (kSpecRing - 1u)][lane];
+                        const uint32_t L = (uint32_t)(lt >> (16u * k + 9u)) & 0x7Fu;
+                        const double rv = s_ring[(i + L) & (kSpecRing - 1u)][lane];
                         const double wt = wc[r][k];
-                        const double pp = wt + (j >= top ? 0.0 : (L == 1u ? bnx : rv));
-                        const bool take = pres && pp >= prevP;
+                        const double pp = wt + (L == 1u ? bnx : rv);
+                        const bool take = k == 0u || pp >= prv;
                         bestL = take ? L : bestL;
                         bestP = take ? pp : bestP;
                         bestW = take ? wt : bestW;
-                        prevP = pres ? pp : prevP;
-                        lastL = pres ? L : lastL;
-                        lastW = pres ? wt : lastW;
+                        prv = pp;
                     }
                 } else {  // an overflowed record: walk the trie
                     long_items_rc(text, im, 0ull, bs, be, i, [&](uint32_t L, double wt) {
                         const uint32_t j = i + L;
-                        const double b = j >= top ? 0.0 : (L == 1u ? bnx : s_ring[j & (kSpecRing - 1u)][lane]);
+                        const double b = j >= top || L >= kSpecRing
+                                             ? 0.0
+                                             : (L == 1u ? bnx : s_ring[j & (kSpecRing - 1u)][lane]);
                         const double pp = wt + b;
                         if (pp >= prevP) {
                             bestL = L;
@@ -2553,34 +2553,78 @@ __device__ __forceinline__ void long_spec_body(const uint8_t* __restrict__ text,
                         lastW = wt;
                     });
                 }
-                if (bestL == 0) {  // no item qualified: the last item (or none)
+                if (bestL == 0) {  // (walk) no item qualified: the last item (or none)
                     bestL = lastL;
                     bestP = prevP;
                     bestW = lastW;
                 }
                 s_ring[i & (kSpecRing - 1u)][lane] = bestP;
                 bnx = bestP;
-                if (i < lim) {
-                    // (mode 2, testing only: some choices made wrong on purpose, so that
-                    // k_long_dp's verification and exact chain run)
-                    const uint8_t d = (uint8_t)(mode == 2u && i % 97u == 0u && bestL > 1u ? 1u : bestL);
-                    gbl[s0 + i] = d;
-                    gbest[s0 + i] = bestW;
-                    s_cd[lane][i - a] = d;
+                // the choice and its weight into the lane's 64 slots in LDS, unconditionally: a rune
+                // past the segment is overwritten by the segment's own rune there later (no global
+                // store in the loop: its wait counts made every trip wait for the record loads)
+                // (mode 2, testing only: some choices made wrong on purpose, so that
+                // k_long_dp's verification and exact chain run)
+                s_cd[lane][(i - a) & (kSeg - 1u)] = (uint8_t)(mode == 2u && i % 97u == 0u && bestL > 1u ? 1u : bestL);
+                s_bw[lane][(i - a) & (kSeg - 1u)] = bestW;
+            }
+        };
+        // best = 0.0 (the guess) for the 8 runes from the top up (a record's items are at most
+        // 8 runes long; the walk path tests i + L >= top itself)
+#pragma unroll
+        for (uint32_t t = 0; t < 8u; t++) s_ring[(top + t) & (kSpecRing - 1u)][lane] = 0.0;
+        if (s_wt) {
+            // four record sets in rotation, four groups per loop trip: a set is reloaded for
+            // the group four ahead right after its own group (copying the sets instead made
+            // every trip wait for the loads it had just issued)
+            uint64_t r0[4], r1[4], r2[4], r3[4];
+            ld_rc(gtop, r0);
+            ld_rc(gtop - 4, r1);
+            ld_rc(gtop - 8, r2);
+            ld_rc(gtop - 12, r3);
+            auto step = [&](int32_t g, uint64_t (&rc)[4]) __attribute__((always_inline)) {
+                double wc[4][4];
+                ld_w(rc, wc, s_wt);
+                group(g, rc, wc);
+                ld_rc(g - 16, rc);
+            };
+            for (int32_t g = gtop; g >= (int32_t)a; g -= 16) {
+                step(g, r0);
+                if (g - 4 < (int32_t)a) break;
+                step(g - 4, r1);
+                if (g - 8 < (int32_t)a) break;
+                step(g - 8, r2);
+                if (g - 12 < (int32_t)a) break;
+                step(g - 12, r3);
+            }
+        } else {
+            uint64_t rcc[4], rcn[4];
+            double wc[4][4];
+            ld_rc(gtop, rcc);
+            ld_w(rcc, wc, im.wtab1);
+            ld_rc(gtop - 4, rcn);
+            for (int32_t g = gtop; g >= (int32_t)a; g -= 4) {
+                uint64_t rcnn[4];
+                ld_rc(g - 8, rcnn);
+                double wn[4][4];
+                ld_w(rcn, wn, im.wtab1);
+                group(g, rcc, wc);
+#pragma unroll
+                for (uint32_t r = 0; r < 4u; r++) {
+                    rcc[r] = rcn[r];
+                    rcn[r] = rcnn[r];
+#pragma unroll
+                    for (uint32_t k = 0; k < 4u; k++) wc[r][k] = wn[r][k];
                 }
             }
-#pragma unroll
-            for (uint32_t r = 0; r < 4u; r++) {
-                rcn[r] = rcnn[r];
-#pragma unroll
-                for (uint32_t k = 0; k < 4u; k++) wc[r][k] = wn[r][k];
-            }
-            mkc = mkn;
         }
         // the segment's exit codes under these choices (k_long_seg's rule; the path chain
         // finds the path of the decisions from them)
         for (uint32_t p = lim; p-- > a;) {
-            const uint32_t L = max(1u, (uint32_t)s_cd[lane][p - a]), q = p + L;
+            const uint32_t d = s_cd[lane][p - a];
+            gbl[s0 + p] = (uint8_t)d;
+            gbest[s0 + p] = s_bw[lane][p - a];
+            const uint32_t L = max(1u, d), q = p + L;
             const uint8_t c = q >= lim ? (L == 1u ? (uint8_t)0xFFu : (uint8_t)(q - lim)) : s_cd[lane][q - a];
             s_cd[lane][p - a] = c;
             lcode[s0 + p] = c;
@@ -2604,7 +2648,10 @@ __global__ __launch_bounds__(64) void k_long_spec(const uint8_t* __restrict__ te
                                                   uint8_t* __restrict__ lmap, uint32_t* __restrict__ lflag, uint32_t mode) {
     __shared__ double s_ring[kSpecRing][64];
     __shared__ uint8_t s_cd[64][kSeg];  // the lane's segment: its decisions, then its exit codes
-    long_spec_body(text, im, erec, longblk, lsegb, counters, tile4, gbl, gbest, lcode, lmap, lflag, mode, blockIdx.x, gridDim.x, s_ring, s_cd);
+    __shared__ double s_wt[kZhWtab];
+    __shared__ double s_bw[64][kSeg];  // the lane's segment's chosen weights
+    long_spec_body(text, im, erec, longblk, lsegb, counters, tile4, gbl, gbest, lcode, lmap, lflag, mode, blockIdx.x,
+                   gridDim.x, s_ring, s_cd, s_wt, s_bw);
 }
 
 template <bool HMM>
@@ -3894,6 +3941,8 @@ union LongAll {  // the phases' LDS
     struct {
         double ring[kSpecRing][64];
         uint8_t cd[64][kSeg];
+        double wt[kZhWtab];
+        double bw[64][kSeg];
     } sp;                             // k_long_spec (wave 0)
     LongLds dp;                       // k_long_dp
     uint32_t m32[kLpBatch * kLpMap / 4u];  // k_long_path (wave 0)
@@ -3921,7 +3970,7 @@ __global__ __launch_bounds__(256) void k_long(const uint8_t* __restrict__ text, 
     if (spec) {
         if (w0)
             long_spec_body(text, im, erec, longblk, lsegb, counters, tile4, gbl, gbest, lcode, lmap, lflag, spec, wg,
-                           ng, U.sp.ring, U.sp.cd);
+                           ng, U.sp.ring, U.sp.cd, U.sp.wt, U.sp.bw);
         grid_sync(gs, ++bar * ng, err);
         if (spec != 3u) {
             if (w0) long_path_body(longblk, lsegb, counters, lflag, lcode, lmap, lcx, 3u, 3u, wg, ng, U.m32);
