@@ -4,9 +4,12 @@
 // spans the test computed with the oracle; prints the call rate of one thread and
 // of all threads together.
 //
-//   concurrent_cut DICT EMIT SENTENCES EXPECTED THREADS CALLS
+//   concurrent_cut DICT EMIT SENTENCES EXPECTED THREADS CALLS [mixed]
 // SENTENCES: one sentence per line; EXPECTED: per sentence "n s0 e0 s1 e1 ..."
-// (byte offsets in the sentence).  Output: "serial ..." and "concurrent ..." lines.
+// (byte offsets in the sentence), or "P" where the reference panics (JB_EPANIC
+// expected).  With "mixed", EXPECTED has two lines per sentence (hmm on, then off)
+// and the calls alternate hmm, so that coalesced batches mix both settings.
+// Output: "serial ..." and "concurrent ..." lines.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -22,11 +25,12 @@
 #include "jiebahip.h"
 
 struct Expect {
+    bool panic = false;
     std::vector<uint64_t> s, e;
 };
 
-static int run(jb_ctx* ctx, const std::vector<std::string>& sent, const std::vector<Expect>& want, int nth,
-               int calls, double* secs, uint64_t* bad) {
+static int run(jb_ctx* ctx, const std::vector<std::string>& sent, const std::vector<Expect>& want, bool mixed,
+               int nth, int calls, double* secs, uint64_t* bad) {
     std::atomic<uint64_t> mism{0}, errs{0};
     std::atomic<int> ready{0};
     std::atomic<bool> go{false};
@@ -35,13 +39,21 @@ static int run(jb_ctx* ctx, const std::vector<std::string>& sent, const std::vec
         while (!go.load()) std::this_thread::yield();
         for (int i = 0; i < calls; i++) {
             const size_t k = ((size_t)t * 7919u + (size_t)i * 31u) % sent.size();
+            const int hmm = mixed ? (int)((t + i) & 1) : 1;
+            const Expect& w = want[mixed ? 2 * k + (hmm ? 0 : 1) : k];
             jb_spans sp;
-            const int rc = jb_cut(ctx, (const uint8_t*)sent[k].data(), sent[k].size(), 1, &sp);
+            const int rc = jb_cut(ctx, (const uint8_t*)sent[k].data(), sent[k].size(), hmm, &sp);
+            if (w.panic) {  // the reference panics here: JB_EPANIC for this call alone
+                if (rc != JB_EPANIC) {
+                    mism++;
+                    if (rc == 0) jb_spans_free(&sp);
+                }
+                continue;
+            }
             if (rc) {
                 if (errs++ == 0) fprintf(stderr, "jb_cut rc=%d: %s\n", rc, jb_last_error());
                 continue;
             }
-            const Expect& w = want[k];
             bool ok = sp.ntokens == w.s.size();
             for (uint64_t j = 0; ok && j < sp.ntokens; j++) ok = sp.start[j] == w.s[j] && sp.end[j] == w.e[j];
             if (!ok) mism++;
@@ -60,10 +72,11 @@ static int run(jb_ctx* ctx, const std::vector<std::string>& sent, const std::vec
 }
 
 int main(int argc, char** argv) {
-    if (argc != 7) {
-        fprintf(stderr, "usage: %s DICT EMIT SENTENCES EXPECTED THREADS CALLS\n", argv[0]);
+    if (argc != 7 && argc != 8) {
+        fprintf(stderr, "usage: %s DICT EMIT SENTENCES EXPECTED THREADS CALLS [mixed]\n", argv[0]);
         return 2;
     }
+    const bool mixed = argc == 8 && strcmp(argv[7], "mixed") == 0;
     const int nth = atoi(argv[5]), calls = atoi(argv[6]);
     std::vector<std::string> sent;
     {
@@ -76,17 +89,22 @@ int main(int argc, char** argv) {
         std::ifstream f(argv[4]);
         std::string line;
         while (std::getline(f, line)) {
+            Expect x;
+            if (!line.empty() && line[0] == 'P') {
+                x.panic = true;
+                want.push_back(x);
+                continue;
+            }
             std::istringstream is(line);
             size_t n;
             is >> n;
-            Expect x;
             x.s.resize(n);
             x.e.resize(n);
             for (size_t j = 0; j < n; j++) is >> x.s[j] >> x.e[j];
             want.push_back(x);
         }
     }
-    if (sent.empty() || sent.size() != want.size()) {
+    if (sent.empty() || want.size() != sent.size() * (mixed ? 2u : 1u)) {
         fprintf(stderr, "%zu sentences, %zu expectations\n", sent.size(), want.size());
         return 2;
     }
@@ -103,11 +121,11 @@ int main(int argc, char** argv) {
     }
     double s1 = 0, sn = 0;
     uint64_t b1 = 0, bn = 0;
-    run(ctx, sent, want, 1, 200, &s1, &b1);  // warm-up
-    rc = run(ctx, sent, want, 1, calls, &s1, &b1);
+    run(ctx, sent, want, mixed, 1, 200, &s1, &b1);  // warm-up
+    rc = run(ctx, sent, want, mixed, 1, calls, &s1, &b1);
     printf("serial threads 1 calls %d mismatches %llu seconds %.4f calls_per_s %.0f\n", calls,
            (unsigned long long)b1, s1, calls / s1);
-    rc |= run(ctx, sent, want, nth, calls, &sn, &bn);
+    rc |= run(ctx, sent, want, mixed, nth, calls, &sn, &bn);
     printf("concurrent threads %d calls %d mismatches %llu seconds %.4f calls_per_s %.0f\n", nth, nth * calls,
            (unsigned long long)bn, sn, (double)nth * calls / sn);
     jb_close(ctx);

@@ -971,3 +971,41 @@ def test_concurrent_cut_calls(syn_small, tmp_path, slots):
     assert r.returncode == 0, r.stdout + r.stderr
     rates = {ln.split()[0]: float(ln.split()[-1]) for ln in r.stdout.splitlines()}
     assert rates["concurrent"] > rates["serial"]
+
+
+def test_concurrent_cut_mixed_hmm_and_panics(tmp_path, mini_paths):
+    """The coalescing paths the test above leaves out: calls with hmm on and
+    off at once (a batch takes only the queue head's setting, the others wait for the
+    next), and calls whose text makes the reference panic (cutDAG: a lone 文 has no DAG
+    edge under this dictionary) coalesced with good ones (the batch reruns its requests
+    one by one, so JB_EPANIC reaches only the caller whose text caused it)."""
+    import subprocess
+    dp = str(tmp_path / "dict.txt")
+    with open(dp, "w", encoding="utf-8") as f:
+        for w, c in [("中", 5), ("文", -9), ("中文", 1), ("天氣", 2), ("上海", 3), ("很好", 4)]:
+            f.write(f"{w} {c}\n")
+    exe = str(tmp_path / "concurrent_cut")
+    lib = os.path.join(ROOT, "jieba-go_amd", "lib")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-pthread", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "concurrent_cut.cpp"), "-L", lib, "-ljiebahip",
+                           "-Wl,-rpath," + lib, "-o", exe])
+    o = O.Oracle.from_files(dp, mini_paths[1], 0)
+    sents = ["中文", "中文上海天氣很好", "上海很好", "文", "天氣文", "abc 中文 def", "中文上海", "很好中文天氣", "",
+             "上海 天氣 中文"]
+    with open(tmp_path / "sent.txt", "wb") as f:
+        f.write(b"\n".join(x.encode() for x in sents) + b"\n")
+    npanic = 0
+    with open(tmp_path / "want.txt", "w") as f:
+        for x in sents:
+            for hmm in (True, False):
+                try:
+                    a, b = o.cut_spans(x.encode(), hmm)
+                    f.write(" ".join([str(len(a))] + [f"{int(p)} {int(q)}" for p, q in zip(a, b)]) + "\n")
+                except (RuntimeError, ValueError):
+                    f.write("P\n")
+                    npanic += 1
+    assert npanic >= 2  # (the texts with a lone 文)
+    r = subprocess.run([exe, dp, mini_paths[1], str(tmp_path / "sent.txt"), str(tmp_path / "want.txt"), "16", "300",
+                        "mixed"], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
