@@ -281,7 +281,7 @@ def roofline_of(kernels, units, traffic_of, per_byte):
     """Per kernel: algorithmic bytes per launch = `per_byte` (alg_bytes_per_byte of the
     step) x the unit bytes the launch processes, over its average launch time.  Units:
     every input byte for k_mark_walk (it classifies and walks the whole batch), the Han
-    bytes for k_zh / k_long_dp (DP + Viterbi over zh blocks)."""
+    bytes for k_zh / k_long / k_long_dp (DP + Viterbi over zh blocks)."""
     out = {}
     for kname, u in units.items():
         kk = kernels.get(kname)
@@ -402,8 +402,9 @@ def run(args, world, rank, dist, agg_dev, make_cutter, open_oracle, log=print):
     if rank != 0:
         return None
     units = {"k_mark_walk": float(nbytes), "k_zh": float(hbytes)}
-    if args.workload == "long-oov":  # one unpunctuated block: its Han bytes all go through the k_long_* chain
-        units["k_long_dp"] = float(hbytes)
+    if args.workload == "long-oov":  # one unpunctuated block: its Han bytes all go through the long-block path
+        units["k_long"] = float(hbytes)  # (its kernels as one launch, JB_LONG_FUSED=1)
+        units["k_long_dp"] = float(hbytes)  # (separate launches)
     wkey = f"{args.workload}:{nbytes}:{'hmm' if args.hmm else 'nohmm'}:{args.dict_kind}"
     rooflines = roofline_of(kernels, units, lambda k: load_pmc_traffic(k, wkey), alg_bytes_per_byte(nbytes, ntok))
     roof = None
