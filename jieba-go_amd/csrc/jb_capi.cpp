@@ -1455,7 +1455,7 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         const Piece& p = pcs[k];
         HIPCHK(hipEventSynchronize(d->ev_comp[k]));
         const volatile uint32_t* c = d->h_pcnt + k * kSnapWords;
-        if (c[CNT_ERR] & 2u) return fail(JB_EDEVICE, "k_long: a grid barrier ran out of polls");
+        if (c[CNT_ERR] & 2u) return fail(JB_EDEVICE, "k_long: a phase wait ran out of polls");
         if (c[CNT_ERR]) return fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)");
         if (c[CNT_NTOK] != c[CNT_NTOKE])
             return fail(JB_EDEVICE, "internal: %u token starts vs %u ends", c[CNT_NTOK], c[CNT_NTOKE]);

@@ -36,9 +36,10 @@ enum {
     CNT_NTOK = 2,   // token starts
     CNT_NTOKE = 3,  // token ends (== CNT_NTOK when consistent)
     CNT_ERR = 4,    // bit 0: a zh block reached a tail index -1 (the reference panics); bit 1: a k_long
-                    // grid barrier ran out of polls
+                    // phase wait ran out of polls
     CNT_WORK = 5,   // k_zh work counter: next group (kZhGroupBytes of text)
-    CNT_GSYNC = 6,  // k_long's grid barriers (arrivals)
+    CNT_PHASE = 32, // k_long's phases: claimed items at 32 + 2 p, finished items at 33 + 2 p
+    CNT_ALL = 64,   // (u32 slots of the counters buffer; k_docbits clears them all)
     CNT_TIES = 7,   // exact Viterbi route ties (Q12)
     CNT_NWORDS = 8, // u64 token count lives at u32 slots 8-9 (byte offset 32)
     CNT_NLONG = 10, // long zh blocks k_zh left to k_long_* (u64 with CNT_NLSEG: one atomic)

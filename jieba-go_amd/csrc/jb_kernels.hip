@@ -142,7 +142,7 @@ struct LdsEmitter {
 __global__ void k_docbits(const uint64_t* __restrict__ doc_off, uint32_t ndocs, uint64_t nbytes,
                           uint32_t* __restrict__ bits, uint32_t* __restrict__ counters) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-    if (d < CNT_CLEAR) counters[d] = 0u;
+    if (d < CNT_ALL) counters[d] = 0u;
     if (d >= ndocs) return;
     const uint64_t o = doc_off[d];
     if (o < nbytes) atomicOr(bits + (o >> 5), 1u << (o & 31u));
@@ -2436,21 +2436,26 @@ __device__ __forceinline__ uint32_t long_block_of(const uint32_t* __restrict__ l
 constexpr uint32_t kSpecOver = 1024;
 constexpr uint32_t kSpecRing = 128;  // best values kept per lane (an item longer takes the guess)
 constexpr uint32_t kSpecGrid = 256;  // 64-lane workgroups, one per CU (140 KB of LDS each)
+// the weight table in LDS when it fits (kZhWtab entries, as k_zh's wide form: else nullptr,
+// and k_long_spec gathers the weights), and the records' length table (one wave)
+__device__ __forceinline__ double* long_spec_setup(const DevImage& im, double* s_wtl) {
+    const uint32_t lane = threadIdx.x & 63u;
+    double* const s_wt = im.nw1 <= kZhWtab ? s_wtl : nullptr;
+    if (s_wt)
+        for (uint32_t k = lane; k < im.nw1; k += 64u) s_wt[k] = im.wtab1[k];
+    for (uint32_t k = lane; k < 256u; k += 64u) s_ltab[k] = ltab_entry(k);
+    wave_sync();
+    return s_wt;
+}
 __device__ __forceinline__ void long_spec_body(const uint8_t* __restrict__ text, DevImage im,
                                                   const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
                                                   const uint32_t* __restrict__ lsegb, const uint32_t* __restrict__ counters,
                                                   const uint32_t* __restrict__ tile4, uint8_t* __restrict__ gbl,
                                                   double* __restrict__ gbest, uint8_t* __restrict__ lcode,
                                                   uint8_t* __restrict__ lmap, uint32_t* __restrict__ lflag, uint32_t mode,
-        uint32_t wg, uint32_t ng, double (*s_ring)[64], uint8_t (*s_cd)[kSeg], double* s_wtl, double (*s_bw)[kSeg]) {
+        uint32_t wg, uint32_t ng, double (*s_ring)[64], uint8_t (*s_cd)[kSeg], double* s_wt, double (*s_bw)[kSeg]) {
     const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG], lane = threadIdx.x & 63u;
     if (!im.plainw) return;  // (k_long_dp runs the exact chain)
-    // the weight table in LDS when it fits (kZhWtab entries, as k_zh's wide form)
-    double* const s_wt = im.nw1 <= kZhWtab ? s_wtl : nullptr;
-    if (s_wt)
-        for (uint32_t k = lane; k < im.nw1; k += 64u) s_wt[k] = im.wtab1[k];
-    for (uint32_t k = lane; k < 256u; k += 64u) s_ltab[k] = ltab_entry(k);  // (the records' lengths)
-    wave_sync();
     for (uint32_t g0 = wg * 64u; g0 < nseg; g0 += ng * 64u) {  // (wave-uniform)
         const uint32_t g = g0 + lane;
         const bool act = g < nseg;
@@ -2650,8 +2655,9 @@ __global__ __launch_bounds__(64) void k_long_spec(const uint8_t* __restrict__ te
     __shared__ uint8_t s_cd[64][kSeg];  // the lane's segment: its decisions, then its exit codes
     __shared__ double s_wt[kZhWtab];
     __shared__ double s_bw[64][kSeg];  // the lane's segment's chosen weights
+    double* const wt = long_spec_setup(im, s_wt);
     long_spec_body(text, im, erec, longblk, lsegb, counters, tile4, gbl, gbest, lcode, lmap, lflag, mode, blockIdx.x,
-                   gridDim.x, s_ring, s_cd, s_wt, s_bw);
+                   gridDim.x, s_ring, s_cd, wt, s_bw);
 }
 
 template <bool HMM>
@@ -3907,89 +3913,6 @@ __global__ __launch_bounds__(256) void k_long_tail(const uint8_t* __restrict__ t
     long_tail_body<HMM>(text, im, gbl, longblk, lsegb, lflag, counters, lcode, lcx, bp, sbits, ebits, blockIdx.x, gridDim.x, s_cd);
 }
 
-// ---------------------------------------------------------------------------
-// k_long: the long-block kernels above as the phases of one launch (VERDICT r04
-// item 5), so that a batch without a long block (CNT_NLONG 0: every batch of
-// short documents) pays one launch instead of seven.  A grid barrier between the
-// phases (DESIGN §6's rule for inter-workgroup waits: every thread's stores made
-// visible at agent scope, a counter bumped by one thread per workgroup, polled with
-// agent-scope atomic loads, an acquire fence after; the wait is bounded and sets
-// CNT_ERR bit 1 when it runs out).  One workgroup per CU at most (the phases' LDS,
-// unioned, is 132 KB), and the grid is at most the CU count, so all its workgroups
-// are resident together.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kGridSpins = 1u << 21;  // polls before a grid barrier gives up (seconds)
-__device__ __forceinline__ void grid_sync(uint32_t* cnt, uint32_t target, uint32_t* err) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // (every thread: its stores, device-wide)
-    __syncthreads();
-    if (threadIdx.x == 0u) {
-        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t spins = 0;
-        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins == kGridSpins) {
-                __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-    }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (every thread: the others' stores)
-}
-
-union LongAll {  // the phases' LDS
-    struct {
-        double ring[kSpecRing][64];
-        uint8_t cd[64][kSeg];
-        double wt[kZhWtab];
-        double bw[64][kSeg];
-    } sp;                             // k_long_spec (wave 0)
-    LongLds dp;                       // k_long_dp
-    uint32_t m32[kLpBatch * kLpMap / 4u];  // k_long_path (wave 0)
-    uint4 cd4[256][kSeg / 16u];       // k_long_pbits, k_long_tail
-    uint8_t bl[256][kSeg];            // k_long_seg
-};
-
-template <bool HMM>
-__global__ __launch_bounds__(256) void k_long(const uint8_t* __restrict__ text, DevImage im,
-                                              const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
-                                              const uint32_t* __restrict__ lsegb, uint32_t* __restrict__ counters,
-                                              const uint32_t* __restrict__ tile4, uint8_t* __restrict__ gbl,
-                                              double* __restrict__ gbest, uint8_t* __restrict__ lcode,
-                                              uint8_t* __restrict__ lmap, uint8_t* __restrict__ lcx,
-                                              uint64_t* __restrict__ lpath, uint32_t* __restrict__ lflag,
-                                              uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
-                                              uint64_t* __restrict__ dbg, uint32_t spec) {
-    __shared__ LongAll U;
-    if (counters[CNT_NLONG] == 0u) return;  // (the whole grid: k_zh wrote it before this launch)
-    const uint32_t wg = blockIdx.x, ng = gridDim.x;
-    const bool w0 = threadIdx.x < 64u;  // (the one-wave phases)
-    uint32_t* const gs = counters + CNT_GSYNC;
-    uint32_t* const err = counters + CNT_ERR;
-    uint32_t bar = 0;
-    if (spec) {
-        if (w0)
-            long_spec_body(text, im, erec, longblk, lsegb, counters, tile4, gbl, gbest, lcode, lmap, lflag, spec, wg,
-                           ng, U.sp.ring, U.sp.cd, U.sp.wt, U.sp.bw);
-        grid_sync(gs, ++bar * ng, err);
-        if (spec != 3u) {
-            if (w0) long_path_body(longblk, lsegb, counters, lflag, lcode, lmap, lcx, 3u, 3u, wg, ng, U.m32);
-            grid_sync(gs, ++bar * ng, err);
-            long_pbits_body(longblk, lsegb, counters, lflag, gbl, lcode, lcx, lpath, wg, ng, U.cd4);
-            grid_sync(gs, ++bar * ng, err);
-        }
-    }
-    long_dp_body<HMM>(text, im, erec, gbl, gbest, longblk, counters, sbits, ebits, lflag, lsegb, lpath, dbg, spec,
-                      wg, ng, U.dp);
-    grid_sync(gs, ++bar * ng, err);
-    long_seg_body(text, im, erec, longblk, lsegb, counters, lflag, gbest, gbl, lcode, lmap, wg, ng, U.bl);
-    grid_sync(gs, ++bar * ng, err);
-    if (w0) long_path_body(longblk, lsegb, counters, lflag, lcode, lmap, lcx, 2u, 1u, wg, ng, U.m32);
-    grid_sync(gs, ++bar * ng, err);
-    // (the Viterbi back-pointers go to gbest's bytes: the exit codes in lcode are read to the end)
-    long_tail_body<HMM>(text, im, gbl, longblk, lsegb, lflag, counters, lcode, lcx, reinterpret_cast<uint8_t*>(gbest),
-                        sbits, ebits, wg, ng, U.cd4);
-}
 
 // ---------------------------------------------------------------------------
 // k_nonzh: one lane per non-Han block (cutNonZh, tokenizer.go:289-310)
@@ -4070,22 +3993,21 @@ __device__ __forceinline__ uint32_t alnum_mask16(uint4 x) {
 // block's first alnum byte (the block starts in the chunk, or walking back from it
 // to the block start meets no alnum byte).  Block bounds come from the lane masks
 // of k_mark_walk, so the kernel touches neither the block list nor the Han blocks.
-__global__ __launch_bounds__(256) void k_nonzh(const uint8_t* __restrict__ text, uint32_t nbytes,
-                                               const uint32_t* __restrict__ lanemask,
-                                               const uint2* __restrict__ tile_cnt, uint32_t ntiles,
-                                               const uint64_t* __restrict__ alnum16, uint32_t* __restrict__ sbits,
-                                               uint32_t* __restrict__ ebits, uint32_t* __restrict__ docbits,
-                                               const uint64_t* __restrict__ doc_off, uint32_t ndocs) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[256][80];
+__device__ __forceinline__ void nonzh_body(const uint8_t* __restrict__ text, uint32_t nbytes,
+                                           const uint32_t* __restrict__ lanemask, const uint2* __restrict__ tile_cnt,
+                                           uint32_t ntiles, const uint64_t* __restrict__ alnum16,
+                                           uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
+                                           uint32_t* __restrict__ docbits, const uint64_t* __restrict__ doc_off,
+                                           uint32_t ndocs, uint32_t wg, uint32_t ng, uint8_t (*s_win)[80]) {
     const uint32_t nch = (nbytes + 15u) >> 4, nw = (nch + 63u) >> 6;
     // the words k_docbits set back to zero for the next run (k_mark_walk, their only
     // reader, is done): one store per document
-    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < ndocs; d += gridDim.x * blockDim.x) {
+    for (uint32_t d = wg * 256u + threadIdx.x; d < ndocs; d += ng * 256u) {
         const uint64_t o = doc_off[d];
         if (o < nbytes) docbits[o >> 5] = 0u;
     }
     Emitter em(sbits, ebits);
-    for (uint32_t wi = blockIdx.x * blockDim.x + threadIdx.x; wi < nw; wi += gridDim.x * blockDim.x) {
+    for (uint32_t wi = wg * 256u + threadIdx.x; wi < nw; wi += ng * 256u) {
         uint64_t a = alnum16[wi];
         // the next alnum chunk's text and lane mask load while this one is cut
         uint32_t cn = a ? wi * 64u + (uint32_t)__builtin_ctzll(a) : 0u;
@@ -4148,24 +4070,35 @@ __global__ __launch_bounds__(256) void k_nonzh(const uint8_t* __restrict__ text,
     }
     em.flush();
 }
+__global__ __launch_bounds__(256) void k_nonzh(const uint8_t* __restrict__ text, uint32_t nbytes,
+                                               const uint32_t* __restrict__ lanemask,
+                                               const uint2* __restrict__ tile_cnt, uint32_t ntiles,
+                                               const uint64_t* __restrict__ alnum16, uint32_t* __restrict__ sbits,
+                                               uint32_t* __restrict__ ebits, uint32_t* __restrict__ docbits,
+                                               const uint64_t* __restrict__ doc_off, uint32_t ndocs) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[256][80];
+    nonzh_body(text, nbytes, lanemask, tile_cnt, ntiles, alnum16, sbits, ebits, docbits, doc_off, ndocs, blockIdx.x,
+               gridDim.x, s_win);
+}
 
 // ---------------------------------------------------------------------------
 // token bitmaps -> spans
 // ---------------------------------------------------------------------------
+constexpr uint32_t kTokCap = 3072;  // tokens per tile staged in LDS (k_tok's write pass)
+// block `blk` of `nblk` (the write pass: token tile blk; the count pass: tiles 2 blk, 2 blk + 1)
 template <bool WRITE>
-__global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits, const uint32_t* __restrict__ ebits,
-                                             uint64_t nwords, uint2* __restrict__ tile_cnt,
-                                             const uint2* __restrict__ supt, uint32_t* __restrict__ counters,
-                                             uint32_t* __restrict__ tok_start, uint32_t* __restrict__ tok_end) {
+__device__ __forceinline__ void tok_body(const uint32_t* __restrict__ sbits, const uint32_t* __restrict__ ebits,
+                                         uint64_t nwords, uint2* __restrict__ tile_cnt,
+                                         const uint2* __restrict__ supt, uint32_t* __restrict__ counters,
+                                         uint32_t* __restrict__ tok_start, uint32_t* __restrict__ tok_end,
+                                         uint32_t blk, uint32_t nblk, uint32_t* lds, uint32_t* s_s, uint32_t* s_e) {
     // bitmap words per lane: the write pass takes a token tile per workgroup, the count
     // pass two (16-byte loads, half the workgroups; a tile's count is the half's sum)
     constexpr uint32_t W = (WRITE ? 1u : 2u) * (kTokTileWords / 256);
-    constexpr uint32_t kCap = 3072;              // tokens per tile staged in LDS (write pass)
-    __shared__ uint32_t lds[8];
-    __shared__ __attribute__((aligned(16))) uint32_t s_s[WRITE ? kCap + 4 : 1], s_e[WRITE ? kCap + 4 : 1];
-    const uint64_t w0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * W;
+    constexpr uint32_t kCap = kTokCap;
+    const uint64_t w0 = ((uint64_t)blk * 256u + threadIdx.x) * W;
     PrefixLoads pl{0u, 0u};
-    if (WRITE) pl = pf_load(tile_cnt, supt, blockIdx.x);
+    if (WRITE) pl = pf_load(tile_cnt, supt, blk);
     uint32_t s[W], e[W];
     if (w0 + W <= nwords) {
         if constexpr (W == 4u) {
@@ -4197,13 +4130,13 @@ __global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits,
     const uint32_t xe = block_scan_u32(ce, lds, &te);
     if (!WRITE) {  // lanes 0-127 hold the first tile: its count is lane 128's exclusive prefix
         if (threadIdx.x == 128u) {
-            tile_cnt[2u * blockIdx.x] = make_uint2(xs, xe);
-            tile_cnt[2u * blockIdx.x + 1u] = make_uint2(ts - xs, te - xe);
+            tile_cnt[2u * blk] = make_uint2(xs, xe);
+            tile_cnt[2u * blk + 1u] = make_uint2(ts - xs, te - xe);
         }
         return;
     }
     const uint2 to = pf_sum(pl, lds);
-    if (blockIdx.x == gridDim.x - 1u && threadIdx.x == 0) {  // token totals
+    if (blk == nblk - 1u && threadIdx.x == 0) {  // token totals
         counters[CNT_NTOK] = to.x + ts;
         counters[CNT_NTOKE] = to.y + te;
         *reinterpret_cast<uint64_t*>(counters + CNT_NWORDS) = to.x + ts;
@@ -4256,6 +4189,16 @@ __global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits,
         for (uint32_t k = threadIdx.x; k < te; k += 256u) __builtin_nontemporal_store(s_e[k], tok_end + to.y + k);
     }
 }
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits, const uint32_t* __restrict__ ebits,
+                                             uint64_t nwords, uint2* __restrict__ tile_cnt,
+                                             const uint2* __restrict__ supt, uint32_t* __restrict__ counters,
+                                             uint32_t* __restrict__ tok_start, uint32_t* __restrict__ tok_end) {
+    __shared__ uint32_t lds[8];
+    __shared__ __attribute__((aligned(16))) uint32_t s_s[WRITE ? kTokCap + 4 : 1], s_e[WRITE ? kTokCap + 4 : 1];
+    tok_body<WRITE>(sbits, ebits, nwords, tile_cnt, supt, counters, tok_start, tok_end, blockIdx.x, gridDim.x, lds, s_s,
+                    s_e);
+}
 
 // tokens of document d: [doc_tok[d], doc_tok[d+1]) = lower_bound over starts.
 // G lanes per document.  G = 16 (a small batch: few documents, so the kernel's time
@@ -4264,11 +4207,11 @@ __global__ __launch_bounds__(256) void k_tok(const uint32_t* __restrict__ sbits,
 // target, log16 loads instead of log2.  G = 1 (many documents: their searches hide
 // each other's latency, and 16 lanes each would cost more loads in all): binary.
 template <uint32_t G>
-__global__ __launch_bounds__(256) void k_doc_tok(const uint64_t* __restrict__ doc_off, uint32_t ndocs,
-                                                 const uint32_t* __restrict__ tok_start,
-                                                 const uint32_t* __restrict__ counters, uint64_t* __restrict__ doc_tok) {
+__device__ __forceinline__ void doc_tok_body(const uint64_t* __restrict__ doc_off, uint32_t ndocs,
+                                             const uint32_t* __restrict__ tok_start,
+                                             const uint32_t* __restrict__ counters, uint64_t* __restrict__ doc_tok,
+                                             uint32_t g) {
     static_assert(G == 1u || G == 16u, "binary or 16-ary");
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t d = g / G, k = threadIdx.x & (G - 1u), gsh = threadIdx.x & (63u & ~(G - 1u));
     if (d > ndocs) return;  // (whole groups: a group is one document)
     const uint32_t n = counters[CNT_NTOK];
@@ -4297,7 +4240,146 @@ __global__ __launch_bounds__(256) void k_doc_tok(const uint64_t* __restrict__ do
     }
     if (k == 0u) doc_tok[d] = lo;
 }
+template <uint32_t G>
+__global__ __launch_bounds__(256) void k_doc_tok(const uint64_t* __restrict__ doc_off, uint32_t ndocs,
+                                                 const uint32_t* __restrict__ tok_start,
+                                                 const uint32_t* __restrict__ counters, uint64_t* __restrict__ doc_tok) {
+    doc_tok_body<G>(doc_off, ndocs, tok_start, counters, doc_tok, blockIdx.x * blockDim.x + threadIdx.x);
+}
 constexpr uint32_t kDocTokWide = 16384;  // documents from which k_doc_tok searches one lane each
+
+// ---------------------------------------------------------------------------
+// k_long: the long-block kernels above as the phases of one launch (VERDICT r04
+// item 5), so that a batch without a long block (CNT_NLONG 0: every batch of
+// short documents) pays one launch instead of seven.  A grid barrier between the
+// phases (DESIGN §6's rule for inter-workgroup waits: every thread's stores made
+// visible at agent scope, a counter bumped by one thread per workgroup, polled with
+// agent-scope atomic loads, an acquire fence after; the wait is bounded and sets
+// CNT_ERR bit 1 when it runs out).  One workgroup per CU at most (the phases' LDS,
+// unioned, is 132 KB), and the grid is at most the CU count, so all its workgroups
+// are resident together.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kGridSpins = 1u << 21;  // polls before a phase wait gives up (seconds)
+// A phase's work items are claimed from a counter (CNT_PHASE + 2 p) by running workgroups,
+// in phase order, so a workgroup waits only on items that running workgroups claimed: the
+// grid need not be resident all at once (another kernel, e.g. a second pipeline on the
+// same GPU, may hold CUs).  A workgroup adds its finished items to CNT_PHASE + 2 p + 1.
+__device__ __forceinline__ uint32_t wg_claim(uint32_t* ctr, uint32_t* s_x) {  // (the whole workgroup)
+    if (threadIdx.x == 0u) *s_x = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t it = *s_x;
+    __syncthreads();
+    return it;
+}
+__device__ __forceinline__ uint32_t wave_claim(uint32_t* ctr) {  // (one wave)
+    uint32_t it = 0;
+    if ((threadIdx.x & 63u) == 0u) it = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)it);
+}
+// the end of a phase: every thread's stores released at agent scope, the workgroup's
+// finished items (thread 0's count) added, then a wait until all nitems are done and an
+// acquire; a wait that runs out of polls sets CNT_ERR bit 1 (the host reports it)
+__device__ __forceinline__ void phase_end(uint32_t* done, uint32_t mine, uint32_t nitems, uint32_t* err) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (threadIdx.x == 0u) {
+        if (mine) __hip_atomic_fetch_add(done, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t spins = 0;
+        while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nitems) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins == kGridSpins) {
+                __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+union LongAll {  // the phases' LDS
+    struct {
+        double ring[kSpecRing][64];
+        uint8_t cd[64][kSeg];
+        double wt[kZhWtab];
+        double bw[64][kSeg];
+    } sp;                             // k_long_spec (wave 0)
+    LongLds dp;                       // k_long_dp
+    uint32_t m32[kLpBatch * kLpMap / 4u];  // k_long_path (wave 0)
+    uint4 cd4[256][kSeg / 16u];       // k_long_pbits, k_long_tail
+    uint8_t bl[256][kSeg];            // k_long_seg
+};
+
+template <bool HMM>
+__global__ __launch_bounds__(256) void k_long(const uint8_t* __restrict__ text, DevImage im,
+                                              const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
+                                              const uint32_t* __restrict__ lsegb, uint32_t* __restrict__ counters,
+                                              const uint32_t* __restrict__ tile4, uint8_t* __restrict__ gbl,
+                                              double* __restrict__ gbest, uint8_t* __restrict__ lcode,
+                                              uint8_t* __restrict__ lmap, uint8_t* __restrict__ lcx,
+                                              uint64_t* __restrict__ lpath, uint32_t* __restrict__ lflag,
+                                              uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
+                                              uint64_t* __restrict__ dbg, uint32_t spec) {
+    __shared__ __attribute__((aligned(16))) LongAll U;
+    __shared__ uint32_t s_claim;
+    const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG];  // (k_zh wrote them before this launch)
+    if (nlong == 0u) return;
+    const bool w0 = threadIdx.x < 64u;  // (the one-wave phases)
+    uint32_t* const ph = counters + CNT_PHASE;
+    uint32_t* const err = counters + CNT_ERR;
+    uint32_t p = 0;  // the phase
+    // a phase of nitems items, f(item) on the whole workgroup / on wave 0 only
+    auto wg_phase = [&](uint32_t nitems, auto&& f) {
+        uint32_t mine = 0;
+        for (uint32_t it; (it = wg_claim(ph + 2u * p, &s_claim)) < nitems; mine++) f(it);
+        phase_end(ph + 2u * p + 1u, mine, nitems, err);
+        p++;
+    };
+    auto wave_phase = [&](uint32_t nitems, auto&& f) {
+        uint32_t mine = 0;
+        if (w0)
+            for (uint32_t it; (it = wave_claim(ph + 2u * p)) < nitems; mine++) f(it);
+        phase_end(ph + 2u * p + 1u, mine, nitems, err);
+        p++;
+    };
+    const uint32_t nsg64 = (nseg + 63u) / 64u, nsg256 = (nseg + 255u) / 256u;
+    {
+        if (spec) {
+            double* const wt = w0 ? long_spec_setup(im, U.sp.wt) : nullptr;
+            wave_phase(nsg64, [&](uint32_t it) {
+                long_spec_body(text, im, erec, longblk, lsegb, counters, tile4, gbl, gbest, lcode, lmap, lflag, spec,
+                               it, nsg64, U.sp.ring, U.sp.cd, wt, U.sp.bw);
+            });
+            if (spec != 3u) {
+                wave_phase(nlong, [&](uint32_t it) {
+                    long_path_body(longblk, lsegb, counters, lflag, lcode, lmap, lcx, 3u, 3u, it, nlong, U.m32);
+                });
+                wg_phase(nsg256, [&](uint32_t it) {
+                    long_pbits_body(longblk, lsegb, counters, lflag, gbl, lcode, lcx, lpath, it, nsg256, U.cd4);
+                });
+            } else {
+                p += 2u;
+            }
+        } else {
+            p += 3u;
+        }
+        wg_phase(nlong, [&](uint32_t it) {
+            long_dp_body<HMM>(text, im, erec, gbl, gbest, longblk, counters, sbits, ebits, lflag, lsegb, lpath, dbg,
+                              spec, it, nlong, U.dp);
+        });
+        wg_phase(nsg256, [&](uint32_t it) {
+            long_seg_body(text, im, erec, longblk, lsegb, counters, lflag, gbest, gbl, lcode, lmap, it, nsg256, U.bl);
+        });
+        wave_phase(nlong, [&](uint32_t it) {
+            long_path_body(longblk, lsegb, counters, lflag, lcode, lmap, lcx, 2u, 1u, it, nlong, U.m32);
+        });
+        // (the Viterbi back-pointers go to gbest's bytes: the exit codes in lcode are read to the end;
+        // the last phase: nothing waits for it inside the kernel)
+        for (uint32_t it; (it = wg_claim(ph + 2u * p, &s_claim)) < nsg256;)
+            long_tail_body<HMM>(text, im, gbl, longblk, lsegb, lflag, counters, lcode, lcx,
+                                reinterpret_cast<uint8_t*>(gbest), sbits, ebits, it, nsg256, U.cd4);
+    }
+}
 
 // Boundary-mask output (jb_cut_batch_mask): a piece's token bitmaps (bit j = byte j
 // of the piece, u32 words) into the range's u64 bitmaps at bit offset `rel`, bits
