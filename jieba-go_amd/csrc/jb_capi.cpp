@@ -695,6 +695,9 @@ static int init_launch_cfg(Device* d) {
     if (lf < 0 || lf > 1) return fail(JB_EINVAL, "JB_LONG_FUSED=%d: want 0 or 1", lf);
     lc.long_fused = (uint32_t)lf;
     lc.ncu = std::max(1u, d->ncu);
+    const int t1 = env_int("JB_TOK1", 1);
+    if (t1 < 0 || t1 > 1) return fail(JB_EINVAL, "JB_TOK1=%d: want 0 or 1", t1);
+    lc.tok1 = (uint32_t)t1;
     const int ss = env_int("JB_SMALL_SLOTS", 4);
     if (ss < 1 || ss > 4) return fail(JB_EINVAL, "JB_SMALL_SLOTS=%d: want 1 .. 4", ss);
     d->small_slots = (uint32_t)ss;

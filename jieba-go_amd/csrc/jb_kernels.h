@@ -38,6 +38,7 @@ enum {
     CNT_ERR = 4,    // bit 0: a zh block reached a tail index -1 (the reference panics); bit 1: a k_long
                     // phase wait ran out of polls
     CNT_WORK = 5,   // k_zh work counter: next group (kZhGroupBytes of text)
+    CNT_TOKT = 30,  // k_tok1's tile tickets
     CNT_PHASE = 32, // k_long's phases: claimed items at 32 + 2 p, finished items at 33 + 2 p
     CNT_ALL = 64,   // (u32 slots of the counters buffer; k_docbits clears them all)
     CNT_TIES = 7,   // exact Viterbi route ties (Q12)
@@ -75,7 +76,7 @@ struct Work {
     uint64_t bits_stride;  // words between docbits, sbits and ebits (one allocation)
     uint2* supt;           // per 256 token tiles: (starts, ends) (k_sup)
     uint2* tile_cnt;       // per k_mark_walk tile: (blocks, zh blocks) starting in it
-    uint2* ttile_cnt;      // per token tile (starts, ends)
+    uint2* ttile_cnt;      // per token tile (starts, ends); k_tok1: its look-back status word
     uint64_t* alnum16;     // 1 bit per 16 bytes of text: some [0-9A-Za-z] byte there
     uint64_t* erec;        // per Han rune (slot = byte / 3): packed DAG edges (k_mark_walk -> k_zh)
     uint32_t* lanemask;    // per 16 bytes: block starts | Han block starts << 16 (k_zh and k_nonzh read
@@ -106,7 +107,7 @@ struct Work {
 enum KernelId {
     K_DOCBITS = 0, K_MARK_WALK, K_ZH, K_NONZH,
     K_TOK_COUNT, K_SCAN_TOK, K_TOK_WRITE, K_DOC_TOK, K_LONG_SPEC, K_LONG_DP, K_LONG_SEG, K_LONG_PATH, K_LONG_TAIL, K_MASK_MERGE,
-    K_LONG_PBITS, K_LONG,
+    K_LONG_PBITS, K_LONG, K_TOK1,
     K_NUM
 };
 extern const char* const kKernelNames[K_NUM];
@@ -133,6 +134,8 @@ struct LaunchCfg {
                              // some choices wrong on purpose, so that the exact chain redoes the block
     uint32_t long_fused;     // the long-block kernels as one launch, k_long (JB_LONG_FUSED: 1 default, 0 separate)
     uint32_t ncu;            // the device's CUs (k_long's grid: at most one workgroup per CU)
+    uint32_t tok1;           // the span kernels as one pass, k_tok1, for batches of <= 256 token tiles
+                             // (JB_TOK1: 1 default, 0 the count/write passes always)
 };
 
 // k_zh's group split: g1 groups of grp bytes, then groups of *sgrp bytes to the end.

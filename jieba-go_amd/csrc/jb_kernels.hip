@@ -41,7 +41,7 @@ namespace jb {
 
 const char* const kKernelNames[K_NUM] = {"k_docbits", "k_mark_walk", "k_zh", "k_nonzh", "k_tok_count", "k_scan_tok",
                                          "k_tok_write", "k_doc_tok", "k_long_spec", "k_long_dp", "k_long_seg", "k_long_path",
-                                         "k_long_tail", "k_mask_merge", "k_long_pbits", "k_long"};
+                                         "k_long_tail", "k_mask_merge", "k_long_pbits", "k_long", "k_tok1"};
 
 // newJiebaHMM literals (tokenizer.go:629-652)
 #define START_B (-0.26268660809250016)
@@ -140,9 +140,11 @@ struct LdsEmitter {
 // set (one per document), after k_mark_walk (their only reader) is done with them.  The first
 // launch also clears the run's counters (no kernel before it uses them).
 __global__ void k_docbits(const uint64_t* __restrict__ doc_off, uint32_t ndocs, uint64_t nbytes,
-                          uint32_t* __restrict__ bits, uint32_t* __restrict__ counters) {
+                          uint32_t* __restrict__ bits, uint32_t* __restrict__ counters,
+                          uint64_t* __restrict__ tstat, uint32_t ntt) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d < CNT_ALL) counters[d] = 0u;
+    if (d < ntt) tstat[d] = 0ull;  // (k_tok1's look-back: every token tile not ready)
     if (d >= ndocs) return;
     const uint64_t o = doc_off[d];
     if (o < nbytes) atomicOr(bits + (o >> 5), 1u << (o & 31u));
@@ -4248,6 +4250,181 @@ __global__ __launch_bounds__(256) void k_doc_tok(const uint64_t* __restrict__ do
 }
 constexpr uint32_t kDocTokWide = 16384;  // documents from which k_doc_tok searches one lane each
 
+// k_tok1: the span kernels in one pass (round 5): k_tok's count pass, k_sup, its write
+// pass and k_doc_tok.  A workgroup takes the next token tile by a ticket (tiles in
+// claim order), counts its tokens, publishes the count, and finds its exclusive prefix
+// by looking back over the tiles before it (decoupled look-back: a tile's status word is
+// its count, flag 1, or its inclusive prefix, flag 2; it waits only on tiles claimed
+// before it, so by running workgroups).  Then it writes its spans as k_tok's write pass
+// does, and the per-document first tokens of the documents that start in its bytes
+// (k_doc_tok's lower bound, here over the tile's own starts in LDS).
+// Status: flag << 62 | starts prefix (31 bits) << 31 | ends prefix (31 bits).
+__device__ __forceinline__ uint64_t ts_pack(uint32_t f, uint32_t x, uint32_t y) {
+    return ((uint64_t)f << 62) | ((uint64_t)x << 31) | (uint64_t)y;
+}
+__global__ __launch_bounds__(256) void k_tok1(const uint32_t* __restrict__ sbits, const uint32_t* __restrict__ ebits,
+                                              uint64_t nwords, uint32_t ntt, uint64_t* __restrict__ tstat,
+                                              uint32_t* __restrict__ counters, uint32_t* __restrict__ tok_start,
+                                              uint32_t* __restrict__ tok_end, const uint64_t* __restrict__ doc_off,
+                                              uint32_t ndocs, uint64_t* __restrict__ doc_tok) {
+    constexpr uint32_t W = kTokTileWords / 256u;
+    constexpr uint32_t kCap = kTokCap;
+    constexpr uint64_t TB = (uint64_t)kTokTileWords * 32u;  // bytes per token tile
+    __shared__ uint32_t lds[8];
+    __shared__ uint32_t s_t, s_d0;
+    __shared__ uint2 s_to;
+    __shared__ __attribute__((aligned(16))) uint32_t s_s[kCap + 4], s_e[kCap + 4];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0u) s_t = __hip_atomic_fetch_add(counters + CNT_TOKT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t t = s_t;
+    const uint64_t w0 = ((uint64_t)t * 256u + threadIdx.x) * W;
+    uint32_t s[W], e[W];
+    if (w0 + W <= nwords) {
+        const uint2 a = *reinterpret_cast<const uint2*>(sbits + w0);
+        const uint2 b = *reinterpret_cast<const uint2*>(ebits + w0);
+        s[0] = a.x; s[1] = a.y;
+        e[0] = b.x; e[1] = b.y;
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < W; k++) {
+            s[k] = w0 + k < nwords ? sbits[w0 + k] : 0u;
+            e[k] = w0 + k < nwords ? ebits[w0 + k] : 0u;
+        }
+    }
+    // the first document that starts in the tile (or after it): a 16-ary lower bound over
+    // doc_off (wave 1, its loads beside the bitmap loads)
+    if (wave == 1u) {
+        const uint64_t target = (uint64_t)t * TB;
+        const uint32_t k = lane & 15u;
+        uint32_t lo = 0, hi = ndocs + 1u;  // the answer in [lo, hi]
+        while (lo < hi) {
+            const uint32_t sx = (hi - lo + 15u) >> 4;
+            const uint32_t i = lo + (k + 1u) * sx - 1u;
+            const bool before = i < hi && doc_off[i] < target;
+            const uint32_t c = (uint32_t)__popcll(__ballot(before) & 0xFFFFull);
+            const uint32_t nlo = lo + c * sx;
+            if (sx == 1u || nlo >= hi) {
+                lo = min(nlo, hi);
+                break;
+            }
+            hi = min(hi, nlo + sx - 1u);
+            lo = nlo;
+        }
+        if (lane == 0u) s_d0 = lo;
+    }
+    uint32_t cs = 0, ce = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < W; k++) {
+        cs += __popc(s[k]);
+        ce += __popc(e[k]);
+    }
+    uint32_t ts, te;
+    const uint32_t xs = block_scan_u32(cs, lds, &ts);
+    const uint32_t xe = block_scan_u32(ce, lds, &te);
+    // publish the count, then look back (wave 0)
+    if (threadIdx.x == 0u)
+        __hip_atomic_store(tstat + t, ts_pack(t == 0u ? 2u : 1u, ts, te), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wave == 0u) {
+        uint32_t px = 0, py = 0;
+        for (int64_t base = (int64_t)t - 1; base >= 0;) {
+            const int64_t j = base - (int64_t)lane;
+            uint64_t v = j >= 0 ? __hip_atomic_load(tstat + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ts_pack(2u, 0u, 0u);
+            const uint64_t incl = __ballot((v >> 62) == 2u), ready = __ballot((v >> 62) != 0u);
+            // the nearest inclusive prefix, and every tile between ready
+            const uint32_t k2 = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;
+            const uint64_t need = k2 == 64u ? ~0ull : ((2ull << k2) - 1ull);
+            if ((ready & need) != need) {
+                __builtin_amdgcn_s_sleep(1);
+                continue;  // (a tile before is still counting: read again)
+            }
+            uint32_t x = lane <= k2 ? (uint32_t)(v >> 31) & 0x7FFFFFFFu : 0u;
+            uint32_t y = lane <= k2 ? (uint32_t)v & 0x7FFFFFFFu : 0u;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+                x += (uint32_t)__shfl_xor((int)x, d, 64);
+                y += (uint32_t)__shfl_xor((int)y, d, 64);
+            }
+            px += x;
+            py += y;
+            if (k2 < 64u) break;
+            base -= 64;
+        }
+        if (lane == 0u) {
+            s_to = make_uint2(px, py);
+            if (t > 0u)
+                __hip_atomic_store(tstat + t, ts_pack(2u, px + ts, py + te), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    const uint2 to = s_to;
+    if (t == ntt - 1u && threadIdx.x == 0) {  // token totals
+        counters[CNT_NTOK] = to.x + ts;
+        counters[CNT_NTOKE] = to.y + te;
+        *reinterpret_cast<uint64_t*>(counters + CNT_NWORDS) = to.x + ts;
+    }
+    // the spans (k_tok's write pass)
+    const bool staged = ts <= kCap && te <= kCap;
+    const bool v4 = (((uintptr_t)tok_start | (uintptr_t)tok_end) & 15u) == 0u;
+    const uint32_t shs = v4 ? (to.x & 3u) : 0u, she = v4 ? (to.y & 3u) : 0u;
+    uint32_t* os = staged ? s_s + shs : tok_start + to.x;
+    uint32_t* oe = staged ? s_e + she : tok_end + to.y;
+    uint32_t gs = xs, ge = xe;
+#pragma unroll
+    for (uint32_t k = 0; k < W; k++) {
+        const uint32_t base = (uint32_t)((w0 + k) << 5);
+        uint32_t m = s[k];
+        while (m) {
+            os[gs++] = base + (uint32_t)__builtin_ctz(m);
+            m &= m - 1;
+        }
+        m = e[k];
+        while (m) {
+            oe[ge++] = base + (uint32_t)__builtin_ctz(m) + 1u;
+            m &= m - 1;
+        }
+    }
+    __syncthreads();  // (the staged starts, or this workgroup's global ones, for the documents below)
+    // the documents that start in the tile (the last tile: all that are left, with the end
+    // sentinel d = ndocs): their first token is the first start >= their offset
+    {
+        const uint32_t d0 = s_d0;
+        const uint64_t hiB = t == ntt - 1u ? ~0ull : ((uint64_t)t + 1u) * TB;
+        for (uint32_t d = d0 + threadIdx.x; d <= ndocs; d += 256u) {
+            const uint64_t o = doc_off[d];
+            if (o >= hiB) break;
+            const uint32_t* st = staged ? s_s + shs : tok_start + to.x;
+            uint32_t lo = 0, hi = ts;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if ((uint64_t)st[mid] < o) lo = mid + 1;
+                else hi = mid;
+            }
+            doc_tok[d] = to.x + lo;
+        }
+    }
+    if (!staged) return;
+    if (v4) {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        auto out = [&](const uint32_t* a, uint32_t sh, uint32_t n, uint32_t* g) {  // g: output at LDS index 0
+            const uint32_t lo = (sh + 3u) & ~3u, hi = (sh + n) & ~3u;  // whole vectors: [lo, hi)
+            if (lo < hi) {
+                for (uint32_t p = lo + 4u * threadIdx.x; p < hi; p += 1024u)
+                    __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(a + p), reinterpret_cast<u32x4*>(g + p));
+                if (threadIdx.x < lo - sh) __builtin_nontemporal_store(a[sh + threadIdx.x], g + sh + threadIdx.x);
+                if (threadIdx.x < sh + n - hi) __builtin_nontemporal_store(a[hi + threadIdx.x], g + hi + threadIdx.x);
+            } else if (threadIdx.x < n) {
+                __builtin_nontemporal_store(a[sh + threadIdx.x], g + sh + threadIdx.x);
+            }
+        };
+        out(s_s, shs, ts, tok_start + to.x - shs);
+        out(s_e, she, te, tok_end + to.y - she);
+        return;
+    }
+    for (uint32_t k = threadIdx.x; k < ts; k += 256u) __builtin_nontemporal_store(s_s[k], tok_start + to.x + k);
+    for (uint32_t k = threadIdx.x; k < te; k += 256u) __builtin_nontemporal_store(s_e[k], tok_end + to.y + k);
+}
+
 // ---------------------------------------------------------------------------
 // k_long: the long-block kernels above as the phases of one launch (VERDICT r04
 // item 5), so that a batch without a long block (CNT_NLONG 0: every batch of
@@ -5300,8 +5477,9 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     // clears the counters and k_mark_walk the token bitmaps, tile by tile.
     if (nbytes == 0)  // (kernels, not hipMemsetAsync: see k_zero)
         return run_zero(w.doc_tok, (ndocs + 1) * sizeof(uint64_t), stream, w.counters, CNT_CLEAR * sizeof(uint32_t));
-    JB_TIMED(K_DOCBITS, hipLaunchKernelGGL(k_docbits, dim3(std::max(1u, (ndocs + 255) / 256)), dim3(256), 0, stream,
-                                           d_doc_off, ndocs, nbytes, w.docbits, w.counters));
+    JB_TIMED(K_DOCBITS, hipLaunchKernelGGL(k_docbits, dim3(std::max(1u, (std::max(ndocs, nttiles) + 255) / 256)),
+                                           dim3(256), 0, stream, d_doc_off, ndocs, nbytes, w.docbits, w.counters,
+                                           reinterpret_cast<uint64_t*>(w.ttile_cnt), nttiles));
     JB_TIMED(K_MARK_WALK, hipLaunchKernelGGL(k_mark_walk, dim3(ntiles), dim3(256), 0, stream, d_text, nbytes,
                                              w.docbits, im, w.lanemask, w.tile_cnt, w.erec + kErecPad,
                                              w.tile4, w.alnum16, w.sbits, w.ebits, diag, w.dbg_walk));
@@ -5385,6 +5563,14 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                                   dim3(256), 0,
                                                   stream, w.sbits, w.ebits, nbytes, mask->rel, mask->s, mask->e,
                                                   w.counters));
+        return hipGetLastError();
+    }
+    // the span kernels in one pass for batches of at most 256 token tiles (4 MiB): at 1 GiB
+    // (65K tiles) the look-back chains cost more than the passes it saves (0.33 -> 0.84 ms)
+    if (lc.tok1 && nttiles <= 256u) {
+        JB_TIMED(K_TOK1, hipLaunchKernelGGL(k_tok1, dim3(nttiles), dim3(256), 0, stream, w.sbits, w.ebits, nwords,
+                                            nttiles, reinterpret_cast<uint64_t*>(w.ttile_cnt), w.counters, w.tok_start,
+                                            w.tok_end, d_doc_off, ndocs, w.doc_tok));
         return hipGetLastError();
     }
     JB_TIMED(K_TOK_COUNT, hipLaunchKernelGGL((k_tok<false>), dim3((nttiles + 1u) / 2u), dim3(256), 0, stream, w.sbits, w.ebits,
