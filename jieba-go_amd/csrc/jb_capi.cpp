@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cmath>
 #include <memory>
@@ -166,13 +167,17 @@ struct Device {
     // per in-flight k_small batch (cut_small keeps up to kSmallSlots launched at once)
     struct SmallSlot {
         uint8_t* h_sin = nullptr;    // text (kSmallBytes + 128), then u64 doc offsets (kSmallDocs + 1)
-        uint32_t* h_sout = nullptr;  // header, spans, doc_tok (kSmallOutBytes)
+        // header, spans, doc_tok (kSmallOutBytes), two of them: batches alternate, so the
+        // slot's next batch runs while the callers of the last one get their spans
+        uint32_t* h_sout[2] = {nullptr, nullptr};
         uint8_t* d_sin = nullptr;    // their device addresses
-        uint32_t* d_sout = nullptr;
+        uint32_t* d_sout[2] = {nullptr, nullptr};
+        uint32_t ob = 0;             // the output buffer of the slot's current batch
+        std::atomic<bool> reading[2] = {false, false};  // spans still being split out of h_sout[i]
         uint32_t seq = 0;            // the kernel writes this number last
         bool busy = false;
         hipStream_t st = nullptr;    // this slot's stream, masked to its own CU
-    } slots[4];
+    } slots[8];
     // jb_last_stats' view of the last batch: last_small, small_hdr and has_stats, under
     // stats_mu alone (a finished k_small batch publishes them without waiting for d->mu,
     // which a host-batch pipeline holds for its whole run; lock order: mu, then stats_mu)
@@ -182,8 +187,11 @@ struct Device {
     std::mutex small_mu;
     std::condition_variable small_cv;
     std::deque<SmallReq*> small_q;
-    std::atomic<uint32_t> small_gen{0};  // k_small batches completed (waiters spin on it)
-    uint32_t small_slots = 4;            // k_small batches in flight at most (JB_SMALL_SLOTS, 1..4)
+    uint32_t small_sleepers = 0;         // callers asleep on small_cv (under small_mu)
+    // JB_SMALL_TRACE=path (diagnostics): per batch its slot, calls, and the clocks (us) of
+    // staging, launch return, completion word and split, written to path at jb_close
+    std::vector<std::array<double, 6>> small_trace;
+    uint32_t small_slots = 4;            // k_small batches in flight at most (JB_SMALL_SLOTS, 1..8)
     uint32_t small_hdr[kSmallHdr] = {0};
     uint32_t ncu = 0;
     uint64_t piece_bytes = 64ull << 20;  // host-batch pipeline piece (JB_PIECE_KIB)
@@ -699,7 +707,7 @@ static int init_launch_cfg(Device* d) {
     if (t1 < 0 || t1 > 1) return fail(JB_EINVAL, "JB_TOK1=%d: want 0 or 1", t1);
     lc.tok1 = (uint32_t)t1;
     const int ss = env_int("JB_SMALL_SLOTS", 4);
-    if (ss < 1 || ss > 4) return fail(JB_EINVAL, "JB_SMALL_SLOTS=%d: want 1 .. 4", ss);
+    if (ss < 1 || ss > 8) return fail(JB_EINVAL, "JB_SMALL_SLOTS=%d: want 1 .. 8", ss);
     d->small_slots = (uint32_t)ss;
     return JB_OK;
 }
@@ -900,11 +908,13 @@ static int open_device(Device* d, int ordinal, const Image& img) {
                         "JB_SMALL_CU=%d, JB_SMALL_CU_STRIDE=%d, JB_SMALL_SLOTS=%u: slot k runs on CU "
                         "JB_SMALL_CU + k x JB_SMALL_CU_STRIDE, and the last one (%d) is past the device's %u CUs",
                         cu, cs, d->small_slots, last, d->ncu);
+        const bool masked = env_int("JB_SMALL_CUMASK", 1) != 0;  // (0: plain streams, diagnostics)
         for (int k = 0; k < (int)d->small_slots; k++) {
             std::vector<uint32_t> mask((d->ncu + 31) / 32, 0u);
             const int c = cu + k * cs;
             mask[c / 32] = 1u << (c % 32);
-            HIPCHK(hipExtStreamCreateWithCUMask(&d->slots[k].st, (uint32_t)mask.size(), mask.data()));
+            if (masked) HIPCHK(hipExtStreamCreateWithCUMask(&d->slots[k].st, (uint32_t)mask.size(), mask.data()));
+            else HIPCHK(hipStreamCreateWithFlags(&d->slots[k].st, hipStreamNonBlocking));
         }
     }
     return JB_OK;
@@ -960,6 +970,12 @@ extern "C" int jb_open(const jb_config* cfg, jb_ctx** out) {
 extern "C" void jb_close(jb_ctx* ctx) {
     if (!ctx) return;
     for (auto& d : ctx->devs) {
+        if (const char* tp = getenv("JB_SMALL_TRACE"); tp && !d->small_trace.empty())
+            if (FILE* f = fopen(tp, "a")) {
+                for (const auto& r : d->small_trace)
+                    fprintf(f, "%g %g %.3f %.3f %.3f %.3f\n", r[0], r[1], r[2], r[3], r[4], r[5]);
+                fclose(f);
+            }
         (void)hipSetDevice(d->ordinal);
         (void)hipStreamSynchronize(d->stream);
         for (auto& sl : d->slots)
@@ -978,7 +994,8 @@ extern "C" void jb_close(jb_ctx* ctx) {
         hfree(d->h_text); hfree(d->h_misc);
         for (auto& sl : d->slots) {
             hfree(sl.h_sin);
-            hfree(sl.h_sout);
+            hfree(sl.h_sout[0]);
+            hfree(sl.h_sout[1]);
         }
         free_outs(d.get());
         hfree(d->h_pcnt); dfree(d->d_mask); hfree(d->h_mask); hfree(d->h_zero);
@@ -1003,14 +1020,15 @@ extern "C" const char* jb_last_error(void) { return g_err.c_str(); }
 // call, BASELINE config 1) is one k_small launch that reads the text and offsets
 // from mapped pinned host memory (or its kernel arguments) and writes the spans
 // there.  Concurrent calls on a device are coalesced (the reference runs Cut calls
-// side by side under RLock, tokenizer.go:151-153): each call queues a SmallReq;
-// a caller whose request is still queued takes a free slot (one of four pinned
-// input/output buffer pairs, each with its own stream on its own CU), launches the
-// queue's head requests (same hmm, up to the k_small limits together) as ONE k_small
-// batch on it, their documents back to back, waits for that batch's completion word
-// and hands each caller its own spans by its documents' doc_tok ranges.  Up to
-// JB_SMALL_SLOTS batches run at once, side by side on their CUs.  One caller alone:
-// a batch of one, as before.
+// side by side under RLock, tokenizer.go:151-153): each call queues a SmallReq.  A
+// caller that finds a slot free (one of JB_SMALL_SLOTS pinned input/output buffer pairs,
+// each with its own stream on its own CU) launches the queue's head requests (same hmm,
+// up to the k_small limits together) as ONE k_small batch on it, their documents back to
+// back, waits for that batch's completion word and hands each caller its own spans by its
+// documents' doc_tok ranges.  The slot then goes straight to the caller of the next
+// queued request, with the next batch: callers wait on their own request's state word,
+// so a finished batch wakes the callers it served and the one it hands the slot to, not
+// every waiting caller.  One caller alone: a batch of one.
 namespace {
 struct SmallReq {
     const uint8_t* text;
@@ -1020,14 +1038,19 @@ struct SmallReq {
     SpanBuf* out;
     int rc = JB_OK;
     std::string err;
-    bool launched = false;  // taken into a k_small batch
-    bool done = false;
+    // kQueued, then kDone; or kLaunch first: this caller launches `batch` (its own request at
+    // the head) on slot `sl`, which the caller that finished that slot's last batch handed over
+    std::atomic<uint32_t> state{0};
+    Device::SmallSlot* sl = nullptr;
+    std::vector<SmallReq*> batch;
 };
+enum : uint32_t { kQueued = 0, kLaunch = 1, kDone = 2 };
 }  // namespace
 
-// One k_small launch over requests rq[0..n) (together within the limits): stage, launch,
-// wait for the completion word, split the spans.  Sets each request's rc / err.
-static void small_batch(Device* d, Device::SmallSlot* sl, SmallReq* const* rq, uint32_t n) {
+// One k_small launch over requests rq[0..n) (together within the limits) on the slot's
+// next output buffer: stage, launch, wait for the completion word.  Returns the output
+// (header, spans, doc_tok), or nullptr with each request's rc / err set.
+static const uint32_t* small_launch(Device* d, Device::SmallSlot* sl, SmallReq* const* rq, uint32_t n) {
     auto fail_all = [&](int rc) {
         for (uint32_t i = 0; i < n; i++) {
             rq[i]->rc = rc;
@@ -1039,16 +1062,22 @@ static void small_batch(Device* d, Device::SmallSlot* sl, SmallReq* const* rq, u
         fail_all(fail(e == hipErrorOutOfMemory ? JB_ENOMEM : JB_EDEVICE, "%s: %s", what, hipGetErrorString(e)));
         return false;
     };
-    if (!chk(hipSetDevice(d->ordinal), "hipSetDevice")) return;
+    if (!chk(hipSetDevice(d->ordinal), "hipSetDevice")) return nullptr;
     if (!sl->h_sin) {
         const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
         if (!chk(hipHostMalloc(&sl->h_sin, kSmallBytes + 128 + 8 * (kSmallDocs + 1), fl), "hipHostMalloc") ||
-            !chk(hipHostMalloc(&sl->h_sout, kSmallOutBytes, fl), "hipHostMalloc") ||
-            !chk(hipHostGetDevicePointer((void**)&sl->d_sin, sl->h_sin, 0), "hipHostGetDevicePointer") ||
-            !chk(hipHostGetDevicePointer((void**)&sl->d_sout, sl->h_sout, 0), "hipHostGetDevicePointer"))
-            return;
-        sl->h_sout[SM_DONE] = 0;  // (recycled pinned memory may hold any value; seq starts at 1)
+            !chk(hipHostGetDevicePointer((void**)&sl->d_sin, sl->h_sin, 0), "hipHostGetDevicePointer"))
+            return nullptr;
+        for (int k = 0; k < 2; k++) {
+            if (!chk(hipHostMalloc(&sl->h_sout[k], kSmallOutBytes, fl), "hipHostMalloc") ||
+                !chk(hipHostGetDevicePointer((void**)&sl->d_sout[k], sl->h_sout[k], 0), "hipHostGetDevicePointer"))
+                return nullptr;
+            sl->h_sout[k][SM_DONE] = 0;  // (recycled pinned memory may hold any value; seq starts at 1)
+        }
     }
+    // the other buffer: the last batch's callers may still be taking their spans from this one
+    sl->ob ^= 1u;
+    while (sl->reading[sl->ob].load(std::memory_order_acquire)) __builtin_ia32_pause();
     const bool hmm = rq[0]->hmm;
     uint64_t nbytes = 0;
     uint32_t nd = 0;
@@ -1084,27 +1113,36 @@ static void small_batch(Device* d, Device::SmallSlot* sl, SmallReq* const* rq, u
     // the kernel writes the call's sequence number after everything else (system-scope
     // release); spinning on it returns as soon as the results are in host memory
     const uint32_t seq = ++sl->seq;
-    volatile uint32_t* done = sl->h_sout + SM_DONE;
+    volatile uint32_t* done = sl->h_sout[sl->ob] + SM_DONE;
     if (!chk(run_small(d->dim, inl ? nullptr : sl->d_sin, (uint32_t)nbytes,
                        inl ? nullptr : reinterpret_cast<const uint64_t*>(sl->d_sin + kSmallBytes + 128), nd, hmm,
-                       sl->d_sout, seq, in, sl->st),
+                       sl->d_sout[sl->ob], seq, in, sl->st),
              "k_small launch"))
-        return;
+        return nullptr;
     const auto c1 = std::chrono::steady_clock::now();
     for (uint32_t spin = 0; *done != seq; spin++) {
         if ((spin & 1023u) != 1023u) continue;
         const hipError_t q = hipStreamQuery(sl->st);
         if (q == hipErrorNotReady) continue;
-        if (!chk(q, "k_small")) return;
+        if (!chk(q, "k_small")) return nullptr;
         if (*done != seq) {
             fail_all(fail(JB_EDEVICE, "k_small finished without its completion word"));
-            return;
+            return nullptr;
         }
         break;
     }
     std::atomic_thread_fence(std::memory_order_acquire);
     const auto c2 = std::chrono::steady_clock::now();
-    const uint32_t* h = sl->h_sout;
+    static const bool trace = getenv("JB_SMALL_TRACE") != nullptr;
+    if (trace) {
+        auto us = [](std::chrono::steady_clock::time_point t) {
+            return std::chrono::duration<double, std::micro>(t.time_since_epoch()).count();
+        };
+        std::lock_guard<std::mutex> g(d->stats_mu);
+        d->small_trace.push_back({(double)(sl - d->slots), (double)n, us(c0), us(c1), us(c2),
+                                  us(std::chrono::steady_clock::now())});
+    }
+    const uint32_t* h = sl->h_sout[sl->ob];
     {
         std::lock_guard<std::mutex> g(d->stats_mu);  // (jb_last_stats reads these; not d->mu: see Device)
         memcpy(d->small_hdr, h, sizeof d->small_hdr);
@@ -1123,23 +1161,41 @@ static void small_batch(Device* d, Device::SmallSlot* sl, SmallReq* const* rq, u
                 h[SM_CLK + 17], h[SM_CLK + 18]);
         fprintf(stderr, "\n");
     }
+    return h;
+}
+
+// After a batch: its errors.  0 = spans to split; 1 = each request's rc / err set (a
+// panic on one request of several: they were rerun one by one on the slot).
+static void small_batch(Device* d, Device::SmallSlot* sl, SmallReq* const* rq, uint32_t n);
+static int small_check(Device* d, Device::SmallSlot* sl, const uint32_t* h, SmallReq* const* rq, uint32_t n) {
+    auto fail_all = [&](int rc) {
+        for (uint32_t i = 0; i < n; i++) {
+            rq[i]->rc = rc;
+            rq[i]->err = g_err;
+        }
+    };
     if (h[SM_ERR]) {  // the reference panics on some document: find whose (each call alone)
         if (n > 1) {
             for (uint32_t i = 0; i < n; i++) small_batch(d, sl, rq + i, 1);
-            return;
+            return 1;
         }
         fail_all(fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)"));
-        return;
+        return 1;
     }
     if (h[SM_NTOK] != h[SM_NTOKE]) {
         fail_all(fail(JB_EDEVICE, "internal: %u token starts vs %u ends", h[SM_NTOK], h[SM_NTOKE]));
-        return;
+        return 1;
     }
+    return 0;
+}
+
+// Each request's spans out of a batch's output h (batch offsets -> the call's own text).
+static void small_split(const uint32_t* h, SmallReq* const* rq, uint32_t n) {
+    uint64_t at = 0;
+    uint32_t k = 0;
     const uint32_t* hs = h + kSmallHdr;
     const uint32_t* he = hs + kSmallBytes;
     const uint64_t* dt = reinterpret_cast<const uint64_t*>(he + kSmallBytes);
-    at = 0;
-    k = 0;
     for (uint32_t i = 0; i < n; i++) {
         SmallReq& r = *rq[i];
         SpanBuf* out = r.out;
@@ -1167,64 +1223,110 @@ static void small_batch(Device* d, Device::SmallSlot* sl, SmallReq* const* rq, u
     }
 }
 
+// One whole batch, its callers' spans split before it returns (a lone rerun).
+static void small_batch(Device* d, Device::SmallSlot* sl, SmallReq* const* rq, uint32_t n) {
+    const uint32_t* h = small_launch(d, sl, rq, n);
+    if (h && !small_check(d, sl, h, rq, n)) small_split(h, rq, n);
+}
+
+// The queue's head requests (same hmm as the head, together within the k_small limits),
+// taken off the queue.  Under small_mu.
+static std::vector<SmallReq*> take_batch(Device* d) {
+    std::vector<SmallReq*> b;
+    uint64_t bytes = 0;
+    uint32_t docs = 0;
+    const bool h = d->small_q.front()->hmm;
+    for (auto it = d->small_q.begin(); it != d->small_q.end();) {
+        SmallReq* q = *it;
+        const uint64_t len = q->doc_off[q->nd] - q->doc_off[0];
+        if (q->hmm != h || bytes + len > d->lc.small_max || docs + q->nd > kSmallDocs) {
+            ++it;
+            continue;
+        }
+        bytes += len;
+        docs += q->nd;
+        b.push_back(q);
+        it = d->small_q.erase(it);
+    }
+    return b;
+}
+
+// Runs batch b on slot sl, completes its requests, and passes the slot on: the next batch
+// from the queue goes to its head request's caller (which is waiting on its own state word,
+// so a finished batch wakes one caller, not every waiting one), else the slot goes free.
+static void small_run(Device* d, Device::SmallSlot* sl, std::vector<SmallReq*> b) {
+    const uint32_t n = (uint32_t)b.size();
+    const uint32_t* h = small_launch(d, sl, b.data(), n);
+    const bool split = h && !small_check(d, sl, h, b.data(), n);
+    const uint32_t ob = sl->ob;
+    if (split) sl->reading[ob].store(true, std::memory_order_relaxed);  // (the slot is still ours)
+    std::unique_lock<std::mutex> lk(d->small_mu);
+    if (!d->small_q.empty()) {
+        std::vector<SmallReq*> nb = take_batch(d);
+        SmallReq* const next = nb[0];
+        next->sl = sl;
+        next->batch = std::move(nb);
+        next->state.store(kLaunch, std::memory_order_release);
+    } else {
+        sl->busy = false;
+    }
+    const bool asleep = d->small_sleepers > 0;
+    lk.unlock();
+    if (asleep) d->small_cv.notify_all();  // (the caller handed the slot may be asleep)
+    if (split) {  // (the slot's next batch writes the other buffer meanwhile)
+        small_split(h, b.data(), n);
+        sl->reading[ob].store(false, std::memory_order_release);
+    }
+    for (SmallReq* q : b) q->state.store(kDone, std::memory_order_release);  // (q may be gone after this)
+    lk.lock();  // (a caller asleep on small_cv checked its state under small_mu)
+    const bool wake = d->small_sleepers > 0;
+    lk.unlock();
+    if (wake) d->small_cv.notify_all();
+}
+
 static int cut_small(Device* d, const uint8_t* text, const uint64_t* doc_off, uint32_t nd, bool hmm,
                      SpanBuf* out) {
     SmallReq r{text, doc_off, nd, hmm, out};
-    std::unique_lock<std::mutex> lk(d->small_mu);
-    d->small_q.push_back(&r);
-    for (;;) {
-        if (r.done) break;
+    {
+        std::unique_lock<std::mutex> lk(d->small_mu);
+        d->small_q.push_back(&r);
         Device::SmallSlot* sl = nullptr;
-        if (!r.launched)
-            for (uint32_t k = 0; k < d->small_slots; k++)
-                if (!d->slots[k].busy) {
-                    sl = &d->slots[k];
-                    break;
-                }
-        if (!sl) {  // own request in flight (its launcher completes it), or every slot busy
-            // spin up to ~100 us for the next completion before sleeping: a batch takes
-            // 20-30 us, and a sleeping caller's wake-up costs about as much again
-            const uint32_t g0 = d->small_gen.load(std::memory_order_relaxed);
+        for (uint32_t k = 0; k < d->small_slots && !sl; k++)
+            if (!d->slots[k].busy) sl = &d->slots[k];
+        if (sl) {  // a free slot: launch the queue's head requests on it now
+            sl->busy = true;
+            std::vector<SmallReq*> b = take_batch(d);
             lk.unlock();
-            bool moved = false;
-            const auto t0 = std::chrono::steady_clock::now();
-            for (uint32_t i = 1; !moved; i++) {
-                moved = d->small_gen.load(std::memory_order_acquire) != g0;
-                if (!moved && (i & 63u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(100))
-                    break;
-                __builtin_ia32_pause();
-            }
-            lk.lock();
-            if (!moved && d->small_gen.load(std::memory_order_relaxed) == g0) d->small_cv.wait(lk);
-            continue;
+            small_run(d, sl, std::move(b));
         }
-        // launch the queue's head requests (same hmm, within the limits) on the free slot,
-        // then complete them: launches on other slots can go on meanwhile
-        std::vector<SmallReq*> b;
-        uint64_t bytes = 0;
-        uint32_t docs = 0;
-        const bool h = d->small_q.front()->hmm;
-        for (auto it = d->small_q.begin(); it != d->small_q.end();) {
-            SmallReq* q = *it;
-            const uint64_t len = q->doc_off[q->nd] - q->doc_off[0];
-            if (q->hmm != h || bytes + len > d->lc.small_max || docs + q->nd > kSmallDocs) {
-                ++it;
-                continue;
+    }
+    // wait on this request's own word: done by another caller's batch, or handed a slot to
+    // launch on.  Spin up to ~100 us first (a batch takes 20-40 us; a sleeping caller's
+    // wake-up costs about as much again), then yield the CPU between looks up to ~2 ms
+    // (queued behind other batches), then sleep on small_cv.
+    for (;;) {
+        uint32_t st = r.state.load(std::memory_order_acquire);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t i = 1; st == kQueued; i++) {
+            if ((i & 63u) == 0) {
+                const auto w = std::chrono::steady_clock::now() - t0;
+                if (w > std::chrono::microseconds(2000)) break;
+                if (w > std::chrono::microseconds(100)) std::this_thread::yield();
             }
-            bytes += len;
-            docs += q->nd;
-            q->launched = true;
-            b.push_back(q);
-            it = d->small_q.erase(it);
+            __builtin_ia32_pause();
+            st = r.state.load(std::memory_order_acquire);
         }
-        sl->busy = true;
-        lk.unlock();
-        small_batch(d, sl, b.data(), (uint32_t)b.size());
-        lk.lock();
-        sl->busy = false;
-        for (SmallReq* q : b) q->done = true;
-        d->small_gen.fetch_add(1, std::memory_order_release);
-        d->small_cv.notify_all();
+        if (st == kQueued) {
+            std::unique_lock<std::mutex> lk(d->small_mu);
+            d->small_sleepers++;
+            d->small_cv.wait(lk, [&] { return r.state.load(std::memory_order_acquire) != kQueued; });
+            d->small_sleepers--;
+            st = r.state.load(std::memory_order_acquire);
+        }
+        if (st == kDone) break;
+        // kLaunch: this caller runs the batch it was handed (its own request among them)
+        r.state.store(kQueued, std::memory_order_relaxed);
+        small_run(d, r.sl, std::move(r.batch));
     }
     if (r.rc) g_err = r.err;
     return r.rc;

@@ -937,12 +937,12 @@ def test_document_bitmap_between_runs(small):
                 _cmp_batch(tk, o, buf, off, hmm, f"layout {i} rep {rep}")
 
 
-@pytest.mark.parametrize("slots", [1, 2, 4])
+@pytest.mark.parametrize("slots", [1, 2, 4, 8])
 def test_concurrent_cut_calls(syn_small, tmp_path, slots):
     """16 threads x 1,000 jb_cut calls at once on one context (Go code calling Cut
     from many goroutines; the reference takes only an RLock, tokenizer.go:151-153):
     every result equals the oracle's, and the calls are coalesced into shared
-    k_small launches (tests/concurrent_cut.cpp prints both rates), with 1, 2 or 4
+    k_small launches (tests/concurrent_cut.cpp prints both rates), with 1, 2, 4 or 8
     batches in flight (JB_SMALL_SLOTS)."""
     import subprocess
     dp, ep, s = syn_small
@@ -961,8 +961,11 @@ def test_concurrent_cut_calls(syn_small, tmp_path, slots):
         for x in sents:
             a, b = o.cut_spans(x, True)
             f.write(" ".join([str(len(a))] + [f"{int(p)} {int(q)}" for p, q in zip(a, b)]) + "\n")
+    env = dict(os.environ, JB_SMALL_SLOTS=str(slots))
+    if os.environ.get("JB_CONC_LOG"):  # (diagnostics: the per-batch clocks, JB_SMALL_TRACE)
+        env["JB_SMALL_TRACE"] = f"{os.environ['JB_CONC_LOG']}.trace{slots}.txt"
     r = subprocess.run([exe, dp, ep, str(tmp_path / "sent.txt"), str(tmp_path / "want.txt"), "16", "1000"],
-                       capture_output=True, text=True, timeout=300, env=dict(os.environ, JB_SMALL_SLOTS=str(slots)))
+                       capture_output=True, text=True, timeout=300, env=env)
     print(f"JB_SMALL_SLOTS={slots}")
     print(r.stdout)
     if os.environ.get("JB_CONC_LOG"):  # (diagnostics: JB_DEBUG's per-batch lines)
