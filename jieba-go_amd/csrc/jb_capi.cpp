@@ -1157,8 +1157,8 @@ static const uint32_t* small_launch(Device* d, Device::SmallSlot* sl, SmallReq* 
         fprintf(stderr, "[jb] k_small %llu bytes, %u calls: stage+launch %.2f us, sync %.2f us; phases (us):",
                 (unsigned long long)nbytes, n, us(c0, c1), us(c1, c2));
         for (int q = 0; q < 15; q++) fprintf(stderr, " %.2f", h[SM_CLK + q] * 0.01);
-        fprintf(stderr, "; %u clocks (walk end %u, viterbi fwd %u, traceback %u)", h[SM_CLK + 15], h[SM_CLK + 16],
-                h[SM_CLK + 17], h[SM_CLK + 18]);
+        fprintf(stderr, "; %u clocks (walk end %u, viterbi fwd %u, traceback %u; dp %u %u %u)", h[SM_CLK + 15],
+                h[SM_CLK + 16], h[SM_CLK + 17], h[SM_CLK + 18], h[SM_CLK + 19], h[SM_CLK + 20], h[SM_CLK + 21]);
         fprintf(stderr, "\n");
     }
     return h;

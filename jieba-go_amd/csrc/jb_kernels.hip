@@ -4721,7 +4721,8 @@ struct SmallLds {
     uint32_t eb[kSmallWords];      // token last bytes
     uint32_t swp[kSmallWords];     // token starts before each word
     uint32_t scan[16];
-    uint64_t clk[19];  // phase clocks of thread 0 (JB_DEBUG): 0..15 realtime, 16..18 shader cycles of the last run
+    uint64_t clk[22];  // phase clocks of thread 0 (JB_DEBUG): 0..15 realtime, 16..18 shader cycles of the last run,
+                       // 19..21 shader cycles of the last DP (descriptors read, loop entered, done)
     uint32_t nh, nblk, nzh, err, ties;
     uint16_t doff[kSmallDocs + 1];  // document offsets
     uint16_t hpos[kSmallSlots];     // Han rune starts, text order
@@ -4972,7 +4973,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
     if (t == 0) {
         clk[0] = __builtin_amdgcn_s_memrealtime();
         cyc0 = __builtin_amdgcn_s_memtime();
-        xc[0] = xc[1] = xc[2] = 0;
+        xc[0] = xc[1] = xc[2] = xc[3] = xc[4] = xc[5] = 0;
     }
     const uint32_t nt = blockDim.x;  // a multiple of 64 with 4 * nt >= nbytes (run_small)
     // 1. text (zero past nbytes, up to 64 bytes on) and document offsets -> LDS (one
@@ -5146,6 +5147,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
         // a wave's LDS accesses complete in order), so no LDS round trip is on the chain.
         const uint32_t h0 = s.hord[bs / 3u], h1 = s.hord[z_prev(v, be, bs) / 3u] + 1u;
         uint32_t h = h1 - 1u;
+        if (t == 0) xc[3] = __builtin_amdgcn_s_memtime();
         if (!((s.slowb[h0 >> 5] >> (h0 & 31u)) & 1u)) {
             // Up to 4 items per rune without a branch: an absent item has a NaN weight, so
             // its sum is NaN and no compare takes it.  With finite or -Inf weights (plainw)
@@ -5191,6 +5193,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
             load_b(A);
             load_desc(B, clampd(h, 1u));
             double bnx = 0.0;
+            if (t == 0) xc[4] = __builtin_amdgcn_s_memtime();
             for (;;) {
                 load_b(B);  // rune h - 1's best(h - 1 + L >= 2): written by the steps before
                 load_desc(C, clampd(h, 2u));
@@ -5242,7 +5245,10 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
                 if (h == h0) break;
             }
         }
-        if (t == 0) clk[12] = __builtin_amdgcn_s_memrealtime();
+        if (t == 0) {
+            xc[5] = __builtin_amdgcn_s_memtime();
+            clk[12] = __builtin_amdgcn_s_memrealtime();
+        }
 #ifndef JB_SM_FUSED
 #define JB_SM_FUSED 1
 #endif
@@ -5399,7 +5405,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(const uint8_t* __restri
         out[SM_ZHBLOCKS] = s.nzh;
         for (int k = 1; k < 16; k++) out[SM_CLK + k - 1] = (uint32_t)(clk[k] - clk[0]);
         out[SM_CLK + 15] = (uint32_t)(__builtin_amdgcn_s_memtime() - cyc0);  // shader clock cycles
-        for (int k = 0; k < 3; k++) out[SM_CLK + 16 + k] = xc[k] ? (uint32_t)(xc[k] - cyc0) : 0u;
+        for (int k = 0; k < 6; k++) out[SM_CLK + 16 + k] = xc[k] ? (uint32_t)(xc[k] - cyc0) : 0u;
     }
     // every thread's writes reach host memory before the completion word
     __threadfence_system();
