@@ -706,6 +706,9 @@ static int init_launch_cfg(Device* d) {
     const int t1 = env_int("JB_TOK1", 1);
     if (t1 < 0 || t1 > 1) return fail(JB_EINVAL, "JB_TOK1=%d: want 0 or 1", t1);
     lc.tok1 = (uint32_t)t1;
+    const int nzm = env_int("JB_NZ_FUSE_MIB", 4);
+    if (nzm < 0 || nzm > 1024) return fail(JB_EINVAL, "JB_NZ_FUSE_MIB=%d: want 0 .. 1024", nzm);
+    lc.nz_fuse_mib = (uint32_t)nzm;
     const int ss = env_int("JB_SMALL_SLOTS", 4);
     if (ss < 1 || ss > 8) return fail(JB_EINVAL, "JB_SMALL_SLOTS=%d: want 1 .. 8", ss);
     d->small_slots = (uint32_t)ss;

@@ -136,6 +136,8 @@ struct LaunchCfg {
     uint32_t ncu;            // the device's CUs (k_long's grid: at most one workgroup per CU)
     uint32_t tok1;           // the span kernels as one pass, k_tok1, for batches of <= 256 token tiles
                              // (JB_TOK1: 1 default, 0 the count/write passes always)
+    uint32_t nz_fuse_mib;    // k_nonzh's work inside k_long (fused) for batches of at most this many MiB
+                             // (JB_NZ_FUSE_MIB: 4 default, 0 never)
 };
 
 // k_zh's group split: g1 groups of grp bytes, then groups of *sgrp bytes to the end.

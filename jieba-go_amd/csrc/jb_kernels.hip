@@ -4485,9 +4485,19 @@ union LongAll {  // the phases' LDS
     uint32_t m32[kLpBatch * kLpMap / 4u];  // k_long_path (wave 0)
     uint4 cd4[256][kSeg / 16u];       // k_long_pbits, k_long_tail
     uint8_t bl[256][kSeg];            // k_long_seg
+    uint8_t nz[256][80];              // k_nonzh's windows (k_long<.., true>, before the long phases)
 };
 
-template <bool HMM>
+// k_nonzh's arguments, for k_long<.., true>
+struct NzArgs {
+    uint32_t nbytes, ntiles, ndocs;
+    const uint32_t* lanemask;
+    const uint2* tile_cnt;
+    const uint64_t* alnum16;
+    uint32_t* docbits;
+    const uint64_t* doc_off;
+};
+template <bool HMM, bool NZ>
 __global__ __launch_bounds__(256) void k_long(const uint8_t* __restrict__ text, DevImage im,
                                               const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
                                               const uint32_t* __restrict__ lsegb, uint32_t* __restrict__ counters,
@@ -4496,9 +4506,14 @@ __global__ __launch_bounds__(256) void k_long(const uint8_t* __restrict__ text, 
                                               uint8_t* __restrict__ lmap, uint8_t* __restrict__ lcx,
                                               uint64_t* __restrict__ lpath, uint32_t* __restrict__ lflag,
                                               uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
-                                              uint64_t* __restrict__ dbg, uint32_t spec) {
+                                              uint64_t* __restrict__ dbg, uint32_t spec, NzArgs nz) {
     __shared__ __attribute__((aligned(16))) LongAll U;
     __shared__ uint32_t s_claim;
+    if (NZ) {  // k_nonzh's work first (it needs only k_mark_walk's outputs): one launch less for small batches
+        nonzh_body(text, nz.nbytes, nz.lanemask, nz.tile_cnt, nz.ntiles, nz.alnum16, sbits, ebits, nz.docbits,
+                   nz.doc_off, nz.ndocs, blockIdx.x, gridDim.x, U.nz);
+        __syncthreads();  // (U.nz is the long phases' LDS too)
+    }
     const uint32_t nlong = counters[CNT_NLONG], nseg = counters[CNT_NLSEG];  // (k_zh wrote them before this launch)
     if (nlong == 0u) return;
     const bool w0 = threadIdx.x < 64u;  // (the one-wave phases)
@@ -5501,6 +5516,7 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         else JB_ZH_LAUNCH(false, 4u);
     }
 #undef JB_ZH_LAUNCH
+    bool nz_done = false;  // (k_nonzh's work ran inside k_long)
     {
         // long blocks: the chain, then one lane per 64-rune segment (at most
         // nbytes / 192 + nbytes / kZhLongMin segments), one wave per block
@@ -5508,18 +5524,22 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
         const uint32_t gseg = (uint32_t)std::min<uint64_t>(1024u, (segs + 255u) / 256u);
         const uint32_t spec = lc.long_spec;
         if (lc.long_fused) {
-            // one workgroup per 64 segments (k_long_spec's lanes), at most one per CU
-            const uint32_t gl = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(lc.ncu, (segs + 63u) / 64u));
-            if (hmm)
-                JB_TIMED(K_LONG, hipLaunchKernelGGL((k_long<true>), dim3(gl), dim3(256), 0, stream, d_text, im,
-                                                    w.erec + kErecPad, w.longblk, w.lsegb, w.counters, w.tile4, w.gbl,
-                                                    w.gbest, w.lbp, w.lmap, w.lcx, w.lpath, w.lflag, w.sbits, w.ebits,
-                                                    w.dbg, spec));
-            else
-                JB_TIMED(K_LONG, hipLaunchKernelGGL((k_long<false>), dim3(gl), dim3(256), 0, stream, d_text, im,
-                                                    w.erec + kErecPad, w.longblk, w.lsegb, w.counters, w.tile4, w.gbl,
-                                                    w.gbest, w.lbp, w.lmap, w.lcx, w.lpath, w.lflag, w.sbits, w.ebits,
-                                                    w.dbg, spec));
+            // one workgroup per 64 segments (k_long_spec's lanes), at most one per CU; a batch of at most
+            // JB_NZ_FUSE_MIB MiB (default 4) runs k_nonzh's work in it too (one launch less)
+            uint32_t gl = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(lc.ncu, (segs + 63u) / 64u));
+            const bool nzf = nbytes <= ((uint64_t)lc.nz_fuse_mib << 20);
+            const NzArgs nz{(uint32_t)nbytes, ntiles, ndocs, w.lanemask, w.tile_cnt, w.alnum16, w.docbits, d_doc_off};
+            if (nzf) gl = std::max(gl, (uint32_t)((nbytes + 1023u) / 1024u + 255u) / 256u);
+#define JB_LONG_LAUNCH(H, N)                                                                                           \
+    JB_TIMED(K_LONG, hipLaunchKernelGGL((k_long<H, N>), dim3(gl), dim3(256), 0, stream, d_text, im, w.erec + kErecPad, \
+                                        w.longblk, w.lsegb, w.counters, w.tile4, w.gbl, w.gbest, w.lbp, w.lmap, w.lcx, \
+                                        w.lpath, w.lflag, w.sbits, w.ebits, w.dbg, spec, nz))
+            if (hmm && nzf) JB_LONG_LAUNCH(true, true);
+            else if (hmm) JB_LONG_LAUNCH(true, false);
+            else if (nzf) JB_LONG_LAUNCH(false, true);
+            else JB_LONG_LAUNCH(false, false);
+#undef JB_LONG_LAUNCH
+            nz_done = nzf;
         } else {
         if (spec)
             JB_TIMED(K_LONG_SPEC, hipLaunchKernelGGL(k_long_spec, dim3(kSpecGrid), dim3(64), 0, stream, d_text, im,
@@ -5556,7 +5576,7 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                                      w.sbits, w.ebits));
         }
     }
-    {
+    if (!nz_done) {
         const uint32_t nw = (uint32_t)((nbytes + 1023u) / 1024u);  // alnum16 words
         JB_TIMED(K_NONZH, hipLaunchKernelGGL(k_nonzh, dim3((nw + 255u) / 256u), dim3(256), 0, stream, d_text,
                                              (uint32_t)nbytes, w.lanemask, w.tile_cnt, ntiles, w.alnum16, w.sbits,

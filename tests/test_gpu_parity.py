@@ -28,8 +28,9 @@ def _pair_env(dp, ep, env, **kw):
 
 # k_zh's two forms: 4-wave workgroups with the weights gathered from HBM (what batches
 # under 16 MiB get), and 16-wave workgroups with the weight table in LDS (the headline
-# batches' form), forced with JB_ZH_WIDE=1 on these small ones
-ZH_FORMS = {"auto": {}, "wide": {"JB_ZH_WIDE": "1"}}
+# batches' form), forced with JB_ZH_WIDE=1 on these small ones; and k_nonzh as a launch of
+# its own (JB_NZ_FUSE_MIB=0), where batches under 4 MiB otherwise run its work inside k_long
+ZH_FORMS = {"auto": {}, "wide": {"JB_ZH_WIDE": "1"}, "nzapart": {"JB_NZ_FUSE_MIB": "0"}}
 
 
 @pytest.fixture(scope="module", params=list(ZH_FORMS))
