@@ -1943,6 +1943,158 @@ __device__ __noinline__ uint2 lm_collect(const uint32_t* lmv, uint32_t* tbl, uin
     return make_uint2(rw, used);
 }
 
+// ---------------------------------------------------------------------------
+// k_nonzh: one lane per non-Han block (cutNonZh, tokenizer.go:289-310)
+// ---------------------------------------------------------------------------
+// cutNonZh for one block [bs, be) (tokenizer.go:289-310).  The block's bytes
+// come in 16-byte loads issued together (a byte-by-byte walk over global
+// memory made every byte a dependent round trip); the tokenizing pass reads
+// them from the lane's 80-byte LDS window.
+__device__ __forceinline__ uint32_t nz_keep(uint32_t base, uint32_t bs, uint32_t be) {  // bytes in [bs, be)
+    const uint32_t lo = bs > base ? min(bs - base, 4u) : 0u, hi = be > base ? min(be - base, 4u) : 0u;
+    if (hi <= lo) return 0u;
+    return (uint32_t)(((1ull << (8u * hi)) - 1ull) & ~((1ull << (8u * lo)) - 1ull));
+}
+// W: the bytes tokenized per round of loads (64 with the lane's 80-byte window; 48 with a
+// 64-byte one)
+template <uint32_t W>
+__device__ void nonzh_block(const uint8_t* __restrict__ text, uint32_t bs, uint32_t be, Emitter& em, uint8_t* buf) {
+    static_assert(W == 64u || W == 48u, "window");
+    bool has = false;  // alnum.FindAllIndex found nothing -> no tokens (:290-293)
+    for (uint32_t a = bs & ~15u; a < be && !has; a += 64u) {
+        uint4 c[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            c[k] = (a + 16u * k < be) ? *reinterpret_cast<const uint4*>(text + a + 16u * k) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t b = a + 16u * k;
+            has |= jb_any_alnum4(c[k].x & nz_keep(b, bs, be)) || jb_any_alnum4(c[k].y & nz_keep(b + 4u, bs, be)) ||
+                   jb_any_alnum4(c[k].z & nz_keep(b + 8u, bs, be)) || jb_any_alnum4(c[k].w & nz_keep(b + 12u, bs, be));
+        }
+    }
+    if (!has) return;
+    uint32_t p = bs, run = 0;
+    bool in_run = false;
+    while (p < be) {
+        const uint32_t a = p & ~15u;
+#pragma unroll
+        for (int k = 0; k < (int)(W / 16u) + 1; k++)  // bytes up to be + 3 (decode reads 4; padding follows the text)
+            if (a + 16u * k < be + 4u)
+                reinterpret_cast<uint4*>(buf)[k] = *reinterpret_cast<const uint4*>(text + a + 16u * k);
+        const uint32_t pe = min(be, a + W);
+        while (p < pe) {
+            const uint32_t x = lds4(buf, p - a);
+            if (jb_is_alnum(x & 0xFFu)) {  // alnum runs are kept whole
+                if (!in_run) {
+                    in_run = true;
+                    run = p;
+                }
+                p++;
+                continue;
+            }
+            if (in_run) {
+                em.token(run, p);
+                in_run = false;
+            }
+            uint32_t r;
+            const uint32_t w = jb_decode(x, min(4u, be - p), &r);
+            if (!jb_is_space(r)) em.token(p, p + w);  // one token per rune; spaces dropped
+            p += w;
+        }
+    }
+    if (in_run) em.token(run, be);
+}
+
+// Bit k set for each byte k of the 16 bytes x that is [0-9A-Za-z] (jb_is_alnum).
+__device__ __forceinline__ uint32_t alnum_mask16(uint4 x) {
+    const uint32_t v[4] = {x.x, x.y, x.z, x.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t f = (jb_bytes_between(v[j], 0x2Fu, 0x3Au) | jb_bytes_between(v[j] | 0x20202020u, 0x60u, 0x7Bu)) >> 7;
+        m |= ((f * 0x204081u) >> 21 & 0xFu) << (4 * j);  // bits 0/8/16/24 -> 0..3
+    }
+    return m;
+}
+
+// The non-Han blocks whose first alnum byte lies in alnum16 word wi's 1 KiB (k_nonzh's unit).
+template <uint32_t W>
+__device__ __forceinline__ void nonzh_word(const uint8_t* __restrict__ text, uint32_t nbytes, uint32_t nch,
+                                           const uint32_t* __restrict__ lanemask, const uint2* __restrict__ tile_cnt,
+                                           uint32_t ntiles, const uint64_t* __restrict__ alnum16, uint32_t wi,
+                                           Emitter& em, uint8_t* buf) {
+    uint64_t a = alnum16[wi];
+    // the next alnum chunk's text and lane mask load while this one is cut
+    uint32_t cn = a ? wi * 64u + (uint32_t)__builtin_ctzll(a) : 0u;
+    uint4 txn = make_uint4(0, 0, 0, 0);
+    uint32_t lmn = 0;
+    if (a && cn < nch) {
+        txn = *reinterpret_cast<const uint4*>(text + cn * 16u);
+        lmn = lanemask[cn];
+    }
+    while (a) {
+        const uint32_t c = cn;
+        const uint4 tx = txn;
+        const uint32_t lm = lmn;
+        a &= a - 1ull;
+        if (c >= nch) break;  // (padding past the batch)
+        if (a) {
+            cn = wi * 64u + (uint32_t)__builtin_ctzll(a);
+            if (cn < nch) {
+                txn = *reinterpret_cast<const uint4*>(text + cn * 16u);
+                lmn = lanemask[cn];
+            }
+        }
+        const uint32_t c0 = c * 16u;
+        uint32_t A = alnum_mask16(tx);
+        if (c0 + 16u > nbytes) A &= (1u << (nbytes - c0)) - 1u;
+        const uint32_t bm = lm & 0xFFFFu;
+        while (A) {  // a block with an alnum byte in this chunk
+            const uint32_t i = (uint32_t)__builtin_ctz(A);
+            const uint32_t le = bm & ((2u << i) - 1u), after = bm & ~((2u << i) - 1u);
+            A &= after ? ~((1u << __builtin_ctz(after)) - 1u) : 0u;  // the block's bytes of this chunk
+            uint32_t bs;
+            bool own = true;
+            if (le) {
+                bs = c0 + 31u - (uint32_t)__builtin_clz(le);
+            } else {  // the block began before this chunk: walk back to its start
+                uint32_t k = c;
+                bs = 0;
+                while (k > 0u) {  // (byte 0 starts a block, so the walk ends there at the latest)
+                    --k;
+                    const uint32_t m = lanemask[k] & 0xFFFFu;
+                    const bool al = (alnum16[k >> 6] >> (k & 63u)) & 1ull;
+                    if (m) {
+                        const uint32_t o = 31u - (uint32_t)__builtin_clz(m);
+                        bs = k * 16u + o;
+                        if (al) own = (alnum_mask16(*reinterpret_cast<const uint4*>(text + k * 16u)) >> o) == 0u;
+                        break;
+                    }
+                    if (al) {
+                        own = false;
+                        break;
+                    }
+                }
+            }
+            if (!own) continue;
+            const uint32_t be = after ? c0 + (uint32_t)__builtin_ctz(after)
+                                      : nz_block_end(lanemask, tile_cnt, ntiles, nbytes, c);
+            nonzh_block<W>(text, bs, be, em, buf);
+        }
+    }
+}
+
+// k_nonzh's arguments, for its work inside k_long<.., true>
+struct NzArgs {
+    uint32_t nbytes, ntiles, ndocs;
+    const uint32_t* lanemask;
+    const uint2* tile_cnt;
+    const uint64_t* alnum16;
+    uint32_t* docbits;
+    const uint64_t* doc_off;
+};
+
 // At least 4 waves per SIMD (at most 128 VGPRs): the DP is latency-bound and
 // needs them; left alone the allocator lands just above 128 (3 waves, k_zh +17 %).
 #ifndef JB_ZH_WAVES
@@ -3916,77 +4068,6 @@ __global__ __launch_bounds__(256) void k_long_tail(const uint8_t* __restrict__ t
 }
 
 
-// ---------------------------------------------------------------------------
-// k_nonzh: one lane per non-Han block (cutNonZh, tokenizer.go:289-310)
-// ---------------------------------------------------------------------------
-// cutNonZh for one block [bs, be) (tokenizer.go:289-310).  The block's bytes
-// come in 16-byte loads issued together (a byte-by-byte walk over global
-// memory made every byte a dependent round trip); the tokenizing pass reads
-// them from the lane's 80-byte LDS window.
-__device__ __forceinline__ uint32_t nz_keep(uint32_t base, uint32_t bs, uint32_t be) {  // bytes in [bs, be)
-    const uint32_t lo = bs > base ? min(bs - base, 4u) : 0u, hi = be > base ? min(be - base, 4u) : 0u;
-    if (hi <= lo) return 0u;
-    return (uint32_t)(((1ull << (8u * hi)) - 1ull) & ~((1ull << (8u * lo)) - 1ull));
-}
-__device__ void nonzh_block(const uint8_t* __restrict__ text, uint32_t bs, uint32_t be, Emitter& em, uint8_t* buf) {
-    bool has = false;  // alnum.FindAllIndex found nothing -> no tokens (:290-293)
-    for (uint32_t a = bs & ~15u; a < be && !has; a += 64u) {
-        uint4 c[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            c[k] = (a + 16u * k < be) ? *reinterpret_cast<const uint4*>(text + a + 16u * k) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t b = a + 16u * k;
-            has |= jb_any_alnum4(c[k].x & nz_keep(b, bs, be)) || jb_any_alnum4(c[k].y & nz_keep(b + 4u, bs, be)) ||
-                   jb_any_alnum4(c[k].z & nz_keep(b + 8u, bs, be)) || jb_any_alnum4(c[k].w & nz_keep(b + 12u, bs, be));
-        }
-    }
-    if (!has) return;
-    uint32_t p = bs, run = 0;
-    bool in_run = false;
-    while (p < be) {
-        const uint32_t a = p & ~15u;
-#pragma unroll
-        for (int k = 0; k < 5; k++)  // bytes up to be + 3 (decode reads 4; padding follows the text)
-            if (a + 16u * k < be + 4u)
-                reinterpret_cast<uint4*>(buf)[k] = *reinterpret_cast<const uint4*>(text + a + 16u * k);
-        const uint32_t pe = min(be, a + 64u);
-        while (p < pe) {
-            const uint32_t x = lds4(buf, p - a);
-            if (jb_is_alnum(x & 0xFFu)) {  // alnum runs are kept whole
-                if (!in_run) {
-                    in_run = true;
-                    run = p;
-                }
-                p++;
-                continue;
-            }
-            if (in_run) {
-                em.token(run, p);
-                in_run = false;
-            }
-            uint32_t r;
-            const uint32_t w = jb_decode(x, min(4u, be - p), &r);
-            if (!jb_is_space(r)) em.token(p, p + w);  // one token per rune; spaces dropped
-            p += w;
-        }
-    }
-    if (in_run) em.token(run, be);
-}
-
-// Bit k set for each byte k of the 16 bytes x that is [0-9A-Za-z] (jb_is_alnum).
-__device__ __forceinline__ uint32_t alnum_mask16(uint4 x) {
-    const uint32_t v[4] = {x.x, x.y, x.z, x.w};
-    uint32_t m = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const uint32_t f = (jb_bytes_between(v[j], 0x2Fu, 0x3Au) | jb_bytes_between(v[j] | 0x20202020u, 0x60u, 0x7Bu)) >> 7;
-        m |= ((f * 0x204081u) >> 21 & 0xFu) << (4 * j);  // bits 0/8/16/24 -> 0..3
-    }
-    return m;
-}
-
 // k_nonzh: cutNonZh (tokenizer.go:289-310) for exactly the non-Han blocks that hold
 // a [0-9A-Za-z] byte; every other non-Han block has no tokens (:290-293).  An alnum
 // byte is never Han, so it always lies in a non-Han block.  One thread per alnum16
@@ -4009,67 +4090,8 @@ __device__ __forceinline__ void nonzh_body(const uint8_t* __restrict__ text, uin
         if (o < nbytes) docbits[o >> 5] = 0u;
     }
     Emitter em(sbits, ebits);
-    for (uint32_t wi = wg * 256u + threadIdx.x; wi < nw; wi += ng * 256u) {
-        uint64_t a = alnum16[wi];
-        // the next alnum chunk's text and lane mask load while this one is cut
-        uint32_t cn = a ? wi * 64u + (uint32_t)__builtin_ctzll(a) : 0u;
-        uint4 txn = make_uint4(0, 0, 0, 0);
-        uint32_t lmn = 0;
-        if (a && cn < nch) {
-            txn = *reinterpret_cast<const uint4*>(text + cn * 16u);
-            lmn = lanemask[cn];
-        }
-        while (a) {
-            const uint32_t c = cn;
-            const uint4 tx = txn;
-            const uint32_t lm = lmn;
-            a &= a - 1ull;
-            if (c >= nch) break;  // (padding past the batch)
-            if (a) {
-                cn = wi * 64u + (uint32_t)__builtin_ctzll(a);
-                if (cn < nch) {
-                    txn = *reinterpret_cast<const uint4*>(text + cn * 16u);
-                    lmn = lanemask[cn];
-                }
-            }
-            const uint32_t c0 = c * 16u;
-            uint32_t A = alnum_mask16(tx);
-            if (c0 + 16u > nbytes) A &= (1u << (nbytes - c0)) - 1u;
-            const uint32_t bm = lm & 0xFFFFu;
-            while (A) {  // a block with an alnum byte in this chunk
-                const uint32_t i = (uint32_t)__builtin_ctz(A);
-                const uint32_t le = bm & ((2u << i) - 1u), after = bm & ~((2u << i) - 1u);
-                A &= after ? ~((1u << __builtin_ctz(after)) - 1u) : 0u;  // the block's bytes of this chunk
-                uint32_t bs;
-                bool own = true;
-                if (le) {
-                    bs = c0 + 31u - (uint32_t)__builtin_clz(le);
-                } else {  // the block began before this chunk: walk back to its start
-                    uint32_t k = c;
-                    bs = 0;
-                    while (k > 0u) {  // (byte 0 starts a block, so the walk ends there at the latest)
-                        --k;
-                        const uint32_t m = lanemask[k] & 0xFFFFu;
-                        const bool al = (alnum16[k >> 6] >> (k & 63u)) & 1ull;
-                        if (m) {
-                            const uint32_t o = 31u - (uint32_t)__builtin_clz(m);
-                            bs = k * 16u + o;
-                            if (al) own = (alnum_mask16(*reinterpret_cast<const uint4*>(text + k * 16u)) >> o) == 0u;
-                            break;
-                        }
-                        if (al) {
-                            own = false;
-                            break;
-                        }
-                    }
-                }
-                if (!own) continue;
-                const uint32_t be = after ? c0 + (uint32_t)__builtin_ctz(after)
-                                          : nz_block_end(lanemask, tile_cnt, ntiles, nbytes, c);
-                nonzh_block(text, bs, be, em, s_win[threadIdx.x]);
-            }
-        }
-    }
+    for (uint32_t wi = wg * 256u + threadIdx.x; wi < nw; wi += ng * 256u)
+        nonzh_word<64>(text, nbytes, nch, lanemask, tile_cnt, ntiles, alnum16, wi, em, s_win[threadIdx.x]);
     em.flush();
 }
 __global__ __launch_bounds__(256) void k_nonzh(const uint8_t* __restrict__ text, uint32_t nbytes,
@@ -4488,15 +4510,6 @@ union LongAll {  // the phases' LDS
     uint8_t nz[256][80];              // k_nonzh's windows (k_long<.., true>, before the long phases)
 };
 
-// k_nonzh's arguments, for k_long<.., true>
-struct NzArgs {
-    uint32_t nbytes, ntiles, ndocs;
-    const uint32_t* lanemask;
-    const uint2* tile_cnt;
-    const uint64_t* alnum16;
-    uint32_t* docbits;
-    const uint64_t* doc_off;
-};
 template <bool HMM, bool NZ>
 __global__ __launch_bounds__(256) void k_long(const uint8_t* __restrict__ text, DevImage im,
                                               const uint64_t* __restrict__ erec, const uint2* __restrict__ longblk,
