@@ -899,11 +899,11 @@ static int open_device(Device* d, int ordinal, const Image& img) {
     if ((rc = install_image(d, &b, img))) return rc;
     if ((rc = init_launch_cfg(d))) return rc;  // (sets small_slots)
     {
-        // k_small runs one workgroup per batch: each slot's stream is pinned to one CU
-        // (JB_SMALL_CU + slot x JB_SMALL_CU_STRIDE) so its batch finds its 21 KB of code in
-        // that CU's instruction cache (and the trie's hot lines in that XCD's L2) instead of
-        // fetching them cold on whichever CU the dispatcher picks, and so batches of
-        // different slots run side by side instead of one after another
+        // k_small runs one workgroup per batch, one stream per slot.  With JB_SMALL_CUMASK=1
+        // (round 4's default) each slot's stream is masked to one CU (JB_SMALL_CU + slot x
+        // JB_SMALL_CU_STRIDE), so that its batch finds the trie's hot lines in that XCD's L2;
+        // round 5 measured plain streams faster (the sentence 21.8-22.2 -> 20.0-21.0 us per
+        // call; concurrent calls the same at 4 slots and better at 8), so they are the default
         const int cu = env_int("JB_SMALL_CU", 0), cs = env_int("JB_SMALL_CU_STRIDE", 1);
         const int last = cu + ((int)d->small_slots - 1) * cs;  // (only the slots in use get a stream)
         if (cu < 0 || cs < 0 || last >= (int)d->ncu)
@@ -911,7 +911,7 @@ static int open_device(Device* d, int ordinal, const Image& img) {
                         "JB_SMALL_CU=%d, JB_SMALL_CU_STRIDE=%d, JB_SMALL_SLOTS=%u: slot k runs on CU "
                         "JB_SMALL_CU + k x JB_SMALL_CU_STRIDE, and the last one (%d) is past the device's %u CUs",
                         cu, cs, d->small_slots, last, d->ncu);
-        const bool masked = env_int("JB_SMALL_CUMASK", 1) != 0;  // (0: plain streams, diagnostics)
+        const bool masked = env_int("JB_SMALL_CUMASK", 0) != 0;
         for (int k = 0; k < (int)d->small_slots; k++) {
             std::vector<uint32_t> mask((d->ncu + 31) / 32, 0u);
             const int c = cu + k * cs;
