@@ -4314,17 +4314,22 @@ __global__ __launch_bounds__(256) void k_tok1(const uint32_t* __restrict__ sbits
             e[k] = w0 + k < nwords ? ebits[w0 + k] : 0u;
         }
     }
-    // the first document that starts in the tile (or after it): a 16-ary lower bound over
-    // doc_off (wave 1, its loads beside the bitmap loads)
+    // the first document that starts in the tile (or after it): a JB_TOK1_ARY-ary lower bound
+    // over doc_off (wave 1, its loads beside the bitmap loads)
+#ifndef JB_TOK1_ARY
+#define JB_TOK1_ARY 16
+#endif
+    static_assert(JB_TOK1_ARY == 16 || JB_TOK1_ARY == 64, "k_tok1's search: 16 or 64 lanes");
     if (wave == 1u) {
+        constexpr uint32_t AR = JB_TOK1_ARY, SH = AR == 64u ? 6u : 4u;
         const uint64_t target = (uint64_t)t * TB;
-        const uint32_t k = lane & 15u;
+        const uint32_t k = lane & (AR - 1u);
         uint32_t lo = 0, hi = ndocs + 1u;  // the answer in [lo, hi]
         while (lo < hi) {
-            const uint32_t sx = (hi - lo + 15u) >> 4;
+            const uint32_t sx = (hi - lo + AR - 1u) >> SH;
             const uint32_t i = lo + (k + 1u) * sx - 1u;
             const bool before = i < hi && doc_off[i] < target;
-            const uint32_t c = (uint32_t)__popcll(__ballot(before) & 0xFFFFull);
+            const uint32_t c = (uint32_t)__popcll(__ballot(before) & (AR == 64u ? ~0ull : 0xFFFFull));
             const uint32_t nlo = lo + c * sx;
             if (sx == 1u || nlo >= hi) {
                 lo = min(nlo, hi);
