@@ -4317,7 +4317,7 @@ __global__ __launch_bounds__(256) void k_tok1(const uint32_t* __restrict__ sbits
     // the first document that starts in the tile (or after it): a JB_TOK1_ARY-ary lower bound
     // over doc_off (wave 1, its loads beside the bitmap loads)
 #ifndef JB_TOK1_ARY
-#define JB_TOK1_ARY 16
+#define JB_TOK1_ARY 64
 #endif
     static_assert(JB_TOK1_ARY == 16 || JB_TOK1_ARY == 64, "k_tok1's search: 16 or 64 lanes");
     if (wave == 1u) {
