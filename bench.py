@@ -226,10 +226,12 @@ class GpuCutter:
         return k, ms
 
     def results(self):
-        """(starts u32, ends u32, doc_tok u64[ndocs+1]) of the last step."""
+        """(starts u32, ends u32, doc_tok u64[ndocs+1]) of the last step; raises if that
+        pipeline reported an error (jb_device_status)."""
         J = self.J
         ps, pe, pd, pn = self.ptrs
         self.sync()
+        self.tk.device_status(self.stream)
         ntok = int(J.dev_to_host(pn, 8, np.uint64)[0])
         return (J.dev_to_host(ps, 4 * ntok, np.uint32), J.dev_to_host(pe, 4 * ntok, np.uint32),
                 J.dev_to_host(pd, 8 * (self.ndocs + 1), np.uint64))
@@ -318,7 +320,15 @@ def run(args, world, rank, dist, agg_dev, make_cutter, open_oracle, log=print):
     s = synth.Synth(nwords=args.nwords)
     sharded = args.workload == "docs"
     buf, off, wdesc = make_workload(args, s, rank, world, dist)
-    sbuf, soff, d0, base = shard_for(buf, off, world, rank, sharded)
+    emul = sharded and world == 1 and args.shard_of > 1  # one GPU's shard of an N-GPU job, on one GPU
+    if emul:
+        if not 0 <= args.shard_rank < args.shard_of:
+            raise ValueError(f"--shard-rank {args.shard_rank} outside 0..{args.shard_of - 1}")
+        sbuf, soff, d0, base = shard_for(buf, off, args.shard_of, args.shard_rank, True)
+        wdesc += f"; ONLY shard {args.shard_rank} of {args.shard_of} (one GPU's share at {args.shard_of} GPUs)"
+        del buf
+    else:
+        sbuf, soff, d0, base = shard_for(buf, off, world, rank, sharded)
     if sharded and world > 1:
         del buf
         dist.barrier()  # every rank holds its own copy of its shard: the shared corpus file can go
@@ -432,6 +442,7 @@ def run(args, world, rank, dist, agg_dev, make_cutter, open_oracle, log=print):
                    "corpus_bytes": int(tot_bytes), "corpus_chars": int(tot_runes), "corpus_han_bytes": int(tot_han),
                    "corpus_docs": int(tot_docs), "rank0_shard_bytes": nbytes, "dict_words": s.nwords,
                    "parallelism": f"doc-shard x{world} (byte-balanced contiguous ranges), no collectives",
+                   "emulated_shard": {"of": args.shard_of, "rank": args.shard_rank} if emul else None,
                    "per_rank": per_rank},
         "roofline": roof,
         "roofline_kernels": rooflines,
@@ -708,6 +719,11 @@ def parse_args(argv=None):
     ap.add_argument("--workload", choices=["docs", "sentence", "s10k", "long-punct", "long-oov"], default="docs")
     ap.add_argument("--corpus-mib", type=float, default=1024.0,
                     help="docs: the fixed corpus (MiB), strong-scaled over the ranks; 1024 = config 4")
+    ap.add_argument("--shard-of", type=int, default=1,
+                    help="docs, one process: cut only shard --shard-rank of the corpus split N ways (the shard one "
+                         "GPU of an N-GPU job gets), to know the per-GPU rate at N GPUs on one GPU; the line's "
+                         "value is then that one GPU's chars/s, not a job's")
+    ap.add_argument("--shard-rank", type=int, default=0)
     ap.add_argument("--hmm", type=int, default=1)
     ap.add_argument("--nwords", type=int, default=350_000)
     ap.add_argument("--dict-kind", choices=["prefix", "txt"], default="prefix",

@@ -160,6 +160,15 @@ int jb_cut_device_into(jb_ctx *ctx, const uint8_t *d_text, uint64_t nbytes, cons
                        uint32_t ndocs, int hmm, void *stream, uint32_t *d_start, uint32_t *d_end, uint64_t cap,
                        uint64_t *d_doc_tok, uint64_t *d_ntok);
 
+/* Error state of the last jb_cut_device / jb_cut_device_into pipeline on ctx's first
+ * device (from any thread): synchronises `stream` (the one that call was queued on) and
+ * the pipeline, then returns JB_OK, JB_EPANIC (input on which the reference panics:
+ * the spans are not the reference's) or JB_EDEVICE (a long-block phase wait gave up,
+ * JB_LONG_WAIT_US: the spans are incomplete).  The device calls themselves return
+ * before their kernels run, so a caller that must know checks here (a host batch,
+ * jb_cut_batch*, returns these codes itself). */
+int jb_device_status(jb_ctx *ctx, void *stream);
+
 /* Contiguous byte-balanced ranges of whole documents (the reference's
  * CutParallel deals blocks to goroutines instead, tokenizer.go:81-148), the partition
  * bench.py's one-process-per-GPU runs use (jb_cut_batch itself uses jb_split_points,
@@ -201,6 +210,8 @@ int64_t jb_dict_size(jb_ctx *ctx);
 
 /* Counters of the last cut on each device of ctx, summed over the devices (a host
  * batch cut in pieces: summed over its pieces).  Synchronises the devices' streams.
+ * After a device pipeline (jb_cut_device*) it fills *out and also returns that
+ * pipeline's error state, as jb_device_status does.
  * Concurrent small calls (jb_cut of at most 4 KiB) are coalesced into shared k_small
  * batches: after one, the counters are those of the k_small batch that finished last
  * on the device, which may hold other callers' documents beside this caller's. */

@@ -709,6 +709,10 @@ static int init_launch_cfg(Device* d) {
     const int nzm = env_int("JB_NZ_FUSE_MIB", 4);
     if (nzm < 0 || nzm > 1024) return fail(JB_EINVAL, "JB_NZ_FUSE_MIB=%d: want 0 .. 1024", nzm);
     lc.nz_fuse_mib = (uint32_t)nzm;
+    // k_long's phase waits give up after this long without progress (100 MHz ticks)
+    const int lw = env_int("JB_LONG_WAIT_US", 20000000);
+    if (lw < 1 || lw > 40000000) return fail(JB_EINVAL, "JB_LONG_WAIT_US=%d: want 1 .. 40000000", lw);
+    lc.long_wait_ticks = (uint32_t)lw * 100u;
     const int ss = env_int("JB_SMALL_SLOTS", 4);
     if (ss < 1 || ss > 8) return fail(JB_EINVAL, "JB_SMALL_SLOTS=%d: want 1 .. 8", ss);
     d->small_slots = (uint32_t)ss;
@@ -1066,15 +1070,31 @@ static const uint32_t* small_launch(Device* d, Device::SmallSlot* sl, SmallReq* 
         return false;
     };
     if (!chk(hipSetDevice(d->ordinal), "hipSetDevice")) return nullptr;
-    if (!sl->h_sin) {
+    if (!sl->h_sin || !sl->h_sout[0] || !sl->h_sout[1]) {
+        // all three buffers or none: a failure part way frees what was allocated, so the
+        // next call on the slot allocates again instead of using a null buffer
+        auto drop = [&]() {
+            for (void** p : {(void**)&sl->h_sin, (void**)&sl->h_sout[0], (void**)&sl->h_sout[1]})
+                if (*p) {
+                    (void)hipHostFree(*p);
+                    *p = nullptr;
+                }
+            sl->d_sin = nullptr;
+            sl->d_sout[0] = sl->d_sout[1] = nullptr;
+        };
+        drop();
         const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
         if (!chk(hipHostMalloc(&sl->h_sin, kSmallBytes + 128 + 8 * (kSmallDocs + 1), fl), "hipHostMalloc") ||
-            !chk(hipHostGetDevicePointer((void**)&sl->d_sin, sl->h_sin, 0), "hipHostGetDevicePointer"))
+            !chk(hipHostGetDevicePointer((void**)&sl->d_sin, sl->h_sin, 0), "hipHostGetDevicePointer")) {
+            drop();
             return nullptr;
+        }
         for (int k = 0; k < 2; k++) {
             if (!chk(hipHostMalloc(&sl->h_sout[k], kSmallOutBytes, fl), "hipHostMalloc") ||
-                !chk(hipHostGetDevicePointer((void**)&sl->d_sout[k], sl->h_sout[k], 0), "hipHostGetDevicePointer"))
+                !chk(hipHostGetDevicePointer((void**)&sl->d_sout[k], sl->h_sout[k], 0), "hipHostGetDevicePointer")) {
+                drop();
                 return nullptr;
+            }
             sl->h_sout[k][SM_DONE] = 0;  // (recycled pinned memory may hold any value; seq starts at 1)
         }
     }
@@ -1563,7 +1583,7 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         const Piece& p = pcs[k];
         HIPCHK(hipEventSynchronize(d->ev_comp[k]));
         const volatile uint32_t* c = d->h_pcnt + k * kSnapWords;
-        if (c[CNT_ERR] & 2u) return fail(JB_EDEVICE, "k_long: a phase wait ran out of polls");
+        if (c[CNT_ERR] & 2u) return fail(JB_EDEVICE, "k_long: a phase wait gave up (no progress for JB_LONG_WAIT_US)");
         if (c[CNT_ERR]) return fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)");
         if (c[CNT_NTOK] != c[CNT_NTOKE])
             return fail(JB_EDEVICE, "internal: %u token starts vs %u ends", c[CNT_NTOK], c[CNT_NTOKE]);
@@ -2324,6 +2344,7 @@ extern "C" int jb_save(jb_ctx* ctx, const char* path) {
 extern "C" int jb_last_stats(jb_ctx* ctx, jb_stats* out) {
     if (!ctx || !out) return fail(JB_EINVAL, "jb_last_stats: null argument");
     memset(out, 0, sizeof *out);
+    uint32_t err = 0;  // CNT_ERR of a device pipeline (jb_cut_device*)
     std::shared_lock<std::shared_mutex> rl(ctx->lock);
     for (auto& d : ctx->devs) {
         {
@@ -2366,7 +2387,27 @@ extern "C" int jb_last_stats(jb_ctx* ctx, jb_stats* out) {
         }
         out->long_blocks += c[CNT_NLONG];
         out->viterbi_ties += c[CNT_TIES];
+        err |= c[CNT_ERR];
     }
+    // (a host batch already returned these from its own call; a device pipeline reports them here)
+    if (err & 2u) return fail(JB_EDEVICE, "k_long: a phase wait gave up (no progress for JB_LONG_WAIT_US)");
+    if (err) return fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)");
+    return JB_OK;
+}
+
+extern "C" int jb_device_status(jb_ctx* ctx, void* stream) {
+    if (!ctx) return fail(JB_EINVAL, "jb_device_status: null ctx");
+    std::shared_lock<std::shared_mutex> rl(ctx->lock);
+    Device* d = ctx->devs[0].get();
+    std::lock_guard<std::mutex> g(d->mu);
+    if (!d->w.counters) return JB_OK;  // no device pipeline has run
+    HIPCHK(hipSetDevice(d->ordinal));
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    if (d->ws_done) HIPCHK(hipEventSynchronize(d->ws_done));
+    uint32_t e = 0;
+    HIPCHK(hipMemcpy(&e, d->w.counters + CNT_ERR, sizeof e, hipMemcpyDeviceToHost));
+    if (e & 2u) return fail(JB_EDEVICE, "k_long: a phase wait gave up (no progress for JB_LONG_WAIT_US)");
+    if (e) return fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)");
     return JB_OK;
 }
 

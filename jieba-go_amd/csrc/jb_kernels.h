@@ -36,7 +36,7 @@ enum {
     CNT_NTOK = 2,   // token starts
     CNT_NTOKE = 3,  // token ends (== CNT_NTOK when consistent)
     CNT_ERR = 4,    // bit 0: a zh block reached a tail index -1 (the reference panics); bit 1: a k_long
-                    // phase wait ran out of polls
+                    // phase wait gave up (no progress for LaunchCfg::long_wait_ticks)
     CNT_WORK = 5,   // k_zh work counter: next group (kZhGroupBytes of text)
     CNT_TOKT = 30,  // k_tok1's tile tickets
     CNT_PHASE = 32, // k_long's phases: claimed items at 32 + 2 p, finished items at 33 + 2 p
@@ -138,6 +138,8 @@ struct LaunchCfg {
                              // (JB_TOK1: 1 default, 0 the count/write passes always)
     uint32_t nz_fuse_mib;    // k_nonzh's work inside k_long (fused) for batches of at most this many MiB
                              // (JB_NZ_FUSE_MIB: 4 default, 0 never)
+    uint32_t long_wait_ticks;  // k_long: a phase wait gives up after this many 100 MHz ticks without progress
+                               // (JB_LONG_WAIT_US x 100; default 20 s)
 };
 
 // k_zh's group split: g1 groups of grp bytes, then groups of *sgrp bytes to the end.

@@ -4455,19 +4455,23 @@ __global__ __launch_bounds__(256) void k_tok1(const uint32_t* __restrict__ sbits
 // ---------------------------------------------------------------------------
 // k_long: the long-block kernels above as the phases of one launch (VERDICT r04
 // item 5), so that a batch without a long block (CNT_NLONG 0: every batch of
-// short documents) pays one launch instead of seven.  A grid barrier between the
-// phases (DESIGN §6's rule for inter-workgroup waits: every thread's stores made
-// visible at agent scope, a counter bumped by one thread per workgroup, polled with
-// agent-scope atomic loads, an acquire fence after; the wait is bounded and sets
-// CNT_ERR bit 1 when it runs out).  One workgroup per CU at most (the phases' LDS,
-// unioned, is 132 KB), and the grid is at most the CU count, so all its workgroups
-// are resident together.
+// short documents) pays one launch instead of seven.
+// A phase's work items (the separate kernel's workgroups) are claimed from a counter
+// (CNT_PHASE + 2 p) by running workgroups, in phase order, and a workgroup adds its
+// finished items to CNT_PHASE + 2 p + 1 (after an agent-scope release by every thread)
+// and waits until the phase's count is complete (agent-scope atomic loads, then an
+// agent-scope acquire: DESIGN §6's rule for inter-workgroup waits).  Since items are
+// claimed in phase order, a workgroup only ever waits for items that running
+// workgroups hold: the grid need not be resident all at once (another kernel, e.g. a
+// second pipeline on the same GPU, may hold CUs), and no grid barrier is used.
+// The wait is bounded in time, not in polls: it gives up only when the phase's done
+// count has not moved for wait_ticks ticks of the 100 MHz real-time counter
+// (JB_LONG_WAIT_US, default 20 s), so one legitimately long item (k_long_dp's chain
+// over a very long block) is waited for as long as other items keep finishing.
+// A workgroup whose wait gives up sets CNT_ERR bit 1 and leaves the kernel, as does
+// every workgroup that then finds the bit set: nothing reads a phase's outputs
+// before the phase is complete, and the host reports JB_EDEVICE.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kGridSpins = 1u << 21;  // polls before a phase wait gives up (seconds)
-// A phase's work items are claimed from a counter (CNT_PHASE + 2 p) by running workgroups,
-// in phase order, so a workgroup waits only on items that running workgroups claimed: the
-// grid need not be resident all at once (another kernel, e.g. a second pipeline on the
-// same GPU, may hold CUs).  A workgroup adds its finished items to CNT_PHASE + 2 p + 1.
 __device__ __forceinline__ uint32_t wg_claim(uint32_t* ctr, uint32_t* s_x) {  // (the whole workgroup)
     if (threadIdx.x == 0u) *s_x = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
@@ -4482,23 +4486,41 @@ __device__ __forceinline__ uint32_t wave_claim(uint32_t* ctr) {  // (one wave)
 }
 // the end of a phase: every thread's stores released at agent scope, the workgroup's
 // finished items (thread 0's count) added, then a wait until all nitems are done and an
-// acquire; a wait that runs out of polls sets CNT_ERR bit 1 (the host reports it)
-__device__ __forceinline__ void phase_end(uint32_t* done, uint32_t mine, uint32_t nitems, uint32_t* err) {
+// acquire.  Returns false (the workgroup must leave the kernel) when the wait gave up
+// (no progress for wait_ticks) or another workgroup's did (CNT_ERR bit 1).
+__device__ __forceinline__ bool phase_end(uint32_t* done, uint32_t mine, uint32_t nitems, uint32_t* err,
+                                          uint32_t wait_ticks, uint32_t* s_x) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __syncthreads();
     if (threadIdx.x == 0u) {
         if (mine) __hip_atomic_fetch_add(done, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t spins = 0;
-        while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nitems) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins == kGridSpins) {
-                __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t ok = 1u, seen = 0xFFFFFFFFu;
+        uint64_t since = 0;
+        for (;;) {
+            if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2u) {
+                ok = 0u;  // a workgroup gave up: leave too (the kernel drains at once)
                 break;
             }
+            const uint32_t d = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (d >= nitems) break;
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();  // (100 MHz)
+            if (d != seen) {  // progress: the bound starts again
+                seen = d;
+                since = now;
+            } else if (now - since > wait_ticks) {
+                __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0u;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
         }
+        *s_x = ok;
     }
     __syncthreads();
+    const bool ok = *s_x != 0u;
+    __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return ok;
 }
 
 union LongAll {  // the phases' LDS
@@ -4524,7 +4546,8 @@ __global__ __launch_bounds__(256) void k_long(const uint8_t* __restrict__ text, 
                                               uint8_t* __restrict__ lmap, uint8_t* __restrict__ lcx,
                                               uint64_t* __restrict__ lpath, uint32_t* __restrict__ lflag,
                                               uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
-                                              uint64_t* __restrict__ dbg, uint32_t spec, NzArgs nz) {
+                                              uint64_t* __restrict__ dbg, uint32_t spec, NzArgs nz,
+                                              uint32_t wait_ticks) {
     __shared__ __attribute__((aligned(16))) LongAll U;
     __shared__ uint32_t s_claim;
     if (NZ) {  // k_nonzh's work first (it needs only k_mark_walk's outputs): one launch less for small batches
@@ -4538,51 +4561,57 @@ __global__ __launch_bounds__(256) void k_long(const uint8_t* __restrict__ text, 
     uint32_t* const ph = counters + CNT_PHASE;
     uint32_t* const err = counters + CNT_ERR;
     uint32_t p = 0;  // the phase
-    // a phase of nitems items, f(item) on the whole workgroup / on wave 0 only
+    // a phase of nitems items, f(item) on the whole workgroup / on wave 0 only; false:
+    // the wait gave up, the workgroup leaves the kernel
     auto wg_phase = [&](uint32_t nitems, auto&& f) {
         uint32_t mine = 0;
         for (uint32_t it; (it = wg_claim(ph + 2u * p, &s_claim)) < nitems; mine++) f(it);
-        phase_end(ph + 2u * p + 1u, mine, nitems, err);
-        p++;
+        return phase_end(ph + 2u * p + 1u, mine, nitems, err, wait_ticks, &s_claim) && (++p, true);
     };
     auto wave_phase = [&](uint32_t nitems, auto&& f) {
         uint32_t mine = 0;
         if (w0)
             for (uint32_t it; (it = wave_claim(ph + 2u * p)) < nitems; mine++) f(it);
-        phase_end(ph + 2u * p + 1u, mine, nitems, err);
-        p++;
+        return phase_end(ph + 2u * p + 1u, mine, nitems, err, wait_ticks, &s_claim) && (++p, true);
     };
     const uint32_t nsg64 = (nseg + 63u) / 64u, nsg256 = (nseg + 255u) / 256u;
     {
         if (spec) {
             double* const wt = w0 ? long_spec_setup(im, U.sp.wt) : nullptr;
-            wave_phase(nsg64, [&](uint32_t it) {
-                long_spec_body(text, im, erec, longblk, lsegb, counters, tile4, gbl, gbest, lcode, lmap, lflag, spec,
-                               it, nsg64, U.sp.ring, U.sp.cd, wt, U.sp.bw);
-            });
+            if (!wave_phase(nsg64, [&](uint32_t it) {
+                    long_spec_body(text, im, erec, longblk, lsegb, counters, tile4, gbl, gbest, lcode, lmap, lflag,
+                                   spec, it, nsg64, U.sp.ring, U.sp.cd, wt, U.sp.bw);
+                }))
+                return;
             if (spec != 3u) {
-                wave_phase(nlong, [&](uint32_t it) {
-                    long_path_body(longblk, lsegb, counters, lflag, lcode, lmap, lcx, 3u, 3u, it, nlong, U.m32);
-                });
-                wg_phase(nsg256, [&](uint32_t it) {
-                    long_pbits_body(longblk, lsegb, counters, lflag, gbl, lcode, lcx, lpath, it, nsg256, U.cd4);
-                });
+                if (!wave_phase(nlong, [&](uint32_t it) {
+                        long_path_body(longblk, lsegb, counters, lflag, lcode, lmap, lcx, 3u, 3u, it, nlong, U.m32);
+                    }))
+                    return;
+                if (!wg_phase(nsg256, [&](uint32_t it) {
+                        long_pbits_body(longblk, lsegb, counters, lflag, gbl, lcode, lcx, lpath, it, nsg256, U.cd4);
+                    }))
+                    return;
             } else {
                 p += 2u;
             }
         } else {
             p += 3u;
         }
-        wg_phase(nlong, [&](uint32_t it) {
-            long_dp_body<HMM>(text, im, erec, gbl, gbest, longblk, counters, sbits, ebits, lflag, lsegb, lpath, dbg,
-                              spec, it, nlong, U.dp);
-        });
-        wg_phase(nsg256, [&](uint32_t it) {
-            long_seg_body(text, im, erec, longblk, lsegb, counters, lflag, gbest, gbl, lcode, lmap, it, nsg256, U.bl);
-        });
-        wave_phase(nlong, [&](uint32_t it) {
-            long_path_body(longblk, lsegb, counters, lflag, lcode, lmap, lcx, 2u, 1u, it, nlong, U.m32);
-        });
+        if (!wg_phase(nlong, [&](uint32_t it) {
+                long_dp_body<HMM>(text, im, erec, gbl, gbest, longblk, counters, sbits, ebits, lflag, lsegb, lpath,
+                                  dbg, spec, it, nlong, U.dp);
+            }))
+            return;
+        if (!wg_phase(nsg256, [&](uint32_t it) {
+                long_seg_body(text, im, erec, longblk, lsegb, counters, lflag, gbest, gbl, lcode, lmap, it, nsg256,
+                              U.bl);
+            }))
+            return;
+        if (!wave_phase(nlong, [&](uint32_t it) {
+                long_path_body(longblk, lsegb, counters, lflag, lcode, lmap, lcx, 2u, 1u, it, nlong, U.m32);
+            }))
+            return;
         // (the Viterbi back-pointers go to gbest's bytes: the exit codes in lcode are read to the end;
         // the last phase: nothing waits for it inside the kernel)
         for (uint32_t it; (it = wg_claim(ph + 2u * p, &s_claim)) < nsg256;)
@@ -5551,7 +5580,7 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
 #define JB_LONG_LAUNCH(H, N)                                                                                           \
     JB_TIMED(K_LONG, hipLaunchKernelGGL((k_long<H, N>), dim3(gl), dim3(256), 0, stream, d_text, im, w.erec + kErecPad, \
                                         w.longblk, w.lsegb, w.counters, w.tile4, w.gbl, w.gbest, w.lbp, w.lmap, w.lcx, \
-                                        w.lpath, w.lflag, w.sbits, w.ebits, w.dbg, spec, nz))
+                                        w.lpath, w.lflag, w.sbits, w.ebits, w.dbg, spec, nz, lc.long_wait_ticks))
             if (hmm && nzf) JB_LONG_LAUNCH(true, true);
             else if (hmm) JB_LONG_LAUNCH(true, false);
             else if (nzf) JB_LONG_LAUNCH(false, true);

@@ -31,7 +31,7 @@ EXPORTS = [
     "jb_add_word", "jb_dict_get", "jb_dict_size", "jb_save", "jb_profile_enable", "jb_profile_read",
     "jb_profile_reset", "jb_image_build", "jb_image_free", "jb_image_save", "jb_image_dict_info", "jb_image_lookup",
     "jb_image_stats", "jb_image_emit", "jb_go_log", "jb_shard_bounds", "jb_last_stats",
-    "jb_suggest_freq", "jb_add_log", "jb_image_log_keys",
+    "jb_suggest_freq", "jb_add_log", "jb_image_log_keys", "jb_device_status",
 ]
 
 
@@ -128,6 +128,7 @@ def lib():
         L.jb_suggest_freq.argtypes = [vp, cp, C.c_size_t, C.POINTER(C.c_int64)]
         L.jb_add_log.argtypes = [vp, vp, vp, C.c_size_t]
         L.jb_last_stats.argtypes = [vp, C.POINTER(jb_stats)]
+        L.jb_device_status.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -382,6 +383,10 @@ class Tokenizer:
         _check(lib().jb_cut_device_into(self.h, C.c_void_p(d_text_ptr), nbytes, C.c_void_p(d_doc_off_ptr), ndocs,
                                         int(hmm), C.c_void_p(stream_ptr), C.c_void_p(d_start), C.c_void_p(d_end),
                                         cap, C.c_void_p(d_doc_tok), C.c_void_p(d_ntok)))
+
+    def device_status(self, stream_ptr=0):
+        """jb_device_status: raises JbError when the last device pipeline hit an error."""
+        _check(lib().jb_device_status(self.h, C.c_void_p(stream_ptr)))
 
     def last_stats(self):
         """Counters of the last pipeline run (jb_last_stats); synchronises."""
