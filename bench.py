@@ -500,8 +500,11 @@ def end_to_end(tk, buf, off, hmm, nrunes, reps=3):
                    "(SURVEY.md §8d's output format); checked against the spans below")
     out["tokens"] = int(ntok)
     out["same_tokens_as_spans"] = ok_mask
-    out["spans"] = dict(rate(s_sp), what="jb_cut_batch_into from pageable host memory: the same pipeline with u32 "
-                                         "spans back (8 B per token), widened to u64 batch offsets in caller arrays")
+    out["spans"] = dict(rate(s_sp), what="jb_cut_batch_into from pageable host memory (what the Go binding's "
+                                         "Cut / CutParallel use): the same pipeline with the spans packed on the GPU "
+                                         "(k_span_pack: 2 B per token, gap | length, rare escapes in a side list), "
+                                         "decoded on the host into u64 batch offsets in caller arrays",
+                        span_pack=os.environ.get("JB_SPAN_PACK", "1") != "0")
     out["masks_pinned"] = dict(rate(s_p), what="jb_cut_batch_mask with the text in jb_host_alloc (pinned) memory: "
                                                "no staging copy", same_as_pageable=ok_pin)
     return out

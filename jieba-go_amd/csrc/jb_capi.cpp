@@ -152,7 +152,17 @@ struct Device {
         uint64_t* hdt = nullptr; // pinned doc_tok
         uint64_t hcap_tok = 0;
         uint32_t hcap_docs = 0;
+        // packed spans (span_pack): device u32 per token + block headers, side list; pinned copies
+        uint16_t* pk = nullptr;
+        uint32_t* phdr = nullptr;
+        uint4* pside = nullptr;
+        uint64_t cap_pk = 0, cap_phdr = 0, cap_pside = 0;
+        uint16_t* hpk = nullptr;  // pinned copies
+        uint32_t* hhdr = nullptr;
+        uint4* hside = nullptr;
+        uint64_t hcap_pk = 0, hcap_hdr = 0, hcap_side = 0;
     } outs[kSets];
+    bool span_pack = true;  // host batches' spans come back packed, 2 B per token (JB_SPAN_PACK, default 1)
     uint32_t* h_pcnt = nullptr;  // mapped pinned: kSnapWords u32 per piece (k_snap writes them)
     uint32_t* d_pcnt = nullptr;  // its device address
     uint64_t h_pcnt_cap = 0;
@@ -644,6 +654,7 @@ static int grow_mapped(T** p, T** dp, uint64_t* cap, uint64_t want) {
 static void free_outs(Device* d) {
     for (auto& o : d->outs) {
         dfree(o.ts); dfree(o.te); dfree(o.dt); hfree(o.hs); hfree(o.hdt);
+        dfree(o.pk); dfree(o.phdr); dfree(o.pside); hfree(o.hpk); hfree(o.hhdr); hfree(o.hside);
         o = Device::OutSet{};
     }
 }
@@ -709,6 +720,9 @@ static int init_launch_cfg(Device* d) {
     const int nzm = env_int("JB_NZ_FUSE_MIB", 4);
     if (nzm < 0 || nzm > 1024) return fail(JB_EINVAL, "JB_NZ_FUSE_MIB=%d: want 0 .. 1024", nzm);
     lc.nz_fuse_mib = (uint32_t)nzm;
+    const int sp = env_int("JB_SPAN_PACK", 1);
+    if (sp < 0 || sp > 1) return fail(JB_EINVAL, "JB_SPAN_PACK=%d: want 0 or 1", sp);
+    d->span_pack = sp != 0;
     // k_long's phase waits give up after this long without progress (100 MHz ticks)
     const int lw = env_int("JB_LONG_WAIT_US", 20000000);
     if (lw < 1 || lw > 40000000) return fail(JB_EINVAL, "JB_LONG_WAIT_US=%d: want 1 .. 40000000", lw);
@@ -1390,6 +1404,40 @@ static void put_mask_words(const MaskDst* m, uint64_t rw, uint64_t nw, uint64_t 
     run_threads(nth, work);
 }
 
+// k_span_pack's packed spans of one piece back to u64 batch offsets (base = the piece's
+// first byte in the batch): blocks of kPackBlock tokens decode independently from their
+// header, a token at a time (start = previous end + gap, end = start + length), on
+// kCopyThreads threads; an escaped token (0xFFFF) takes its span from the side list,
+// sorted by token index first (on ordinary text it is empty or nearly so).
+static void unpack_spans(const uint16_t* pk, const uint32_t* hdr, uint4* side, uint32_t nside, uint32_t nt,
+                         uint64_t base, uint64_t* os, uint64_t* oe) {
+    if (nside > 1) std::sort(side, side + nside, [](const uint4& a, const uint4& b) { return a.x < b.x; });
+    const uint32_t nb = (nt + kPackBlock - 1u) / kPackBlock;
+    const unsigned nth = nt >= (1u << 18) ? kCopyThreads : 1u;
+    auto work = [&](unsigned t) {
+        const uint32_t b0 = (uint32_t)((uint64_t)nb * t / nth), b1 = (uint32_t)((uint64_t)nb * (t + 1) / nth);
+        for (uint32_t b = b0; b < b1; b++) {
+            const uint32_t i0 = b * kPackBlock, i1 = std::min(nt, i0 + kPackBlock);
+            uint64_t e = base + hdr[b];
+            for (uint32_t i = i0; i < i1; i++) {
+                const uint32_t x = pk[i];
+                uint64_t s;
+                if (x != 0xFFFFu) {
+                    s = e + (x & kPackGapEsc);
+                    e = s + (x >> kPackGapBits);
+                } else {
+                    const uint4* q = std::lower_bound(side, side + nside, i, [](const uint4& a, uint32_t v) { return a.x < v; });
+                    s = base + q->y;
+                    e = base + q->z;
+                }
+                os[i] = s;
+                oe[i] = e;
+            }
+        }
+    };
+    run_threads(nth, work);
+}
+
 // Text already in pinned memory (jb_host_alloc): the pieces are copied to the device
 // straight from it, without staging.
 struct HostAlloc { uintptr_t a; size_t n; };
@@ -1477,6 +1525,8 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
             HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             v->push_back(e);
         }
+    const bool pack = !mask && d->span_pack;
+    const uint32_t side_cap = pack_side_cap(maxb);
     if (!mask) {
         for (auto& o : d->outs) {
             uint64_t ct = o.cap_tok, cd = o.cap_docs;
@@ -1484,6 +1534,10 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
                 (rc = grow_dev(&o.dt, &cd, (uint64_t)maxd + 2)))
                 return rc;
             o.cap_docs = (uint32_t)cd;
+            if (pack && ((rc = grow_dev(&o.pk, &o.cap_pk, maxb + 4)) ||
+                         (rc = grow_dev(&o.phdr, &o.cap_phdr, (maxb + 4) / kPackBlock + 2)) ||
+                         (rc = grow_dev(&o.pside, &o.cap_pside, side_cap))))
+                return rc;
         }
     } else {
         if ((rc = grow_dev(&d->d_mask, &d->mask_cap, 2 * nw)) || (rc = grow_pinned(&d->h_mask, &d->mask_cap_h, 2 * nw)))
@@ -1571,6 +1625,12 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
                         mask ? &mo : nullptr)))
             return r;
         d->last_nbytes = len;
+        if (pack) {  // the spans packed for the trip back: 4 B per token (k_span_pack)
+            const Device::OutSet& o = d->outs[k % Device::kSets];
+            const hipError_t ep = run_span_pack(o.ts, o.te, d->w.counters, o.pk, o.phdr, o.pside, side_cap,
+                                                len + 1, d->stream);
+            if (ep != hipSuccess) return fail(JB_EDEVICE, "k_span_pack: %s", hipGetErrorString(ep));
+        }
         // counters and block counts by a kernel into mapped memory: a copy-engine transfer here
         // would queue behind the bulk copies of later pieces and hold up this stream
         const hipError_t es = run_snap(d->w, len, d->d_pcnt + k * kSnapWords, d->stream);
@@ -1584,6 +1644,7 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         HIPCHK(hipEventSynchronize(d->ev_comp[k]));
         const volatile uint32_t* c = d->h_pcnt + k * kSnapWords;
         if (c[CNT_ERR] & 2u) return fail(JB_EDEVICE, "k_long: a phase wait gave up (no progress for JB_LONG_WAIT_US)");
+        if (c[CNT_ERR] & 4u) return fail(JB_EDEVICE, "internal: k_span_pack's side list overflowed");
         if (c[CNT_ERR]) return fail(JB_EPANIC, "a Han block has no DAG path (the reference panics in cutDAG)");
         if (c[CNT_NTOK] != c[CNT_NTOKE])
             return fail(JB_EDEVICE, "internal: %u token starts vs %u ends", c[CNT_NTOK], c[CNT_NTOKE]);
@@ -1593,11 +1654,23 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
             Device::OutSet& o = d->outs[k % Device::kSets];
             uint64_t hd = o.hcap_docs;
             int r;
-            if ((r = grow_pinned(&o.hs, &o.hcap_tok, 2ull * nt + 2)) ||
+            if ((!pack && (r = grow_pinned(&o.hs, &o.hcap_tok, 2ull * nt + 2))) ||
                 (r = grow_pinned(&o.hdt, &hd, (uint64_t)(p.d1 - p.d0) + 2)))
                 return r;
             o.hcap_docs = (uint32_t)hd;
-            if (nt) {
+            if (pack) {
+                const uint32_t nside = c[CNT_SIDE], nb = (nt + kPackBlock - 1u) / kPackBlock;
+                if ((r = grow_pinned(&o.hpk, &o.hcap_pk, (uint64_t)nt + 1)) ||
+                    (r = grow_pinned(&o.hhdr, &o.hcap_hdr, (uint64_t)nb + 1)) ||
+                    (r = grow_pinned(&o.hside, &o.hcap_side, (uint64_t)nside + 1)))
+                    return r;
+                if (nt) {
+                    HIPCHK(hipMemcpyAsync(o.hpk, o.pk, (uint64_t)nt * 2, hipMemcpyDeviceToHost, d->dstream));
+                    HIPCHK(hipMemcpyAsync(o.hhdr, o.phdr, (uint64_t)nb * 4, hipMemcpyDeviceToHost, d->dstream));
+                }
+                if (nside)
+                    HIPCHK(hipMemcpyAsync(o.hside, o.pside, (uint64_t)nside * 16, hipMemcpyDeviceToHost, d->dstream));
+            } else if (nt) {
                 HIPCHK(hipMemcpyAsync(o.hs, o.ts, (uint64_t)nt * 4, hipMemcpyDeviceToHost, d->dstream));
                 HIPCHK(hipMemcpyAsync(o.hs + nt, o.te, (uint64_t)nt * 4, hipMemcpyDeviceToHost, d->dstream));
             }
@@ -1639,7 +1712,10 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         const Device::OutSet& o = d->outs[k % Device::kSets];
         const bool write = out->reserve(out->n + nt);
         if (!write && !out->external) return fail(JB_ENOMEM, "out of host memory for %u tokens", nt);
-        if (write) {
+        if (write && pack) {
+            const uint32_t nside = d->h_pcnt[k * kSnapWords + CNT_SIDE];
+            unpack_spans(o.hpk, o.hhdr, o.hside, nside, nt, doc_off[p.d0], out->s + out->n, out->e + out->n);
+        } else if (write) {
             const uint64_t base = doc_off[p.d0];
             uint64_t* const os = out->s + out->n;
             uint64_t* const oe = out->e + out->n;

@@ -36,8 +36,10 @@ enum {
     CNT_NTOK = 2,   // token starts
     CNT_NTOKE = 3,  // token ends (== CNT_NTOK when consistent)
     CNT_ERR = 4,    // bit 0: a zh block reached a tail index -1 (the reference panics); bit 1: a k_long
-                    // phase wait gave up (no progress for LaunchCfg::long_wait_ticks)
+                    // phase wait gave up (no progress for LaunchCfg::long_wait_ticks); bit 2: k_span_pack's
+                    // side list overflowed (internal)
     CNT_WORK = 5,   // k_zh work counter: next group (kZhGroupBytes of text)
+    CNT_SIDE = 6,   // k_span_pack: tokens in the side list
     CNT_TOKT = 30,  // k_tok1's tile tickets
     CNT_PHASE = 32, // k_long's phases: claimed items at 32 + 2 p, finished items at 33 + 2 p
     CNT_ALL = 64,   // (u32 slots of the counters buffer; k_docbits clears them all)
@@ -203,6 +205,18 @@ constexpr uint32_t kSnapWords = CNT_CLEAR + 4;
 // (and, in the same launch, bytes2 <= 1024 at p2)
 hipError_t run_zero(void* p, uint64_t bytes, hipStream_t stream, void* p2 = nullptr, uint32_t bytes2 = 0);
 hipError_t run_snap(const Work& w, uint64_t nbytes, uint32_t* out, hipStream_t stream);
+// The spans of a pipeline run (ts/te, its counters' token count) packed for the host:
+// pk[i] = gap from token i-1's end | length << kPackGapBits (u16), or 0xFFFF with
+// (i, start, end) in the side list (counters[CNT_SIDE] entries, at most side_cap);
+// hdr[b] = token b x kPackBlock - 1's end (0 for b = 0).  max_tokens bounds the count (the grid).
+constexpr uint32_t kPackBlock = 4096;
+constexpr uint32_t kPackGapBits = 6;
+constexpr uint32_t kPackGapEsc = (1u << kPackGapBits) - 1u;         // gaps from here on are escaped
+constexpr uint32_t kPackLenEsc = (1u << (16u - kPackGapBits)) - 1u;  // lengths from here on are escaped
+// (an escaped gap covers >= 63 bytes, an escaped token >= 1,023: at most nbytes / 63 + nbytes / 1023 + 2)
+inline uint32_t pack_side_cap(uint64_t nbytes) { return (uint32_t)(nbytes / kPackGapEsc + nbytes / kPackLenEsc + 4u); }
+hipError_t run_span_pack(const uint32_t* ts, const uint32_t* te, uint32_t* counters, uint16_t* pk, uint32_t* hdr,
+                         uint4* side, uint32_t side_cap, uint64_t max_tokens, hipStream_t stream);
 
 // Resident k_zh waves per CU (occupancy API), 4-wave or wide workgroups.
 uint32_t zh_waves_per_cu(bool hmm, bool wide);

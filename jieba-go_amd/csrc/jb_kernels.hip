@@ -4688,6 +4688,41 @@ hipError_t run_snap(const Work& w, uint64_t nbytes, uint32_t* out, hipStream_t s
     return hipGetLastError();
 }
 
+// Spans packed for the trip back to the host (jb_cut_batch's spans mode): token i as
+// one u16, the gap from the previous token's end (0 for the first) in the low 6 bits and
+// its length in the high 10, so the host link carries 2 bytes per token instead of 8 (on
+// the C_syn corpus gaps stay under 63 bytes and tokens under 1,023: 0 escapes in 4.36M
+// tokens).  A gap of 63 or more or a length of 1,023 or more is written as 0xFFFF, with
+// the token's (index, start, end) appended to a side list.  hdr[b] is the end of the token
+// before token b x kPackBlock (0 for b = 0), so the host decodes blocks of kPackBlock
+// tokens independently.
+__global__ __launch_bounds__(256) void k_span_pack(const uint32_t* __restrict__ ts, const uint32_t* __restrict__ te,
+                                                   uint32_t* __restrict__ counters, uint16_t* __restrict__ pk,
+                                                   uint32_t* __restrict__ hdr, uint4* __restrict__ side,
+                                                   uint32_t side_cap) {
+    const uint32_t nt = counters[CNT_NWORDS];  // (the u64 token count's low word: a piece has < 2^31 tokens)
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nt; i += gridDim.x * 256u) {
+        const uint32_t a = ts[i], b = te[i], p = i ? te[i - 1u] : 0u;
+        const uint32_t g = a - p, l = b - a;
+        uint32_t x = g | (l << kPackGapBits);
+        if (g >= kPackGapEsc || l >= kPackLenEsc) {
+            x = 0xFFFFu;
+            const uint32_t k = atomicAdd(counters + CNT_SIDE, 1u);
+            if (k < side_cap) side[k] = make_uint4(i, a, b, 0u);
+            else atomicOr(counters + CNT_ERR, 4u);  // (cannot happen: side_cap bounds the escapes)
+        }
+        pk[i] = (uint16_t)x;
+        if ((i & (kPackBlock - 1u)) == 0u) hdr[i / kPackBlock] = p;
+    }
+}
+
+hipError_t run_span_pack(const uint32_t* ts, const uint32_t* te, uint32_t* counters, uint16_t* pk, uint32_t* hdr,
+                         uint4* side, uint32_t side_cap, uint64_t max_tokens, hipStream_t stream) {
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(4096u, (max_tokens + 255u) / 256u));
+    hipLaunchKernelGGL(k_span_pack, dim3(grid), dim3(256), 0, stream, ts, te, counters, pk, hdr, side, side_cap);
+    return hipGetLastError();
+}
+
 constexpr uint32_t kMergeWords = 16;  // k_mask_merge: output words per thread
 __global__ __launch_bounds__(256) void k_mask_merge(const uint32_t* __restrict__ sbits,
                                                     const uint32_t* __restrict__ ebits, uint64_t n, uint64_t rel,

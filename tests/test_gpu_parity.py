@@ -611,6 +611,48 @@ def test_cut_batch_into_caller_arrays(small):
         assert np.array_equal(ts2, gs) and np.array_equal(td2, gd)
 
 
+@pytest.mark.parametrize("pack", ["1", "0"])
+def test_packed_spans_escapes(syn_small, pack, monkeypatch):
+    """Host batches' spans come back packed (JB_SPAN_PACK=1, the default: k_span_pack's
+    u16 gap | length << 6 per token, decoded on the host by blocks of 4,096 tokens) or as
+    u32 spans (0).  Escapes (gap >= 63 or length >= 1,023): long gaps (a non-Han block
+    without an alnum byte has no tokens, tokenizer.go:290-293), long tokens (an alnum run
+    is one token, :296-300), gaps of exactly 62 / 63 bytes and tokens of exactly 1,022 /
+    1,023 bytes, thousands of escapes in a row (an unsorted side list), blocks of 4,096
+    tokens that start right after an escape; several pieces (JB_PIECE_KIB=256) and two
+    devices (JB_DEVICE_WRAP): every span and doc_tok against the oracle, through
+    jb_cut_batch and jb_cut_batch_into."""
+    monkeypatch.setenv("JB_SPAN_PACK", pack)
+    monkeypatch.setenv("JB_PIECE_KIB", "256")
+    dp, ep, _ = syn_small
+    rng = random.Random(23)
+    pool = [chr(c) for c in range(0x4E00, 0x4E00 + 3000)]
+    han = lambda n: "".join(rng.choice(pool) for _ in range(n))  # noqa: E731
+    texts = [
+        han(50) + "，" * 30000 + han(20),          # 90 KB without a token
+        "a" * 70000 + han(30),                       # one 70,000-byte token
+        han(10) + "；" * 21 + han(5) + "；" * 20 + "é" + han(5),  # gaps of exactly 63 (escaped) and 62 bytes
+        "b" * 1023 + " " + "c" * 1022 + " " + "d" * 1024 + han(8),  # tokens of 1,023 / 1,024 (escaped) and 1,022
+        "".join("e" * 1100 + "，" * 30 for _ in range(3000)),  # 6,000 escapes in a row
+        han(4096 * 3) + "x" * 66000 + han(4096),       # escapes in the middle of 4,096-token blocks
+        "".join(han(rng.randint(1, 30)) + rng.choice(["，", "。", " ab1 ", "ーー"]) for _ in range(3000)),
+    ]
+    buf, off = _batch_of(texts)
+    for ndev, wrap in ((1, None), (2, "1")):
+        if wrap:
+            monkeypatch.setenv("JB_DEVICE_WRAP", wrap)
+        tk = J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep, ndevices=ndev))
+        o = O.Oracle.from_files(dp, ep, 0, 0)
+        try:
+            for hmm in (False, True):
+                _cmp_batch(tk, o, buf, off, hmm, f"packed={pack} ndev={ndev} hmm={hmm}")
+                os_, oe, od = o.cut_batch(buf, off, hmm, nthreads=8)
+                ts, te, td, _ = tk.cut_batch_into(buf, off, hmm)
+                assert np.array_equal(ts, os_) and np.array_equal(te, oe) and np.array_equal(td, od)
+        finally:
+            tk.close()
+
+
 def _tie_emissions():
     """Emissions under which the 3-rune HMM run 甲乙丙 has an exact route tie
     vE + T_EB == vS + T_SB > minFloat at its third rune (state B, Q12), found by
