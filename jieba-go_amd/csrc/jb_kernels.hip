@@ -387,7 +387,7 @@ __device__ __forceinline__ bool dat_hit(uint64_t child, uint32_t id) { return jb
 #ifndef JB_MW_WALKS
 #define JB_MW_WALKS 1  // trie walks per lane at once (2 measured slower)
 #endif
-#define JB_MW_ATTR __attribute__((amdgpu_num_sgpr(JB_MW_SGPR)))
+#define JB_MW_ATTR __attribute__((amdgpu_num_sgpr(JB_MW_SGPR), amdgpu_waves_per_eu(8, 8)))
 __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __restrict__ text, uint64_t nbytes,
                                                    const uint32_t* __restrict__ docbits, DevImage im,
                                                    uint32_t* __restrict__ lanemask, uint2* __restrict__ tile_cnt,
@@ -474,10 +474,16 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     __syncthreads();
     if (stamps) c0b = __builtin_amdgcn_s_memtime();  // (text staged)
     const uint8_t* win = s_t + 12 + threadIdx.x * 16u;  // window index 0
+    // The window's words, read once (one LDS round trip): as separate reads behind the
+    // alnum test's short-circuit || and then again for the leads, they were six round
+    // trips in a row (ISA audit).
+    uint32_t xw[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) xw[j] = reinterpret_cast<const uint32_t*>(win)[j];
     {  // some [0-9A-Za-z] byte in the lane's 16 bytes (k_nonzh skips blocks without one; padding
        // bytes past the batch can only add false positives)
-        const uint32_t* w4 = reinterpret_cast<const uint32_t*>(win) + 1;
-        const bool al = jb_any_alnum4(w4[0]) || jb_any_alnum4(w4[1]) || jb_any_alnum4(w4[2]) || jb_any_alnum4(w4[3]);
+        const bool al = ((uint32_t)jb_any_alnum4(xw[1]) | (uint32_t)jb_any_alnum4(xw[2]) |
+                         (uint32_t)jb_any_alnum4(xw[3]) | (uint32_t)jb_any_alnum4(xw[4])) != 0u;
         const uint64_t am = __ballot(al);
         if ((threadIdx.x & 63u) == 0) alnum16[(t0 >> 10) + (threadIdx.x >> 6)] = am;
     }
@@ -485,7 +491,7 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     uint32_t lead = 0;
 #pragma unroll
     for (int j = 0; j < 5; j++) {
-        const uint32_t x = reinterpret_cast<const uint32_t*>(win)[j];
+        const uint32_t x = xw[j];
         const uint32_t f = (x & (x << 1) & 0x80808080u) >> 7;  // bit 0/8/16/24
         lead |= ((f * 0x204081u) >> 21 & 0xFu) << (4 * j);
     }
@@ -502,31 +508,40 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         // 7), so that each lead has fixed registers: a Han rune of the common ranges
         // starting in the lane's own bytes issues its level-1 load here (slot i),
         // in flight during the block scan.  Leads past the 7th go to the general decode.
-        uint32_t l = lead, slow = 0;
+        // The seven leads' positions first, then their 4-byte reads all at once (one LDS
+        // round trip; read inside the per-lead branch they were seven in a row), then the
+        // branch-free classification.  A missing lead (fewer than 7) reads position 0 and is
+        // masked out.
+        uint32_t l = lead, slow = 0, xs[7], vm = 0;
+        uint64_t kq = 0;  // the leads' positions, 5 bits each (registers: 63 VGPRs, 8 waves per SIMD)
 #pragma unroll
         for (int i = 0; i < 7; i++) {
-            if (l) {
-                const uint32_t k = __builtin_ctz(l);
-                l &= l - 1u;
-                const uint32_t x = lds4(win, k);
-                const uint32_t b0 = x & 0xFFu;
-                const uint32_t r = ((b0 & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
-                const bool plain = (b0 - 0xE1u < 12u) | (b0 - 0xEEu < 2u);
-                const bool rare = (r - 0x2E80u < 0x180u) | (r - 0xF900u < 0x200u);
-                const bool ok = ((x & 0x00C0C000u) == 0x00808000u) & (((uint32_t)(M >> (k + 1u)) & 3u) == 0u);
-                const uint32_t o = r - 0x3000u;
-                const bool h = (r - 0x4E00u <= 0x9FFCu - 0x4E00u) | (r - 0x3400u <= 0x4DBFu - 0x3400u) |
-                               ((o < 64u) & (((k3000 >> (o & 63u)) & 1ull) != 0ull));
-                const bool fast = plain & !(ok & rare);
-                slow |= (fast ? 0u : 1u) << k;
-                covered |= ((fast & ok) ? 3u : 0u) << (k + 1u);
-                hanb |= ((fast & ok & h) ? 7u : 0u) << k;
-                if (fast & ok & h & (k >= 4u) & (r >= JB_DIRECT_LO)) {  // (rows of U+3400..U+9FFF are direct)
-                    rowp[i >> 1] |= (r - 0x3300u) << (16 * (i & 1));
-                    hsm |= 1u << i;
-                    kp |= (k - 4u) << (4 * i);
-                }
-            }
+            vm |= (l != 0u ? 1u : 0u) << i;
+            const uint32_t k = l ? (uint32_t)__builtin_ctz(l) : 0u;
+            kq |= (uint64_t)k << (5 * i);
+            xs[i] = lds4(win, k);
+            l &= l - 1u;
+        }
+#pragma unroll
+        for (int i = 0; i < 7; i++) {
+            const bool v = (vm >> i) & 1u;
+            const uint32_t k = (uint32_t)(kq >> (5 * i)) & 31u, x = xs[i];
+            const uint32_t b0 = x & 0xFFu;
+            const uint32_t r = ((b0 & 0x0Fu) << 12) | (((x >> 8) & 0x3Fu) << 6) | ((x >> 16) & 0x3Fu);
+            const bool plain = (b0 - 0xE1u < 12u) | (b0 - 0xEEu < 2u);
+            const bool rare = (r - 0x2E80u < 0x180u) | (r - 0xF900u < 0x200u);
+            const bool ok = ((x & 0x00C0C000u) == 0x00808000u) & (((uint32_t)(M >> (k + 1u)) & 3u) == 0u);
+            const uint32_t o = r - 0x3000u;
+            const bool h = (r - 0x4E00u <= 0x9FFCu - 0x4E00u) | (r - 0x3400u <= 0x4DBFu - 0x3400u) |
+                           ((o < 64u) & (((k3000 >> (o & 63u)) & 1ull) != 0ull));
+            const bool fast = plain & !(ok & rare);
+            slow |= ((v & !fast) ? 1u : 0u) << k;
+            covered |= ((v & fast & ok) ? 3u : 0u) << (k + 1u);
+            hanb |= ((v & fast & ok & h) ? 7u : 0u) << k;
+            const bool dr = v & fast & ok & h & (k >= 4u) & (r >= JB_DIRECT_LO);  // (rows of U+3400..U+9FFF are direct)
+            rowp[i >> 1] |= (dr ? r - 0x3300u : 0u) << (16 * (i & 1));
+            hsm |= (dr ? 1u : 0u) << i;
+            kp |= (dr ? k - 4u : 0u) << (4 * i);
         }
         slow |= l;
         lead = slow;
@@ -558,18 +573,25 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
        // taken out of it, not just served faster)
         const uint64_t* s_hv = reinterpret_cast<const uint64_t*>(s_raw + kMwOffHot);
         const uint16_t* s_ht = reinterpret_cast<const uint16_t*>(s_raw + kMwOffHot + 8u * JB_HOT_SLOTS);
-        uint32_t hit = 0;  // (tags first, values after: fewer registers live at once)
+        // every slot's tag and value read at once (14 LDS reads, one round trip; behind the
+        // tag test's && and the hit branch they were fourteen in a row), then the misses gathered
+        uint32_t hit = 0, tg[7];
 #pragma unroll
         for (int i = 0; i < 7; i++) {
             const uint32_t r = ((rowp[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) + 0x3300u;
-            hit |= (((hsm >> i) & 1u) && s_ht[jb_hot_slot(r)] == r ? 1u : 0u) << i;
+            tg[i] = s_ht[jb_hot_slot(r)];
+            cl[i] = s_hv[jb_hot_slot(r)];
+        }
+#pragma unroll
+        for (int i = 0; i < 7; i++) {
+            const uint32_t r = ((rowp[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) + 0x3300u;
+            hit |= (((hsm >> i) & 1u) & (tg[i] == r ? 1u : 0u)) << i;
         }
 #pragma unroll
         for (int i = 0; i < 7; i++) {
             const uint32_t row = (rowp[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-            cl[i] = 0ull;
-            if ((hit >> i) & 1u) cl[i] = s_hv[jb_hot_slot(row + 0x3300u)];
-            else if ((hsm >> i) & 1u) cl[i] = im.l1row[row];
+            if (!((hit >> i) & 1u)) cl[i] = 0ull;
+            if ((~hit & hsm) >> i & 1u) cl[i] = im.l1row[row];
         }
     }
     uint32_t nent;
