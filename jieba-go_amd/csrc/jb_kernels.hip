@@ -477,9 +477,20 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     // The window's words, read once (one LDS round trip): as separate reads behind the
     // alnum test's short-circuit || and then again for the leads, they were six round
     // trips in a row (ISA audit).
+    // Words 1-4 are the lane's own 16 bytes, one 16-byte read (16-byte aligned, so without
+    // the 4-way bank conflicts of 4-byte reads at a 16-byte lane stride); word 0 is the
+    // previous lane's word 4, by a DPP wave shift (lane 0 of the wave reads it).
     uint32_t xw[5];
-#pragma unroll
-    for (int j = 0; j < 5; j++) xw[j] = reinterpret_cast<const uint32_t*>(win)[j];
+    {
+        const uint4 v4 = *reinterpret_cast<const uint4*>(win + 4);
+        xw[1] = v4.x;
+        xw[2] = v4.y;
+        xw[3] = v4.z;
+        xw[4] = v4.w;
+        uint32_t w0 = 0;
+        if ((threadIdx.x & 63u) == 0u) w0 = reinterpret_cast<const uint32_t*>(win)[0];
+        xw[0] = (uint32_t)__builtin_amdgcn_update_dpp((int)w0, (int)xw[4], 0x138, 0xF, 0xF, false);  // wave_shr:1
+    }
     {  // some [0-9A-Za-z] byte in the lane's 16 bytes (k_nonzh skips blocks without one; padding
        // bytes past the batch can only add false positives)
         const bool al = ((uint32_t)jb_any_alnum4(xw[1]) | (uint32_t)jb_any_alnum4(xw[2]) |
