@@ -479,6 +479,10 @@ def end_to_end(tk, buf, off, hmm, nrunes, reps=3):
         return r, (time.perf_counter() - t) / reps
 
     res, s_sp = timed(lambda r: tk.cut_batch_into(buf, off, bool(hmm), r[3] if r else None))
+    r32, s_32 = timed(lambda r: tk.cut_batch_into32(buf, off, bool(hmm), r[3] if r else None))
+    ok32 = bool(np.array_equal(r32[0].astype(np.uint64) + np.uint64(off[0]), res[0]) and
+                np.array_equal(r32[1].astype(np.uint64) + np.uint64(off[0]), res[1]) and np.array_equal(r32[2], res[2]))
+    del r32
     ms, me, _ = tk.cut_batch_mask(buf, off, bool(hmm))
     (ms, me, ntok), s_m = timed(lambda r: tk.cut_batch_mask(buf, off, bool(hmm), (r[0], r[1]) if r else None))
     nb = int(off[-1] - off[0])
@@ -500,11 +504,14 @@ def end_to_end(tk, buf, off, hmm, nrunes, reps=3):
                    "(SURVEY.md §8d's output format); checked against the spans below")
     out["tokens"] = int(ntok)
     out["same_tokens_as_spans"] = ok_mask
-    out["spans"] = dict(rate(s_sp), what="jb_cut_batch_into from pageable host memory (what the Go binding's "
-                                         "Cut / CutParallel use): the same pipeline with the spans packed on the GPU "
-                                         "(k_span_pack: 2 B per token, gap | length, rare escapes in a side list), "
-                                         "decoded on the host into u64 batch offsets in caller arrays",
+    out["spans"] = dict(rate(s_sp), what="jb_cut_batch_into from pageable host memory: the same pipeline with the "
+                                         "spans packed on the GPU (k_span_pack: 2 B per token, gap | length, rare "
+                                         "escapes in a side list), decoded on the host into u64 batch offsets in "
+                                         "caller arrays (16 B written per token)",
                         span_pack=os.environ.get("JB_SPAN_PACK", "1") != "0")
+    out["spans32"] = dict(rate(s_32), what="jb_cut_batch_into32, what the Go binding's Cut / CutBatch call: the same, "
+                                           "decoded into u32 offsets from the batch's first byte in caller arrays "
+                                           "(8 B written per token)", same_as_spans=ok32)
     out["masks_pinned"] = dict(rate(s_p), what="jb_cut_batch_mask with the text in jb_host_alloc (pinned) memory: "
                                                "no staging copy", same_as_pageable=ok_pin)
     return out

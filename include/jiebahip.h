@@ -120,6 +120,15 @@ void jb_spans_free(jb_spans *s);
 int jb_cut_batch_into(jb_ctx *ctx, const uint8_t *text, const uint64_t *doc_off, uint32_t ndocs, int hmm,
                       uint64_t *start, uint64_t *end, uint64_t cap, uint64_t *doc_tok, uint64_t *ntokens);
 
+/* jb_cut_batch_into with u32 outputs, offsets relative to the batch's first byte:
+ * token k is the byte range [doc_off[0] + start[k], doc_off[0] + end[k]).  Half the
+ * output of the u64 form (what a Go caller slices its strings with: the host side of
+ * a host batch is bound by writing the spans, 16 bytes per token there, 8 here).  The
+ * batch must be under 4 GiB (JB_ELIMIT otherwise; a caller cuts larger ones in parts);
+ * JB_ELIMIT with *ntokens set when the arrays are too small, as jb_cut_batch_into. */
+int jb_cut_batch_into32(jb_ctx *ctx, const uint8_t *text, const uint64_t *doc_off, uint32_t ndocs, int hmm,
+                        uint32_t *start, uint32_t *end, uint64_t cap, uint64_t *doc_tok, uint64_t *ntokens);
+
 /* Token boundaries as two bitmaps over the batch's bytes instead of spans (2 bits per
  * input byte; 268 MB per GiB instead of 8 bytes per token): bit i of `starts` (word
  * i / 64, bit i % 64) is set when a token begins at byte doc_off[0] + i, bit i of

@@ -6,6 +6,7 @@
 // happens on the CPU: without a usable HIP device every cut returns
 // JB_EDEVICE.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -240,6 +241,33 @@ void hfree(void* p) {
     if (p) (void)hipHostFree(p);
 }
 
+// memcpy whose destination lines are written without being read first (non-temporal
+// 16-byte stores; plain stores read every destination line before writing it): staging
+// a batch into pinned memory, which the copy engine then reads.  Fenced at the end.
+static void nt_copy(void* dst, const void* src, size_t n) {
+    typedef long long v2i __attribute__((vector_size(16)));
+    char* d = static_cast<char*>(dst);
+    const char* s = static_cast<const char*>(src);
+    const size_t head = std::min(n, (size_t)((16u - ((uintptr_t)d & 15u)) & 15u));
+    memcpy(d, s, head);
+    d += head;
+    s += head;
+    n -= head;
+    for (; n >= 64; n -= 64, d += 64, s += 64) {
+        v2i a, b, c, e;
+        memcpy(&a, s, 16);
+        memcpy(&b, s + 16, 16);
+        memcpy(&c, s + 32, 16);
+        memcpy(&e, s + 48, 16);
+        __builtin_nontemporal_store(a, reinterpret_cast<v2i*>(d));
+        __builtin_nontemporal_store(b, reinterpret_cast<v2i*>(d + 16));
+        __builtin_nontemporal_store(c, reinterpret_cast<v2i*>(d + 32));
+        __builtin_nontemporal_store(e, reinterpret_cast<v2i*>(d + 48));
+    }
+    memcpy(d, s, n);
+    __builtin_ia32_sfence();
+}
+
 // memcpy with a few host threads for large copies (staging into pinned memory)
 void par_copy(void* dst, const void* src, size_t n) {
     const size_t kMin = 8u << 20;
@@ -291,6 +319,10 @@ void par_widen(uint64_t* out, const uint32_t* in, size_t n, uint64_t base) {
 struct SpanBuf {
     uint64_t* s = nullptr;
     uint64_t* e = nullptr;
+    // external u32 arrays instead (jb_cut_batch_into32): token k is s32[k] = start - b32
+    uint32_t* s32 = nullptr;
+    uint32_t* e32 = nullptr;
+    uint64_t b32 = 0;
     size_t n = 0, cap = 0;
     bool external = false;          // caller-owned arrays of fixed capacity
     size_t needed = 0;              // tokens that did not fit an external buffer
@@ -1243,7 +1275,12 @@ static void small_split(const uint32_t* h, SmallReq* const* rq, uint32_t n) {
             r.rc = fail(JB_ENOMEM, "out of host memory for %llu tokens", (unsigned long long)nt);
             r.err = g_err;
         } else {
-            if (write) {
+            if (write && out->s32) {
+                for (uint64_t t = 0; t < nt; t++) {  // (batch offsets -> this call's text, less b32)
+                    out->s32[out->n + t] = (uint32_t)(base - out->b32 + hs[t0 + t] - at);
+                    out->e32[out->n + t] = (uint32_t)(base - out->b32 + he[t0 + t] - at);
+                }
+            } else if (write) {
                 for (uint64_t t = 0; t < nt; t++) {  // (batch offsets -> this call's text)
                     out->s[out->n + t] = base + hs[t0 + t] - at;
                     out->e[out->n + t] = base + he[t0 + t] - at;
@@ -1409,31 +1446,124 @@ static void put_mask_words(const MaskDst* m, uint64_t rw, uint64_t nw, uint64_t 
 // header, a token at a time (start = previous end + gap, end = start + length), on
 // kCopyThreads threads; an escaped token (0xFFFF) takes its span from the side list,
 // sorted by token index first (on ordinary text it is empty or nearly so).
+// One token of a packed piece: start = previous end + gap, end = start + length, or an
+// escaped token's span from the sorted side list.  e: the previous token's end (batch offset).
+static inline void unpack_one(uint32_t x, uint32_t i, const uint4* side, uint32_t nside, uint64_t base, uint64_t& s,
+                              uint64_t& e) {
+    if (x != 0xFFFFu) {
+        s = e + (x & kPackGapEsc);
+        e = s + (x >> kPackGapBits);
+    } else {
+        const uint4* q = std::lower_bound(side, side + nside, i, [](const uint4& a, uint32_t v) { return a.x < v; });
+        s = base + q->y;
+        e = base + q->z;
+    }
+}
+
+// Tokens [i0, i1) of one block, eight at a time with AVX-512: the ends are a running sum
+// of gap + length (an in-register scan: three shifted adds), the starts the ends minus
+// the lengths; a group of eight with an escaped token goes through unpack_one.  T is the
+// output word (u64 batch offsets, or u32 for jb_cut_batch_into32: base is then relative to
+// the caller's first byte).  Stores are streaming where both outputs are aligned alike to
+// the vector width (after a scalar head), plain otherwise.
+template <class T>
+__attribute__((target("avx512f"))) static void unpack_block_avx512(const uint16_t* pk, uint32_t i0, uint32_t i1,
+                                                                  uint64_t e, const uint4* side, uint32_t nside,
+                                                                  uint64_t base, T* os, T* oe) {
+    constexpr uintptr_t kVec = 8u * sizeof(T) - 1u;  // (eight outputs: 64 or 32 bytes)
+    uint32_t i = i0;
+    const bool al = (((uintptr_t)(os + i) ^ (uintptr_t)(oe + i)) & kVec) == 0u;
+    if (al)
+        for (; i < i1 && ((uintptr_t)(os + i) & kVec); i++) {
+            uint64_t s;
+            unpack_one(pk[i], i, side, nside, base, s, e);
+            __builtin_nontemporal_store((T)s, os + i);
+            __builtin_nontemporal_store((T)e, oe + i);
+        }
+    const __m512i m6 = _mm512_set1_epi64(kPackGapEsc), z = _mm512_setzero_si512(), last = _mm512_set1_epi64(7);
+    __m512i cv = _mm512_set1_epi64((long long)e);  // the previous token's end in every lane
+    for (; i + 8u <= i1; i += 8u) {
+        const __m128i raw = _mm_loadu_si128(reinterpret_cast<const __m128i*>(pk + i));
+        if (_mm_movemask_epi8(_mm_cmpeq_epi16(raw, _mm_set1_epi16(-1)))) {  // an escaped token: one at a time
+            e = (uint64_t)_mm_cvtsi128_si64(_mm512_castsi512_si128(cv));
+            for (uint32_t k = i; k < i + 8u; k++) {
+                uint64_t s;
+                unpack_one(pk[k], k, side, nside, base, s, e);
+                os[k] = (T)s;
+                oe[k] = (T)e;
+            }
+            cv = _mm512_set1_epi64((long long)e);
+            continue;
+        }
+        const __m512i x = _mm512_cvtepu16_epi64(raw);
+        const __m512i l = _mm512_srli_epi64(x, kPackGapBits);
+        __m512i t = _mm512_add_epi64(_mm512_and_si512(x, m6), l);  // gap + length
+        t = _mm512_add_epi64(t, _mm512_alignr_epi64(t, z, 7));     // inclusive scan over 8 lanes
+        t = _mm512_add_epi64(t, _mm512_alignr_epi64(t, z, 6));
+        t = _mm512_add_epi64(t, _mm512_alignr_epi64(t, z, 4));
+        const __m512i ev = _mm512_add_epi64(cv, t);
+        const __m512i sv = _mm512_sub_epi64(ev, l);
+        if constexpr (sizeof(T) == 8) {
+            if (al) {
+                _mm512_stream_si512(reinterpret_cast<__m512i*>(os + i), sv);
+                _mm512_stream_si512(reinterpret_cast<__m512i*>(oe + i), ev);
+            } else {
+                _mm512_storeu_si512(os + i, sv);
+                _mm512_storeu_si512(oe + i, ev);
+            }
+        } else {
+            const __m256i s32 = _mm512_cvtepi64_epi32(sv), e32 = _mm512_cvtepi64_epi32(ev);
+            if (al) {
+                _mm256_stream_si256(reinterpret_cast<__m256i*>(os + i), s32);
+                _mm256_stream_si256(reinterpret_cast<__m256i*>(oe + i), e32);
+            } else {
+                _mm256_storeu_si256(reinterpret_cast<__m256i*>(os + i), s32);
+                _mm256_storeu_si256(reinterpret_cast<__m256i*>(oe + i), e32);
+            }
+        }
+        cv = _mm512_permutexvar_epi64(last, ev);
+    }
+    e = (uint64_t)_mm_cvtsi128_si64(_mm512_castsi512_si128(cv));
+    for (; i < i1; i++) {
+        uint64_t s;
+        unpack_one(pk[i], i, side, nside, base, s, e);
+        os[i] = (T)s;
+        oe[i] = (T)e;
+    }
+}
+
+// k_span_pack's packed spans of one piece back to batch offsets (base = the piece's first
+// byte in the batch, or relative to the caller's first byte for u32 outputs): blocks of
+// kPackBlock tokens decode independently from their header, on kCopyThreads threads
+// (eight tokens at a time with AVX-512 where the CPU has it); an escaped token (0xFFFF)
+// takes its span from the side list, sorted by token index first (on ordinary text it is
+// empty or nearly so).  The outputs are written without reading the caller's lines first
+// (streaming stores), fenced before each thread ends.
+template <class T>
 static void unpack_spans(const uint16_t* pk, const uint32_t* hdr, uint4* side, uint32_t nside, uint32_t nt,
-                         uint64_t base, uint64_t* os, uint64_t* oe) {
+                         uint64_t base, T* os, T* oe) {
     if (nside > 1) std::sort(side, side + nside, [](const uint4& a, const uint4& b) { return a.x < b.x; });
     const uint32_t nb = (nt + kPackBlock - 1u) / kPackBlock;
-    const unsigned nth = nt >= (1u << 18) ? kCopyThreads : 1u;
+    static const unsigned kDecodeThreads = (unsigned)std::min(32, std::max(1, env_int("JB_DECODE_THREADS", 8)));
+    static const bool avx512 = __builtin_cpu_supports("avx512f") && env_int("JB_DECODE_AVX512", 1) != 0;
+    const unsigned nth = nt >= (1u << 18) ? kDecodeThreads : 1u;
     auto work = [&](unsigned t) {
         const uint32_t b0 = (uint32_t)((uint64_t)nb * t / nth), b1 = (uint32_t)((uint64_t)nb * (t + 1) / nth);
         for (uint32_t b = b0; b < b1; b++) {
             const uint32_t i0 = b * kPackBlock, i1 = std::min(nt, i0 + kPackBlock);
             uint64_t e = base + hdr[b];
+            if (avx512) {
+                unpack_block_avx512<T>(pk, i0, i1, e, side, nside, base, os, oe);
+                continue;
+            }
             for (uint32_t i = i0; i < i1; i++) {
-                const uint32_t x = pk[i];
                 uint64_t s;
-                if (x != 0xFFFFu) {
-                    s = e + (x & kPackGapEsc);
-                    e = s + (x >> kPackGapBits);
-                } else {
-                    const uint4* q = std::lower_bound(side, side + nside, i, [](const uint4& a, uint32_t v) { return a.x < v; });
-                    s = base + q->y;
-                    e = base + q->z;
-                }
-                os[i] = s;
-                oe[i] = e;
+                unpack_one(pk[i], i, side, nside, base, s, e);
+                __builtin_nontemporal_store((T)s, os + i);
+                __builtin_nontemporal_store((T)e, oe + i);
             }
         }
+        __builtin_ia32_sfence();  // (the streaming stores are visible before the thread is joined)
     };
     run_threads(nth, work);
 }
@@ -1569,6 +1699,7 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
     }
     uint64_t mask_done = 0;
 
+    static const bool nt_stage = env_int("JB_NT_STAGE", 1) != 0;  // (A/B switch)
     auto stage = [&](size_t k) -> int {
         const Piece& p = pcs[k];
         const uint64_t pb = doc_off[p.d0], len = doc_off[p.d1] - pb;
@@ -1592,7 +1723,10 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
                 const uint64_t lo = std::min(total, t * share), hi = std::min(total, lo + share);
                 for (uint64_t o = lo; o < hi; o += kSub) {
                     const uint64_t l = std::min(kSub, hi - o);
-                    if (o < len) memcpy(d->h_text + p.off + o, text + pb + o, std::min(l, len - o));
+                    if (o < len) {
+                        if (nt_stage) nt_copy(d->h_text + p.off + o, text + pb + o, std::min(l, len - o));
+                        else memcpy(d->h_text + p.off + o, text + pb + o, std::min(l, len - o));
+                    }
                     if (hipMemcpyAsync(d->text + p.off + o, d->h_text + p.off + o, l, hipMemcpyHostToDevice,
                                        d->cstream) != hipSuccess)
                         err = 1;
@@ -1714,7 +1848,23 @@ static int cut_range(Device* d, const uint8_t* text, const uint64_t* doc_off, ui
         if (!write && !out->external) return fail(JB_ENOMEM, "out of host memory for %u tokens", nt);
         if (write && pack) {
             const uint32_t nside = d->h_pcnt[k * kSnapWords + CNT_SIDE];
-            unpack_spans(o.hpk, o.hhdr, o.hside, nside, nt, doc_off[p.d0], out->s + out->n, out->e + out->n);
+            if (out->s32)
+                unpack_spans(o.hpk, o.hhdr, o.hside, nside, nt, doc_off[p.d0] - out->b32, out->s32 + out->n,
+                             out->e32 + out->n);
+            else
+                unpack_spans(o.hpk, o.hhdr, o.hside, nside, nt, doc_off[p.d0], out->s + out->n, out->e + out->n);
+        } else if (write && out->s32) {
+            const uint32_t b = (uint32_t)(doc_off[p.d0] - out->b32);
+            uint32_t* const os = out->s32 + out->n;
+            uint32_t* const oe = out->e32 + out->n;
+            const uint32_t* const hs = o.hs;
+            const unsigned nth = nt >= (1u << 20) ? kCopyThreads : 1u;
+            auto work = [&](unsigned t) {
+                const uint64_t a = (uint64_t)nt * t / nth, c = (uint64_t)nt * (t + 1) / nth;
+                for (uint64_t i = a; i < c; i++) os[i] = b + hs[i];
+                for (uint64_t i = a; i < c; i++) oe[i] = b + hs[nt + i];
+            };
+            run_threads(nth, work);
         } else if (write) {
             const uint64_t base = doc_off[p.d0];
             uint64_t* const os = out->s + out->n;
@@ -2174,6 +2324,58 @@ extern "C" int jb_cut_batch_into(jb_ctx* ctx, const uint8_t* text, const uint64_
             if (sb[k].n) {
                 memcpy(start + w, sb[k].s, sb[k].n * 8);
                 memcpy(end + w, sb[k].e, sb[k].n * 8);
+            }
+            w += sb[k].n;
+        }
+    }
+    fill_doc_tok(sb, ndocs, doc_tok, unit_doc);
+    release_all();
+    return JB_OK;
+}
+
+extern "C" int jb_cut_batch_into32(jb_ctx* ctx, const uint8_t* text, const uint64_t* doc_off, uint32_t ndocs,
+                                   int hmm, uint32_t* start, uint32_t* end, uint64_t cap, uint64_t* doc_tok,
+                                   uint64_t* ntokens) {
+    if (!ctx || !ntokens || !doc_tok || (!doc_off && ndocs) || (cap && (!start || !end)))
+        return fail(JB_EINVAL, "jb_cut_batch_into32: null argument");
+    *ntokens = 0;
+    const uint64_t b0 = ndocs ? doc_off[0] : 0;
+    if (ndocs && doc_off[ndocs] - b0 > 0xFFFFFFFFull)
+        return fail(JB_ELIMIT, "jb_cut_batch_into32: a batch of %llu bytes (u32 offsets: under 4 GiB)",
+                    (unsigned long long)(doc_off[ndocs] - b0));
+    std::shared_lock<std::shared_mutex> rl(ctx->lock);
+    const size_t nd = ctx->devs.size();
+    std::vector<SpanBuf> sb(nd);
+    if (nd == 1) {  // the pieces' spans are decoded straight into the caller's arrays
+        sb[0].s32 = start;
+        sb[0].e32 = end;
+        sb[0].b32 = b0;
+        sb[0].cap = cap;
+        sb[0].external = true;
+    }
+    auto release_all = [&] {
+        for (auto& b : sb) b.release();
+    };
+    std::vector<uint32_t> unit_doc;
+    int rc = cut_sharded(ctx, text, doc_off, ndocs, hmm, &sb, nullptr, &unit_doc);
+    if (rc) {
+        release_all();
+        return rc;
+    }
+    uint64_t nt = 0;
+    for (size_t k = 0; k < nd; k++) nt += sb[k].n;
+    *ntokens = nt;
+    if (nt > cap) {
+        release_all();
+        return fail(JB_ELIMIT, "%llu tokens do not fit the %llu-token output arrays", (unsigned long long)nt,
+                    (unsigned long long)cap);
+    }
+    if (nd > 1) {  // (several devices: each one's u64 spans, narrowed here)
+        uint64_t w = 0;
+        for (size_t k = 0; k < nd; k++) {
+            for (uint64_t i = 0; i < sb[k].n; i++) {
+                start[w + i] = (uint32_t)(sb[k].s[i] - b0);
+                end[w + i] = (uint32_t)(sb[k].e[i] - b0);
             }
             w += sb[k].n;
         }

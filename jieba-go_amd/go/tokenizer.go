@@ -145,6 +145,50 @@ func spansToTokens(text string, s *C.jb_spans, doc int) []string {
 	return out
 }
 
+// cut32 cuts a batch held in buf (documents [off[d], off[d+1]), off[0] == 0) into u32
+// spans (jb_cut_batch_into32) in Go slices: half the bytes the library writes for u64
+// spans, which bound a host batch's host side.  A first try has room for one token per
+// three bytes; on JB_ELIMIT a second one has the count the library returned.  The slices
+// hold no Go pointers, so cgo lets C write them during the call (it keeps none).
+func (t *Tokenizer) cut32(buf []byte, off []uint64, hmm C.int) (starts, ends []uint32, docTok []uint64) {
+	n := len(off) - 1
+	total := int(off[n] - off[0])
+	docTok = make([]uint64, n+1)
+	capTok := total/3 + 64
+	for try := 0; try < 2; try++ {
+		starts = make([]uint32, capTok)
+		ends = make([]uint32, capTok)
+		var nt C.uint64_t
+		rc := C.jb_cut_batch_into32(t.ctx, (*C.uint8_t)(unsafe.Pointer(&buf[0])), (*C.uint64_t)(unsafe.Pointer(&off[0])),
+			C.uint32_t(n), hmm, (*C.uint32_t)(unsafe.Pointer(&starts[0])), (*C.uint32_t)(unsafe.Pointer(&ends[0])),
+			C.uint64_t(capTok), (*C.uint64_t)(unsafe.Pointer(&docTok[0])), &nt)
+		if rc == C.JB_OK {
+			return starts[:int(nt)], ends[:int(nt)], docTok
+		}
+		if rc == C.JB_ELIMIT && int(nt) > capTok {
+			capTok = int(nt)
+			continue
+		}
+		// JB_EPANIC: the reference panics on this input (cutDAG slice with tail -1)
+		panic("jiebahip: " + lastError())
+	}
+	panic("jiebahip: " + lastError())
+}
+
+// tokens [a, b) of u32 spans over text (offsets from text's first byte) as strings.
+func tokens32(text string, starts, ends []uint32, a, b int) []string {
+	out := make([]string, 0, b-a)
+	for k := a; k < b; k++ {
+		st, en := int(starts[k]), int(ends[k])
+		if en-st == 1 && text[st] >= 0x80 {
+			out = append(out, "�") // invalid UTF-8 byte (tokenizer.go:301-306)
+		} else {
+			out = append(out, text[st:en])
+		}
+	}
+	return out
+}
+
 // Cut segments one text (tokenizer.go:151).  Never returns nil.
 func (t *Tokenizer) Cut(text string, useHmm bool) []string {
 	t.mu.RLock()
@@ -156,6 +200,10 @@ func (t *Tokenizer) Cut(text string, useHmm bool) []string {
 	hmm := C.int(0)
 	if useHmm {
 		hmm = 1
+	}
+	if uint64(len(b)) < 1<<32 { // u32 spans (jb_cut_batch_into32)
+		starts, ends, _ := t.cut32(b, []uint64{0, uint64(len(b))}, hmm)
+		return tokens32(text, starts, ends, 0, len(starts))
 	}
 	var s C.jb_spans
 	if rc := C.jb_cut(t.ctx, (*C.uint8_t)(unsafe.Pointer(&b[0])), C.size_t(len(b)), hmm, &s); rc != C.JB_OK {
@@ -194,16 +242,23 @@ func (t *Tokenizer) CutBatch(docs []string, useHmm bool) [][]string {
 	if useHmm {
 		hmm = 1
 	}
+	all := string(buf[:total])
+	out := make([][]string, len(docs))
+	if uint64(total) < 1<<32 { // u32 spans (jb_cut_batch_into32); tokens share one copy of the batch text
+		starts, ends, docTok := t.cut32(buf, off, hmm)
+		for i := range docs {
+			out[i] = tokens32(all, starts, ends, int(docTok[i]), int(docTok[i+1]))
+		}
+		return out
+	}
 	var s C.jb_spans
 	if rc := C.jb_cut_batch(t.ctx, (*C.uint8_t)(unsafe.Pointer(&buf[0])), (*C.uint64_t)(unsafe.Pointer(&off[0])),
 		C.uint32_t(len(docs)), hmm, &s); rc != C.JB_OK {
 		panic("jiebahip: " + lastError())
 	}
 	defer C.jb_spans_free(&s)
-	all := string(buf[:total])
-	out := make([][]string, len(docs))
 	for i := range docs {
-		out[i] = spansToTokens(all, &s, i) // tokens share one copy of the batch text
+		out[i] = spansToTokens(all, &s, i)
 	}
 	return out
 }

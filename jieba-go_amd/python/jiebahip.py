@@ -31,7 +31,7 @@ EXPORTS = [
     "jb_add_word", "jb_dict_get", "jb_dict_size", "jb_save", "jb_profile_enable", "jb_profile_read",
     "jb_profile_reset", "jb_image_build", "jb_image_free", "jb_image_save", "jb_image_dict_info", "jb_image_lookup",
     "jb_image_stats", "jb_image_emit", "jb_go_log", "jb_shard_bounds", "jb_last_stats",
-    "jb_suggest_freq", "jb_add_log", "jb_image_log_keys", "jb_device_status",
+    "jb_suggest_freq", "jb_add_log", "jb_image_log_keys", "jb_device_status", "jb_cut_batch_into32",
 ]
 
 
@@ -129,6 +129,8 @@ def lib():
         L.jb_add_log.argtypes = [vp, vp, vp, C.c_size_t]
         L.jb_last_stats.argtypes = [vp, C.POINTER(jb_stats)]
         L.jb_device_status.argtypes = [vp, vp]
+        L.jb_cut_batch_into32.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, vp, vp, C.c_uint64, vp,
+                                          C.POINTER(C.c_uint64)]
         _lib = L
     return _lib
 
@@ -350,6 +352,29 @@ class Tokenizer:
                                          C.byref(n))
             if rc == JB_ELIMIT and n.value > len(out[0]):
                 out = (np.empty(n.value, np.uint64), np.empty(n.value, np.uint64), out[2])
+                continue
+            _check(rc)
+            break
+        k = n.value
+        return out[0][:k], out[1][:k], out[2], out
+
+    def cut_batch_into32(self, buf, doc_off, hmm, out=None):
+        """jb_cut_batch_into32: u32 spans relative to doc_off[0] in caller-owned arrays.
+        `out` = (starts u32, ends u32, doc_tok u64[ndocs+1]) to reuse; grown when too
+        small.  Returns (starts[:n], ends[:n], doc_tok, out)."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
+        nd = len(doc_off) - 1
+        if out is None or len(out[2]) != nd + 1:
+            cap = max(1024, int(doc_off[-1] - doc_off[0]) // 2)
+            out = (np.empty(cap, np.uint32), np.empty(cap, np.uint32), np.empty(nd + 1, np.uint64))
+        n = C.c_uint64()
+        for _ in range(2):
+            rc = lib().jb_cut_batch_into32(self.h, buf.ctypes.data, doc_off.ctypes.data, nd, int(hmm),
+                                           out[0].ctypes.data, out[1].ctypes.data, len(out[0]), out[2].ctypes.data,
+                                           C.byref(n))
+            if rc == JB_ELIMIT and n.value > len(out[0]):
+                out = (np.empty(n.value, np.uint32), np.empty(n.value, np.uint32), out[2])
                 continue
             _check(rc)
             break

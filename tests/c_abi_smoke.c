@@ -132,6 +132,27 @@ int main(int argc, char **argv) {
     free(st);
     free(en);
 
+    /* the same as u32 offsets from the batch's first byte (what the Go binding calls) */
+    {
+        uint32_t *s32 = (uint32_t *)malloc((size_t)(cap ? cap : 1) * sizeof(uint32_t));
+        uint32_t *e32 = (uint32_t *)malloc((size_t)(cap ? cap : 1) * sizeof(uint32_t));
+        uint64_t k;
+        if (!s32 || !e32) return die("malloc", -1);
+        if ((rc = jb_cut_batch_into32(ctx, (const uint8_t *)text, off, 2, 1, s32, e32, cap, doc_tok, &ntok)))
+            return die("jb_cut_batch_into32", rc);
+        st = (uint64_t *)malloc((size_t)(ntok ? ntok : 1) * sizeof(uint64_t));
+        en = (uint64_t *)malloc((size_t)(ntok ? ntok : 1) * sizeof(uint64_t));
+        for (k = 0; k < ntok; k++) {
+            st[k] = off[0] + s32[k];
+            en[k] = off[0] + e32[k];
+        }
+        print_spans("into32", st, en, ntok);
+        free(st);
+        free(en);
+        free(s32);
+        free(e32);
+    }
+
     /* AddWord(word, 0): suggestFreq's value, then Cut again */
     if ((rc = jb_suggest_freq(ctx, argv[4], strlen(argv[4]), &freq))) return die("jb_suggest_freq", rc);
     if ((rc = jb_add_word(ctx, argv[4], strlen(argv[4]), 0))) return die("jb_add_word", rc);

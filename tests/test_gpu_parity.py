@@ -612,6 +612,40 @@ def test_cut_batch_into_caller_arrays(small):
 
 
 @pytest.mark.parametrize("pack", ["1", "0"])
+def test_cut_batch_into32(syn_small, pack, monkeypatch):
+    """jb_cut_batch_into32 (u32 spans relative to doc_off[0], what the Go binding slices its
+    strings with) gives jb_cut_batch_into's spans less doc_off[0]: a batch that does not
+    start at byte 0 of its buffer, cut in several pieces (JB_PIECE_KIB=256), over two
+    devices (JB_DEVICE_WRAP), as a k_small batch (<= 4 KiB), with arrays too small (the
+    binding retries with the count the library returns); packed spans on and off."""
+    monkeypatch.setenv("JB_SPAN_PACK", pack)
+    monkeypatch.setenv("JB_PIECE_KIB", "256")
+    dp, ep, s = syn_small
+    buf, off, _ = s.corpus(synth.KIND_SENTENCES, 41, max_docs=4000, target_bytes=1 << 20)
+    off = np.asarray(off, np.uint64)
+    lo = 37  # documents 37.. : the batch starts inside the buffer
+    sub = off[lo:]
+    small = off[lo:lo + 12]
+    for ndev, wrap in ((1, None), (2, "1")):
+        if wrap:
+            monkeypatch.setenv("JB_DEVICE_WRAP", wrap)
+        tk = J.Tokenizer(J.make_config(dict_path=dp, emit_path=ep, ndevices=ndev))
+        try:
+            for hmm in (False, True):
+                for o_ in (sub, small):
+                    ws, we, wd, _ = tk.cut_batch_into(buf, o_, hmm)
+                    b0 = int(o_[0])
+                    tiny = (np.empty(2, np.uint32), np.empty(2, np.uint32), np.empty(len(o_), np.uint64))
+                    for out in (None, tiny):
+                        gs, ge, gd, _ = tk.cut_batch_into32(buf, o_, hmm, out)
+                        assert gs.dtype == np.uint32 and len(gs) == len(ws), (ndev, hmm, len(o_))
+                        assert np.array_equal(gs.astype(np.uint64) + b0, ws) and np.array_equal(ge.astype(np.uint64) + b0, we)
+                        assert np.array_equal(gd, wd)
+        finally:
+            tk.close()
+
+
+@pytest.mark.parametrize("pack", ["1", "0"])
 def test_packed_spans_escapes(syn_small, pack, monkeypatch):
     """Host batches' spans come back packed (JB_SPAN_PACK=1, the default: k_span_pack's
     u16 gap | length << 6 per token, decoded on the host by blocks of 4,096 tokens) or as
@@ -649,6 +683,9 @@ def test_packed_spans_escapes(syn_small, pack, monkeypatch):
                 os_, oe, od = o.cut_batch(buf, off, hmm, nthreads=8)
                 ts, te, td, _ = tk.cut_batch_into(buf, off, hmm)
                 assert np.array_equal(ts, os_) and np.array_equal(te, oe) and np.array_equal(td, od)
+                t32, e32, d32, _ = tk.cut_batch_into32(buf, off, hmm)
+                assert np.array_equal(t32.astype(np.uint64), os_) and np.array_equal(e32.astype(np.uint64), oe)
+                assert np.array_equal(d32, od)
         finally:
             tk.close()
 
@@ -743,6 +780,7 @@ def test_c_abi_smoke_program(syn_small, tmp_path):
     assert list(map(int, out["doc_tok"].split()[1:])) == bd.tolist()
     hs, he, _ = o.cut_batch(both, off2, True)
     assert _spans_line(out["into"]) == (hs.tolist(), he.tolist())
+    assert _spans_line(out["into32"]) == (hs.tolist(), he.tolist())
     freq = int(out["freq"].split()[1])
     o.add_term(word, freq)
     assert int(out["freq"].split()[3]) == o.size

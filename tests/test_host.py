@@ -21,7 +21,7 @@ def test_library_exports_every_declared_symbol():
     L = J.lib()
     with open(os.path.join(ROOT, "include", "jiebahip.h")) as f:
         hdr = f.read()
-    declared = set(re.findall(r"\b(jb_[a-z_]+)\s*\(", hdr))
+    declared = set(re.findall(r"\b(jb_[a-z0-9_]+)\s*\(", hdr))
     assert declared == set(J.EXPORTS)
     for name in declared:
         assert hasattr(L, name), name

@@ -63,6 +63,13 @@ def main():
         res = tk.cut_batch_into(buf, off, True, res[3])
         dt = time.perf_counter() - t
         print(f"cut_batch_into rep {r}: {dt * 1e3:.2f} ms, {nchars / dt / 1e9:.2f} G chars/s", flush=True)
+    r32 = tk.cut_batch_into32(buf, off, True)
+    for r in range(4):
+        t = time.perf_counter()
+        r32 = tk.cut_batch_into32(buf, off, True, r32[3])
+        dt = time.perf_counter() - t
+        print(f"cut_batch_into32 rep {r}: {dt * 1e3:.2f} ms, {nchars / dt / 1e9:.2f} G chars/s", flush=True)
+    del r32
     if hasattr(tk, "cut_batch_mask"):
         m = tk.cut_batch_mask(buf, off, True)
         for r in range(4):
