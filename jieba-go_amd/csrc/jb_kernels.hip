@@ -1146,6 +1146,33 @@ __device__ __forceinline__ TblPeek tbl_peek(const TblSrc& src, uint32_t j) {
     }
     return p;
 }
+// The same blocks read into registers once (a lane holds at most kZhChunk / 64 = 3, and
+// only the last can be ~0u): a block change in the DP then takes its next block and the
+// one after it from registers, not from LDS.  A lane's blocks end at different steps, so
+// nearly every DP step has some lane changing block, and as TblSrc loops those were two
+// LDS round trips (next, then the peek for the prefetch) on the wave's path.
+struct RegSrc {
+    uint32_t x0, x1, x2;  // the next three entries, ~0u past the lane's last
+    uint32_t wb;
+    __device__ __forceinline__ explicit RegSrc(const TblSrc& s) : wb(s.wb) {
+        static_assert(kZhChunk <= 3u * 64u, "k_zh: a lane holds at most three blocks of a chunk");
+        x0 = s.nseg > 0u ? s.t[0] : ~0u;
+        x1 = s.nseg > 1u ? s.t[64] : ~0u;
+        x2 = s.nseg > 2u ? s.t[128] : ~0u;
+    }
+    __device__ __forceinline__ bool next(uint32_t&, uint32_t& bs, uint32_t& be) {
+        if (x0 == ~0u) return false;
+        bs = wb + (x0 & 0xFFFFu);
+        be = wb + (x0 >> 16);
+        x0 = x1;
+        x1 = x2;
+        x2 = ~0u;
+        return true;
+    }
+};
+__device__ __forceinline__ TblPeek tbl_peek(const RegSrc& src, uint32_t) {
+    return TblPeek{src.wb + (src.x0 & 0xFFFFu), src.wb + (src.x0 >> 16), src.x0 != ~0u};
+}
 struct OneSrc {  // a single block
     uint32_t bs0, be0;
     __device__ __forceinline__ bool next(uint32_t& j, uint32_t& bs, uint32_t& be) const {
@@ -1434,7 +1461,7 @@ __device__ __forceinline__ uint32_t zh_dp(const V& v, const DevImage& im, const 
 constexpr uint64_t kLtabOvf = 0x8000u;  // (bit 15 of field 0: no effect on a ring offset)
 template <bool WL, class Src>
 __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const uint64_t* __restrict__ erec,
-                             double* __restrict__ gbest, double* ring, const char* rb0, uint32_t lb, const Src& src) {
+                             double* __restrict__ gbest, double* ring, const char* rb0, uint32_t lb, Src src) {
     uint32_t j = 0, bs = 0, be = 0;
     if (!src.next(j, bs, be)) return 0;
     uint32_t key0 = 0, steps = 0, q = 0, c = 1, s = 0, bi = 0;
@@ -1841,7 +1868,14 @@ __device__ __forceinline__ void zh_chunk_main(const uint8_t* __restrict__ text, 
                               uint32_t* __restrict__ counters, uint32_t winw, uint32_t& nties, uint64_t* st) {
     const GrpZvT<A3> v{text, bls, wb};
     uint32_t steps;
+#ifndef JB_ZH_REGSRC
+#define JB_ZH_REGSRC 1
+#endif
+#if JB_ZH_REGSRC
+    if constexpr (A3) steps = zh_dp_a3<WL>(v, im, erec, gbest, ring, rb0, lb, RegSrc(src));
+#else
     if constexpr (A3) steps = zh_dp_a3<WL>(v, im, erec, gbest, ring, rb0, lb, src);
+#endif
     else steps = zh_dp(v, im, erec, gbest, ring, src);
     wave_sync();  // ring dead: its space takes the window's token bitmaps
     if (st) {
@@ -2189,6 +2223,7 @@ __global__ __launch_bounds__(NW * 64) JB_ZH_ATTR void k_zh(const uint8_t* __rest
     const uint32_t nwv = gridDim.x * (blockDim.x >> 6);
     uint32_t g = blockIdx.x * (blockDim.x >> 6) + wv;
     auto next_group = [&]() -> uint32_t {
+        if (nwv >= ngroups) return ngroups;  // every group was some wave's first: no claim (a round trip) needed
         uint32_t x = 0;
         if (lane == 0) x = atomicAdd(counters + CNT_WORK, 1u);
         return nwv + __builtin_amdgcn_readfirstlane(x);
