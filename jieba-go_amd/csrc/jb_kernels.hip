@@ -1160,8 +1160,9 @@ struct RegSrc {
         x1 = s.nseg > 1u ? s.t[64] : ~0u;
         x2 = s.nseg > 2u ? s.t[128] : ~0u;
     }
-    __device__ __forceinline__ bool next(uint32_t&, uint32_t& bs, uint32_t& be) {
+    __device__ __forceinline__ bool next(uint32_t& j, uint32_t& bs, uint32_t& be) {  // j: the block's ordinal + 1
         if (x0 == ~0u) return false;
+        j++;
         bs = wb + (x0 & 0xFFFFu);
         be = wb + (x0 >> 16);
         x0 = x1;
@@ -1459,14 +1460,20 @@ __device__ __forceinline__ uint32_t zh_dp(const V& v, const DevImage& im, const 
 // with q.  Length-table entries carry kLtabOvf for record 0 (an overflowed
 // record: dp_walk_rune folds that rune).
 constexpr uint64_t kLtabOvf = 0x8000u;  // (bit 15 of field 0: no effect on a ring offset)
+// A block with an edge past the ring (an overflowed record's walk found L > kZhRing) is
+// left at once, its ordinal set in redom, and the caller redoes it with zh_dp, which keeps
+// every best value in gbest.  So the loop has no global store: stores and loads pending
+// together on vmcnt made the compiler wait for vmcnt(0) at every wait in it (gfx9 counts
+// both on one counter, and their order is not known), which drained the record pairs
+// loaded steps ahead once per four steps.
 template <bool WL, class Src>
 __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const uint64_t* __restrict__ erec,
-                             double* __restrict__ gbest, double* ring, const char* rb0, uint32_t lb, Src src) {
+                             double* __restrict__ gbest, double* ring, const char* rb0, uint32_t lb, Src src,
+                             uint32_t& redom) {
     uint32_t j = 0, bs = 0, be = 0;
     if (!src.next(j, bs, be)) return 0;
-    uint32_t key0 = 0, steps = 0, q = 0, c = 1, s = 0, bi = 0;
+    uint32_t steps = 0, q = 0, c = 1, s = 0, bi = 0;
     uint64_t lc = 0;
-    bool longm = false;
     // Slots before a block (or before the text: erec has kErecPad slots of padding in
     // front) are garbage that `more` masks at the use.
     uint64_t xl = 0, xh = 0, yl = 0, yh = 0;
@@ -1480,7 +1487,6 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
         return *reinterpret_cast<double*>(const_cast<char*>(rb0) + ring_off(cs, lb));
     };
     auto setup = [&]() __attribute__((always_inline)) {  // (re)start at the last rune of [bs, be)
-        key0 = be / 3u;
         q = be - 3u;
         c = 1;
         s = q / 3u;
@@ -1550,14 +1556,13 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
         bool redo = false;
         if (lc & kLtabOvf) {  // overflowed record (rare)
             DpFold f;
-            dp_walk_rune(v, im, q, be, f, c, ring, longm, gbest, key0);
+            dp_walk_rune(v, im, q, be, f, c, ring, false, gbest, 0u);
             f.finish();
             bLs = f.bestL << 9;
             bP = f.bestP;
             redo = f.redo;
         }
         ring_at(cs) = bP;
-        if (longm) gbest[key0 - c] = bP;
         v.bls[bi] = (uint8_t)(bLs >> 9);
         steps++;
         const bool restart = redo || !more;
@@ -1569,14 +1574,8 @@ __device__ uint32_t zh_dp_a3(const GrpZvT<true>& v, const DevImage& im, const ui
             ++c;
             return false;
         }
-        if (redo) {  // an edge past the ring: this block again, every best value kept in gbest
-            longm = true;
-            setup();
-            prime((P + 1) & 3, wn, ld_e(0), ld_e(2));  // (pre keeps the next block's records)
-            return false;
-        }
+        if (redo) redom |= 1u << (j - 1u);  // an edge past the ring: the caller redoes this block
         if (!src.next(j, bs, be)) return true;
-        longm = false;
         setup();
         prime((P + 1) & 3, wn, pre, pre0);  // the next step is the next kind
         return false;
@@ -1871,12 +1870,22 @@ __device__ __forceinline__ void zh_chunk_main(const uint8_t* __restrict__ text, 
 #ifndef JB_ZH_REGSRC
 #define JB_ZH_REGSRC 1
 #endif
+    if constexpr (A3) {
+        uint32_t redom = 0;
 #if JB_ZH_REGSRC
-    if constexpr (A3) steps = zh_dp_a3<WL>(v, im, erec, gbest, ring, rb0, lb, RegSrc(src));
+        steps = zh_dp_a3<WL>(v, im, erec, gbest, ring, rb0, lb, RegSrc(src), redom);
 #else
-    if constexpr (A3) steps = zh_dp_a3<WL>(v, im, erec, gbest, ring, rb0, lb, src);
+        steps = zh_dp_a3<WL>(v, im, erec, gbest, ring, rb0, lb, src, redom);
 #endif
-    else steps = zh_dp(v, im, erec, gbest, ring, src);
+        while (redom) {  // (rare) blocks with an edge past the ring, best values in gbest
+            const uint32_t k = (uint32_t)__builtin_ctz(redom);
+            redom &= redom - 1u;
+            const uint32_t x = src.t[k * 64u];
+            steps += zh_dp(v, im, erec, gbest, ring, OneSrc{wb + (x & 0xFFFFu), wb + (x >> 16)});
+        }
+    } else {
+        steps = zh_dp(v, im, erec, gbest, ring, src);
+    }
     wave_sync();  // ring dead: its space takes the window's token bitmaps
     if (st) {
         const uint64_t t = __builtin_amdgcn_s_memtime();
