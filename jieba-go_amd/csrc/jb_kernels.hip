@@ -394,7 +394,7 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
                                                    uint64_t* __restrict__ erec, uint32_t* __restrict__ tile4,
                                                    uint64_t* __restrict__ alnum16, uint32_t* __restrict__ sbits,
                                                    uint32_t* __restrict__ ebits, uint32_t diag,
-                                                   uint64_t* __restrict__ dbg) {
+                                                   uint64_t* __restrict__ dbg, uint32_t split) {
     // LDS: 20.2 KB, so that 8 workgroups fit a CU (160 KB).  The staged text is
     // dead once the entries are decoded; the entry cells/records reuse its bytes.
     __shared__ __attribute__((aligned(16))) uint8_t s_raw[kMwLds];
@@ -412,7 +412,12 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
 #endif
     uint64_t c0 = stamps ? __builtin_amdgcn_s_memtime() : 0, c1 = 0, c2 = 0, c3 = 0, c0b = 0, c1b = 0;
     uint32_t trips = 0;
-    const uint64_t t0 = (uint64_t)blockIdx.x * kTileBytes;
+    // split 1 (small batches, fewer tiles than CUs): two workgroups per tile; both run the
+    // tile's phases 1 and 2 (their stores are the same values), and each walks and writes the
+    // records of half of the tile's entries, by entry index (the walk list's order comes from
+    // LDS atomics, so it differs between the two and cannot be what splits the work)
+    const uint32_t tile = blockIdx.x >> split, half = blockIdx.x & split;
+    const uint64_t t0 = (uint64_t)tile * kTileBytes;
     // The prologue's global loads (the staged text, the tile's document words and the
     // lane's window words for M below) are all issued before any is waited on: as a
     // staging loop and separate stores they were four round trips in a row.
@@ -571,10 +576,10 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     if (nbytes < p0 + 16) valid = nbytes > p0 ? ((1u << (uint32_t)(nbytes - p0)) - 1u) << 4 : 0u;
     const uint32_t bs = ~covered & valid & ((uint32_t)M | (hanb ^ (hanb << 1)));
     const uint32_t bmask = (bs >> 4) & 0xFFFFu, zmask = ((bs & hanb) >> 4) & 0xFFFFu;
-    __builtin_nontemporal_store(bmask | (zmask << 16), lanemask + blockIdx.x * 256u + threadIdx.x);  // (read on other XCDs)
+    __builtin_nontemporal_store(bmask | (zmask << 16), lanemask + tile * 256u + threadIdx.x);  // (read on other XCDs)
     uint32_t tot;
     block_scan_u32(__popc(bmask) | (__popc(zmask) << 16), lds, &tot);
-    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = make_uint2(tot & 0xFFFFu, tot >> 16);
+    if (threadIdx.x == 0) tile_cnt[tile] = make_uint2(tot & 0xFFFFu, tot >> 16);
     if (stamps) c1 = __builtin_amdgcn_s_memtime();
 
     // ---- (2) Han rune entries of the tile, in text order ---------------------------
@@ -739,6 +744,8 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         }
         if (!go) {
             s_c[i] = r1;
+        } else if (split && (i >= (nent >> 1)) != (half != 0u)) {
+            // (the other workgroup walks it)
         } else {
 #if JB_MW_SORT
             // Walks whose first probes fall in one 128-byte line of cells go next to each
@@ -758,7 +765,7 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         }
     }
     const int any4 = __syncthreads_or(has4);  // (also the barrier after the run links)
-    if (threadIdx.x == 0) tile4[blockIdx.x] = any4 ? 1u : 0u;  // k_zh: general rune stepping near this tile
+    if (threadIdx.x == 0) tile4[tile] = any4 ? 1u : 0u;  // k_zh: general rune stepping near this tile
 #if JB_MW_SORT
     if (threadIdx.x < 64u) {  // bucket offsets: wave 0, a bucket per lane
         const uint32_t h = s_hist[threadIdx.x];
@@ -876,10 +883,13 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     __syncthreads();
     // records out in entry (= text) order: consecutive lanes, mostly consecutive slots
     // (non-temporal: k_zh reads them on another XCD; kept out of this L2, where the trie's hot lines live)
-    for (uint32_t i = threadIdx.x; i < nent; i += 256u)
-        __builtin_nontemporal_store(s_c[i], erec + (t0 + ent_pos(s_e[i])) / 3u);
-    if (stamps && (threadIdx.x & 63u) == 0) {  // per-wave phase clocks, summed on the host
-        uint64_t* o = dbg + ((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * 8u;
+    {
+        const uint32_t e0 = split && half ? nent >> 1 : 0u, e1 = split && !half ? nent >> 1 : nent;
+        for (uint32_t i = e0 + threadIdx.x; i < e1; i += 256u)
+            __builtin_nontemporal_store(s_c[i], erec + (t0 + ent_pos(s_e[i])) / 3u);
+    }
+    if (stamps && half == 0u && (threadIdx.x & 63u) == 0) {  // per-wave phase clocks, summed on the host
+        uint64_t* o = dbg + ((uint64_t)tile * 4u + (threadIdx.x >> 6)) * 8u;
         o[0] = c1 - c0;
         o[1] = c2 - c1;
         o[2] = c3 - c2;
@@ -5660,9 +5670,11 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     JB_TIMED(K_DOCBITS, hipLaunchKernelGGL(k_docbits, dim3(std::max(1u, (std::max(ndocs, nttiles) + 255) / 256)),
                                            dim3(256), 0, stream, d_doc_off, ndocs, nbytes, w.docbits, w.counters,
                                            reinterpret_cast<uint64_t*>(w.ttile_cnt), nttiles));
-    JB_TIMED(K_MARK_WALK, hipLaunchKernelGGL(k_mark_walk, dim3(ntiles), dim3(256), 0, stream, d_text, nbytes,
+    // a batch with fewer tiles than CUs: two workgroups per tile (k_mark_walk's split)
+    const uint32_t mws = (lc.mw_split > 0 || (lc.mw_split < 0 && ntiles <= lc.ncu)) ? 1u : 0u;
+    JB_TIMED(K_MARK_WALK, hipLaunchKernelGGL(k_mark_walk, dim3(ntiles << mws), dim3(256), 0, stream, d_text, nbytes,
                                              w.docbits, im, w.lanemask, w.tile_cnt, w.erec + kErecPad,
-                                             w.tile4, w.alnum16, w.sbits, w.ebits, diag, w.dbg_walk));
+                                             w.tile4, w.alnum16, w.sbits, w.ebits, diag, w.dbg_walk, mws));
 #define JB_ZH_LAUNCH(H, N)                                                                                      \
     JB_TIMED(K_ZH, hipLaunchKernelGGL((k_zh<H, N>), dim3(grid_zh), dim3((N) * 64), 0, stream, d_text, nbytes,       \
                                       w.lanemask, w.tile_cnt, w.tile4, w.counters, im, w.erec + kErecPad, w.gbl,     \
