@@ -717,7 +717,7 @@ static int init_launch_cfg(Device* d) {
     if (wide < -1 || wide > 1) return fail(JB_EINVAL, "JB_ZH_WIDE=%d: want -1 (by batch size), 0 or 1", wide);
     lc.zh_wide = wide;
     const int mws = env_int("JB_MW_SPLIT", -1);
-    if (mws < -1 || mws > 1) return fail(JB_EINVAL, "JB_MW_SPLIT=%d: want -1 (by tile count), 0 or 1", mws);
+    if (mws < -1 || mws > 3) return fail(JB_EINVAL, "JB_MW_SPLIT=%d: want -1 (by tile count) or 0-3", mws);
     lc.mw_split = mws;
     const int grp = env_int("JB_ZH_GROUP", 0);
     if (grp != 0) {

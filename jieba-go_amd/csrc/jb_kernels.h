@@ -142,8 +142,8 @@ struct LaunchCfg {
                              // (JB_NZ_FUSE_MIB: 4 default, 0 never)
     uint32_t long_wait_ticks;  // k_long: a phase wait gives up after this many 100 MHz ticks without progress
                                // (JB_LONG_WAIT_US x 100; default 20 s)
-    int32_t mw_split;        // k_mark_walk: two workgroups per tile, each walking half of its walk list
-                             // (JB_MW_SPLIT: -1 when the batch has at most one tile per CU, 0 never, 1 always)
+    int32_t mw_split;        // k_mark_walk: 2^s workgroups per tile, each walking its share of the entries
+                             // (JB_MW_SPLIT: -1 = 1 when the batch has at most one tile per CU, else 0; 0-3 fixed)
 };
 
 // k_zh's group split: g1 groups of grp bytes, then groups of *sgrp bytes to the end.

@@ -412,11 +412,11 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
 #endif
     uint64_t c0 = stamps ? __builtin_amdgcn_s_memtime() : 0, c1 = 0, c2 = 0, c3 = 0, c0b = 0, c1b = 0;
     uint32_t trips = 0;
-    // split 1 (small batches, fewer tiles than CUs): two workgroups per tile; both run the
+    // split s > 0 (small batches, fewer tiles than CUs): 2^s workgroups per tile; all run the
     // tile's phases 1 and 2 (their stores are the same values), and each walks and writes the
-    // records of half of the tile's entries, by entry index (the walk list's order comes from
-    // LDS atomics, so it differs between the two and cannot be what splits the work)
-    const uint32_t tile = blockIdx.x >> split, half = blockIdx.x & split;
+    // records of its 2^-s of the tile's entries, by entry index (the walk list's order comes
+    // from LDS atomics, so it differs between them and cannot be what splits the work)
+    const uint32_t tile = blockIdx.x >> split, part = blockIdx.x & ((1u << split) - 1u);
     const uint64_t t0 = (uint64_t)tile * kTileBytes;
     // The prologue's global loads (the staged text, the tile's document words and the
     // lane's window words for M below) are all issued before any is waited on: as a
@@ -744,8 +744,8 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
         }
         if (!go) {
             s_c[i] = r1;
-        } else if (split && (i >= (nent >> 1)) != (half != 0u)) {
-            // (the other workgroup walks it)
+        } else if (i < ((nent * part) >> split) || i >= ((nent * (part + 1u)) >> split)) {
+            // (another workgroup of the tile walks it)
         } else {
 #if JB_MW_SORT
             // Walks whose first probes fall in one 128-byte line of cells go next to each
@@ -884,11 +884,11 @@ __global__ __launch_bounds__(256) JB_MW_ATTR void k_mark_walk(const uint8_t* __r
     // records out in entry (= text) order: consecutive lanes, mostly consecutive slots
     // (non-temporal: k_zh reads them on another XCD; kept out of this L2, where the trie's hot lines live)
     {
-        const uint32_t e0 = split && half ? nent >> 1 : 0u, e1 = split && !half ? nent >> 1 : nent;
+        const uint32_t e0 = (nent * part) >> split, e1 = (nent * (part + 1u)) >> split;
         for (uint32_t i = e0 + threadIdx.x; i < e1; i += 256u)
             __builtin_nontemporal_store(s_c[i], erec + (t0 + ent_pos(s_e[i])) / 3u);
     }
-    if (stamps && half == 0u && (threadIdx.x & 63u) == 0) {  // per-wave phase clocks, summed on the host
+    if (stamps && part == 0u && (threadIdx.x & 63u) == 0) {  // per-wave phase clocks, summed on the host
         uint64_t* o = dbg + ((uint64_t)tile * 4u + (threadIdx.x >> 6)) * 8u;
         o[0] = c1 - c0;
         o[1] = c2 - c1;
@@ -5671,7 +5671,7 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
                                            dim3(256), 0, stream, d_doc_off, ndocs, nbytes, w.docbits, w.counters,
                                            reinterpret_cast<uint64_t*>(w.ttile_cnt), nttiles));
     // a batch with fewer tiles than CUs: two workgroups per tile (k_mark_walk's split)
-    const uint32_t mws = (lc.mw_split > 0 || (lc.mw_split < 0 && ntiles <= lc.ncu)) ? 1u : 0u;
+    const uint32_t mws = lc.mw_split >= 0 ? (uint32_t)lc.mw_split : (ntiles <= lc.ncu ? 1u : 0u);
     JB_TIMED(K_MARK_WALK, hipLaunchKernelGGL(k_mark_walk, dim3(ntiles << mws), dim3(256), 0, stream, d_text, nbytes,
                                              w.docbits, im, w.lanemask, w.tile_cnt, w.erec + kErecPad,
                                              w.tile4, w.alnum16, w.sbits, w.ebits, diag, w.dbg_walk, mws));
