@@ -1788,12 +1788,13 @@ __device__ bool zh_fwd_lane(const V& v, const DevImage& im, const Src& src, E& e
 }
 
 // The same for an all-3-byte window (the common case), leaner: a piece's length is
-// read by slot ((q - wb) / 3 kept beside q, no division), and each token ORs its two bits
+// read by slot ((q - wb) / 3 kept beside q, no division), the lane's blocks come from
+// registers (RegSrc: a block change is no LDS loop), and each token ORs its two bits
 // straight into the wave's LDS bitmaps (two LDS atomics, no register state to flush
 // when the word changes).  Runs of single-rune pieces go to the run list as before
 // (a run of one rune is "S", its own token).
 template <bool HMM, class Src>
-__device__ __forceinline__ bool zh_fwd_a3(const GrpZvT<true>& v, const DevImage& im, const Src& src,
+__device__ __forceinline__ bool zh_fwd_a3(const GrpZvT<true>& v, const DevImage& im, Src src,
                                           uint32_t* sb, uint32_t* eb, LdsEmitter& le, RunList* rl) {
     const uint32_t w0 = v.wb >> 5;
     auto token = [&](uint32_t a, uint32_t b) __attribute__((always_inline)) {
@@ -1922,7 +1923,11 @@ __device__ __forceinline__ void zh_chunk_main(const uint8_t* __restrict__ text, 
         if constexpr (A3) {
             if (lane == 0u) *nrun = 0u;
             wave_sync();
+#if JB_ZH_REGSRC
+            ok = zh_fwd_a3<HMM>(v, im, RegSrc(src), sb, eb, le, &rl);
+#else
             ok = zh_fwd_a3<HMM>(v, im, src, sb, eb, le, &rl);
+#endif
             wave_sync();
             const uint32_t nr = min(*nrun, kZhRuns * 64u);  // the pool's entries k = lane + 64 r are this lane's
             rl.n = nr > lane ? (nr - lane + 63u) / 64u : 0u;
