@@ -596,6 +596,27 @@ def test_synthetic_golden_vectors(syn_golden):
             tk.close()
 
 
+@pytest.mark.parametrize("split", ["-1", "0", "1", "2"])
+def test_repeat_runs_identical(syn_small, split):
+    """The same batch cut several times gives the same tokens every time (and the oracle's):
+    k_mark_walk with 1, 2 or 4 workgroups per tile (JB_MW_SPLIT; -1 = 2 for a batch of at most
+    one tile per CU, as here), whose entries are shared out by index.  A split by walk-list
+    position, whose order comes from LDS atomics, once walked some entries twice and some never,
+    which only showed as two runs of one batch disagreeing."""
+    dp, ep, s = syn_small
+    tk, o = _pair_env(dp, ep, {"JB_MW_SPLIT": split})
+    try:
+        buf, off, _ = s.corpus(synth.KIND_SENTENCES, 51, max_docs=3000, target_bytes=512 << 10)
+        for hmm in (False, True):
+            _cmp_batch(tk, o, buf, off, hmm, f"split {split} hmm {hmm}")
+            first = tk.cut_batch(buf, off, hmm)
+            for _ in range(3):
+                again = tk.cut_batch(buf, off, hmm)
+                assert all(np.array_equal(a, b) for a, b in zip(first, again)), f"split {split} hmm {hmm}"
+    finally:
+        tk.close()
+
+
 def test_cut_batch_into_caller_arrays(small):
     """jb_cut_batch_into: same spans as jb_cut_batch; too-small arrays give
     JB_ELIMIT with the needed count, and the binding retries."""
