@@ -860,6 +860,9 @@ static int launch_pipeline_(Device* d, const Work& w, const uint8_t* d_text, uin
         fprintf(stderr, "[jb] k_zh Viterbi forward half per chunk: longest lane %.2f runes, longest single run %.2f, "
                         "the wave's runes split evenly %.2f\n",
                 a[11] / (a[3] + 1e-9), a[12] / (a[3] + 1e-9), a[13] / (a[3] + 1e-9));
+        fprintf(stderr, "[jb] k_zh DP per chunk: longest lane %.2f runes, longest single block %.2f, the wave's runes "
+                        "split evenly %.2f\n",
+                a[5] / (a[3] + 1e-9), a[14] / (a[3] + 1e-9), a[4] / (64.0 * (a[3] + 1e-9)));
         HIPCHK(hipMemsetAsync(d->w.dbg, 0, (size_t)nwv * 128, s));
         const uint64_t nww = (nbytes + kTileBytes - 1) / kTileBytes * 4;
         std::vector<uint64_t> sw(nww * 8);

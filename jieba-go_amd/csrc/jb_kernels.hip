@@ -2232,7 +2232,8 @@ __global__ __launch_bounds__(NW * 64) JB_ZH_ATTR void k_zh(const uint8_t* __rest
     __syncthreads();
     // diagnostic per-wave clocks (JB_ABLATE bit 8): [0] setup [1] DP [2] forward+Viterbi+flush [3] chunks
     // [4] sum of lane DP steps [5] sum of per-chunk max lane DP steps [6] blocks past the window [7] scratch
-    uint64_t stv[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // [8] forward walk [9] Viterbi forward half
+    uint64_t stv[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // [8] forward walk [9] Viterbi forward half
+    // [14] sum over chunks of the chunk's longest in-window block (runes): no dealing takes the DP below it
     // [10] lanes' summed Viterbi run runes [11] 64 x max ... (Viterbi lane use)
 #if JB_STAMPS
     uint64_t* st = (diag & 0x100u) ? stv : nullptr;
@@ -2363,6 +2364,14 @@ __global__ __launch_bounds__(NW * 64) JB_ZH_ATTR void k_zh(const uint8_t* __rest
             wave_sync();
             const TblSrc src{tbl + lane, (nin + 63u) >> 6, wb};
             if (st) {
+                uint32_t lb3 = 0;
+#pragma unroll
+                for (int i = 0; i < 3; i++) lb3 = max(lb3, in[i] ? (bei[i] - bsi[i]) / 3u : 0u);
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) lb3 = max(lb3, (uint32_t)__shfl_xor((int)lb3, d, 64));
+                stv[14] += lb3;
+            }
+            if (st) {
                 const uint64_t t = __builtin_amdgcn_s_memtime();
                 stv[0] += t - stv[7];
                 stv[7] = t;
@@ -2441,6 +2450,7 @@ __global__ __launch_bounds__(NW * 64) JB_ZH_ATTR void k_zh(const uint8_t* __rest
             o[11] = stv[11];
             o[12] = stv[12];
             o[13] = stv[13];
+            o[14] = stv[14];
             o[0] = stv[0];
             o[1] = stv[1];
             o[2] = stv[2];
