@@ -69,6 +69,12 @@ inline uint32_t zh_group_for(uint64_t nbytes) { return nbytes < kZhSmallBatch ? 
 // table (up to kZhWtab entries of wtab1) for the DP's weight reads
 constexpr uint32_t kZhWgWide = 16;
 constexpr uint32_t kZhWtab = 5120;
+// ... of which k_zh's wide form holds up to kZhWtabWide (its LDS also holds the per-wave slots
+// and block tables, which larger groups make larger)
+#ifndef JB_ZH_WTAB
+#define JB_ZH_WTAB 5120
+#endif
+constexpr uint32_t kZhWtabWide = JB_ZH_WTAB;
 
 // Per-call device workspace, sized for `nbytes` of text.
 struct Work {

@@ -953,8 +953,16 @@ __device__ uint32_t block_end_at(const uint32_t* __restrict__ lanemask, const ui
 // past the group window (kZhWin bytes) runs the same code on global memory.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kZhRing = 8;                            // LDS best ring per lane (runes)
-constexpr uint32_t kZhWin = kZhGroupBytes + 1024u;         // window: group span + slack for the last blocks
-constexpr uint32_t kZhChunk = 192;                         // blocks ranked together (3 per lane)
+#ifndef JB_ZH_SLACK
+#define JB_ZH_SLACK 1024
+#endif
+#ifndef JB_ZH_CHUNK
+#define JB_ZH_CHUNK 192
+#endif
+constexpr uint32_t kZhWin = kZhGroupBytes + JB_ZH_SLACK;  // window: group span + slack for the last blocks
+constexpr uint32_t kZhChunk = JB_ZH_CHUNK;                // blocks ranked together (kZhPer per lane)
+constexpr uint32_t kZhPer = kZhChunk / 64u;
+static_assert(kZhChunk % 64u == 0u && kZhPer >= 1u && kZhPer <= 4u, "k_zh: 1-4 blocks per lane and chunk");
 // (a block whose end lm_collect did not find spans its round and the lookahead round
 // after it, so it is over 1 KiB long: a group has at most one per KiB, plus one)
 static_assert(kZhGroupBytes / 1024u + 1u <= 64u, "k_zh: a chunk's unresolved blocks fit the wave's 64 hist words");
@@ -968,7 +976,7 @@ constexpr uint32_t kZhBlBytes = kZhWin / 3u + 4u;
 // LDS of the wide form: per wave the slots, ring, block table and histogram, plus the
 // length table and the weight table; all of it within one CU's 160 KiB
 static_assert(kZhWgWide * (((kZhBlBytes + 15u) & ~15u) + 8u * kZhRing * 64u + 4u * kZhChunk + 256u + 4u) + 2048u +
-                      8u * kZhWtab <= 163840u,
+                      8u * kZhWtabWide <= 163840u,
               "k_zh wide form: LDS");
 static_assert(kZhWin < 65536u, "window offsets are packed in 16 bits");
 // k_zh stages a group's lane-mask words plus two 64-word rounds after them (lm_collect reads
@@ -1162,27 +1170,25 @@ __device__ __forceinline__ TblPeek tbl_peek(const TblSrc& src, uint32_t j) {
 // nearly every DP step has some lane changing block, and as TblSrc loops those were two
 // LDS round trips (next, then the peek for the prefetch) on the wave's path.
 struct RegSrc {
-    uint32_t x0, x1, x2;  // the next three entries, ~0u past the lane's last
+    uint32_t x[kZhPer];  // the lane's next entries, ~0u past its last
     uint32_t wb;
     __device__ __forceinline__ explicit RegSrc(const TblSrc& s) : wb(s.wb) {
-        static_assert(kZhChunk <= 3u * 64u, "k_zh: a lane holds at most three blocks of a chunk");
-        x0 = s.nseg > 0u ? s.t[0] : ~0u;
-        x1 = s.nseg > 1u ? s.t[64] : ~0u;
-        x2 = s.nseg > 2u ? s.t[128] : ~0u;
+#pragma unroll
+        for (uint32_t i = 0; i < kZhPer; i++) x[i] = s.nseg > i ? s.t[64u * i] : ~0u;
     }
     __device__ __forceinline__ bool next(uint32_t& j, uint32_t& bs, uint32_t& be) {  // j: the block's ordinal + 1
-        if (x0 == ~0u) return false;
+        if (x[0] == ~0u) return false;
         j++;
-        bs = wb + (x0 & 0xFFFFu);
-        be = wb + (x0 >> 16);
-        x0 = x1;
-        x1 = x2;
-        x2 = ~0u;
+        bs = wb + (x[0] & 0xFFFFu);
+        be = wb + (x[0] >> 16);
+#pragma unroll
+        for (uint32_t i = 0; i + 1u < kZhPer; i++) x[i] = x[i + 1u];
+        x[kZhPer - 1u] = ~0u;
         return true;
     }
 };
 __device__ __forceinline__ TblPeek tbl_peek(const RegSrc& src, uint32_t) {
-    return TblPeek{src.wb + (src.x0 & 0xFFFFu), src.wb + (src.x0 >> 16), src.x0 != ~0u};
+    return TblPeek{src.wb + (src.x[0] & 0xFFFFu), src.wb + (src.x[0] >> 16), src.x[0] != ~0u};
 }
 struct OneSrc {  // a single block
     uint32_t bs0, be0;
@@ -1276,7 +1282,7 @@ __device__ __forceinline__ void dp_walk_rune(const V& v, const DevImage& im, uin
 // step kept that unit saturated; LDS reads take the LDS pipe instead.
 typedef const __attribute__((address_space(1))) char gchar;  // global memory, whatever inference concludes
 typedef const __attribute__((address_space(3))) char lchar;  // LDS
-__shared__ __attribute__((aligned(32))) double s_wt[kZhWtab];  // wtab1 in LDS (k_zh<.., kZhWgWide>: one copy per CU)
+__shared__ __attribute__((aligned(32))) double s_wt[kZhWtabWide];  // wtab1 in LDS (k_zh<.., kZhWgWide>: one copy per CU)
 template <bool WL = false>
 __device__ __forceinline__ void rec_weights(const DevImage& im, uint64_t rc, double w[4]) {
     gchar* const wb = (gchar*)im.wtab1;
@@ -2313,10 +2319,10 @@ __global__ __launch_bounds__(NW * 64) JB_ZH_ATTR void k_zh(const uint8_t* __rest
             // not find in its two rounds (at least 1 KiB long; they may still end inside the
             // window) are cut one by one after the chunk: their starts wait in the wave's
             // hist words meanwhile, so nothing of them stays in registers across the DP.
-            uint32_t bsi[3], bei[3];
-            bool in[3], out[3];
+            uint32_t bsi[kZhPer], bei[kZhPer];
+            bool in[kZhPer], out[kZhPer];
 #pragma unroll
-            for (int i = 0; i < 3; i++) {
+            for (int i = 0; i < (int)kZhPer; i++) {
                 const uint32_t k = lane + 64u * (uint32_t)i;
                 const uint32_t x = k < m ? tbl[k] : 0x80000000u;
                 in[i] = !(x & 0x80000000u);
@@ -2328,9 +2334,9 @@ __global__ __launch_bounds__(NW * 64) JB_ZH_ATTR void k_zh(const uint8_t* __rest
             hist[lane] = 0u;
             wave_sync();
             for (uint32_t k = lane; k < kZhChunk; k += 64u) tbl[k] = ~0u;
-            uint32_t bkt[3], idx[3];
+            uint32_t bkt[kZhPer], idx[kZhPer];
 #pragma unroll
-            for (int i = 0; i < 3; i++) {
+            for (int i = 0; i < (int)kZhPer; i++) {
                 bkt[i] = min(63u, (bei[i] - bsi[i]) >> 2);
                 idx[i] = in[i] ? atomicAdd(hist + bkt[i], 1u) : 0u;
             }
@@ -2344,7 +2350,7 @@ __global__ __launch_bounds__(NW * 64) JB_ZH_ATTR void k_zh(const uint8_t* __rest
             wave_sync();
             uint32_t nin = 0;
 #pragma unroll
-            for (int i = 0; i < 3; i++) {
+            for (int i = 0; i < (int)kZhPer; i++) {
                 nin += (uint32_t)__popcll(__ballot(in[i]));
                 if (in[i]) {
                     const uint32_t r = hist[bkt[i]] + idx[i];
@@ -2356,7 +2362,7 @@ __global__ __launch_bounds__(NW * 64) JB_ZH_ATTR void k_zh(const uint8_t* __rest
             wave_sync();
             uint32_t nout = 0;  // (hist is free once the blocks are dealt)
 #pragma unroll
-            for (int i = 0; i < 3; i++) {
+            for (int i = 0; i < (int)kZhPer; i++) {
                 const uint64_t ob = __ballot(out[i]);
                 if (out[i]) hist[nout + __builtin_amdgcn_mbcnt_hi((uint32_t)(ob >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ob, 0u))] = bsi[i];
                 nout += (uint32_t)__popcll(ob);
@@ -2366,7 +2372,7 @@ __global__ __launch_bounds__(NW * 64) JB_ZH_ATTR void k_zh(const uint8_t* __rest
             if (st) {
                 uint32_t lb3 = 0;
 #pragma unroll
-                for (int i = 0; i < 3; i++) lb3 = max(lb3, in[i] ? (bei[i] - bsi[i]) / 3u : 0u);
+                for (int i = 0; i < (int)kZhPer; i++) lb3 = max(lb3, in[i] ? (bei[i] - bsi[i]) / 3u : 0u);
 #pragma unroll
                 for (int d = 32; d >= 1; d >>= 1) lb3 = max(lb3, (uint32_t)__shfl_xor((int)lb3, d, 64));
                 stv[14] += lb3;
@@ -5673,7 +5679,7 @@ hipError_t run_pipeline(const DevImage& im, const Work& w, const uint8_t* d_text
     const uint64_t ngroups = zh_tail_groups(nbytes, grp, lc, &g1, &sgrp);
     // the wide form (16 waves per workgroup, weights in LDS) for batches in 6 KiB groups whose
     // weight table fits; JB_ZH_WIDE (lc.zh_wide) forces either form
-    const bool wide = im.nw1 <= kZhWtab && (lc.zh_wide > 0 || (lc.zh_wide < 0 && grp == kZhGroupBytes));
+    const bool wide = im.nw1 <= kZhWtabWide && (lc.zh_wide > 0 || (lc.zh_wide < 0 && grp == kZhGroupBytes));
     const uint32_t nw = wide ? kZhWgWide : 4u;
     const uint32_t grid_zh = (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>((wide ? lc.zh_waves_wide : lc.zh_waves) / nw, (ngroups + nw - 1) / nw));
