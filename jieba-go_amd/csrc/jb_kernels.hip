@@ -102,6 +102,16 @@ struct Emitter {
         at(b - 1u);
         e |= 1u << ((b - 1u) & 31u);
     }
+    // start / end bits sm, em_ of bitmap word w
+    __device__ __forceinline__ void bits(uint32_t w, uint32_t sm, uint32_t em_) {
+        if (!(sm | em_)) return;
+        if (w != word) {
+            flush();
+            word = w;
+        }
+        s |= sm;
+        e |= em_;
+    }
 };
 
 // The same for a wave's LDS token bitmaps: word index = global word - w0.
@@ -2054,9 +2064,69 @@ __device__ __forceinline__ uint32_t nz_keep(uint32_t base, uint32_t bs, uint32_t
 }
 // W: the bytes tokenized per round of loads (64 with the lane's 80-byte window; 48 with a
 // 64-byte one)
+__device__ __forceinline__ uint32_t alnum_mask16(uint4 x);
+// Bit k for each byte k of the 16 bytes x: >= 0x80 (hi), an ASCII space (sp: 0x09-0x0D, 0x20)
+__device__ __forceinline__ void hi_space_mask16(uint4 x, uint32_t& hi, uint32_t& sp) {
+    const uint32_t v[4] = {x.x, x.y, x.z, x.w};
+    hi = sp = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t h = (v[j] & 0x80808080u) >> 7;
+        const uint32_t s = (jb_bytes_between(v[j], 0x08u, 0x0Eu) | jb_bytes_between(v[j], 0x1Fu, 0x21u)) >> 7;
+        hi |= ((h * 0x204081u) >> 21 & 0xFu) << (4 * j);
+        sp |= ((s * 0x204081u) >> 21 & 0xFu) << (4 * j);
+    }
+}
 template <uint32_t W>
 __device__ void nonzh_block(const uint8_t* __restrict__ text, uint32_t bs, uint32_t be, Emitter& em, uint8_t* buf) {
-    static_assert(W == 64u || W == 48u, "window");
+    static_assert(W == 64u, "the 80-byte window");
+    const uint32_t a0 = bs & ~15u;
+    if (be <= a0 + 64u) {
+        // The block lies in one round of four loads: its tokens come from bit masks over
+        // those 64 bytes (the byte-at-a-time walk below: k_nonzh 0.165 -> 0.139 ms at 1 GiB).
+        // alnum runs -> one token each; other ASCII bytes -> one token each unless a space;
+        // runes from bytes >= 0x80 (never alnum, never ASCII) are decoded one by one.
+        uint4 c[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            c[k] = (a0 + 16u * k < be) ? *reinterpret_cast<const uint4*>(text + a0 + 16u * k) : make_uint4(0, 0, 0, 0);
+        const uint32_t lo = bs - a0, hb = be - a0;  // the block's bytes: [lo, hb) of the 64, hb in 1..64
+        const uint64_t inb = (hb == 64u ? ~0ull : (1ull << hb) - 1ull) & ~((1ull << lo) - 1ull);
+        uint64_t A = 0, H = 0, S = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            uint32_t h, s;
+            hi_space_mask16(c[k], h, s);
+            A |= (uint64_t)alnum_mask16(c[k]) << (16 * k);
+            H |= (uint64_t)h << (16 * k);
+            S |= (uint64_t)s << (16 * k);
+        }
+        A &= inb;
+        if (!A) return;  // alnum.FindAllIndex found nothing -> no tokens (:290-293)
+        H &= inb;
+        const uint64_t O = inb & ~(A | H | S);  // one-byte tokens
+        uint64_t st = (A & ~(A << 1)) | O, en = (A & ~(A >> 1)) | O;
+        if (H) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) reinterpret_cast<uint4*>(buf)[k] = c[k];
+            do {
+                const uint32_t p = (uint32_t)__builtin_ctzll(H);
+                uint32_t r;
+                const uint32_t w = jb_decode(lds4(buf, p), min(4u, hb - p), &r);  // (lds4 reads up to byte 66)
+                if (!jb_is_space(r)) {
+                    st |= 1ull << p;
+                    en |= 1ull << (p + w - 1u);
+                }
+                H &= p + w >= 64u ? 0ull : ~((1ull << (p + w)) - 1ull);
+            } while (H);
+        }
+        // 64 bits from a0 (a0 % 32 is 0 or 16) -> bitmap words a0 / 32 .. + 2
+        const uint32_t sh = a0 & 31u, w0 = a0 >> 5;
+        em.bits(w0, (uint32_t)st << sh, (uint32_t)en << sh);
+        em.bits(w0 + 1u, (uint32_t)((st << sh) >> 32), (uint32_t)((en << sh) >> 32));
+        if (sh) em.bits(w0 + 2u, (uint32_t)(st >> 48), (uint32_t)(en >> 48));
+        return;
+    }
     bool has = false;  // alnum.FindAllIndex found nothing -> no tokens (:290-293)
     for (uint32_t a = bs & ~15u; a < be && !has; a += 64u) {
         uint4 c[4];
@@ -2115,34 +2185,13 @@ __device__ __forceinline__ uint32_t alnum_mask16(uint4 x) {
     return m;
 }
 
-// The non-Han blocks whose first alnum byte lies in alnum16 word wi's 1 KiB (k_nonzh's unit).
+// The non-Han blocks whose first alnum byte lies in chunk c (text tx, lane mask lm).
 template <uint32_t W>
-__device__ __forceinline__ void nonzh_word(const uint8_t* __restrict__ text, uint32_t nbytes, uint32_t nch,
-                                           const uint32_t* __restrict__ lanemask, const uint2* __restrict__ tile_cnt,
-                                           uint32_t ntiles, const uint64_t* __restrict__ alnum16, uint32_t wi,
-                                           Emitter& em, uint8_t* buf) {
-    uint64_t a = alnum16[wi];
-    // the next alnum chunk's text and lane mask load while this one is cut
-    uint32_t cn = a ? wi * 64u + (uint32_t)__builtin_ctzll(a) : 0u;
-    uint4 txn = make_uint4(0, 0, 0, 0);
-    uint32_t lmn = 0;
-    if (a && cn < nch) {
-        txn = *reinterpret_cast<const uint4*>(text + cn * 16u);
-        lmn = lanemask[cn];
-    }
-    while (a) {
-        const uint32_t c = cn;
-        const uint4 tx = txn;
-        const uint32_t lm = lmn;
-        a &= a - 1ull;
-        if (c >= nch) break;  // (padding past the batch)
-        if (a) {
-            cn = wi * 64u + (uint32_t)__builtin_ctzll(a);
-            if (cn < nch) {
-                txn = *reinterpret_cast<const uint4*>(text + cn * 16u);
-                lmn = lanemask[cn];
-            }
-        }
+__device__ __forceinline__ void nonzh_chunk(const uint8_t* __restrict__ text, uint32_t nbytes,
+                                            const uint32_t* __restrict__ lanemask, const uint2* __restrict__ tile_cnt,
+                                            uint32_t ntiles, const uint64_t* __restrict__ alnum16, uint32_t c, uint4 tx,
+                                            uint32_t lm, Emitter& em, uint8_t* buf) {
+    {
         const uint32_t c0 = c * 16u;
         uint32_t A = alnum_mask16(tx);
         if (c0 + 16u > nbytes) A &= (1u << (nbytes - c0)) - 1u;
@@ -2178,6 +2227,55 @@ __device__ __forceinline__ void nonzh_word(const uint8_t* __restrict__ text, uin
             const uint32_t be = after ? c0 + (uint32_t)__builtin_ctz(after)
                                       : nz_block_end(lanemask, tile_cnt, ntiles, nbytes, c);
             nonzh_block<W>(text, bs, be, em, buf);
+        }
+    }
+}
+
+// k_nonzh's unit is a wave's 64 alnum16 words (64 KiB of text).  Their chunks with an
+// alnum byte (about 0.8 per KiB on C_syn, up to 8 in one word) are dealt to the
+// wave's lanes in order through an LDS list, kNzCap per round (two per lane, their
+// loads issued together): a lane per word instead made every wave as slow as its
+// busiest word's serial chain of dependent loads.
+constexpr uint32_t kNzCap = 128u;
+struct NzLds {
+    uint8_t win[256][80];          // the lanes' nonzh_block windows
+    uint32_t list[4][kNzCap];      // each wave's chunks of the round
+};
+template <uint32_t W>
+__device__ __forceinline__ void nonzh_waves(const uint8_t* __restrict__ text, uint32_t nbytes, uint32_t nch,
+                                            const uint32_t* __restrict__ lanemask, const uint2* __restrict__ tile_cnt,
+                                            uint32_t ntiles, const uint64_t* __restrict__ alnum16, uint32_t wave,
+                                            uint32_t nwaves, Emitter& em, NzLds& L) {
+    const uint32_t lane = threadIdx.x & 63u, nw = (nch + 63u) >> 6;
+    uint32_t* const list = L.list[threadIdx.x >> 6];
+    uint8_t* const buf = L.win[threadIdx.x];
+    for (uint32_t w0 = wave * 64u; w0 < nw; w0 += nwaves * 64u) {  // (uniform in the wave)
+        const uint32_t wi = w0 + lane;
+        uint64_t a = wi < nw ? alnum16[wi] : 0ull;
+        const uint32_t cnt = (uint32_t)__builtin_popcountll(a);
+        const uint32_t inc = wave_incl_scan(cnt);
+        const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
+        uint32_t pos = inc - cnt;  // this lane's next chunk's place in the wave's order
+        for (uint32_t r0 = 0; r0 < total; r0 += kNzCap) {
+            for (; a && pos < r0 + kNzCap; pos++, a &= a - 1ull) list[pos - r0] = wi * 64u + (uint32_t)__builtin_ctzll(a);
+            wave_sync();
+            const uint32_t m = min(kNzCap, total - r0);
+            uint32_t c[kNzCap / 64u], lm[kNzCap / 64u];
+            uint4 tx[kNzCap / 64u];
+#pragma unroll
+            for (uint32_t j = 0; j < kNzCap / 64u; j++) {
+                c[j] = lane + 64u * j < m ? list[lane + 64u * j] : ~0u;
+                tx[j] = make_uint4(0, 0, 0, 0);
+                lm[j] = 0;
+                if (c[j] < nch) {  // (chunks past the batch: padding)
+                    tx[j] = *reinterpret_cast<const uint4*>(text + c[j] * 16u);
+                    lm[j] = lanemask[c[j]];
+                }
+            }
+            wave_sync();  // the list is read before the next round writes it
+#pragma unroll
+            for (uint32_t j = 0; j < kNzCap / 64u; j++)
+                if (c[j] < nch) nonzh_chunk<W>(text, nbytes, lanemask, tile_cnt, ntiles, alnum16, c[j], tx[j], lm[j], em, buf);
         }
     }
 }
@@ -4178,19 +4276,20 @@ __global__ __launch_bounds__(256) void k_long_tail(const uint8_t* __restrict__ t
 
 // k_nonzh: cutNonZh (tokenizer.go:289-310) for exactly the non-Han blocks that hold
 // a [0-9A-Za-z] byte; every other non-Han block has no tokens (:290-293).  An alnum
-// byte is never Han, so it always lies in a non-Han block.  One thread per alnum16
-// word (1 KiB of text); for each 16-byte chunk with an alnum byte and each block
-// with an alnum byte there, the thread cuts the block when this chunk holds the
-// block's first alnum byte (the block starts in the chunk, or walking back from it
-// to the block start meets no alnum byte).  Block bounds come from the lane masks
-// of k_mark_walk, so the kernel touches neither the block list nor the Han blocks.
+// byte is never Han, so it always lies in a non-Han block.  One wave per 64 alnum16
+// words (64 KiB of text), their alnum chunks dealt over its lanes (nonzh_waves); for
+// each such chunk and each block with an alnum byte there, the lane cuts the block
+// when this chunk holds the block's first alnum byte (the block starts in the chunk,
+// or walking back from it to the block start meets no alnum byte).  Block bounds come
+// from the lane masks of k_mark_walk, so the kernel touches neither the block list nor
+// the Han blocks.
 __device__ __forceinline__ void nonzh_body(const uint8_t* __restrict__ text, uint32_t nbytes,
                                            const uint32_t* __restrict__ lanemask, const uint2* __restrict__ tile_cnt,
                                            uint32_t ntiles, const uint64_t* __restrict__ alnum16,
                                            uint32_t* __restrict__ sbits, uint32_t* __restrict__ ebits,
                                            uint32_t* __restrict__ docbits, const uint64_t* __restrict__ doc_off,
-                                           uint32_t ndocs, uint32_t wg, uint32_t ng, uint8_t (*s_win)[80]) {
-    const uint32_t nch = (nbytes + 15u) >> 4, nw = (nch + 63u) >> 6;
+                                           uint32_t ndocs, uint32_t wg, uint32_t ng, NzLds& L) {
+    const uint32_t nch = (nbytes + 15u) >> 4;
     // the words k_docbits set back to zero for the next run (k_mark_walk, their only
     // reader, is done): one store per document
     for (uint32_t d = wg * 256u + threadIdx.x; d < ndocs; d += ng * 256u) {
@@ -4198,8 +4297,7 @@ __device__ __forceinline__ void nonzh_body(const uint8_t* __restrict__ text, uin
         if (o < nbytes) docbits[o >> 5] = 0u;
     }
     Emitter em(sbits, ebits);
-    for (uint32_t wi = wg * 256u + threadIdx.x; wi < nw; wi += ng * 256u)
-        nonzh_word<64>(text, nbytes, nch, lanemask, tile_cnt, ntiles, alnum16, wi, em, s_win[threadIdx.x]);
+    nonzh_waves<64>(text, nbytes, nch, lanemask, tile_cnt, ntiles, alnum16, wg * 4u + (threadIdx.x >> 6), ng * 4u, em, L);
     em.flush();
 }
 __global__ __launch_bounds__(256) void k_nonzh(const uint8_t* __restrict__ text, uint32_t nbytes,
@@ -4208,9 +4306,9 @@ __global__ __launch_bounds__(256) void k_nonzh(const uint8_t* __restrict__ text,
                                                const uint64_t* __restrict__ alnum16, uint32_t* __restrict__ sbits,
                                                uint32_t* __restrict__ ebits, uint32_t* __restrict__ docbits,
                                                const uint64_t* __restrict__ doc_off, uint32_t ndocs) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[256][80];
+    __shared__ __attribute__((aligned(16))) NzLds s_nz;
     nonzh_body(text, nbytes, lanemask, tile_cnt, ntiles, alnum16, sbits, ebits, docbits, doc_off, ndocs, blockIdx.x,
-               gridDim.x, s_win);
+               gridDim.x, s_nz);
 }
 
 // ---------------------------------------------------------------------------
@@ -4642,7 +4740,7 @@ union LongAll {  // the phases' LDS
     uint32_t m32[kLpBatch * kLpMap / 4u];  // k_long_path (wave 0)
     uint4 cd4[256][kSeg / 16u];       // k_long_pbits, k_long_tail
     uint8_t bl[256][kSeg];            // k_long_seg
-    uint8_t nz[256][80];              // k_nonzh's windows (k_long<.., true>, before the long phases)
+    NzLds nz;                         // k_nonzh's windows and chunk lists (k_long<.., true>, before the long phases)
 };
 
 template <bool HMM, bool NZ>
