@@ -2236,7 +2236,11 @@ __device__ __forceinline__ void nonzh_chunk(const uint8_t* __restrict__ text, ui
 // wave's lanes in order through an LDS list, kNzCap per round (two per lane, their
 // loads issued together): a lane per word instead made every wave as slow as its
 // busiest word's serial chain of dependent loads.
-constexpr uint32_t kNzCap = 128u;
+#ifndef JB_NZ_CAP
+#define JB_NZ_CAP 128
+#endif
+constexpr uint32_t kNzCap = JB_NZ_CAP;
+static_assert(kNzCap % 64u == 0u && kNzCap >= 64u && kNzCap <= 256u, "whole rounds of the wave's lanes");
 struct NzLds {
     uint8_t win[256][80];          // the lanes' nonzh_block windows
     uint32_t list[4][kNzCap];      // each wave's chunks of the round
