@@ -923,6 +923,46 @@ def test_nonzh_blocks_across_chunks_and_tiles(small):
     _cmp_batch(tk, o, buf1, off1, True, "nonzh one document")
 
 
+def test_nonzh_mask_tokenizer_rune_classes(small):
+    """k_nonzh tokenizes a block that fits one round of four 16-byte loads from bit
+    masks (nonzh_masks) and decodes only its bytes >= 0x80 rune by rune; longer
+    blocks take the per-byte path.  cutNonZh's rules (tokenizer.go:289-310) over
+    every class the masks separate: alnum runs, ASCII punctuation, all six ASCII
+    spaces, the non-ASCII spaces of unicode.IsSpace (U+0085, U+00A0, U+1680, U+2000,
+    U+200A, U+2028, U+2029, U+202F, U+205F, U+3000), 2/3/4-byte runes, invalid and
+    truncated sequences, at every start offset of a chunk and with block lengths
+    around the 48/64-byte edges of the mask path, between Han runs."""
+    tk, o, s = small
+    rng = random.Random(4242)
+    spaces = [" ", "\t", "\n", "\v", "\f", "\r", "\u0085", " ", " ", " ", " ",
+              " ", " ", " ", " ", "　"]
+    others = ["a", "Zq", "09", "x1y2", "!", "#", "-", ".", "，", "é", "ß", "—", "😀", "Ω", "ｱ", "k"]
+    bad = [b"\x80", b"\xff", b"\xc3", b"\xe4\xb8", b"\xf0\x9f\x98", b"\xc0\xaf", b"\xed\xa0\x80", b"\xf4\x90\x80\x80"]
+    docs = []
+    for n in range(400):
+        parts = [b"\xe4\xb8\xad" * rng.randint(0, 20)]  # Han before the block: every start offset
+        k = rng.choice([1, 2, 5, 15, 16, 17, 31, 32, 33, 46, 47, 48, 49, 50, 63, 64, 65, 70, 100])
+        blk = b""
+        while len(blk) < k:
+            r = rng.random()
+            if r < 0.3:
+                blk += rng.choice(spaces).encode()
+            elif r < 0.9:
+                blk += rng.choice(others).encode()
+            else:
+                blk += rng.choice(bad)
+        if not any(ch in b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789" for ch in blk):
+            blk += b"7"  # (a block without alnum has no tokens at all)
+        parts.append(blk)
+        parts.append("国".encode() * rng.randint(0, 3))
+        docs.append(b"".join(parts))
+    buf, off = _batch_of(docs)
+    for hmm in (False, True):
+        _cmp_batch(tk, o, buf, off, hmm, "nonzh rune classes")
+    buf1, off1 = _batch_of([b"".join(docs)])
+    _cmp_batch(tk, o, buf1, off1, True, "nonzh rune classes, one document")
+
+
 @pytest.mark.parametrize("group", [1024, 6144])
 def test_zh_blocks_from_lane_masks(syn_small, group, monkeypatch):
     """k_zh takes its groups' Han blocks from k_mark_walk's lane masks: groups with
