@@ -4318,7 +4318,10 @@ __global__ __launch_bounds__(256) void k_nonzh(const uint8_t* __restrict__ text,
 // ---------------------------------------------------------------------------
 // token bitmaps -> spans
 // ---------------------------------------------------------------------------
-constexpr uint32_t kTokCap = 3072;  // tokens per tile staged in LDS (k_tok's write pass)
+#ifndef JB_TOK_CAP
+#define JB_TOK_CAP 3072
+#endif
+constexpr uint32_t kTokCap = JB_TOK_CAP;  // tokens per tile staged in LDS (k_tok's write pass)
 // block `blk` of `nblk` (the write pass: token tile blk; the count pass: tiles 2 blk, 2 blk + 1)
 template <bool WRITE>
 __device__ __forceinline__ void tok_body(const uint32_t* __restrict__ sbits, const uint32_t* __restrict__ ebits,
